@@ -1,0 +1,207 @@
+"""Headline benchmark: aggregated edges/s (+ epoch time) of GraphSAGE training
+on ogbn-products-shaped mini-batches, fanout [15,10], batch 1024 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Workload (config.workload = "products-[15,10]-bs1024"): synthetic graph with
+ogbn-products' published sizes (N=2,449,029, 123.7 M directed entries, F=100,
+C=47, 196,615 train seeds; datasets cannot be downloaded here), model
+SAGE(100, 256, 47, num_layers=2, dropout=0.5) + Adam(1e-3), fp32 — the
+reference's PipelineCO baseline loop (pipeline.py:152-169).
+
+A "step" = one training iteration over one mini-batch already resident in HBM
+(sampled on the GPU before the timed region): forward of both SAGE layers over
+the whole block, cross-entropy on the seed rows, backward, RCCL gradient
+all-reduce (N>1) and Adam.  Aggregated edges per step = num_layers x E_batch
+(every layer aggregates all E edges of the block, sage.py:33-34).
+value = sum over ranks of edges / max-over-ranks wall time.
+
+Also reported: epoch_time_s — one full pass over this rank's train seeds
+INCLUDING GPU sampling + feature gather (193 batches at N=1); the roofline
+of the dominant kernel (HIP events around every launch inside the timed
+region); the reference-equivalent CPU path timed on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "noise-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch-size", type=int, default=1024)
+    ap.add_argument("--fanout", type=str, default="15,10")
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--scale", type=float, default=1.0, help="graph size scale (tests)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-epoch", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def train_step(model, opt, reducer, b):
+    out = model(b.x, b.edge_index)[:b.batch_size]
+    loss = F.cross_entropy(out, b.y[:b.batch_size])
+    opt.zero_grad(set_to_none=False)
+    loss.backward()
+    reducer()
+    opt.step()
+    return loss
+
+
+def cpu_baseline(batch, args, layers):
+    """The reference's CPU path: the PyG 2.5.1 op sequence restated in torch
+    (oracle/pyg_ref.py), one training step (fwd + bwd + Adam) on ONE sampled
+    block of the same workload, repeated for ~args.cpu_seconds."""
+    from oracle import pyg_ref
+    torch.manual_seed(0)
+    threads = torch.get_num_threads()
+    m = pyg_ref.SAGE(100, args.hidden, 47, layers, dropout=0.5)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    x, ei, y = batch.x.cpu(), batch.edge_index.cpu(), batch.y.cpu()
+    E = ei.shape[1]
+    pyg_ref.train_step(m, opt, x, ei, y, batch.batch_size)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        pyg_ref.train_step(m, opt, x, ei, y, batch.batch_size)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds or n >= 50:
+            break
+    return {"value": layers * E * n / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "ms_per_step": 1e3 * dt / n,
+            "sample": f"{n} training steps (fwd+bwd+Adam) on one products-[15,10] bs=1024 block "
+                      f"(E={E}, N={batch.num_nodes}), torch {torch.__version__} CPU, "
+                      f"{threads} threads, PyG 2.5.1 op sequence restated in oracle/pyg_ref.py"}
+
+
+def main():
+    args = parse()
+    import torch.distributed as dist
+
+    import ngnn
+    from ngnn import _timing
+    from ngnn.distributed import GradAllReduce, init
+    from ngnn.loader import NeighborLoader, sample_block, synthetic_graph
+
+    rank, world, local = init()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    fanout = [int(v) for v in args.fanout.split(",")]
+    layers = len(fanout)
+
+    graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
+    torch.manual_seed(1234)  # identical init on every rank
+    model = ngnn.SAGE(100, args.hidden, 47, layers, dropout=0.5).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    reducer = GradAllReduce(model.parameters())
+    model.train()
+
+    # pre-sample this rank's batches (inputs resident in HBM before timing)
+    loader = NeighborLoader(graph, graph.train_idx, fanout, args.batch_size, shuffle=True, seed=7,
+                            rank=rank, world_size=world)
+    it = iter(loader)
+    nb = min(len(loader), args.steps + args.warmup)
+    batches = [next(it) for _ in range(nb)]
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        train_step(model, opt, reducer, batches[i % nb])
+    barrier()
+    timer = _timing.KernelTimer()
+    edges = 0
+    t0 = time.perf_counter()
+    with timer:
+        for i in range(args.steps):
+            b = batches[(args.warmup + i) % nb]
+            train_step(model, opt, reducer, b)
+            edges += layers * b.edge_index.shape[1]
+    barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt, float(edges)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, edges = float(tmax[0]), float(t[1])
+    else:
+        dt, edges = float(t[0]), float(t[1])
+
+    # dominant kernel roofline from the live events of the timed region
+    summ = timer.summary()
+    dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
+    roof = None
+    if dom:
+        name, (n, ms, nbytes) = dom
+        ach = nbytes / (ms * 1e-3) / 1e9
+        roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "launches": n, "avg_us": round(1e3 * ms / n, 2),
+                "alg_bytes_per_launch": int(nbytes / n),
+                "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
+                                    "GBps": round(v[2] / (v[1] * 1e-3) / 1e9, 1)}
+                                for k, v in summ.items()}}
+
+    # full epoch incl. GPU sampling (this rank's shard)
+    epoch_s = None
+    if not args.no_epoch:
+        barrier()
+        t1 = time.perf_counter()
+        for b in loader:
+            train_step(model, opt, reducer, b)
+        barrier()
+        epoch_s = time.perf_counter() - t1
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(batches[0], args, layers)
+
+    if rank == 0:
+        E_avg = sum(b.edge_index.shape[1] for b in batches) / nb
+        N_avg = sum(b.num_nodes for b in batches) / nb
+        line = {
+            "metric": "aggregated edges/sec (GraphSAGE train step), ogbn-products fanout=[15,10] bs=1024",
+            "value": round(edges / dt, 1), "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded Chung-Lu graph with ogbn-products sizes; random features)",
+            "config": {"workload": f"products-[{args.fanout}]-bs{args.batch_size}",
+                       "model": f"SAGE(100,{args.hidden},47,L={layers}) mean-aggr + Adam",
+                       "global_batch": args.batch_size * world, "fanout": fanout,
+                       "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
+                       "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},
+            "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
+            "epoch_batches_per_rank": len(loader),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

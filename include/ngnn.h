@@ -1,0 +1,129 @@
+/*
+ * ngnn.h — C ABI of the MI355X-native GraphSAGE / GCN aggregation path.
+ *
+ * The reference (hhilsber/noise-GNN) is pure Python: its hot path is
+ * SAGE.forward -> PyG SAGEConv.forward (src/models/layers/sage.py:30-40,
+ * conv call at :34) and SimpleGCN.forward -> PyG GCNConv.forward
+ * (src/models/layers/convolution.py:29-35, call at :31).  PyG 2.5.1 [ext]
+ * implements each conv as index_select (gather) + scatter_add_/scatter_reduce_
+ * (scatter) + Linear.  The reference has no FFI of its own; the entry points
+ * below are what a ctypes binding of those PyG internals would bind, and are
+ * what noise-gnn_amd/ngnn/_lib.py binds (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers unless stated; the caller owns every
+ *     buffer (PyTorch caching-allocator tensors).  The library never
+ *     allocates, frees or retains pointers beyond the call.
+ *   - Every call is asynchronous and stream-ordered on `stream`
+ *     (a hipStream_t passed as void*; NULL = the legacy default stream).
+ *   - Return 0 on success, a negative NGNN_E_* for argument errors (nothing
+ *     is launched), or a positive hipError_t from a failed launch.
+ *   - Index arrays are int32 internally (N, E < 2^31), rows of feature
+ *     matrices are addressed with an explicit leading dimension (elements).
+ *   - No global mutable state: re-entrant, safe from any host thread.
+ */
+#ifndef NGNN_H
+#define NGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGNN_ABI_VERSION 2
+
+/* error codes (negative); positive values are hipError_t */
+#define NGNN_OK 0
+#define NGNN_E_ARG (-1)        /* null pointer / negative size / bad enum   */
+#define NGNN_E_DTYPE (-2)      /* unsupported dtype                          */
+#define NGNN_E_SHAPE (-3)      /* F / leading dimension / size out of range  */
+#define NGNN_E_ALIGN (-4)      /* pointer alignment not supported            */
+#define NGNN_E_RANGE (-5)      /* N or E does not fit int32                  */
+#define NGNN_E_WORKSPACE (-6)  /* workspace too small                        */
+
+/* reductions: PyG `aggr` names (utils/scatter.py [ext]) */
+#define NGNN_REDUCE_SUM 0  /* GCNConv aggr='add'                             */
+#define NGNN_REDUCE_MEAN 1 /* SAGEConv default aggr='mean' (sage.py:16-19)   */
+#define NGNN_REDUCE_MAX 2  /* SAGEConv(aggr='max'): build extension          */
+
+/* dtypes */
+#define NGNN_F32 0
+#define NGNN_BF16 1
+
+int ngnn_abi_version(void);
+const char *ngnn_strerror(int rc);
+
+/* ------------------------------------------------------------------ edges
+ * Validate a PyG edge_index [2,E] int64 (row 0 = source, row 1 = target,
+ * flow source_to_target) before any kernel indexes with it.
+ * status (device int32[4], caller zeroes it):
+ *   [0] != 0  some source id outside [0, n_src)
+ *   [1] != 0  some target id outside [0, n_dst)
+ *   [2] != 0  targets are NOT non-decreasing (needs the sorting CSR path)
+ *   [3] != 0  sources are NOT non-decreasing
+ * Replaces PyG's implicit index checks in index_select / scatter [ext]
+ * (reached from sage.py:34 / convolution.py:31). */
+int ngnn_edge_probe(const int64_t *edge_index, int64_t E, int64_t n_src, int64_t n_dst,
+                    int32_t *status, void *stream);
+
+/* Workspace bytes ngnn_csr_build needs for the unsorted path. */
+size_t ngnn_csr_workspace_bytes(int64_t E, int64_t n_rows);
+
+/* Group the E edges by `keys` (int64, values in [0,n_rows)) into CSR:
+ *   rowptr[n_rows+1] (int32), col[E] = vals in grouped order (int32),
+ *   eid[E] = original edge position (int32, nullable).
+ * Grouping is STABLE (edge order kept inside a row), so per-row reductions
+ * run in the same order as PyG's CPU scatter_add_ / index_add_.
+ * keys_sorted=1 claims keys are non-decreasing (fast path, no workspace);
+ * keys_sorted=0 uses a stable radix sort in `ws`.
+ * Forward CSR: keys = edge_index[1] (targets), vals = edge_index[0].
+ * Transposed CSR for the backward gather: keys = edge_index[0], vals = edge_index[1]. */
+int ngnn_csr_build(const int64_t *keys, const int64_t *vals, int64_t E, int64_t n_rows,
+                   int keys_sorted, int32_t *rowptr, int32_t *col, int32_t *eid,
+                   void *ws, size_t ws_bytes, void *stream);
+
+/* ------------------------------------------------------------ aggregation
+ * out[i, :F] = reduce_{e in rowptr[i]..rowptr[i+1]} x[col[e], :F]
+ * SUM : edge-order fp32 sum; MEAN: sum / max(deg,1) (IEEE division);
+ * MAX : NaN-propagating max, empty rows -> 0 (scatter_reduce amax,
+ *       include_self=False on a zero tensor).
+ * Replaces PyG MessagePassing.propagate (gather x_j + utils.scatter) [ext]. */
+int ngnn_seg_agg_fwd(const void *x, int64_t ldx, int64_t F, const int32_t *rowptr,
+                     const int32_t *col, int64_t n_dst, int reduce, int dtype,
+                     void *out, int64_t ldo, void *stream);
+
+/* grad_x[j, :F] = sum over edges e with source j (transposed CSR, edge
+ * order) of  SUM : g[dst_e]   MEAN: g[dst_e] / max(deg(dst_e),1)
+ *            MAX : [x[j]==agg[dst_e]] * g[dst_e] / ties(dst_e)
+ * where ties = #tied sources + [agg == 0] (torch scatter_reduce amax
+ * backward, FunctionsManual.cpp [ext]).  grad_x is fully overwritten
+ * (rows with no out-edges get 0).  For MAX, `ws` must hold n_dst*F floats
+ * (ngnn_seg_agg_bwd_workspace_bytes) and x/agg/rowptr/col (forward CSR)
+ * are required; for SUM/MEAN they may be NULL except rowptr (degrees). */
+size_t ngnn_seg_agg_bwd_workspace_bytes(int64_t n_dst, int64_t F, int reduce);
+int ngnn_seg_agg_bwd(const void *grad_out, int64_t ldg, int64_t F,
+                     const int32_t *rowptr, const int32_t *col, int64_t n_dst,
+                     const int32_t *rowptr_t, const int32_t *col_t, int64_t n_src,
+                     int reduce, int dtype, const void *x, int64_t ldx,
+                     const void *agg, int64_t lda, void *grad_x, int64_t ldgx,
+                     void *ws, size_t ws_bytes, void *stream);
+
+/* ---------------------------------------------------------- sampling
+ * One hop of uniform neighbour sampling without replacement (PyG
+ * NeighborLoader / pyg-lib neighbor_sample semantics [ext], constructed at
+ * pipeline.py:75-83): for frontier node v (global id) with in-degree d,
+ * take min(d, fanout) distinct in-neighbours from graph CSR
+ * (g_rowptr int64[N+1], g_col int32[nnz]) in Floyd order.
+ *   out_nbr[i*fanout + k] = global neighbour id (or -1 past the count),
+ *   out_cnt[i]            = number taken.
+ * Deterministic in (seed, frontier position). */
+int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t *frontier,
+                    int64_t n_frontier, int fanout, uint64_t seed, int64_t *out_nbr,
+                    int32_t *out_cnt, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NGNN_H */

@@ -1,0 +1,34 @@
+// Internal helpers shared by the ngnn HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ngnn.h"
+
+#define NGNN_RETURN_IF(cond, code) \
+    do {                           \
+        if (cond) return (code);   \
+    } while (0)
+
+namespace ngnn {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+inline int launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NGNN_OK : static_cast<int>(e);
+}
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool fits_i32(int64_t v) { return v >= 0 && v <= INT32_MAX; }
+
+inline bool aligned(const void *p, size_t a) {
+    return (reinterpret_cast<uintptr_t>(p) % a) == 0;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace ngnn

@@ -1,0 +1,80 @@
+"""ctypes binding of libngnn.so (C ABI declared in include/ngnn.h).
+
+The library is built in-tree by ``noise-gnn_amd/csrc/Makefile`` into
+``noise-gnn_amd/ngnn/lib/libngnn.so``.  There is no fallback: if the library
+is missing, every op raises.  Loading the library needs no GPU (it only links
+libamdhip64), so CPU tests can check the exported symbols.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
+ABI_VERSION = 2
+
+OK = 0
+REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
+F32, BF16 = 0, 1
+
+# name -> (restype, argtypes); mirrors include/ngnn.h one to one
+_i64, _i32, _sz, _p, _int = ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+SIGNATURES = {
+    "ngnn_abi_version": (_int, []),
+    "ngnn_strerror": (ctypes.c_char_p, [_int]),
+    "ngnn_edge_probe": (_int, [_p, _i64, _i64, _i64, _p, _p]),
+    "ngnn_csr_workspace_bytes": (_sz, [_i64, _i64]),
+    "ngnn_csr_build": (_int, [_p, _p, _i64, _i64, _int, _p, _p, _p, _p, _sz, _p]),
+    "ngnn_seg_agg_fwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _int, _int, _p, _i64, _p]),
+    "ngnn_seg_agg_bwd_workspace_bytes": (_sz, [_i64, _i64, _int]),
+    "ngnn_seg_agg_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _i64, _int, _int,
+                                _p, _i64, _p, _i64, _p, _i64, _p, _sz, _p]),
+    "ngnn_sample_hop": (_int, [_p, _p, _p, _i64, _int, ctypes.c_uint64, _p, _p, _p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NGNNError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NGNNError(
+                    f"libngnn.so not found at {LIB_PATH}: build it with "
+                    "`make -C noise-gnn_amd/csrc` (or __graft_entry__.build()); "
+                    "there is no CPU fallback")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype, fn.argtypes = res, args
+            v = lib.ngnn_abi_version()
+            if v != ABI_VERSION:
+                raise NGNNError(f"libngnn ABI {v} != expected {ABI_VERSION}; rebuild")
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != OK:
+        msg = load().ngnn_strerror(rc).decode()
+        raise NGNNError(f"{what}: {msg} (rc={rc})" if what else f"{msg} (rc={rc})")
+
+
+def ptr(t) -> int:
+    """Device address of a tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,146 @@
+"""Device-resident CSR view of a PyG ``edge_index`` block.
+
+PyG's ``MessagePassing.propagate`` [ext] re-reads ``edge_index`` on every
+conv call (``sage.py:34`` runs it once per layer, and autograd runs the
+transposed scatter again).  Here an edge_index is validated and grouped by
+target ONCE per mini-batch; every layer, the backward pass and the
+transposed (by-source) CSR reuse it.
+
+* ``rowptr`` int32 [N+1], ``col`` int32 [E]: edges grouped by target
+  (``edge_index[1]``), edge order kept inside a row (stable).
+* ``transposed()``: the same grouped by source, for input gradients.
+
+Validation replaces the index errors PyG / ATen raise from ``index_select``:
+an out-of-range id raises ``IndexError`` before any kernel touches memory.
+That check reads four status words back to the host (one sync per block).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+
+import torch
+
+from . import _lib
+
+
+def _require_device_index(edge_index: torch.Tensor) -> None:
+    if not isinstance(edge_index, torch.Tensor):
+        raise TypeError("edge_index must be a torch.Tensor (SparseTensor is not supported)")
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError(f"edge_index must have shape [2, E], got {tuple(edge_index.shape)}")
+    if edge_index.dtype != torch.long:
+        raise TypeError(f"edge_index must be int64, got {edge_index.dtype}")
+    if not edge_index.is_cuda:
+        raise RuntimeError("ngnn runs on the GPU only: edge_index is on the CPU "
+                           "(move the batch with batch.to(device) as pipeline.py:153 does)")
+
+
+class CSR:
+    __slots__ = ("rowptr", "col", "n_rows", "nnz")
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_rows: int):
+        self.rowptr, self.col, self.n_rows, self.nnz = rowptr, col, n_rows, col.numel()
+
+    def degree(self) -> torch.Tensor:
+        return (self.rowptr[1:] - self.rowptr[:-1])
+
+
+def build_csr(keys: torch.Tensor, vals: torch.Tensor, n_rows: int, keys_sorted: bool) -> CSR:
+    lib = _lib.load()
+    dev = keys.device
+    E = keys.numel()
+    rowptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(E, 0), dtype=torch.int32, device=dev)
+    ws, ws_bytes = None, 0
+    if not keys_sorted and E > 0:
+        ws_bytes = lib.ngnn_csr_workspace_bytes(E, n_rows)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    rc = lib.ngnn_csr_build(_lib.ptr(keys), _lib.ptr(vals), E, n_rows, int(keys_sorted),
+                            _lib.ptr(rowptr), _lib.ptr(col), None, _lib.ptr(ws), ws_bytes,
+                            _lib.stream_handle(dev))
+    _lib.check(rc, "ngnn_csr_build")
+    return CSR(rowptr, col, n_rows)
+
+
+class Block:
+    """Validated, CSR-grouped homogeneous block: ``num_nodes`` sources == targets."""
+
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, *, n_dst: int | None = None,
+                 validate: bool = True, dst_sorted: bool | None = None,
+                 src_sorted: bool | None = None):
+        _require_device_index(edge_index)
+        edge_index = edge_index.contiguous()
+        self.edge_index = edge_index
+        self.n_src = int(num_nodes)
+        self.n_dst = int(num_nodes if n_dst is None else n_dst)
+        self.E = edge_index.size(1)
+        self.device = edge_index.device
+        if validate or dst_sorted is None or src_sorted is None:
+            status = torch.zeros(4, dtype=torch.int32, device=self.device)
+            rc = _lib.load().ngnn_edge_probe(_lib.ptr(edge_index), self.E, self.n_src, self.n_dst,
+                                             _lib.ptr(status), _lib.stream_handle(self.device))
+            _lib.check(rc, "ngnn_edge_probe")
+            s = status.tolist()  # host sync: the one validation read-back per block
+            if s[0]:
+                raise IndexError(f"edge_index[0] holds ids outside [0, {self.n_src})")
+            if s[1]:
+                raise IndexError(f"edge_index[1] holds ids outside [0, {self.n_dst})")
+            dst_sorted, src_sorted = not s[2], not s[3]
+        self.dst_sorted, self.src_sorted = bool(dst_sorted), bool(src_sorted)
+        self.csr = build_csr(edge_index[1], edge_index[0], self.n_dst, self.dst_sorted)
+        self._csr_t = None
+
+    @property
+    def rowptr(self):
+        return self.csr.rowptr
+
+    @property
+    def col(self):
+        return self.csr.col
+
+    def transposed(self) -> CSR:
+        """Edges grouped by source (for input gradients); built lazily, cached."""
+        if self._csr_t is None:
+            ei = self.edge_index
+            self._csr_t = build_csr(ei[0], ei[1], self.n_src, self.src_sorted)
+        return self._csr_t
+
+
+class _BlockCache:
+    """Tiny LRU keyed by edge_index identity/version, so the layers of one
+    forward (and its backward) share one Block.  Holding the tensor keeps its
+    storage alive, so a cached data_ptr can never be recycled under us."""
+
+    def __init__(self, capacity: int = 8):
+        self.capacity = capacity
+        self._d: collections.OrderedDict = collections.OrderedDict()
+        self._lock = threading.Lock()
+
+    def get(self, edge_index: torch.Tensor, num_nodes: int) -> Block:
+        key = (edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()),
+               edge_index._version, int(num_nodes), edge_index.device)
+        with self._lock:
+            hit = self._d.get(key)
+            if hit is not None and hit[0] is edge_index:
+                self._d.move_to_end(key)
+                return hit[1]
+        blk = Block(edge_index, num_nodes)
+        with self._lock:
+            self._d[key] = (edge_index, blk)
+            while len(self._d) > self.capacity:
+                self._d.popitem(last=False)
+        return blk
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
+block_cache = _BlockCache()
+
+
+def get_block(edge_index, num_nodes: int) -> Block:
+    if isinstance(edge_index, Block):
+        return edge_index
+    return block_cache.get(edge_index, num_nodes)

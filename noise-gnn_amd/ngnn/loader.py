@@ -1,0 +1,216 @@
+"""Device-resident graphs and a NeighborLoader-style mini-batch sampler.
+
+The reference builds ``torch_geometric.loader.NeighborLoader`` over an
+OGB / PyG dataset (``pipeline.py:75-92``, ``pipeline_s.py:72-89``) whose
+sampler (pyg-lib / torch-sparse, C++ [ext]) runs in a worker process and
+ships every batch host->device (``pipeline.py:153``).  Here the graph CSR and
+the feature table stay resident in HBM and every hop is sampled on the GPU
+by ``ngnn_sample_hop`` (uniform, without replacement, Floyd's algorithm).
+
+Batch layout follows what NeighborLoader hands the model (the contract of
+``pipeline.py:152-160``):
+
+* ``n_id``: the seeds first (``[:batch_size]``), then every newly reached
+  node of hop 1, then hop 2, ... in order of first appearance;
+* ``edge_index`` [2,E] local ids, row 0 = source (sampled neighbour), row 1 =
+  target, grouped by target in frontier order => targets non-decreasing;
+* ``x = x_all[n_id]``, ``y = y_all[n_id]``, ``batch_size``.
+
+Datasets are not downloadable offline, so :func:`synthetic_graph` makes
+seeded graphs with the published sizes of ogbn-products / ogbn-arxiv /
+Amazon-Computers / CitationFull-Cora and a power-law
+(Chung-Lu) degree profile.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import torch
+
+from . import _lib
+
+# name -> (num_nodes, directed entries (symmetric), features, classes, train seeds)
+DATASETS = {
+    "ogbn-products": (2_449_029, 123_718_280, 100, 47, 196_615),
+    "ogbn-arxiv": (169_343, 2_315_598, 128, 40, 90_941),
+    "computers": (13_752, 491_722, 767, 10, 300),
+    "cora": (19_793, 126_842, 8_710, 70, 1_395),
+}
+
+
+@dataclasses.dataclass
+class Graph:
+    rowptr: torch.Tensor   # int64 [N+1], in-neighbours of each node (CSC of the symmetric graph)
+    col: torch.Tensor      # int32 [nnz]
+    x: torch.Tensor        # float32 [N, F]
+    y: torch.Tensor        # int64 [N]
+    train_idx: torch.Tensor
+    num_classes: int
+
+    @property
+    def num_nodes(self) -> int:
+        return self.rowptr.numel() - 1
+
+    @property
+    def num_edges(self) -> int:
+        return self.col.numel()
+
+
+@dataclasses.dataclass
+class Batch:
+    x: torch.Tensor
+    y: torch.Tensor
+    edge_index: torch.Tensor
+    n_id: torch.Tensor
+    batch_size: int
+
+    @property
+    def num_nodes(self) -> int:
+        return self.n_id.numel()
+
+    def to(self, device):
+        return Batch(self.x.to(device), self.y.to(device), self.edge_index.to(device),
+                     self.n_id.to(device), self.batch_size)
+
+
+def _gen(device, seed):
+    return torch.Generator(device=device).manual_seed(seed)
+
+
+def synthetic_graph(name: str = "ogbn-products", device="cuda", seed: int = 0,
+                    scale: float = 1.0, num_features: int | None = None) -> Graph:
+    """Seeded Chung-Lu graph with the dataset's published N / nnz / F / C.
+
+    ``scale`` < 1 shrinks N and nnz proportionally (tests).  Undirected edges
+    are drawn with endpoint probability proportional to a power-law weight
+    (w_i ~ (i+1)^-0.5, shuffled), self-loops dropped, then symmetrised, so
+    nnz comes out within a fraction of a percent of the target.
+    """
+    N0, nnz0, F0, C, n_train0 = DATASETS[name]
+    N = max(int(N0 * scale), 16)
+    nnz = max(int(nnz0 * scale), 32)
+    F = num_features or F0
+    n_train = max(min(int(n_train0 * scale), N), 1)
+    dev = torch.device(device)
+    g = _gen(dev, seed)
+    w = torch.arange(1, N + 1, device=dev, dtype=torch.float64).pow(-0.5)
+    w = w[torch.randperm(N, device=dev, generator=g)]
+    cdf = torch.cumsum(w, 0)
+    cdf = cdf / cdf[-1]
+    m = nnz // 2
+    u = torch.searchsorted(cdf, torch.rand(m, device=dev, generator=g, dtype=torch.float64))
+    v = torch.searchsorted(cdf, torch.rand(m, device=dev, generator=g, dtype=torch.float64))
+    u.clamp_(max=N - 1)
+    v.clamp_(max=N - 1)
+    keep = u != v
+    u, v = u[keep], v[keep]
+    src = torch.cat([u, v])
+    dst = torch.cat([v, u])
+    del u, v, keep
+    order = torch.argsort(dst * N + src)
+    src, dst = src[order], dst[order]
+    del order
+    counts = torch.bincount(dst, minlength=N)
+    rowptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    col = src.to(torch.int32)
+    del src, dst, counts
+    gx = _gen(dev, seed + 1)
+    x = torch.randn(N, F, device=dev, generator=gx, dtype=torch.float32)
+    y = torch.randint(0, C, (N,), device=dev, generator=_gen(dev, seed + 2))
+    train_idx = torch.randperm(N, device=dev, generator=_gen(dev, seed + 3))[:n_train]
+    return Graph(rowptr, col, x, y, train_idx, C)
+
+
+def sample_hop(graph: Graph, frontier: torch.Tensor, fanout: int, seed: int):
+    """[n_frontier, fanout] global neighbour ids (-1 = none) and counts."""
+    nf = frontier.numel()
+    out = torch.empty(nf, fanout, dtype=torch.int64, device=frontier.device)
+    cnt = torch.empty(nf, dtype=torch.int32, device=frontier.device)
+    rc = _lib.load().ngnn_sample_hop(_lib.ptr(graph.rowptr), _lib.ptr(graph.col),
+                                     _lib.ptr(frontier), nf, fanout, seed & (2**64 - 1),
+                                     _lib.ptr(out), _lib.ptr(cnt),
+                                     _lib.stream_handle(frontier.device))
+    _lib.check(rc, "ngnn_sample_hop")
+    return out, cnt
+
+
+def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
+                 gather_features: bool = True) -> Batch:
+    dev = seeds.device
+    n_id = seeds.to(torch.int64)
+    frontier = n_id
+    frontier_local = torch.arange(n_id.numel(), device=dev)
+    srcs, dsts = [], []
+    for hop, k in enumerate(fanouts):
+        nbr, _ = sample_hop(graph, frontier, int(k), seed * 1_000_003 + hop)
+        mask = nbr >= 0
+        dst_local = frontier_local.unsqueeze(1).expand(-1, int(k))[mask]
+        cand = nbr[mask]
+        n_old = n_id.numel()
+        all_ids = torch.cat([n_id, cand])
+        uniq, inv = torch.unique(all_ids, return_inverse=True)
+        pos = torch.arange(all_ids.numel(), device=dev)
+        first = torch.full((uniq.numel(),), all_ids.numel(), dtype=torch.int64, device=dev)
+        first.scatter_reduce_(0, inv, pos, reduce="amin")
+        order = torch.argsort(first)
+        rank = torch.empty_like(order)
+        rank[order] = torch.arange(order.numel(), device=dev)
+        local_all = rank[inv]
+        srcs.append(local_all[n_old:])
+        dsts.append(dst_local)
+        new_nodes = uniq[order[n_old:]]
+        frontier_local = torch.arange(n_old, n_old + new_nodes.numel(), device=dev)
+        n_id = torch.cat([n_id, new_nodes])
+        frontier = new_nodes
+    edge_index = torch.stack([torch.cat(srcs), torch.cat(dsts)]) if srcs else \
+        torch.empty(2, 0, dtype=torch.int64, device=dev)
+    x = graph.x.index_select(0, n_id) if gather_features else None
+    y = graph.y.index_select(0, n_id)
+    return Batch(x, y, edge_index, n_id, int(seeds.numel()))
+
+
+class NeighborLoader:
+    """Iterable of :class:`Batch` over ``input_nodes`` (default: all nodes).
+
+    Mirrors the ``NeighborLoader(data, input_nodes, num_neighbors, batch_size,
+    shuffle)`` arguments of pipeline.py:75-92; ``num_workers`` /
+    ``persistent_workers`` have no meaning here (sampling runs on the GPU).
+    ``rank`` / ``world_size`` shard the (shuffled) seeds for seed-node data
+    parallelism: every rank draws the same permutation and takes its slice.
+    """
+
+    def __init__(self, graph: Graph, input_nodes=None, num_neighbors=(15, 10), batch_size=1024,
+                 shuffle=False, seed: int = 0, rank: int = 0, world_size: int = 1,
+                 drop_last: bool = False, **_ignored):
+        self.graph = graph
+        dev = graph.rowptr.device
+        if input_nodes is None:
+            input_nodes = torch.arange(graph.num_nodes, device=dev)
+        self.input_nodes = input_nodes.to(dev)
+        self.num_neighbors = list(num_neighbors)
+        self.batch_size = int(batch_size)
+        self.shuffle, self.seed = shuffle, seed
+        self.rank, self.world_size = rank, world_size
+        self.drop_last = drop_last
+        self.epoch = 0
+
+    def _seeds(self):
+        nodes = self.input_nodes
+        if self.shuffle:
+            g = _gen(nodes.device, self.seed + 1000 + self.epoch)
+            nodes = nodes[torch.randperm(nodes.numel(), device=nodes.device, generator=g)]
+        return nodes[self.rank::self.world_size]
+
+    def __len__(self):
+        n = (self.input_nodes.numel() - self.rank + self.world_size - 1) // self.world_size
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        seeds = self._seeds()
+        ep = self.epoch
+        self.epoch += 1
+        for b in range(len(self)):
+            s = seeds[b * self.batch_size:(b + 1) * self.batch_size]
+            yield sample_block(self.graph, s, self.num_neighbors,
+                               seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size + self.rank)
