@@ -374,7 +374,8 @@ extern "C" int ngnn_seg_agg_fwd(const void *x, int64_t ldx, int64_t F, const int
     NGNN_RETURN_IF(ldx < F || ldo < F, NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(F) || !fits_i32(n_dst), NGNN_E_RANGE);
     if (F == 0 || n_dst == 0) return NGNN_OK;
-    NGNN_RETURN_IF(!x || !col || !out, NGNN_E_ARG);
+    // col may be NULL when the block has no edges (rowptr is all zeros then)
+    NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
     const int vec = pick_vec(F, {{x, ldx}, {out, ldo}});
     const int lpr = pick_lpr(F, vec);
     const unsigned grid = static_cast<unsigned>(ceil_div(n_dst, 256 / lpr));
@@ -405,7 +406,7 @@ extern "C" int ngnn_seg_agg_bwd(const void *grad_out, int64_t ldg, int64_t F, co
     NGNN_RETURN_IF(ldg < F || ldgx < F, NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(F) || !fits_i32(n_dst) || !fits_i32(n_src), NGNN_E_RANGE);
     if (F == 0 || n_src == 0) return NGNN_OK;
-    NGNN_RETURN_IF(!grad_x || !rowptr_t || !col_t || !rowptr, NGNN_E_ARG);
+    NGNN_RETURN_IF(!grad_x || !rowptr_t || !rowptr, NGNN_E_ARG);  // col_t NULL iff no edges
     hipStream_t st = as_stream(stream);
     const float *gf = static_cast<const float *>(grad_out);
     float *gxf = static_cast<float *>(grad_x);
@@ -423,7 +424,7 @@ extern "C" int ngnn_seg_agg_bwd(const void *grad_out, int64_t ldg, int64_t F, co
                         })));
         return launch_status();
     }
-    NGNN_RETURN_IF(!x || !agg || !col, NGNN_E_ARG);
+    NGNN_RETURN_IF(!x || !agg, NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < F || lda < F, NGNN_E_SHAPE);
     NGNN_RETURN_IF(!ws || ws_bytes < ngnn_seg_agg_bwd_workspace_bytes(n_dst, F, reduce),
                    NGNN_E_WORKSPACE);

@@ -34,12 +34,22 @@ __global__ __launch_bounds__(256) void k_edge_probe(const int64_t *__restrict__ 
             uns_s |= src[e - 1] > s;
         }
     }
-    // one atomic per wave and flag, only when something was found
-    const int lane = threadIdx.x & (kWave - 1);
-    if (__any(bad_s) && lane == 0) atomicOr(status + 0, 1);
-    if (__any(bad_d) && lane == 0) atomicOr(status + 1, 1);
-    if (__any(uns_d) && lane == 0) atomicOr(status + 2, 1);
-    if (__any(uns_s) && lane == 0) atomicOr(status + 3, 1);
+    // block-level OR, then at most one atomic per block and flag (grid <= 256 blocks)
+    const int flags = bad_s | (bad_d << 1) | (uns_d << 2) | (uns_s << 3);
+    const int any = __syncthreads_or(flags != 0);
+    if (!any) return;
+    __shared__ int acc;
+    if (threadIdx.x == 0) acc = 0;
+    __syncthreads();
+    if (flags) atomicOr(&acc, flags);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int f = acc;
+        if (f & 1) atomicOr(status + 0, 1);
+        if (f & 2) atomicOr(status + 1, 1);
+        if (f & 4) atomicOr(status + 2, 1);
+        if (f & 8) atomicOr(status + 3, 1);
+    }
 }
 
 // rowptr[i] = first position p with keys[p] >= i   (i in [0, n_rows])
@@ -124,7 +134,7 @@ extern "C" int ngnn_edge_probe(const int64_t *edge_index, int64_t E, int64_t n_s
     NGNN_RETURN_IF(E > 0 && !edge_index, NGNN_E_ARG);
     NGNN_RETURN_IF(!fits_i32(E) || !fits_i32(n_src) || !fits_i32(n_dst), NGNN_E_RANGE);
     if (E == 0) return NGNN_OK;
-    hipLaunchKernelGGL(k_edge_probe, dim3(stream_grid(E)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(k_edge_probe, dim3(stream_grid(E, 256, 256)), dim3(256), 0, as_stream(stream),
                        edge_index, edge_index + E, E, n_src, n_dst, status);
     return launch_status();
 }
