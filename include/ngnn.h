@@ -123,6 +123,39 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
                     int64_t n_frontier, int fanout, uint64_t seed, int64_t *out_nbr,
                     int32_t *out_cnt, void *stream);
 
+/* ------------------------------------------------------- fused SAGE layer
+ * One SAGEConv layer of SAGE.forward (sage.py:33-39) in one launch:
+ *   out[r] = act( b + x[r] . W_r^T + [deg(r)>0] agg(r) . W_l^T ),   r < n_rows
+ * agg(r) = reduce over the CSR row r of x (MEAN / SUM / MAX as in
+ * ngnn_seg_agg_fwd, bit-identical); act = optional ReLU then optional
+ * dropout with keep probability 1-p_drop and scale 1/(1-p_drop), drawn from a
+ * counter-based hash of (seed, r, c) (no mask tensor; backward uses out > 0).
+ * W_l / W_r are the PyG Linear weights [Fo, K] packed by ngnn_pack_weight;
+ * wl_packed may be NULL (no neighbour term).  bias may be NULL.  Fo <= 512.
+ * x, out fp32; exact fp32 MFMA (v_mfma_f32_16x16x4_f32).
+ * Replaces PyG SAGEConv.forward [ext] + relu + F.dropout. */
+size_t ngnn_pack_weight_bytes(int64_t Fo, int64_t K);
+int ngnn_pack_weight(const float *w, int64_t ldw, int64_t Fo, int64_t K, void *packed,
+                     void *stream);
+int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows, const int32_t *rowptr,
+                  const int32_t *col, int reduce, const void *wl_packed, const void *wr_packed,
+                  const float *bias, int64_t Fo, float *out, int64_t ldo, int relu, float p_drop,
+                  uint64_t seed, void *stream);
+
+/* ------------------------------------------ backward receptive-field bounds
+ * ngnn_row_extent: out[0] = max(out[0], 1 + last row of g[n_rows, F] holding a
+ * nonzero (or NaN)).  The reference's loss reads only the seed rows
+ * (pipeline.py:155 slices [:batch_size]), so the output gradient is zero past
+ * them and every backward product can stop at that row.
+ * ngnn_block_prefix_stats: for the target-grouped CSR and a row bound R
+ * (R >= 0, or R < 0 = read status[0]): status[1] = nnz = rowptr[R],
+ * status[2] = max(status[2], R, 1 + max col[0..nnz)) = rows of the input
+ * gradient that can be nonzero.  E bounds the sweep (total edges). */
+int ngnn_row_extent(const float *g, int64_t ld, int64_t n_rows, int64_t F, int32_t *out,
+                    void *stream);
+int ngnn_block_prefix_stats(const int32_t *rowptr, const int32_t *col, int64_t R, int64_t E,
+                            int32_t *status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

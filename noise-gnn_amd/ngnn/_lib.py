@@ -32,6 +32,12 @@ SIGNATURES = {
     "ngnn_seg_agg_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _i64, _int, _int,
                                 _p, _i64, _p, _i64, _p, _i64, _p, _sz, _p]),
     "ngnn_sample_hop": (_int, [_p, _p, _p, _i64, _int, ctypes.c_uint64, _p, _p, _p]),
+    "ngnn_pack_weight_bytes": (_sz, [_i64, _i64]),
+    "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
+    "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _int, _p, _p, _p, _i64, _p, _i64, _int,
+                             ctypes.c_float, ctypes.c_uint64, _p]),
+    "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
+    "ngnn_block_prefix_stats": (_int, [_p, _p, _i64, _i64, _p, _p]),
 }
 
 _lib = None

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import fused
 from .block import get_block
 from .nn import GCNConv, SAGEConv
 
@@ -43,6 +44,13 @@ class SAGE(nn.Module):
 
     def forward(self, x, edge_index):
         block = get_block(edge_index, x.size(0))
+        if fused.sage_stack_supported(self, x):
+            # one autograd node for the stack: fused layer kernels forward,
+            # receptive-field-bounded backward (ngnn/fused.py)
+            seed = 0
+            if self.training and self.dropout > 0:
+                seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
+            return fused.sage_stack(self, x, block, seed)
         if self.use_bn:
             x = self.bn1(x)
         for i, conv in enumerate(self.convs):

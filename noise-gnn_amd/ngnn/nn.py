@@ -78,6 +78,16 @@ class SAGEConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         block = get_block(edge_index, x.size(0))
+        needs_grad = torch.is_grad_enabled() and (
+            x.requires_grad or any(p.requires_grad for p in self.parameters()))
+        if not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 \
+                and self.out_channels <= 512:
+            # inference (e.g. SAGE.inference, sage.py:52): one fused launch
+            from .fused import sage_layer_fwd
+            aggr = "sum" if self.aggr == "add" else self.aggr
+            xc = x if x.stride(1) == 1 else x.contiguous()
+            return sage_layer_fwd(xc, block, aggr, self.lin_l.weight, self.lin_l.bias,
+                                  self.lin_r.weight, relu=False, p_drop=0.0, seed=0)
         out = self.lin_l(segment_aggregate(x, block, self.aggr))
         return out + self.lin_r(x)
 

@@ -1,0 +1,182 @@
+"""GPU parity of the fused SAGE path (ngnn_sage_fwd + bounded backward).
+
+Tolerances (fp32): outputs rtol = atol = 1e-5 (north star); gradients, one
+more GEMM deep, rtol = 1e-4 / atol = 1e-5; weight gradients (sums over up to
+~1e4 rows) atol = 1e-4.  Dropout in the fused path uses a counter-based hash
+RNG; ``dropout_keep`` below replicates it on the host so train-mode results are
+checked element for element against the oracle with the same mask.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ngnn
+from ngnn.block import Block
+from ngnn.fused import sage_layer_fwd
+from oracle import c_agg, pyg_ref
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+OUT = dict(rtol=1e-5, atol=1e-5)
+GRAD = dict(rtol=1e-4, atol=1e-5)
+WGRAD = dict(rtol=1e-4, atol=1e-4)
+
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z):
+    z = (z + np.uint64(0x9E3779B97F4A7C15)) & M64
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M64
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M64
+    return z ^ (z >> np.uint64(31))
+
+
+def dropout_keep(seed, n_rows, n_cols, p):
+    """Host replica of the kernel's keep mask: uniform01(seed,row,col) >= p."""
+    with np.errstate(over="ignore"):
+        r = np.arange(n_rows, dtype=np.uint64)[:, None]
+        c = np.arange(n_cols, dtype=np.uint64)[None, :]
+        h = _mix64(np.uint64(seed) ^ _mix64((r << np.uint64(20)) ^ c))
+    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return torch.from_numpy(u >= np.float32(p))
+
+
+def rand_block(seed, N, E, order="dst"):
+    g = torch.Generator().manual_seed(seed)
+    ei = torch.randint(0, N, (2, E), generator=g)
+    if order == "dst":
+        ei = ei[:, torch.argsort(ei[1], stable=True)]
+    return ei
+
+
+@pytest.mark.parametrize("K,Fo", [(100, 256), (256, 47), (128, 40), (24, 7), (767, 16),
+                                  (256, 256), (300, 512), (8, 3), (129, 20)])
+@pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
+def test_fused_layer_matches_oracle(K, Fo, reduce):
+    N, E = 700, 5000
+    g = torch.Generator().manual_seed(K * 31 + Fo)
+    ei = rand_block(K + Fo, N, E, "dst" if K % 2 == 0 else None)
+    # leave the last 200 rows without in-edges (skipped W_l half)
+    ei = ei[:, ei[1] < N - 200]
+    x = torch.randn(N, K, generator=g)
+    conv = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
+    with torch.no_grad():
+        want = conv(x, ei)
+    blk = Block(ei.to(DEV), N)
+    for relu in (False, True):
+        got = sage_layer_fwd(x.to(DEV), blk, reduce, conv.lin_l.weight.to(DEV),
+                             conv.lin_l.bias.to(DEV), conv.lin_r.weight.to(DEV), relu=relu,
+                             p_drop=0.0, seed=0).cpu()
+        torch.testing.assert_close(got, want.relu() if relu else want, **OUT)
+
+
+def test_fused_layer_dropout_mask_and_scale():
+    N, K, Fo, p, seed = 500, 64, 128, 0.5, 12345
+    ei = rand_block(1, N, 3000)
+    x = torch.randn(N, K)
+    conv = pyg_ref.SAGEConv(K, Fo)
+    with torch.no_grad():
+        pre = conv(x, ei).relu()
+    blk = Block(ei.to(DEV), N)
+    got = sage_layer_fwd(x.to(DEV), blk, "mean", conv.lin_l.weight.to(DEV), conv.lin_l.bias.to(DEV),
+                         conv.lin_r.weight.to(DEV), relu=True, p_drop=p, seed=seed).cpu()
+    keep = dropout_keep(seed, N, Fo, p)
+    torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)
+    frac = keep.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01
+    # deterministic in the seed, different for another seed
+    again = sage_layer_fwd(x.to(DEV), blk, "mean", conv.lin_l.weight.to(DEV),
+                           conv.lin_l.bias.to(DEV), conv.lin_r.weight.to(DEV), relu=True,
+                           p_drop=p, seed=seed).cpu()
+    assert torch.equal(got, again)
+
+
+class _MaskedSAGE(pyg_ref.SAGE):
+    """Oracle SAGE whose dropout uses given keep masks (one per hidden layer)."""
+
+    def __init__(self, *a, masks=None, **k):
+        super().__init__(*a, **k)
+        self.masks = masks
+
+    def forward(self, x, edge_index):
+        for i, conv in enumerate(self.convs):
+            x = conv(x, edge_index)
+            if i != self.num_layers - 1:
+                x = x.relu()
+                x = x * self.masks[i] * (1.0 / (1.0 - self.dropout))
+        return x
+
+
+@pytest.mark.parametrize("layers,aggr", [(2, "mean"), (3, "mean"), (2, "max")])
+@pytest.mark.parametrize("train", [False, True])
+def test_stack_fwd_bwd_matches_oracle(layers, aggr, train):
+    """Whole SAGE stack on a NeighborLoader-shaped block, loss on the seed rows
+    only (pipeline.py:155-160): outputs, dx and every parameter gradient."""
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=2, scale=0.005)
+    fan = [8, 5, 3][:layers]
+    b = sample_block(graph, graph.train_idx[:128], fan, seed=4)
+    N = b.num_nodes
+    torch.manual_seed(layers)
+    mine = ngnn.SAGE(100, 64, 47, layers, dropout=0.5, aggr=aggr).to(DEV)
+    mine.train(train)
+    seed_box = {}
+    if train:
+        # capture the seed the model draws, to rebuild the masks on the host
+        torch.manual_seed(99)
+        seed_box["seed"] = int(torch.randint(0, 2**62, (1,)).item())
+        torch.manual_seed(99)
+    x = b.x.clone().requires_grad_(True)
+    out = mine(x, b.edge_index)
+    loss = F.cross_entropy(out[:b.batch_size], b.y[:b.batch_size])
+    loss.backward()
+
+    if train:
+        masks = [dropout_keep(seed_box["seed"] + 7919 * i, N, 64, 0.5).float()
+                 for i in range(layers - 1)]
+        ref = _MaskedSAGE(100, 64, 47, layers, dropout=0.5, aggr=aggr, masks=masks)
+    else:
+        ref = pyg_ref.SAGE(100, 64, 47, layers, dropout=0.5, aggr=aggr).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    xr = b.x.cpu().clone().requires_grad_(True)
+    out_r = ref(xr, b.edge_index.cpu())
+    loss_r = F.cross_entropy(out_r[:b.batch_size], b.y[:b.batch_size].cpu())
+    loss_r.backward()
+    torch.testing.assert_close(out.detach().cpu(), out_r.detach(), **OUT)
+    torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
+    for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+
+
+def test_stack_full_output_gradient():
+    """Gradient on EVERY output row (no seed slicing): the bound R = N path."""
+    N = 400
+    ei = rand_block(7, N, 3000, None)
+    x = torch.randn(N, 32)
+    torch.manual_seed(0)
+    mine = ngnn.SAGE(32, 48, 10, 3).to(DEV).eval()
+    ref = pyg_ref.SAGE(32, 48, 10, 3).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    G = torch.randn(N, 10)
+    xd = x.to(DEV).requires_grad_(True)
+    (mine(xd, ei.to(DEV)) * G.to(DEV)).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    (ref(xr, ei) * G).sum().backward()
+    torch.testing.assert_close(xd.grad.cpu(), xr.grad, **GRAD)
+    for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+
+
+def test_zero_gradient_and_no_grad_paths():
+    N = 100
+    ei = rand_block(3, N, 500)
+    m = ngnn.SAGE(16, 16, 4, 2).to(DEV)
+    x = torch.randn(N, 16, device=DEV)
+    out = m(x, ei.to(DEV))
+    (out * 0).sum().backward()
+    for p in m.parameters():
+        assert p.grad is not None and not p.grad.any()
+    with torch.no_grad():
+        o2 = m.eval()(x, ei.to(DEV))
+    assert o2.shape == (N, 4)
