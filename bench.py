@@ -38,6 +38,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_*_f32), same table
 
 
 def parse():
@@ -58,7 +59,7 @@ def parse():
 def train_step(model, opt, reducer, b):
     out = model(b.x, b.edge_index)[:b.batch_size]
     loss = F.cross_entropy(out, b.y[:b.batch_size])
-    opt.zero_grad(set_to_none=False)
+    opt.zero_grad()
     loss.backward()
     reducer()
     opt.step()
@@ -109,7 +110,8 @@ def main():
     graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
     torch.manual_seed(1234)  # identical init on every rank
     model = ngnn.SAGE(100, args.hidden, 47, layers, dropout=0.5).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    # torch's single-kernel Adam on the device (same update rule as the reference's Adam)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     reducer = GradAllReduce(model.parameters())
     model.train()
 
@@ -153,15 +155,24 @@ def main():
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
     roof = None
     if dom:
-        name, (n, ms, nbytes) = dom
-        ach = nbytes / (ms * 1e-3) / 1e9
-        roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "launches": n, "avg_us": round(1e3 * ms / n, 2),
-                "alg_bytes_per_launch": int(nbytes / n),
-                "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
-                                    "GBps": round(v[2] / (v[1] * 1e-3) / 1e9, 1)}
-                                for k, v in summ.items()}}
+        name, (n, ms, nbytes, flops) = dom
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        tfs = flops / (ms * 1e-3) / 1e12
+        f_hbm, f_mfma = gbs / HBM_PEAK_GBS, tfs / MFMA_F32_PEAK_TFS
+        if f_mfma > f_hbm:  # report the roof the kernel is closest to
+            roof = {"kernel": name, "bound": "mfma", "achieved": round(tfs, 2),
+                    "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": round(f_mfma, 4)}
+        else:
+            roof = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(f_hbm, 4)}
+        roof.update({
+            "traffic": None, "launches": n, "avg_us": round(1e3 * ms / n, 2),
+            "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
+            "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),
+            "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
+                                "GBps": round(v[2] / (v[1] * 1e-3) / 1e9, 1),
+                                "TFps": round(v[3] / (v[1] * 1e-3) / 1e12, 2)}
+                            for k, v in summ.items()}})
 
     # full epoch incl. GPU sampling (this rank's shard)
     epoch_s = None

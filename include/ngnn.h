@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 2
+#define NGNN_ABI_VERSION 3
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -131,30 +131,76 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
  * dropout with keep probability 1-p_drop and scale 1/(1-p_drop), drawn from a
  * counter-based hash of (seed, r, c) (no mask tensor; backward uses out > 0).
  * W_l / W_r are the PyG Linear weights [Fo, K] packed by ngnn_pack_weight;
- * wl_packed may be NULL (no neighbour term).  bias may be NULL.  Fo <= 512.
- * x, out fp32; exact fp32 MFMA (v_mfma_f32_16x16x4_f32).
+ * wl_packed may be NULL (no neighbour term; rowptr/col may then be NULL).
+ * bias may be NULL.  x, out fp32 (outputs wider than 512 columns run as
+ * several launches of 512-column slices); exact fp32 MFMA
+ * (v_mfma_f32_16x16x4_f32).  Optional modes:
+ *   n_rows_dev  device int: rows = min(n_rows, *n_rows_dev) (rows past it are
+ *               not written) -- bounds that only the device knows;
+ *   agg_out     [n_rows, ld_agg]: workgroups whose 64 rows have in-edges also
+ *               store those rows' aggregate (saved for the backward);
+ *   xmask       stage x * (xmask > 0 ? xscale : 0) instead of x (ReLU/dropout
+ *               backward fused into a dgrad GEMM's input).
  * Replaces PyG SAGEConv.forward [ext] + relu + F.dropout. */
 size_t ngnn_pack_weight_bytes(int64_t Fo, int64_t K);
 int ngnn_pack_weight(const float *w, int64_t ldw, int64_t Fo, int64_t K, void *packed,
                      void *stream);
-int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows, const int32_t *rowptr,
-                  const int32_t *col, int reduce, const void *wl_packed, const void *wr_packed,
-                  const float *bias, int64_t Fo, float *out, int64_t ldo, int relu, float p_drop,
-                  uint64_t seed, void *stream);
+/* Pack M[Fo][K] = rows [0,rows0) from w0, rows [rows0,Fo) from w1 (either
+ * read transposed: M[n][k] = src[k][n]).  The backward packs
+ * [W_l^T ; W_r^T] for its dgrad GEMM. */
+int ngnn_pack_weight_ex(const float *w0, const float *w1, int64_t ldw, int64_t rows0, int64_t Fo,
+                        int64_t K, int transposed, void *packed, void *stream);
+int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                  const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col, int reduce,
+                  const void *wl_packed, const void *wr_packed, const float *bias, int64_t Fo,
+                  float *out, int64_t ldo, int relu, float p_drop, uint64_t seed, float *agg_out,
+                  int64_t ld_agg, const float *xmask, int64_t ldm, float xscale, void *stream);
 
 /* ------------------------------------------ backward receptive-field bounds
  * ngnn_row_extent: out[0] = max(out[0], 1 + last row of g[n_rows, F] holding a
  * nonzero (or NaN)).  The reference's loss reads only the seed rows
  * (pipeline.py:155 slices [:batch_size]), so the output gradient is zero past
  * them and every backward product can stop at that row.
- * ngnn_block_prefix_stats: for the target-grouped CSR and a row bound R
- * (R >= 0, or R < 0 = read status[0]): status[1] = nnz = rowptr[R],
- * status[2] = max(status[2], R, 1 + max col[0..nnz)) = rows of the input
- * gradient that can be nonzero.  E bounds the sweep (total edges). */
+ * ngnn_block_prefix_stats: R = *r_ptr (device);  *r_next = max(*r_next, R,
+ * 1 + max col[0..rowptr[R]))  = rows of the input gradient that can be
+ * nonzero;  *nnz_out = rowptr[R] (nullable).  E bounds the sweep. */
 int ngnn_row_extent(const float *g, int64_t ld, int64_t n_rows, int64_t F, int32_t *out,
                     void *stream);
-int ngnn_block_prefix_stats(const int32_t *rowptr, const int32_t *col, int64_t R, int64_t E,
-                            int32_t *status, void *stream);
+int ngnn_block_prefix_stats(const int32_t *rowptr, const int32_t *col, const int32_t *r_ptr,
+                            int32_t *nnz_out, int32_t *r_next, int64_t E, void *stream);
+
+/* ------------------------------------------------- fused SAGE layer backward
+ * Weight gradients over rows r < R = *r_ptr (device):
+ *   dz = dy (* [y > 0] * yscale when y != NULL: ReLU+dropout backward)
+ *   dW_r = dz^T h,  dW_l = dz^T agg (agg: the forward's saved aggregate; rows
+ *   with no in-edges read as 0),  db = sum_r dz.
+ * fp32 MFMA over 64-row chunks, per-slice partials in ws, fixed-order
+ * reduction => deterministic.  Outputs are overwritten.
+ * Replaces autograd of lin_l / lin_r (PyG Linear [ext]) in SAGEConv. */
+size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K);
+int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy, float yscale,
+                    const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
+                    const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr, int64_t Fo,
+                    int64_t K, float *dwl, float *dbl, float *dwr, void *ws, size_t ws_bytes,
+                    void *stream);
+/* Input gradient of one layer, rows j < Rn = *rnext_ptr (R = *r_ptr):
+ *   dh[j] = [j < R] droot[j] + sum over edges e with source j and target
+ *           d = col_t[e] < R (transposed CSR, edge order) of
+ *           MEAN: dagg[d] / deg(d)   SUM: dagg[d]
+ *           MAX : [h[j] == agg[d]] * dagg[d] / ties(d)   (torch amax rule)
+ * droot = dz W_r and dagg = dz W_l come from the dgrad GEMM (ngnn_sage_fwd
+ * with packed [W_l^T ; W_r^T]).  Rows >= Rn are zeroed if zero_tail, else
+ * left untouched.  MAX needs ws of n_rows*K floats
+ * (ngnn_sage_dgrad_workspace_bytes).  Replaces autograd of index_select +
+ * scatter (PyG propagate [ext]). */
+size_t ngnn_sage_dgrad_workspace_bytes(int64_t n_rows, int64_t K, int reduce);
+int ngnn_sage_dgrad_gather(const float *dagg, int64_t ld_dagg, const float *droot,
+                           int64_t ld_droot, const int32_t *rowptr, const int32_t *col,
+                           const int32_t *rowptr_t, const int32_t *col_t, int64_t n_rows,
+                           const int32_t *r_ptr, const int32_t *rnext_ptr, int64_t K, int reduce,
+                           const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
+                           float *dh, int64_t ldd, int zero_tail, void *ws, size_t ws_bytes,
+                           void *stream);
 
 #ifdef __cplusplus
 }

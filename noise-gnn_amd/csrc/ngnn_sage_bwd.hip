@@ -1,0 +1,470 @@
+// Backward of one fused SAGE layer on gfx950, bounded by device-side row
+// counts (no host round trip).
+//
+// The reference trains with loss = CE(model(x, ei)[:batch_size], y)
+// (pipeline.py:155-160), so only the seed rows of the output gradient are
+// nonzero.  R = the row bound of dz (device int), R' = rows of the input
+// gradient that can be nonzero (ngnn_block_prefix_stats).  Everything below
+// touches rows < R (weight gradients, dgrad GEMM) or rows < R' (gather).
+//
+//   ngnn_sage_wgrad        dW_r = dz^T h, dW_l = dz^T agg, db = sum dz
+//     k_wgrad_partial: 512-thread workgroups, grid (slice, K-chunk, Fo-chunk);
+//       slice s owns 64-row chunks s, s+S, s+2S, ... below R; per chunk dz
+//       [64 x <=256], h and agg [64 x 128] are staged row-major in LDS (16-B
+//       coalesced loads) and v_mfma_f32_16x16x4_f32 reduces over the rows
+//       (A = dz^T read as ds_read_b32 columns, B = h / agg rows); waves 0-3
+//       own dW_r tiles, waves 4-7 dW_l tiles.  Partials -> ws slabs.
+//     k_wgrad_reduce: fixed-order slab sum => bitwise reproducible.
+//   ngnn_sage_dgrad_gather dh = [j<R] dz W_r + transposed aggregation of dz W_l
+//     over the source-grouped CSR, in edge order, edges into rows >= R skipped.
+#include "ngnn_device.h"
+
+namespace ngnn {
+namespace {
+
+constexpr int WG_BM = 64;       // rows per chunk
+constexpr int WG_KC = 128;      // K columns per workgroup (grid.y)
+constexpr int WG_NC = 256;      // Fo columns per workgroup (grid.z)
+constexpr int LDZ = WG_NC + 16; // LDS strides: +16 floats keeps the two 16-lane
+constexpr int LDH = WG_KC + 16; // row groups of a b32 read on disjoint banks
+constexpr int S_MAX = 128;      // slices (partial slabs)
+
+__host__ __device__ inline size_t slab_floats(int64_t Fo, int64_t K) {
+    return static_cast<size_t>(2 * Fo * K + Fo);
+}
+
+// rows [c0, c0+64) x cols [k0, k0+kc) of src -> LDS (row-major, ld ldl),
+// zero outside [0,R) x [0,K); optional ReLU/dropout mask; optional "deg == 0
+// -> zero row" (saved aggregate).
+template <bool VEC>
+__device__ __forceinline__ void stage_rows(float *lds, int ldl, int ncols, const float *__restrict__ src,
+                                           int64_t lds_src, int64_t c0, int R, int k0, int K,
+                                           const float *__restrict__ mask, int64_t ldm, float mscale,
+                                           const int32_t *__restrict__ rowptr) {
+    if (VEC) {
+        const int c4 = ncols >> 2;
+        for (int idx = threadIdx.x; idx < WG_BM * c4; idx += 512) {
+            const int r = idx / c4, c = (idx - r * c4) << 2;
+            const int64_t row = c0 + r;
+            const int k = k0 + c;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            bool ok = row < R && k < K;
+            if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
+            if (ok) {
+                v = *reinterpret_cast<const float4 *>(src + row * lds_src + k);
+                if (mask) {
+                    const float4 m = *reinterpret_cast<const float4 *>(mask + row * ldm + k);
+                    v.x = m.x > 0.f ? v.x * mscale : 0.f;
+                    v.y = m.y > 0.f ? v.y * mscale : 0.f;
+                    v.z = m.z > 0.f ? v.z * mscale : 0.f;
+                    v.w = m.w > 0.f ? v.w * mscale : 0.f;
+                }
+            }
+            *reinterpret_cast<float4 *>(lds + r * ldl + c) = v;
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < WG_BM * ncols; idx += 512) {
+            const int r = idx / ncols, c = idx - r * ncols;
+            const int64_t row = c0 + r;
+            const int k = k0 + c;
+            float v = 0.0f;
+            bool ok = row < R && k < K;
+            if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
+            if (ok) {
+                v = src[row * lds_src + k];
+                if (mask) v = mask[row * ldm + k] > 0.f ? v * mscale : 0.f;
+            }
+            lds[r * ldl + c] = v;
+        }
+    }
+}
+
+// NTW n-tiles x KTW k-tiles of 16x16 per wave.  SPLIT_N: the 4 waves of a
+// matrix split the Fo tiles (NT >= 4); else they split the K tiles.
+template <int NTW, int KTW, bool SPLIT_N, bool VEC>
+__global__ __launch_bounds__(512, 1) void k_wgrad_partial(
+    const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
+    float yscale, const float *__restrict__ h, int64_t ldh, const float *__restrict__ agg,
+    int64_t ld_agg, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ r_ptr, int Fo,
+    int K, float *__restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) float smem[WG_BM * LDZ + 2 * WG_BM * LDH];  // 140 KB
+    float *sz = smem;                       // [64][LDZ]
+    float *sh = sz + WG_BM * LDZ;           // [64][LDH]
+    float *sa = sh + WG_BM * LDH;           // [64][LDH]
+    const int R = *r_ptr;
+    const int nchunks = (R + WG_BM - 1) / WG_BM;
+    const int S = gridDim.x;
+    const int s = blockIdx.x;
+    if (s >= nchunks) return;  // no rows for this slice: its slab is never read
+    const int k0 = blockIdx.y * WG_KC;
+    const int n0 = blockIdx.z * WG_NC;
+    const int kc = min(WG_KC, K - k0);
+    const int nc = min(WG_NC, Fo - n0);
+    const int KT = (kc + 15) >> 4;
+    const int NTc = (nc + 15) >> 4;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mat = wave >> 2;  // 0: dW_r (B = h), 1: dW_l (B = agg)
+    const int w4 = wave & 3;
+    const int nt0 = SPLIT_N ? w4 * NTW : 0;
+    const int kt0 = SPLIT_N ? 0 : w4 * KTW;
+    const int i16 = lane & 15, kk = lane >> 4;
+
+    v4f acc[NTW][KTW];
+#pragma unroll
+    for (int a = 0; a < NTW; ++a)
+#pragma unroll
+        for (int b = 0; b < KTW; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+    float dbias = 0.0f;  // column sum of dz for column n0 + threadIdx.x
+
+    const int ncp = (nc + 3) & ~3, kcp = (kc + 3) & ~3;
+    for (int c = s; c < nchunks; c += S) {
+        const int64_t c0 = static_cast<int64_t>(c) * WG_BM;
+        __syncthreads();
+        stage_rows<VEC>(sz, LDZ, ncp, dy, ldy, c0, R, n0, Fo, y, ldyy, yscale, nullptr);
+        stage_rows<VEC>(sh, LDH, kcp, h, ldh, c0, R, k0, K, nullptr, 0, 1.0f, nullptr);
+        stage_rows<VEC>(sa, LDH, kcp, agg, ld_agg, c0, R, k0, K, nullptr, 0, 1.0f, rowptr);
+        __syncthreads();
+        if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < nc) {
+            float t = 0.0f;
+            for (int r = 0; r < WG_BM; ++r) t += sz[r * LDZ + threadIdx.x];
+            dbias += t;
+        }
+        const float *sb = mat ? sa : sh;
+        for (int ks = 0; ks < WG_BM / 4; ++ks) {
+            const int rr = ks * 4 + kk;
+            float a[NTW], b[KTW];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) a[t] = sz[rr * LDZ + (nt0 + t) * 16 + i16];
+#pragma unroll
+            for (int t = 0; t < KTW; ++t) b[t] = sb[rr * LDH + (kt0 + t) * 16 + i16];
+#pragma unroll
+            for (int ta = 0; ta < NTW; ++ta)
+#pragma unroll
+                for (int tb = 0; tb < KTW; ++tb)
+                    acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+        }
+    }
+    // ---- partial slab: [Pr Fo x K][Pl Fo x K][Pb Fo]
+    float *slab = ws + static_cast<size_t>(s) * slab_floats(Fo, K);
+    float *P = slab + static_cast<size_t>(mat) * Fo * K;
+#pragma unroll
+    for (int ta = 0; ta < NTW; ++ta)
+#pragma unroll
+        for (int tb = 0; tb < KTW; ++tb) {
+            const int nt = nt0 + ta, kt = kt0 + tb;
+            if (nt >= NTc || kt >= KT) continue;
+            const int k = k0 + kt * 16 + i16;
+            if (k >= K) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + nt * 16 + 4 * kk + j;
+                if (n < Fo) P[static_cast<size_t>(n) * K + k] = acc[ta][tb][j];
+            }
+        }
+    if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < nc)
+        slab[2 * static_cast<size_t>(Fo) * K + n0 + threadIdx.x] = dbias;
+}
+
+// out[i] = sum over slabs s < min(S, nchunks) of slab[s][i], in slab order
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ ws,
+                                                      const int32_t *__restrict__ r_ptr, int S,
+                                                      int Fo, int K, float *__restrict__ dwr,
+                                                      float *__restrict__ dwl,
+                                                      float *__restrict__ db) {
+    const int64_t total = slab_floats(Fo, K);
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int R = *r_ptr;
+    const int used = min(S, (R + WG_BM - 1) / WG_BM);
+    float t = 0.0f;
+    for (int s = 0; s < used; ++s) t += ws[static_cast<size_t>(s) * total + i];
+    const int64_t FK = static_cast<int64_t>(Fo) * K;
+    if (i < FK) dwr[i] = t;
+    else if (i < 2 * FK) dwl[i - FK] = t;
+    else db[i - 2 * FK] = t;
+}
+
+// ---- gather: dh[j] = [j<R] droot[j] + sum_{e in T(j), d=col_t[e] < R} f(dagg[d])
+template <int VEC>
+struct V;
+template <>
+struct V<4> {
+    using T = float4;
+};
+template <>
+struct V<1> {
+    using T = float;
+};
+
+template <int VEC>
+__device__ __forceinline__ float &cmp(typename V<VEC>::T &v, int i) {
+    return reinterpret_cast<float *>(&v)[i];
+}
+
+template <int VEC>
+__device__ __forceinline__ typename V<VEC>::T ldv(const float *p) {
+    return *reinterpret_cast<const typename V<VEC>::T *>(p);
+}
+
+template <int VEC, int LPR, int RED>
+__global__ __launch_bounds__(256) void k_dgrad_gather(
+    const float *__restrict__ dagg, int64_t ld_dagg, const float *__restrict__ droot,
+    int64_t ld_droot, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ rowptr_t,
+    const int32_t *__restrict__ col_t, int n_rows, const int32_t *__restrict__ r_ptr,
+    const int32_t *__restrict__ rn_ptr, int K, const float *__restrict__ h, int64_t ldh,
+    const float *__restrict__ agg, int64_t ld_agg, float *__restrict__ dh, int64_t ldd,
+    int zero_tail) {
+    using T = typename V<VEC>::T;
+    constexpr int GROUPS = 256 / LPR;
+    const int lane = threadIdx.x % LPR;
+    const int64_t row = (int64_t)blockIdx.x * GROUPS + threadIdx.x / LPR;
+    if (row >= n_rows) return;
+    const int R = *r_ptr, Rn = *rn_ptr;
+    const int nchunks = (K + LPR * VEC - 1) / (LPR * VEC);
+    if (row >= Rn) {
+        if (zero_tail)
+            for (int ch = 0; ch < nchunks; ++ch) {
+                const int f = ch * LPR * VEC + lane * VEC;
+                if (f < K) {
+                    T z;
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) cmp<VEC>(z, i) = 0.0f;
+                    *reinterpret_cast<T *>(dh + row * ldd + f) = z;
+                }
+            }
+        return;
+    }
+    const int beg = rowptr_t[row], end = rowptr_t[row + 1];
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int f = ch * LPR * VEC + lane * VEC;
+        const bool act = f < K;
+        T acc, xv;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) cmp<VEC>(acc, i) = 0.0f;
+        if (RED == NGNN_REDUCE_MAX && act) xv = ldv<VEC>(h + row * ldh + f);
+        for (int eb = beg; eb < end; eb += LPR) {
+            const int n = min(LPR, end - eb);
+            int myd = 0x7fffffff;
+            float myc = 1.0f;
+            if (lane < n) {
+                myd = col_t[eb + lane];
+                if (RED == NGNN_REDUCE_MEAN && myd < R) {
+                    const int dg = rowptr[myd + 1] - rowptr[myd];
+                    myc = static_cast<float>(dg > 1 ? dg : 1);
+                }
+            }
+            for (int k = 0; k < n; ++k) {
+                const int d = __shfl(myd, k, LPR);
+                const float cn = __shfl(myc, k, LPR);
+                if (d >= R || !act) continue;  // edge into a row whose gradient is zero
+                const T g = ldv<VEC>(dagg + static_cast<int64_t>(d) * ld_dagg + f);
+                if (RED == NGNN_REDUCE_MAX) {
+                    const T av = ldv<VEC>(agg + static_cast<int64_t>(d) * ld_agg + f);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) {
+                        const float m = (cmp<VEC>(xv, i) == reinterpret_cast<const float *>(&av)[i]) ? 1.0f : 0.0f;
+                        cmp<VEC>(acc, i) += m * reinterpret_cast<const float *>(&g)[i];
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) {
+                        const float t = reinterpret_cast<const float *>(&g)[i];
+                        cmp<VEC>(acc, i) += (RED == NGNN_REDUCE_MEAN) ? t / cn : t;
+                    }
+                }
+            }
+        }
+        if (!act) continue;
+        if (row < R) {
+            const T rt = ldv<VEC>(droot + row * ld_droot + f);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                cmp<VEC>(acc, i) = reinterpret_cast<const float *>(&rt)[i] + cmp<VEC>(acc, i);
+        }
+        *reinterpret_cast<T *>(dh + row * ldd + f) = acc;
+    }
+}
+
+// MAX: gdist[d] = dagg[d] / ([agg[d]==0] + #{e into d: h[src_e]==agg[d]}),  d < R
+template <int VEC, int LPR>
+__global__ __launch_bounds__(256) void k_max_gdist(const float *__restrict__ dagg, int64_t ld_dagg,
+                                                   const int32_t *__restrict__ rowptr,
+                                                   const int32_t *__restrict__ col, int n_rows,
+                                                   const int32_t *__restrict__ r_ptr, int K,
+                                                   const float *__restrict__ h, int64_t ldh,
+                                                   const float *__restrict__ agg, int64_t ld_agg,
+                                                   float *__restrict__ gdist) {
+    using T = typename V<VEC>::T;
+    constexpr int GROUPS = 256 / LPR;
+    const int lane = threadIdx.x % LPR;
+    const int64_t row = (int64_t)blockIdx.x * GROUPS + threadIdx.x / LPR;
+    if (row >= n_rows || row >= *r_ptr) return;
+    const int beg = rowptr[row], end = rowptr[row + 1];
+    if (beg == end) return;  // never referenced by the gather
+    const int nchunks = (K + LPR * VEC - 1) / (LPR * VEC);
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int f = ch * LPR * VEC + lane * VEC;
+        const bool act = f < K;
+        T a, ties;
+        if (act) a = ldv<VEC>(agg + row * ld_agg + f);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i)
+            cmp<VEC>(ties, i) = (act && cmp<VEC>(a, i) == 0.0f) ? 1.0f : 0.0f;
+        for (int eb = beg; eb < end; eb += LPR) {
+            const int n = min(LPR, end - eb);
+            const int myc = lane < n ? col[eb + lane] : 0;
+            for (int k = 0; k < n; ++k) {
+                const int c = __shfl(myc, k, LPR);
+                if (!act) continue;
+                const T v = ldv<VEC>(h + static_cast<int64_t>(c) * ldh + f);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    cmp<VEC>(ties, i) += (reinterpret_cast<const float *>(&v)[i] == cmp<VEC>(a, i)) ? 1.0f : 0.0f;
+            }
+        }
+        if (!act) continue;
+        T g = ldv<VEC>(dagg + row * ld_dagg + f);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) cmp<VEC>(g, i) = cmp<VEC>(g, i) / cmp<VEC>(ties, i);
+        *reinterpret_cast<T *>(gdist + row * static_cast<int64_t>(K) + f) = g;
+    }
+}
+
+int lpr_for(int64_t K, int vec) {
+    const int64_t chunks = ceil_div(K, vec);
+    int l = 4;
+    while (l < 64 && l < chunks) l <<= 1;
+    return l;
+}
+
+}  // namespace
+}  // namespace ngnn
+
+using namespace ngnn;
+
+extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
+    if (Fo <= 0 || K <= 0) return 0;
+    return sizeof(float) * S_MAX * slab_floats(Fo, K);
+}
+
+#define NGNN_WG_LAUNCH(NTW_, KTW_, SPLIT_)                                                        \
+    do {                                                                                       \
+        if (vec)                                                                               \
+            hipLaunchKernelGGL((k_wgrad_partial<NTW_, KTW_, SPLIT_, true>), grid, dim3(512),   \
+                               0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr,   \
+                               r_ptr, (int)Fo, (int)K, wsf);                                   \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_wgrad_partial<NTW_, KTW_, SPLIT_, false>), grid, dim3(512),  \
+                               0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr,   \
+                               r_ptr, (int)Fo, (int)K, wsf);                                   \
+    } while (0)
+
+extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
+                               float yscale, const float *h, int64_t ldh, const float *agg,
+                               int64_t ld_agg, const int32_t *rowptr, int64_t n_rows,
+                               const int32_t *r_ptr, int64_t Fo, int64_t K, float *dwl, float *dbl,
+                               float *dwr, void *ws, size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(!dy || !h || !agg || !rowptr || !r_ptr || !dwl || !dbl || !dwr, NGNN_E_ARG);
+    NGNN_RETURN_IF(Fo <= 0 || K <= 0 || n_rows < 0, NGNN_E_ARG);
+    NGNN_RETURN_IF(ldy < Fo || ldh < K || ld_agg < K || (y && ldyy < Fo), NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    NGNN_RETURN_IF(!ws || ws_bytes < ngnn_sage_wgrad_workspace_bytes(Fo, K), NGNN_E_WORKSPACE);
+    const bool vec = (Fo % 4 == 0) && (K % 4 == 0) && (ldy % 4 == 0) && (ldh % 4 == 0) &&
+                     (ld_agg % 4 == 0) && (!y || ldyy % 4 == 0) && aligned(dy, 16) &&
+                     aligned(h, 16) && aligned(agg, 16) && (!y || aligned(y, 16));
+    hipStream_t st = as_stream(stream);
+    float *wsf = static_cast<float *>(ws);
+    const int S = static_cast<int>(std::min<int64_t>(S_MAX, std::max<int64_t>(1, ceil_div(n_rows, WG_BM))));
+    const dim3 grid(S, static_cast<unsigned>(ceil_div(K, WG_KC)),
+                    static_cast<unsigned>(ceil_div(Fo, WG_NC)));
+    const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
+    if (NT >= 4) {
+        const int ntw = (NT + 3) / 4;
+        if (ntw == 1) NGNN_WG_LAUNCH(1, 8, true);
+        else if (ntw == 2) NGNN_WG_LAUNCH(2, 8, true);
+        else if (ntw == 3) NGNN_WG_LAUNCH(3, 8, true);
+        else NGNN_WG_LAUNCH(4, 8, true);
+    } else if (NT == 1) NGNN_WG_LAUNCH(1, 2, false);
+    else if (NT == 2) NGNN_WG_LAUNCH(2, 2, false);
+    else NGNN_WG_LAUNCH(3, 2, false);
+    int rc = launch_status();
+    if (rc) return rc;
+    const int64_t total = static_cast<int64_t>(slab_floats(Fo, K));
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(ceil_div(total, 256)), dim3(256), 0, st, wsf, r_ptr, S,
+                       (int)Fo, (int)K, dwr, dwl, dbl);
+    return launch_status();
+}
+
+extern "C" size_t ngnn_sage_dgrad_workspace_bytes(int64_t n_rows, int64_t K, int reduce) {
+    if (reduce != NGNN_REDUCE_MAX || n_rows <= 0 || K <= 0) return 0;
+    return sizeof(float) * static_cast<size_t>(n_rows) * static_cast<size_t>(K);
+}
+
+extern "C" int ngnn_sage_dgrad_gather(const float *dagg, int64_t ld_dagg, const float *droot,
+                                      int64_t ld_droot, const int32_t *rowptr, const int32_t *col,
+                                      const int32_t *rowptr_t, const int32_t *col_t, int64_t n_rows,
+                                      const int32_t *r_ptr, const int32_t *rnext_ptr, int64_t K,
+                                      int reduce, const float *h, int64_t ldh, const float *agg,
+                                      int64_t ld_agg, float *dh, int64_t ldd, int zero_tail,
+                                      void *ws, size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
+    NGNN_RETURN_IF(!dagg || !droot || !rowptr || !rowptr_t || !r_ptr || !rnext_ptr || !dh, NGNN_E_ARG);
+    NGNN_RETURN_IF(K <= 0 || n_rows < 0, NGNN_E_ARG);
+    NGNN_RETURN_IF(ld_dagg < K || ld_droot < K || ldd < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    if (n_rows == 0) return NGNN_OK;
+    const bool is_max = reduce == NGNN_REDUCE_MAX;
+    NGNN_RETURN_IF(is_max && (!h || !agg || !col), NGNN_E_ARG);
+    NGNN_RETURN_IF(is_max && (ldh < K || ld_agg < K), NGNN_E_SHAPE);
+    NGNN_RETURN_IF(is_max && (!ws || ws_bytes < ngnn_sage_dgrad_workspace_bytes(n_rows, K, reduce)),
+                   NGNN_E_WORKSPACE);
+    hipStream_t st = as_stream(stream);
+    const bool vec = (K % 4 == 0) && (ld_dagg % 4 == 0) && (ld_droot % 4 == 0) && (ldd % 4 == 0) &&
+                     aligned(dagg, 16) && aligned(droot, 16) && aligned(dh, 16) &&
+                     (!is_max || ((ldh % 4 == 0) && (ld_agg % 4 == 0) && aligned(h, 16) &&
+                                  aligned(agg, 16) && aligned(ws, 16)));
+    const float *src = dagg;
+    int64_t ld_src = ld_dagg;
+    auto go = [&](auto vec_c, auto lpr_c) {
+        constexpr int VECv = decltype(vec_c)::value;
+        constexpr int LPRv = decltype(lpr_c)::value;
+        const unsigned grid = static_cast<unsigned>(ceil_div(n_rows, 256 / LPRv));
+        if (is_max) {
+            float *gd = static_cast<float *>(ws);
+            hipLaunchKernelGGL((k_max_gdist<VECv, LPRv>), dim3(grid), dim3(256), 0, st, dagg,
+                               ld_dagg, rowptr, col, (int)n_rows, r_ptr, (int)K, h, ldh, agg, ld_agg,
+                               gd);
+            src = gd;
+            ld_src = K;
+            hipLaunchKernelGGL((k_dgrad_gather<VECv, LPRv, NGNN_REDUCE_MAX>), dim3(grid), dim3(256),
+                               0, st, src, ld_src, droot, ld_droot, rowptr, rowptr_t, col_t,
+                               (int)n_rows, r_ptr, rnext_ptr, (int)K, h, ldh, agg, ld_agg, dh, ldd,
+                               zero_tail);
+        } else if (reduce == NGNN_REDUCE_MEAN) {
+            hipLaunchKernelGGL((k_dgrad_gather<VECv, LPRv, NGNN_REDUCE_MEAN>), dim3(grid), dim3(256),
+                               0, st, src, ld_src, droot, ld_droot, rowptr, rowptr_t, col_t,
+                               (int)n_rows, r_ptr, rnext_ptr, (int)K, h, ldh, agg, ld_agg, dh, ldd,
+                               zero_tail);
+        } else {
+            hipLaunchKernelGGL((k_dgrad_gather<VECv, LPRv, NGNN_REDUCE_SUM>), dim3(grid), dim3(256),
+                               0, st, src, ld_src, droot, ld_droot, rowptr, rowptr_t, col_t,
+                               (int)n_rows, r_ptr, rnext_ptr, (int)K, h, ldh, agg, ld_agg, dh, ldd,
+                               zero_tail);
+        }
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I1 = std::integral_constant<int, 1>;
+    const int lpr = lpr_for(K, vec ? 4 : 1);
+    auto dispatch_lpr = [&](auto vec_c) {
+        switch (lpr) {
+            case 4: go(vec_c, std::integral_constant<int, 4>{}); break;
+            case 8: go(vec_c, std::integral_constant<int, 8>{}); break;
+            case 16: go(vec_c, std::integral_constant<int, 16>{}); break;
+            case 32: go(vec_c, std::integral_constant<int, 32>{}); break;
+            default: go(vec_c, std::integral_constant<int, 64>{}); break;
+        }
+    };
+    if (vec) dispatch_lpr(I4{});
+    else dispatch_lpr(I1{});
+    return launch_status();
+}

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
@@ -34,10 +34,18 @@ SIGNATURES = {
     "ngnn_sample_hop": (_int, [_p, _p, _p, _i64, _int, ctypes.c_uint64, _p, _p, _p]),
     "ngnn_pack_weight_bytes": (_sz, [_i64, _i64]),
     "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
-    "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _int, _p, _p, _p, _i64, _p, _i64, _int,
-                             ctypes.c_float, ctypes.c_uint64, _p]),
+    "ngnn_pack_weight_ex": (_int, [_p, _p, _i64, _i64, _i64, _i64, _int, _p, _p]),
+    "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
+                             _int, ctypes.c_float, ctypes.c_uint64, _p, _i64, _p, _i64,
+                             ctypes.c_float, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
-    "ngnn_block_prefix_stats": (_int, [_p, _p, _i64, _i64, _p, _p]),
+    "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
+    "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
+    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _i64, _p, _i64, _p, _i64,
+                               _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
+    "ngnn_sage_dgrad_workspace_bytes": (_sz, [_i64, _i64, _int]),
+    "ngnn_sage_dgrad_gather": (_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p, _p, _i64,
+                                      _int, _p, _i64, _p, _i64, _p, _i64, _int, _p, _sz, _p]),
 }
 
 _lib = None

@@ -23,6 +23,7 @@ class Rec:
     bytes: int
     start: torch.cuda.Event
     end: torch.cuda.Event
+    flops: int = 0
 
 
 class KernelTimer:
@@ -39,16 +40,16 @@ class KernelTimer:
         _active = self._prev
 
     def summary(self):
-        """{name: (launches, total_ms, total_bytes)} — call after a synchronize."""
+        """{name: (launches, total_ms, total_bytes, total_flops)} — call after a synchronize."""
         out = {}
         for r in self.recs:
-            n, ms, b = out.get(r.name, (0, 0.0, 0))
-            out[r.name] = (n + 1, ms + r.start.elapsed_time(r.end), b + r.bytes)
+            n, ms, b, f = out.get(r.name, (0, 0.0, 0, 0))
+            out[r.name] = (n + 1, ms + r.start.elapsed_time(r.end), b + r.bytes, f + r.flops)
         return out
 
 
 @contextlib.contextmanager
-def span(name: str, nbytes: int):
+def span(name: str, nbytes: int, flops: int = 0):
     t = _active
     if t is None:
         yield
@@ -58,4 +59,4 @@ def span(name: str, nbytes: int):
     s.record()
     yield
     e.record()
-    t.recs.append(Rec(name, int(nbytes), s, e))
+    t.recs.append(Rec(name, int(nbytes), s, e, int(flops)))

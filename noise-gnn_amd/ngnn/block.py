@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import collections
 import threading
+import weakref
 
 import torch
 
@@ -90,6 +91,7 @@ class Block:
         self.dst_sorted, self.src_sorted = bool(dst_sorted), bool(src_sorted)
         self.csr = build_csr(edge_index[1], edge_index[0], self.n_dst, self.dst_sorted)
         self._csr_t = None
+        self.n_active = None  # leading rows with in-edges, if a producer told us
 
     @property
     def rowptr(self):
@@ -125,7 +127,13 @@ class _BlockCache:
             if hit is not None and hit[0] is edge_index:
                 self._d.move_to_end(key)
                 return hit[1]
-        blk = Block(edge_index, num_nodes)
+        hint = _hint_for(edge_index)
+        if hint is not None:
+            blk = Block(edge_index, num_nodes, validate=False, dst_sorted=hint[0],
+                        src_sorted=hint[1])
+            blk.n_active = hint[2]
+        else:
+            blk = Block(edge_index, num_nodes)
         with self._lock:
             self._d[key] = (edge_index, blk)
             while len(self._d) > self.capacity:
@@ -138,6 +146,34 @@ class _BlockCache:
 
 
 block_cache = _BlockCache()
+
+# Producer hints: a sampler that builds edge_index itself (ngnn.loader) knows it
+# is in range and target-sorted, so the block can skip the validating probe
+# (and its host read-back).  Keyed by tensor identity; a weakref guards reuse.
+_hints: dict = {}
+_hints_lock = threading.Lock()
+
+
+def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: bool,
+                    n_active: int | None = None) -> None:
+    """n_active: number of leading target rows that can have in-edges (all
+    later rows have none) -- only used for roofline accounting."""
+    ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
+    with _hints_lock:
+        _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active)
+
+
+def _drop_hint(key):
+    with _hints_lock:
+        _hints.pop(key, None)
+
+
+def _hint_for(edge_index):
+    with _hints_lock:
+        h = _hints.get(id(edge_index))
+    if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
+        return None
+    return h[2], h[3], h[4]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

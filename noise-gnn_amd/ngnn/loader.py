@@ -28,6 +28,7 @@ import dataclasses
 import torch
 
 from . import _lib
+from .block import hint_edge_index
 
 # name -> (num_nodes, directed entries (symmetric), features, classes, train seeds)
 DATASETS = {
@@ -142,12 +143,14 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
     frontier = n_id
     frontier_local = torch.arange(n_id.numel(), device=dev)
     srcs, dsts = [], []
+    n_active = n_id.numel()
     for hop, k in enumerate(fanouts):
         nbr, _ = sample_hop(graph, frontier, int(k), seed * 1_000_003 + hop)
         mask = nbr >= 0
         dst_local = frontier_local.unsqueeze(1).expand(-1, int(k))[mask]
         cand = nbr[mask]
         n_old = n_id.numel()
+        n_active = n_old  # rows that received in-edges so far (all frontiers up to this hop)
         all_ids = torch.cat([n_id, cand])
         uniq, inv = torch.unique(all_ids, return_inverse=True)
         pos = torch.arange(all_ids.numel(), device=dev)
@@ -165,6 +168,8 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
         frontier = new_nodes
     edge_index = torch.stack([torch.cat(srcs), torch.cat(dsts)]) if srcs else \
         torch.empty(2, 0, dtype=torch.int64, device=dev)
+    # built here: ids are in range and targets non-decreasing -> no probe needed
+    hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active)
     x = graph.x.index_select(0, n_id) if gather_features else None
     y = graph.y.index_select(0, n_id)
     return Batch(x, y, edge_index, n_id, int(seeds.numel()))

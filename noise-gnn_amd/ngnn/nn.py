@@ -80,8 +80,7 @@ class SAGEConv(nn.Module):
         block = get_block(edge_index, x.size(0))
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p.requires_grad for p in self.parameters()))
-        if not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 \
-                and self.out_channels <= 512:
+        if not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2:
             # inference (e.g. SAGE.inference, sage.py:52): one fused launch
             from .fused import sage_layer_fwd
             aggr = "sum" if self.aggr == "add" else self.aggr

@@ -22,24 +22,27 @@ OUT = dict(rtol=1e-5, atol=1e-5)
 GRAD = dict(rtol=1e-4, atol=1e-5)
 WGRAD = dict(rtol=1e-4, atol=1e-4)
 
-M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+M32 = np.uint64(0xFFFFFFFF)
 
 
-def _mix64(z):
-    z = (z + np.uint64(0x9E3779B97F4A7C15)) & M64
-    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M64
-    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M64
-    return z ^ (z >> np.uint64(31))
+def _lowbias32(x):
+    x = x ^ (x >> np.uint64(16))
+    x = (x * np.uint64(0x7FEB352D)) & M32
+    x = x ^ (x >> np.uint64(15))
+    x = (x * np.uint64(0x846CA68B)) & M32
+    return x ^ (x >> np.uint64(16))
 
 
 def dropout_keep(seed, n_rows, n_cols, p):
-    """Host replica of the kernel's keep mask: uniform01(seed,row,col) >= p."""
-    with np.errstate(over="ignore"):
-        r = np.arange(n_rows, dtype=np.uint64)[:, None]
-        c = np.arange(n_cols, dtype=np.uint64)[None, :]
-        h = _mix64(np.uint64(seed) ^ _mix64((r << np.uint64(20)) ^ c))
-    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-    return torch.from_numpy(u >= np.float32(p))
+    """Host replica of ngnn_device.h::Dropout: keep <=> (hash >> 8) >= ceil(p * 2^24)."""
+    import math
+    s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    thresh = math.ceil(float(np.float32(p)) * 16777216.0)
+    r = np.arange(n_rows, dtype=np.uint64)[:, None]
+    c = np.arange(n_cols, dtype=np.uint64)[None, :]
+    rk = _lowbias32(r ^ s0)
+    h = _lowbias32(_lowbias32((rk + c) & M32) ^ s1)
+    return torch.from_numpy((h >> np.uint64(8)) >= np.uint64(thresh))
 
 
 def rand_block(seed, N, E, order="dst"):
@@ -51,7 +54,8 @@ def rand_block(seed, N, E, order="dst"):
 
 
 @pytest.mark.parametrize("K,Fo", [(100, 256), (256, 47), (128, 40), (24, 7), (767, 16),
-                                  (256, 256), (300, 512), (8, 3), (129, 20)])
+                                  (256, 256), (300, 512), (8, 3), (129, 20), (64, 600),
+                                  (767, 1534)])
 @pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
 def test_fused_layer_matches_oracle(K, Fo, reduce):
     N, E = 700, 5000
