@@ -201,6 +201,28 @@ int ngnn_sage_dgrad_gather(const float *dagg, int64_t ld_dagg, const float *droo
                            const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
                            float *dh, int64_t ldd, int zero_tail, void *ws, size_t ws_bytes,
                            void *stream);
+/* Same result through float atomics instead of the source-grouped CSR (no
+ * per-batch sort): dh[j] = [j < R] droot[j] for j < Rn, then every edge
+ * (j -> d), d < R, adds its term into dh[j] (one 256-B atomic wave-instruction
+ * per edge and 64 columns).  Summation order is not fixed (as with the
+ * reference's CUDA index_add_); the gather variant is the deterministic one.
+ * rowptr/col: target-grouped CSR. */
+int ngnn_sage_dgrad_scatter(const float *dagg, int64_t ld_dagg, const float *droot,
+                            int64_t ld_droot, const int32_t *rowptr, const int32_t *col,
+                            int64_t n_rows, const int32_t *r_ptr, const int32_t *rnext_ptr,
+                            int64_t K, int reduce, const float *h, int64_t ldh, const float *agg,
+                            int64_t ld_agg, float *dh, int64_t ldd, int zero_tail, void *stream);
+/* The whole atomic input-gradient path of one layer in two launches, no dgrad
+ * GEMM: zero dh rows < Rn, then one wave per target row d < R computes
+ * dz[d] = dy[d] (* [y>0] * yscale), dz[d] W_r (atomically into dh[d]) and
+ * dz[d] W_l (scaled as in ngnn_sage_dgrad_gather, atomically into every
+ * in-neighbour's row).  wl / wr: the raw PyG weights [Fo, K].  Fo <= 512. */
+int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
+                          float yscale, const float *wl, const float *wr, int64_t Fo, int64_t K,
+                          const int32_t *rowptr, const int32_t *col, int64_t n_rows,
+                          const int32_t *r_ptr, const int32_t *rnext_ptr, int reduce,
+                          const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
+                          float *dh, int64_t ldd, int zero_tail, void *stream);
 
 #ifdef __cplusplus
 }

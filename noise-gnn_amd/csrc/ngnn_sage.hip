@@ -29,6 +29,8 @@
 // Roofline: fp32 MFMA peak 157.3 TF; flops = 2*N*K*F_out (root) +
 // 2*N_edge_rows*K*F_out (neighbour); HBM bytes = x (N*K*4) + gathered rows
 // (E*K*4) + col/rowptr + out (N*F_out*4).
+#include <cstdlib>
+
 #include "ngnn_device.h"
 
 namespace ngnn {
@@ -59,6 +61,7 @@ struct Extra {
     const float *xmask;
     int64_t ldm;
     float xscale;
+    int dbg;  // ablation switch for profiling (NGNN_SAGE_ABLATE): 0 in normal runs
 };
 
 // ---- X rows [row0, row0+64) x [k0, k0+128) -> LDS, zero padded
@@ -193,34 +196,43 @@ __device__ __forceinline__ void mfma_chunk(v4f (&acc)[MTW][NTW], const float *s,
                                            int mbase, int nbase, int NT) {
     const int lane = threadIdx.x & 63;
     const int arow = lane & 15, acol = 4 * (lane >> 4);
-    v4f b[NTW], bn[NTW];
+    // B loads are unconditional (tiles past NT read the last valid tile; their
+    // accumulators are never stored) so the compiler can count them and keep
+    // the next k-group's fragments in flight behind a partial vmcnt.
+    const v4f *wt[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt)
-        b[nt] = (nbase + nt < NT) ? wpack[(static_cast<int64_t>(nbase + nt) * KG + kg0) * 64 + lane]
-                                  : v4f{0.f, 0.f, 0.f, 0.f};
-    for (int kg = 0; kg < nkg; ++kg) {
-        if (kg + 1 < nkg) {
+        wt[nt] = wpack + (static_cast<int64_t>(min(nbase + nt, NT - 1)) * KG + kg0) * 64 + lane;
+    // ping-pong register sets: the loads for k-group g+1 are issued (and pinned
+    // with a scheduling barrier) before the MFMAs of group g, no register copies
+    v4f b0[NTW], b1[NTW];
 #pragma unroll
-            for (int nt = 0; nt < NTW; ++nt)
-                bn[nt] = (nbase + nt < NT)
-                             ? wpack[(static_cast<int64_t>(nbase + nt) * KG + kg0 + kg + 1) * 64 + lane]
-                             : v4f{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int nt = 0; nt < NTW; ++nt) b0[nt] = wt[nt][0];
+    auto step = [&](int kg, v4f(&cur)[NTW], v4f(&nxt)[NTW]) {
+        const int kn = min(kg + 1, nkg - 1);  // last group re-reads: harmless, branch-free
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) nxt[nt] = wt[nt][kn * 64];
         v4f a[MTW];
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt)
             a[mt] = *reinterpret_cast<const v4f *>(s + (mbase + mt * 16 + arow) * LDA + kg * 16 + acol);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NTW; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][i], b[nt][i],
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt][i], cur[nt][i],
                                                                        acc[mt][nt], 0, 0, 0);
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) b[nt] = bn[nt];
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int kg = 0;
+    for (; kg + 2 <= nkg; kg += 2) {
+        step(kg, b0, b1);
+        step(kg + 1, b1, b0);
     }
+    if (kg < nkg) step(kg, b0, b1);
 }
 
 template <int MTW, int NTW, int RED, bool VEC>
@@ -251,9 +263,9 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
         const int nkg = (min(KC, K - k0) + 15) >> 4;
         if (!first) __syncthreads();
         first = false;
-        stage_x<VEC>(s, x, ldx, row0, rows, k0, K, ex.xmask, ex.ldm, ex.xscale);
+        if (!(ex.dbg & 4)) stage_x<VEC>(s, x, ldx, row0, rows, k0, K, ex.xmask, ex.ldm, ex.xscale);
         __syncthreads();
-        mfma_chunk<MTW, NTW>(acc, s, wr, KG, k0 >> 4, nkg, mbase, nbase, NT);
+        if (!(ex.dbg & 1)) mfma_chunk<MTW, NTW>(acc, s, wr, KG, k0 >> 4, nkg, mbase, nbase, NT);
     }
     if (has_edges) {
         for (int k0 = 0; k0 < K; k0 += KC) {
@@ -272,57 +284,37 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
         }
     }
 
-    // ---- epilogue: 128-column passes through LDS
+    // ---- epilogue straight from the accumulators (no LDS round trip, no
+    // barrier): in a 16x16 C tile lane l holds rows 4*(l>>4)+j of column l&15,
+    // so one store instruction writes four 64-B row segments; the neighbouring
+    // n-tile completes each 128-B line in L2.
+    if (ex.dbg & 8) return;
     const int q = lane >> 4, cl = lane & 15;
-    const int passes = (NT + 7) >> 3;
-    for (int pass = 0; pass < passes; ++pass) {
-        __syncthreads();
+    (void)vec_out;
+    uint32_t rk[MTW][4];
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            rk[mt][j] = epi.drop.row_key(static_cast<uint32_t>(row0 + mbase + mt * 16 + 4 * q + j));
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        const int c = (nbase + nt) * 16 + cl;
+        if (c >= Fo) continue;
+        const float bc = epi.bias ? epi.bias[c] : 0.0f;
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < NTW; ++nt) {
-                const int ntile = nbase + nt;
-                if (ntile >= NT || (ntile >> 3) != pass) continue;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    s[(mbase + mt * 16 + 4 * q + j) * LDA + (ntile & 7) * 16 + cl] = acc[mt][nt][j];
-            }
-        __syncthreads();
-        const int c_base = pass * 128;
-        const int cols = min(128, Fo - c_base);
-        if (vec_out) {
-            const int c4n = cols >> 2;
-            for (int idx = threadIdx.x; idx < rows * c4n; idx += 256) {
-                const int r = idx / c4n, c = (idx - r * c4n) << 2;
-                const int64_t row = row0 + r;
-                const int gc = c_base + c;
-                const float *sp = s + r * LDA + c;
-                float v[4] = {sp[0], sp[1], sp[2], sp[3]};
-                const uint32_t rk = epi.drop.row_key(static_cast<uint32_t>(row));
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (epi.bias) v[i] += epi.bias[gc + i];
-                    if (epi.relu) v[i] = (v[i] < 0.0f) ? 0.0f : v[i];  // NaN passes, like torch.relu
-                    if (epi.drop.thresh)
-                        v[i] = epi.drop.keep(rk, epi.col_base + gc + i) ? v[i] * epi.drop.scale : 0.0f;
-                }
-                *reinterpret_cast<float4 *>(out + row * ldo + gc) = make_float4(v[0], v[1], v[2], v[3]);
-            }
-        } else {
-            for (int idx = threadIdx.x; idx < rows * cols; idx += 256) {
-                const int r = idx / cols, c = idx - r * cols;
-                const int64_t row = row0 + r;
-                const int gc = c_base + c;
-                float v = s[r * LDA + c];
-                if (epi.bias) v += epi.bias[gc];
-                if (epi.relu) v = (v < 0.0f) ? 0.0f : v;
+            for (int j = 0; j < 4; ++j) {
+                const int r = mbase + mt * 16 + 4 * q + j;
+                if (r >= rows) continue;
+                float v = acc[mt][nt][j];
+                if (epi.bias) v += bc;
+                if (epi.relu) v = (v < 0.0f) ? 0.0f : v;  // NaN passes, like torch.relu
                 if (epi.drop.thresh)
-                    v = epi.drop.keep(epi.drop.row_key(static_cast<uint32_t>(row)), epi.col_base + gc)
-                            ? v * epi.drop.scale
-                            : 0.0f;
-                out[row * ldo + gc] = v;
+                    v = epi.drop.keep(rk[mt][j], epi.col_base + c) ? v * epi.drop.scale : 0.0f;
+                if (!(ex.dbg & 2)) out[(row0 + r) * ldo + c] = v;
             }
-        }
     }
 }
 
@@ -500,7 +492,8 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     for (int64_t c0 = 0; c0 < Fo; c0 += 512) {
         const int64_t Fo_c = std::min<int64_t>(512, Fo - c0);
         const int64_t toff = (c0 / 16) * KG * 64;  // float4 offset of the slice's first n-tile
-        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale};
+        static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
+        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, dbg};
         float *of = out + c0;
         const int vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(of, 16);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));

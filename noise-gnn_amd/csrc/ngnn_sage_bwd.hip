@@ -27,7 +27,7 @@ constexpr int WG_KC = 128;      // K columns per workgroup (grid.y)
 constexpr int WG_NC = 256;      // Fo columns per workgroup (grid.z)
 constexpr int LDZ = WG_NC + 16; // LDS strides: +16 floats keeps the two 16-lane
 constexpr int LDH = WG_KC + 16; // row groups of a b32 read on disjoint banks
-constexpr int S_MAX = 128;      // slices (partial slabs)
+constexpr int S_MAX = 256;      // slices (partial slabs): one workgroup per CU
 
 __host__ __device__ inline size_t slab_floats(int64_t Fo, int64_t K) {
     return static_cast<size_t>(2 * Fo * K + Fo);
@@ -176,8 +176,17 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
     if (i >= total) return;
     const int R = *r_ptr;
     const int used = min(S, (R + WG_BM - 1) / WG_BM);
+    // loads issued 8 at a time (memory-level parallelism), summed in slab order
     float t = 0.0f;
-    for (int s = 0; s < used; ++s) t += ws[static_cast<size_t>(s) * total + i];
+    int s = 0;
+    for (; s + 8 <= used; s += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ws[static_cast<size_t>(s + u) * total + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t += v[u];
+    }
+    for (; s < used; ++s) t += ws[static_cast<size_t>(s) * total + i];
     const int64_t FK = static_cast<int64_t>(Fo) * K;
     if (i < FK) dwr[i] = t;
     else if (i < 2 * FK) dwl[i - FK] = t;
@@ -330,6 +339,136 @@ __global__ __launch_bounds__(256) void k_max_gdist(const float *__restrict__ dag
     }
 }
 
+// ---- atomic path (default; like the reference's CUDA index_add_ backward)
+// dh[j] = [j < R] droot[j] for j < Rn; rows >= Rn zeroed if zero_tail
+__global__ __launch_bounds__(256) void k_dh_init(const float *__restrict__ droot, int64_t ld_droot,
+                                                 int n_rows, const int32_t *__restrict__ r_ptr,
+                                                 const int32_t *__restrict__ rn_ptr, int K,
+                                                 float *__restrict__ dh, int64_t ldd, int zero_tail) {
+    const int R = *r_ptr, Rn = *rn_ptr;
+    const int64_t lim = zero_tail ? n_rows : min(n_rows, Rn);
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < lim * K; idx += nthr) {
+        const int64_t row = idx / K;
+        const int f = static_cast<int>(idx - row * K);
+        dh[row * ldd + f] = (droot && row < R) ? droot[row * ld_droot + f] : 0.0f;
+    }
+}
+
+// one wave per target row d < R: scale dagg[d] once, then one 256-B atomic
+// wave-instruction per (in-edge, 64 columns) into the source row
+template <int RED>
+__global__ __launch_bounds__(256) void k_dgrad_scatter(
+    const float *__restrict__ dagg, int64_t ld_dagg, const int32_t *__restrict__ rowptr,
+    const int32_t *__restrict__ col, int n_rows, const int32_t *__restrict__ r_ptr, int K,
+    const float *__restrict__ h, int64_t ldh, const float *__restrict__ agg, int64_t ld_agg,
+    float *__restrict__ dh, int64_t ldd) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int R = min(n_rows, *r_ptr);
+    for (int64_t d = blockIdx.x * 4 + wave; d < R; d += gridDim.x * 4) {
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        if (beg == end) continue;
+        const float cnt = static_cast<float>(end - beg);
+        for (int f0 = 0; f0 < K; f0 += 64) {
+            const int f = f0 + lane;
+            const bool act = f < K;
+            float v = act ? dagg[d * ld_dagg + f] : 0.0f;
+            float a = 0.0f;
+            if (RED == NGNN_REDUCE_MEAN) v = v / cnt;
+            if (RED == NGNN_REDUCE_MAX) {
+                a = act ? agg[d * ld_agg + f] : 0.0f;
+                float ties = (a == 0.0f) ? 1.0f : 0.0f;
+                for (int e = beg; e < end; ++e) {
+                    const int64_t j = col[e];
+                    if (act) ties += (h[j * ldh + f] == a) ? 1.0f : 0.0f;
+                }
+                v = v / ties;
+            }
+            if (!act) continue;
+            for (int e = beg; e < end; ++e) {
+                const int64_t j = col[e];
+                if (RED == NGNN_REDUCE_MAX && !(h[j * ldh + f] == a)) continue;
+                atomicAdd(dh + j * ldd + f, v);
+            }
+        }
+    }
+}
+
+// ---- fused dgrad (atomic): no dgrad GEMM launch.  One wave per target row
+// d < R (grid-stride, so rows past the device-side bound cost nothing):
+//   dz[d]    = dy[d] (* [y > 0] * yscale)            staged in the wave's LDS slot
+//   root[f]  = sum_n dz[d][n] W_r[n][f]   -> atomic into dh[d][f]
+//   agg[f]   = sum_n dz[d][n] W_l[n][f]   -> scaled (mean: / deg; max: tie split)
+//              and atomically added into dh[j][f] for every in-edge j -> d
+// lanes own 64 consecutive columns per chunk, so every atomic wave-instruction
+// covers 256 contiguous bytes; W rows are read coalesced from L1/L2.
+// dh rows < Rn must be zeroed first (k_dh_init with droot = NULL semantics).
+constexpr int FD_MAXF = 512;  // dz row staged per wave: Fo <= 512 on this path
+
+template <int RED>
+__global__ __launch_bounds__(256) void k_dgrad_fused(
+    const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
+    float yscale, const float *__restrict__ wl, const float *__restrict__ wr, int Fo, int K,
+    const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int n_rows,
+    const int32_t *__restrict__ r_ptr, const float *__restrict__ h, int64_t ldh,
+    const float *__restrict__ agg, int64_t ld_agg, float *__restrict__ dh, int64_t ldd) {
+    __shared__ __attribute__((aligned(16))) float sdz[4][FD_MAXF];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *z = sdz[wave];
+    const int R = min(n_rows, *r_ptr);
+    for (int64_t d = blockIdx.x * 4 + wave; d < R; d += gridDim.x * 4) {
+        for (int n = lane; n < Fo; n += 64) {
+            float v = dy[d * ldy + n];
+            if (y) v = (y[d * ldyy + n] > 0.0f) ? v * yscale : 0.0f;
+            z[n] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // z[] written by all lanes
+        __builtin_amdgcn_wave_barrier();
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        const float cnt = static_cast<float>(end - beg);
+        for (int f0 = 0; f0 < K; f0 += 64) {
+            const int f = f0 + lane;
+            const bool act = f < K;
+            const int fc = act ? f : 0;
+            float ar = 0.0f, al = 0.0f;
+            int n = 0;
+            for (; n + 4 <= Fo; n += 4) {
+                const float4 zz = *reinterpret_cast<const float4 *>(z + n);  // uniform: broadcast
+                const float r0 = wr[(int64_t)(n + 0) * K + fc], r1 = wr[(int64_t)(n + 1) * K + fc];
+                const float r2 = wr[(int64_t)(n + 2) * K + fc], r3 = wr[(int64_t)(n + 3) * K + fc];
+                const float l0 = wl[(int64_t)(n + 0) * K + fc], l1 = wl[(int64_t)(n + 1) * K + fc];
+                const float l2 = wl[(int64_t)(n + 2) * K + fc], l3 = wl[(int64_t)(n + 3) * K + fc];
+                ar += zz.x * r0; ar += zz.y * r1; ar += zz.z * r2; ar += zz.w * r3;
+                al += zz.x * l0; al += zz.y * l1; al += zz.z * l2; al += zz.w * l3;
+            }
+            for (; n < Fo; ++n) {
+                const float zn = z[n];
+                ar += zn * wr[(int64_t)n * K + fc];
+                al += zn * wl[(int64_t)n * K + fc];
+            }
+            if (!act) continue;
+            atomicAdd(dh + d * ldd + f, ar);
+            if (beg == end) continue;
+            float v = al;
+            float a = 0.0f;
+            if (RED == NGNN_REDUCE_MEAN) v = v / cnt;
+            if (RED == NGNN_REDUCE_MAX) {
+                a = agg[d * ld_agg + f];
+                float ties = (a == 0.0f) ? 1.0f : 0.0f;
+                for (int e = beg; e < end; ++e) ties += (h[(int64_t)col[e] * ldh + f] == a) ? 1.0f : 0.0f;
+                v = v / ties;
+            }
+            for (int e = beg; e < end; ++e) {
+                const int64_t j = col[e];
+                if (RED == NGNN_REDUCE_MAX && !(h[j * ldh + f] == a)) continue;
+                atomicAdd(dh + j * ldd + f, v);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // done reading z
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 int lpr_for(int64_t K, int vec) {
     const int64_t chunks = ceil_div(K, vec);
     int l = 4;
@@ -466,5 +605,78 @@ extern "C" int ngnn_sage_dgrad_gather(const float *dagg, int64_t ld_dagg, const 
     };
     if (vec) dispatch_lpr(I4{});
     else dispatch_lpr(I1{});
+    return launch_status();
+}
+
+extern "C" int ngnn_sage_dgrad_scatter(const float *dagg, int64_t ld_dagg, const float *droot,
+                                       int64_t ld_droot, const int32_t *rowptr, const int32_t *col,
+                                       int64_t n_rows, const int32_t *r_ptr,
+                                       const int32_t *rnext_ptr, int64_t K, int reduce,
+                                       const float *h, int64_t ldh, const float *agg,
+                                       int64_t ld_agg, float *dh, int64_t ldd, int zero_tail,
+                                       void *stream) {
+    NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
+    NGNN_RETURN_IF(!dagg || !droot || !rowptr || !r_ptr || !rnext_ptr || !dh, NGNN_E_ARG);
+    NGNN_RETURN_IF(K <= 0 || n_rows < 0, NGNN_E_ARG);
+    NGNN_RETURN_IF(ld_dagg < K || ld_droot < K || ldd < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    if (n_rows == 0) return NGNN_OK;
+    const bool is_max = reduce == NGNN_REDUCE_MAX;
+    NGNN_RETURN_IF(is_max && (!h || !agg), NGNN_E_ARG);
+    NGNN_RETURN_IF(is_max && (ldh < K || ld_agg < K), NGNN_E_SHAPE);
+    hipStream_t st = as_stream(stream);
+    const unsigned g_init = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows * K, 256), 4096));
+    hipLaunchKernelGGL(k_dh_init, dim3(g_init), dim3(256), 0, st, droot, ld_droot, (int)n_rows,
+                       r_ptr, rnext_ptr, (int)K, dh, ldd, zero_tail);
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows, 4), 2048));
+    if (reduce == NGNN_REDUCE_MEAN)
+        hipLaunchKernelGGL((k_dgrad_scatter<NGNN_REDUCE_MEAN>), dim3(g), dim3(256), 0, st, dagg,
+                           ld_dagg, rowptr, col, (int)n_rows, r_ptr, (int)K, h, ldh, agg, ld_agg, dh,
+                           ldd);
+    else if (reduce == NGNN_REDUCE_SUM)
+        hipLaunchKernelGGL((k_dgrad_scatter<NGNN_REDUCE_SUM>), dim3(g), dim3(256), 0, st, dagg,
+                           ld_dagg, rowptr, col, (int)n_rows, r_ptr, (int)K, h, ldh, agg, ld_agg, dh,
+                           ldd);
+    else
+        hipLaunchKernelGGL((k_dgrad_scatter<NGNN_REDUCE_MAX>), dim3(g), dim3(256), 0, st, dagg,
+                           ld_dagg, rowptr, col, (int)n_rows, r_ptr, (int)K, h, ldh, agg, ld_agg, dh,
+                           ldd);
+    return launch_status();
+}
+
+extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
+                                     float yscale, const float *wl, const float *wr, int64_t Fo,
+                                     int64_t K, const int32_t *rowptr, const int32_t *col,
+                                     int64_t n_rows, const int32_t *r_ptr,
+                                     const int32_t *rnext_ptr, int reduce, const float *h,
+                                     int64_t ldh, const float *agg, int64_t ld_agg, float *dh,
+                                     int64_t ldd, int zero_tail, void *stream) {
+    NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
+    NGNN_RETURN_IF(!dy || !wl || !wr || !rowptr || !r_ptr || !rnext_ptr || !dh, NGNN_E_ARG);
+    NGNN_RETURN_IF(Fo <= 0 || K <= 0 || n_rows < 0, NGNN_E_ARG);
+    NGNN_RETURN_IF(Fo > FD_MAXF, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(ldy < Fo || (y && ldyy < Fo) || ldd < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    if (n_rows == 0) return NGNN_OK;
+    const bool is_max = reduce == NGNN_REDUCE_MAX;
+    NGNN_RETURN_IF(is_max && (!h || !agg), NGNN_E_ARG);
+    NGNN_RETURN_IF(is_max && (ldh < K || ld_agg < K), NGNN_E_SHAPE);
+    hipStream_t st = as_stream(stream);
+    const unsigned g_init = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows * K, 256), 4096));
+    hipLaunchKernelGGL(k_dh_init, dim3(g_init), dim3(256), 0, st, (const float *)nullptr, K,
+                       (int)n_rows, r_ptr, rnext_ptr, (int)K, dh, ldd, zero_tail);
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows, 4), 1024));
+    if (reduce == NGNN_REDUCE_MEAN)
+        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_MEAN>), dim3(g), dim3(256), 0, st, dy, ldy, y,
+                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
+                           h, ldh, agg, ld_agg, dh, ldd);
+    else if (reduce == NGNN_REDUCE_SUM)
+        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_SUM>), dim3(g), dim3(256), 0, st, dy, ldy, y,
+                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
+                           h, ldh, agg, ld_agg, dh, ldd);
+    else
+        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_MAX>), dim3(g), dim3(256), 0, st, dy, ldy, y,
+                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
+                           h, ldh, agg, ld_agg, dh, ldd);
     return launch_status();
 }

@@ -46,6 +46,11 @@ SIGNATURES = {
     "ngnn_sage_dgrad_workspace_bytes": (_sz, [_i64, _i64, _int]),
     "ngnn_sage_dgrad_gather": (_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p, _p, _i64,
                                       _int, _p, _i64, _p, _i64, _p, _i64, _int, _p, _sz, _p]),
+    "ngnn_sage_dgrad_scatter": (_int, [_p, _i64, _p, _i64, _p, _p, _i64, _p, _p, _i64, _int, _p,
+                                       _i64, _p, _i64, _p, _i64, _int, _p]),
+    "ngnn_sage_dgrad_fused": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _i64, _i64, _p,
+                                     _p, _i64, _p, _p, _int, _p, _i64, _p, _i64, _p, _i64, _int,
+                                     _p]),
 }
 
 _lib = None

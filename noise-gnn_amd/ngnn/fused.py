@@ -136,7 +136,10 @@ class _SAGEStack(torch.autograd.Function):
         bptr = lambda j: bnd.data_ptr() + 4 * j  # noqa: E731
         _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L), stream),
                    "ngnn_row_extent")
-        t = block.transposed() if (L > 1 or need_dx) else None
+        # input-gradient scatter: float atomics by default (as the reference's CUDA
+        # index_add_); the source-grouped CSR gather when determinism is requested
+        deterministic = torch.are_deterministic_algorithms_enabled()
+        t = block.transposed() if (deterministic and (L > 1 or need_dx)) else None
         red = _lib.REDUCE[reduce]
         for i in reversed(range(L)):
             h_in, y_out, agg = acts[i], acts[i + 1], aggs[i]
@@ -162,6 +165,20 @@ class _SAGEStack(torch.autograd.Function):
             _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
                                                    bptr(i + 1), None, bptr(i), block.E, stream),
                        "ngnn_block_prefix_stats")
+            if not deterministic and Fo <= 512:
+                # atomic path: per-row VALU products + scatter, no dgrad GEMM launch
+                dh = torch.empty(N, K, dtype=torch.float32, device=dev)
+                wlc, wrc = wl.detach().contiguous(), wr.detach().contiguous()
+                with _timing.span("sage_dgrad_fused", 0, 0):
+                    rc = lib.ngnn_sage_dgrad_fused(
+                        _lib.ptr(dy), dy.stride(0), _lib.ptr(ymask),
+                        ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(wlc),
+                        _lib.ptr(wrc), Fo, K, _lib.ptr(block.rowptr), _lib.ptr(block.col), N,
+                        bptr(i + 1), bptr(i), red, _lib.ptr(h_in), h_in.stride(0), _lib.ptr(agg),
+                        agg.stride(0), _lib.ptr(dh), dh.stride(0), int(i == 0), stream)
+                _lib.check(rc, "ngnn_sage_dgrad_fused")
+                dy = dh
+                continue
             # dgrad GEMM: [dz W_l | dz W_r] on rows < R (ReLU/dropout backward in the staging)
             pk = pack_dgrad_weight(wl, wr)
             dg = torch.empty(N, 2 * K, dtype=torch.float32, device=dev)
@@ -169,14 +186,24 @@ class _SAGEStack(torch.autograd.Function):
                 _gemm_layer(dy, Fo, N, None, "mean", None, pk, None, 2 * K, dg, False, 0.0, 0,
                             n_rows_dev=bptr(i + 1), xmask=ymask, xscale=yscale)
             dh = torch.empty(N, K, dtype=torch.float32, device=dev)
-            gws = _workspace(dev, "dgrad", lib.ngnn_sage_dgrad_workspace_bytes(N, K, red))
-            with _timing.span("sage_dgrad_gather", 0, 0):
-                rc = lib.ngnn_sage_dgrad_gather(
-                    _lib.ptr(dg), 2 * K, _lib.ptr(dg) + 4 * K, 2 * K, _lib.ptr(block.rowptr),
-                    _lib.ptr(block.col), _lib.ptr(t.rowptr), _lib.ptr(t.col), N, bptr(i + 1),
-                    bptr(i), K, red, _lib.ptr(h_in), h_in.stride(0), _lib.ptr(agg), agg.stride(0),
-                    _lib.ptr(dh), dh.stride(0), int(i == 0), _lib.ptr(gws), gws.numel(), stream)
-            _lib.check(rc, "ngnn_sage_dgrad_gather")
+            if deterministic:
+                gws = _workspace(dev, "dgrad", lib.ngnn_sage_dgrad_workspace_bytes(N, K, red))
+                with _timing.span("sage_dgrad_gather", 0, 0):
+                    rc = lib.ngnn_sage_dgrad_gather(
+                        _lib.ptr(dg), 2 * K, _lib.ptr(dg) + 4 * K, 2 * K, _lib.ptr(block.rowptr),
+                        _lib.ptr(block.col), _lib.ptr(t.rowptr), _lib.ptr(t.col), N, bptr(i + 1),
+                        bptr(i), K, red, _lib.ptr(h_in), h_in.stride(0), _lib.ptr(agg),
+                        agg.stride(0), _lib.ptr(dh), dh.stride(0), int(i == 0), _lib.ptr(gws),
+                        gws.numel(), stream)
+                _lib.check(rc, "ngnn_sage_dgrad_gather")
+            else:
+                with _timing.span("sage_dgrad_scatter", 0, 0):
+                    rc = lib.ngnn_sage_dgrad_scatter(
+                        _lib.ptr(dg), 2 * K, _lib.ptr(dg) + 4 * K, 2 * K, _lib.ptr(block.rowptr),
+                        _lib.ptr(block.col), N, bptr(i + 1), bptr(i), K, red, _lib.ptr(h_in),
+                        h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(dh), dh.stride(0),
+                        int(i == 0), stream)
+                _lib.check(rc, "ngnn_sage_dgrad_scatter")
             dy = dh
         dx = dy if (need_dx and L > 0) else None
         return (dx, None, None, None, None, *grads)

@@ -153,6 +153,39 @@ def test_stack_fwd_bwd_matches_oracle(layers, aggr, train):
         torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
 
 
+@pytest.mark.parametrize("aggr", ["mean", "max"])
+def test_stack_deterministic_mode(aggr):
+    """torch.use_deterministic_algorithms(True) switches the input-gradient
+    scatter to the source-grouped CSR gather: same values as the oracle, and
+    bitwise identical across runs."""
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=5, scale=0.005)
+    b = sample_block(graph, graph.train_idx[:128], [8, 5, 3], seed=6)
+    torch.manual_seed(1)
+    mine = ngnn.SAGE(100, 64, 47, 3, dropout=0.5, aggr=aggr).to(DEV).eval()
+    ref = pyg_ref.SAGE(100, 64, 47, 3, dropout=0.5, aggr=aggr).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        runs = []
+        for _ in range(2):
+            mine.zero_grad()
+            x = b.x.clone().requires_grad_(True)
+            out = mine(x, b.edge_index)
+            F.cross_entropy(out[:b.batch_size], b.y[:b.batch_size]).backward()
+            runs.append([x.grad.clone()] + [p.grad.clone() for p in mine.parameters()])
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    for a, c in zip(runs[0], runs[1]):
+        assert torch.equal(a, c)
+    xr = b.x.cpu().clone().requires_grad_(True)
+    F.cross_entropy(ref(xr, b.edge_index.cpu())[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
+    torch.testing.assert_close(runs[0][0].cpu(), xr.grad, **GRAD)
+    for g, (k, q) in zip(runs[0][1:], ref.named_parameters()):
+        torch.testing.assert_close(g.cpu(), q.grad, **WGRAD, msg=k)
+
+
 def test_stack_full_output_gradient():
     """Gradient on EVERY output row (no seed slicing): the bound R = N path."""
     N = 400

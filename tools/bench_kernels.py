@@ -1,0 +1,72 @@
+"""Micro-benchmark of the fused SAGE kernels on one products-[15,10] block.
+
+Times (HIP events, median of --reps) the forward layer kernel in several
+modes to separate gather, GEMM, epilogue and dropout costs, plus the
+backward pieces.  Run on the GPU box:
+
+    python tools/bench_kernels.py [--reps 20] [--scale 1.0]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "noise-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(3):
+        fn()
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3)
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--scale", type=float, default=1.0)
+    a = ap.parse_args()
+    from ngnn.block import Block
+    from ngnn.fused import sage_layer_fwd
+    from ngnn.loader import sample_block, synthetic_graph
+    dev = torch.device("cuda:0")
+    g = synthetic_graph("ogbn-products", dev, seed=0, scale=a.scale)
+    b = sample_block(g, g.train_idx[:1024], [15, 10], seed=1)
+    N, E = b.num_nodes, b.edge_index.shape[1]
+    blk = Block(b.edge_index, N)
+    empty = Block(torch.empty(2, 0, dtype=torch.long, device=dev), N)
+    res = {"N": N, "E": E, "n_active": b.n_id.numel()}
+    torch.manual_seed(0)
+    for (K, Fo) in [(100, 256), (256, 47)]:
+        x = torch.randn(N, K, device=dev)
+        wl = torch.randn(Fo, K, device=dev) * 0.1
+        wr = torch.randn(Fo, K, device=dev) * 0.1
+        bl = torch.randn(Fo, device=dev)
+        agg = torch.empty(N, K, device=dev)
+        tag = f"K{K}_F{Fo}"
+        res[tag + "_full_drop"] = timeit(lambda: sage_layer_fwd(x, blk, "mean", wl, bl, wr, True, 0.5, 7, agg), a.reps)
+        res[tag + "_full"] = timeit(lambda: sage_layer_fwd(x, blk, "mean", wl, bl, wr, True, 0.0, 7, agg), a.reps)
+        res[tag + "_noagg_out"] = timeit(lambda: sage_layer_fwd(x, blk, "mean", wl, bl, wr, True, 0.0, 7), a.reps)
+        res[tag + "_root_only"] = timeit(lambda: sage_layer_fwd(x, empty, "mean", wl, bl, wr, False, 0.0, 7), a.reps)
+        # pure-copy roofline reference: read x + write out
+        out = torch.empty(N, Fo, device=dev)
+        res[tag + "_torch_copy_x"] = timeit(lambda: x.clone(), a.reps)
+        res[tag + "_torch_mm_root"] = timeit(lambda: torch.mm(x, wr.t(), out=out), a.reps)
+        res[tag + "_gflop_root"] = 2 * N * K * Fo / 1e9
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
