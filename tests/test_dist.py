@@ -1,0 +1,91 @@
+"""Seed-node data parallelism on CPU with the gloo backend, world_size 2.
+
+Checks the two pieces of ngnn.distributed the GPU path uses unchanged:
+shard_seeds (same permutation on every rank, disjoint strided slices) and
+GradAllReduce (one flat bucket, SUM / world).  The model here is the oracle
+SAGE on CPU (the product kernels need a GPU); the all-reduce logic is
+device-agnostic.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from ngnn.distributed import GradAllReduce, init, shard_seeds
+        from oracle import pyg_ref
+        r, w, _ = init(backend="gloo")
+        assert (r, w) == (rank, world)
+        # sharding
+        nodes = torch.arange(1000)
+        mine = shard_seeds(nodes, rank, world, epoch=3, seed=11)
+        gathered = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        allseeds = torch.cat(gathered)
+        ok_shard = bool(torch.equal(allseeds.sort().values, nodes))
+        # gradient all-reduce == mean of per-rank gradients
+        torch.manual_seed(0)
+        model = pyg_ref.SAGE(6, 8, 3, 2, dropout=0.0)
+        g = torch.Generator().manual_seed(100)
+        data = [(torch.randn(20, 6, generator=g), torch.randint(0, 20, (2, 60), generator=g),
+                 torch.randint(0, 3, (20,), generator=g)) for _ in range(world)]
+        local_grads = []
+        for (x, ei, y) in data:
+            model.zero_grad()
+            torch.nn.functional.cross_entropy(model(x, ei)[:5], y[:5]).backward()
+            local_grads.append([p.grad.clone() for p in model.parameters()])
+        want = [sum(gs) / world for gs in zip(*local_grads)]
+        model.zero_grad()
+        x, ei, y = data[rank]
+        torch.nn.functional.cross_entropy(model(x, ei)[:5], y[:5]).backward()
+        GradAllReduce(model.parameters())()
+        ok_grad = all(torch.allclose(p.grad, w_, atol=1e-6) for p, w_ in
+                      zip(model.parameters(), want))
+        q.put((rank, ok_shard, ok_grad, mine.numel()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        q.put((rank, False, False, repr(e)))
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_sharding_and_grad_allreduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    res.sort()
+    assert all(r[1] for r in res), res
+    assert all(r[2] for r in res), res
+    assert sum(r[3] for r in res) == 1000
+
+
+def test_shard_seeds_single_process():
+    from ngnn.distributed import shard_seeds
+    nodes = torch.arange(10)
+    a = shard_seeds(nodes, 0, 3, epoch=0, seed=1)
+    b = shard_seeds(nodes, 1, 3, epoch=0, seed=1)
+    c = shard_seeds(nodes, 2, 3, epoch=0, seed=1)
+    assert torch.equal(torch.cat([a, b, c]).sort().values, nodes)
+    assert not torch.equal(shard_seeds(nodes, 0, 1, epoch=0, seed=1),
+                           shard_seeds(nodes, 0, 1, epoch=1, seed=1))
