@@ -139,6 +139,7 @@ def main():
             b = batches[(args.warmup + i) % nb]
             train_step(model, opt, reducer, b)
             edges += layers * b.edge_index.shape[1]
+    t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt, float(edges)], dtype=torch.float64, device=dev)
@@ -203,6 +204,7 @@ def main():
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
                        "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},
+            "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 4),
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
             "epoch_batches_per_rank": len(loader),
             "roofline": roof,

@@ -34,10 +34,23 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 struct Dropout {
     uint32_t s0, s1, thresh;  // thresh == 0: no dropout; > 2^24: drop all
     float scale;
-    __device__ __forceinline__ uint32_t row_key(uint32_t row) const { return lowbias32(row ^ s0); }
-    __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
-        return (lowbias32(lowbias32(rkey + col) ^ s1) >> 8) >= thresh;
+    // one hash per row (seed-mixed), one per element: rkey + col are distinct
+    // within a row and lowbias32 is a bijection
+    __device__ __forceinline__ uint32_t row_key(uint32_t row) const {
+        return lowbias32(row ^ s0) ^ s1;
     }
+    __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
+        return (lowbias32(rkey + col) >> 8) >= thresh;
+    }
+};
+
+// Layer epilogue: bias, optional ReLU, optional dropout; col_base = global
+// column of the launch's column 0 (the dropout key is the global column).
+struct Epi {
+    const float *bias;
+    int relu;
+    Dropout drop;
+    int col_base;
 };
 
 inline Dropout make_dropout(float p, uint64_t seed) {
@@ -59,5 +72,13 @@ inline Dropout make_dropout(float p, uint64_t seed) {
     }
     return d;
 }
+
+// Row-tile forward (ngnn_sage_rt.hip): returns 1 (launch status in *rc) when
+// it takes the call, 0 when the shape is outside its envelope.
+int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+                     int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
+                     int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
+                     float *agg_out, int64_t ld_agg, hipStream_t st, int *rc);
 
 }  // namespace ngnn

@@ -39,13 +39,6 @@ namespace {
 constexpr int BM = kBM, KC = kKC, LDA = kLDA;
 constexpr int LPR = 32;  // lanes per row in the gather
 
-struct Epi {
-    const float *bias;
-    int relu;
-    Dropout drop;
-    int col_base;  // global column of this launch's column 0 (dropout key)
-};
-
 // Optional modes (all off when the pointers are NULL):
 //   n_rows_dev : effective row count = min(n_rows, *n_rows_dev), read on the
 //                device (backward passes whose row bound is never on the host)
@@ -481,6 +474,13 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
     if (n_rows == 0) return NGNN_OK;
     NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
+    if (!xmask) {  // default path: the row-tile kernel (ngnn_sage_rt.hip)
+        int rc = NGNN_OK;
+        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl_packed,
+                             wr_packed, bias, Fo, out, ldo, relu, p_drop, seed, agg_out, ld_agg,
+                             as_stream(stream), &rc))
+            return rc;
+    }
     const int vec_in = (K % 4 == 0) && (ldx % 4 == 0) && aligned(x, 16) &&
                        (!xmask || ((ldm % 4 == 0) && aligned(xmask, 16)));
     const int KG = static_cast<int>(ceil_div(K, 16));

@@ -1,0 +1,570 @@
+// Row-tile fused SAGEConv layer forward for gfx950 (the default forward path
+// of ngnn_sage_fwd whenever the packed W_r fits in LDS).
+//
+// Same contract as the 64-row kernel in ngnn_sage.hip (one SAGEConv layer of
+// sage.py:33-39: out = act(b + x W_r^T + [deg>0] agg(x) W_l^T), relu, hash
+// dropout), re-decomposed for the MFMA / store-issue balance that kernel's
+// ablation showed (profiles/ablation_r01: its dword-store epilogue alone ran
+// at 1.85 TB/s, and the MFMA loop at ~55 % of the f32 MFMA rate):
+//
+//   * one 512-thread workgroup per CU, persistent; W_r (and W_l when both
+//     fit) is copied ONCE per workgroup into LDS in fragment order (the
+//     ngnn_pack_weight layout), bias too;
+//   * each wave owns 16-row tiles: tile t -> workgroup t % G, wave
+//     (t / G) % 8, so consecutive tiles (NeighborLoader puts every row with
+//     in-edges first) spread over all CUs and both waves of a SIMD;
+//   * MFMA operands are swapped w.r.t. the 64-row kernel: A = W (16 output
+//     features from LDS, one ds_read_b128 = 4 k-steps), B = x (16 graph rows
+//     straight from HBM into registers, no LDS staging, no barrier), so each
+//     lane ends with 4 CONSECUTIVE output features of one row -> 16-B stores;
+//   * the next tile's x fragments are prefetched before the current tile's
+//     MFMAs; W fragments for the next k-step are read before the current
+//     k-step's MFMAs (two register sets);
+//   * tiles whose rows have in-edges gather the aggregate into registers in
+//     the same lane layout (per column, edge order, then / max(deg,1): the
+//     fp32 sequence of ngnn_seg_agg_fwd, so the aggregate is bit-identical),
+//     neighbour indices preloaded 16 per row and broadcast by ds_bpermute.
+//
+// Bytes per launch: 4*(N*K + E*K + E + N + 1 + N*F_out) (x, gathered rows,
+// col, rowptr, out) + the optional saved aggregate; flops 2*N*K*F_out +
+// 2*N_edge_rows*K*F_out.
+#include <cstdlib>
+
+#include "ngnn_device.h"
+
+namespace ngnn {
+// raw buffer intrinsics (LLVM names; declared outside the anonymous namespace)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ v4f buf_load4(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ void buf_store4(v4f v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
+__device__ void buf_store1(float v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
+
+namespace {
+
+constexpr int RT_ROWS = 16;  // rows per wave tile (one MFMA n-tile)
+constexpr int RT_KC = 8;     // k-groups of 16 per chunk (128 columns of K)
+// waves per workgroup: 2 per SIMD (<= 256 VGPRs: accumulators, the current
+// and the prefetched x fragments, two W fragment sets)
+constexpr int rt_waves(int) { return 8; }
+
+struct RtArgs {
+    const float *x;
+    int64_t ldx;
+    int K, KG;  // KG = ceil(K / 16)
+    int n_rows;
+    const int32_t *n_rows_dev;
+    const int32_t *rowptr;
+    const int32_t *col;
+    const v4f *wl;  // packed [NT][KG][64] or NULL (no neighbour term)
+    const v4f *wr;  // packed [NT][KG][64]
+    int NT, Fo;
+    float *out;
+    int64_t ldo;
+    int vec_out;
+    float *agg_out;
+    int64_t ld_agg;
+    Epi epi;
+    uint32_t x_bytes, out_bytes, agg_bytes;  // buffer-resource ranges (all < 4 GiB)
+    int dbg;  // ablation bits (NGNN_SAGE_ABLATE, profiling only): 1 no MFMA, 2 no stores, 4 no x loads,
+             // 8 no epilogue, 16 no weight prologue
+};
+
+// -1 (all ones) when a < b, else 0: a lane mask held in a VGPR, built without
+// a compare (no SGPR lane-mask pairs to keep live across the tile loop).
+// Operands stay far from overflow (|a - b| < 2^31).
+__device__ __forceinline__ int lt_mask(int a, int b) { return (a - b) >> 31; }
+
+__device__ __forceinline__ v4f and_mask(v4f v, int m) {
+    v4f o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __int_as_float(__float_as_int(v[i]) & m);
+    return o;
+}
+
+// Raw buffer access (gfx9 buffer resource: 64-bit base, byte range, stride
+// 0).  Loads past the range return 0 and stores past it are dropped, so rows
+// beyond n_rows and padded neighbour slots need no lane predicates; the byte
+// offset is one VGPR and the per-k-group step an immediate.
+
+__device__ __forceinline__ i32x4 make_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    i32x4 r;
+    r.x = static_cast<int>(static_cast<uint32_t>(a));
+    r.y = static_cast<int>(static_cast<uint32_t>(a >> 32));
+    r.z = static_cast<int>(bytes);
+    r.w = 0x00020000;
+    return r;
+}
+constexpr int kOOB = 0x7ffffff0;  // byte offset past every range: load 0 / drop
+
+// x fragments of one 128-column chunk: lane (rl, q) holds
+// x[r][k0 + 16 g + 4 q .. +3]; rows past n_rows read 0 (buffer range).
+// Columns past K (which read the next row) are masked by mask_x at the point
+// of USE, not here: masking right after the loads would make the compiler
+// wait for a prefetch the moment it is issued.
+__device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], const RtArgs &a, i32x4 xr, int r, int k0,
+                                       int q) {
+    const int voff = (r * static_cast<int>(a.ldx) + k0 + 4 * q) * 4;
+#pragma unroll
+    for (int g = 0; g < RT_KC; ++g) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+}
+
+__device__ __forceinline__ void mask_x(v4f (&xc)[RT_KC], const v4f (&xf)[RT_KC], const RtArgs &a,
+                                       int k0, int q) {
+    const int kq = a.K - k0 - 4 * q;  // columns left for this lane's 4-wide slot
+#pragma unroll
+    for (int g = 0; g < RT_KC; ++g) xc[g] = and_mask(xf[g], lt_mask(16 * g, kq));
+}
+
+// W fragment loads for k-group kg, m-tiles [p*H, p*H + H).
+// LDS image: k-group major, [KG][NTW][64] v4f, so for a fixed chunk every
+// (g, m) offset is a compile-time immediate off one per-chunk base (no
+// per-fragment address registers); reads past the image (k-groups beyond a
+// short last chunk, whose MFMAs are skipped) return LDS garbage or 0, never
+// fault.  Global (W_l that does not fit): the packed [NT][KG][64] layout,
+// k-group clamped and padded tiles re-read a valid one (never stored).
+template <int NTW, int H, bool LDSW>
+__device__ __forceinline__ void load_w(v4f (&w)[H], const v4f *__restrict__ wsrc, int KG, int kg,
+                                       int p, int NT, int lane) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        const int m = p * H + h;
+        if (LDSW)
+            w[h] = wsrc[(kg * NTW + m) * 64 + lane];
+        else
+            w[h] = wsrc[(static_cast<int64_t>(min(m, NT - 1)) * KG + min(kg, KG - 1)) * 64 + lane];
+    }
+}
+
+template <int NTW, bool LDSW>
+__device__ __forceinline__ void mfma_chunk_rt(v4f (&acc)[NTW], const v4f (&xf)[RT_KC],
+                                              const v4f *__restrict__ wsrc, int KG, int kg0,
+                                              int nkg, int NT, int lane) {
+    constexpr int P = NTW >= 8 ? NTW / 4 : 1;
+    constexpr int H = NTW / P;
+    v4f wb[2][H];
+    load_w<NTW, H, LDSW>(wb[0], wsrc, KG, kg0, 0, NT, lane);
+#pragma unroll
+    for (int s = 0; s < RT_KC * P; ++s) {
+        const int g = s / P, p = s % P;
+        const int sn = s + 1, gn = sn / P, pn = sn % P;
+        if (sn < RT_KC * P) load_w<NTW, H, LDSW>(wb[sn & 1], wsrc, KG, kg0 + gn, pn, NT, lane);
+        if (g < nkg) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int h = 0; h < H; ++h)
+                    acc[p * H + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[s & 1][h][i], xf[g][i],
+                                                                          acc[p * H + h], 0, 0, 0);
+        }
+    }
+}
+
+// max of v over the 16 lanes of row-group 0 (every row-group holds the same
+// 16 row values here): 4 DPP row shifts, no LDS round trips
+__device__ __forceinline__ int rowgroup_max16(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));  // row_shr:8
+    return __builtin_amdgcn_readlane(v, 15);
+}
+
+template <int RED>
+__device__ __forceinline__ float red_op(float acc, float v) {
+    return (RED == NGNN_REDUCE_MAX) ? nanmax(acc, v) : acc + v;
+}
+
+// aggregate of rows r over columns [k0, k0 + 16 nkg) into ag (same lane
+// layout as load_x).  cb: this lane's 4 preloaded neighbour indices
+// (lane (rl, q) holds neighbours 4q..4q+3 of its row within the current
+// 16-neighbour window).
+template <int RED>
+__device__ __forceinline__ v4f red_mask(v4f v, int m) {
+    // masked slots contribute the reduction's identity: +0.0 for sum (the
+    // running sum starts at +0.0, so it is never -0.0 and s + 0.0 == s
+    // bitwise), -inf for max (nanmax(s, -inf) == s)
+    if (RED == NGNN_REDUCE_MAX) {
+        v4f o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            o[i] = __int_as_float((__float_as_int(v[i]) & m) | (~m & static_cast<int>(0xff800000u)));
+        return o;
+    }
+    return and_mask(v, m);
+}
+
+// aggregate of row r over columns [k0, k0 + 128) into ag (same lane layout
+// as load_x).  Neighbour indices are preloaded 16 per row (lane (rl, q)
+// holds neighbours e0 + 4q .. +3 of its row) and broadcast by ds_bpermute;
+// two neighbours' fragments are in flight at a time.  Per column the
+// reduction runs in edge order from the identity, then / max(deg, 1) for
+// mean: the fp32 sequence of ngnn_seg_agg_fwd.  Padded slots point past the
+// buffer range (read 0 = the sum identity; max masks them to -inf).
+// Columns past K accumulate garbage from the next row and are zeroed at the
+// end.
+template <int RED>
+__device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, i32x4 xr, int beg,
+                                             int deg, int maxdeg, int k0, int nkg, int rl, int q) {
+    const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
+#pragma unroll
+    for (int g = 0; g < RT_KC; ++g) ag[g] = v4f{ident, ident, ident, ident};
+    const int kofs = (k0 + 4 * q) * 4;
+    const int ld4 = static_cast<int>(a.ldx) * 4;
+#pragma unroll 1
+    for (int e0 = 0; e0 < maxdeg; e0 += 16) {
+        int cb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = e0 + 4 * q + j;
+            cb[j] = a.col[(beg + e) & lt_mask(e, deg)];  // invalid slots read col[0]
+        }
+        const int ne = min(16, maxdeg - e0);
+#pragma unroll 1  // one neighbour pair in flight: keep the register budget
+        for (int e4 = 0; 4 * e4 < ne; ++e4) {
+            const int srcl = rl + 16 * e4;
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+                const int e = e0 + 4 * e4 + j;
+                const int m0 = lt_mask(e, deg), m1 = lt_mask(e + 1, deg);
+                const int o0 = m0 ? __shfl(cb[j], srcl) * ld4 + kofs : kOOB;
+                const int o1 = m1 ? __shfl(cb[j + 1], srcl) * ld4 + kofs : kOOB;
+                // all 8 k-groups unconditionally (conditional writes into the
+                // fragment arrays make the compiler copy them whole); groups
+                // past K read the next row or 0 and are zeroed at the end
+                v4f v0[RT_KC], v1[RT_KC];
+#pragma unroll
+                for (int g = 0; g < RT_KC; ++g) {
+                    v0[g] = buf_load4(xr, o0 + 64 * g, 0, 0);
+                    v1[g] = buf_load4(xr, o1 + 64 * g, 0, 0);
+                }
+#pragma unroll
+                for (int g = 0; g < RT_KC; ++g) {
+                    {
+                        v4f w0 = v0[g], w1 = v1[g];
+                        if (RED == NGNN_REDUCE_MAX) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                w0[i] = __int_as_float((__float_as_int(w0[i]) & m0) |
+                                                       (~m0 & static_cast<int>(0xff800000u)));
+                                w1[i] = __int_as_float((__float_as_int(w1[i]) & m1) |
+                                                       (~m1 & static_cast<int>(0xff800000u)));
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            ag[g][i] = red_op<RED>(ag[g][i], w0[i]);
+                            ag[g][i] = red_op<RED>(ag[g][i], w1[i]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // finalize: mean divides once (as scatter mean); max of nothing -> 0;
+    // columns past K exactly 0 (the W padding is 0 too)
+    const float dv = static_cast<float>(deg > 1 ? deg : 1);
+    const int mdeg = lt_mask(0, deg);
+    const int kq = a.K - k0 - 4 * q;
+#pragma unroll
+    for (int g = 0; g < RT_KC; ++g) {
+        v4f v = ag[g];
+        if (RED == NGNN_REDUCE_MEAN) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v[i] / dv;
+        }
+        ag[g] = and_mask(v, (RED == NGNN_REDUCE_MAX ? mdeg : -1) & lt_mask(16 * g, kq));
+    }
+}
+
+// epilogue: lane holds output features m*16 + 4q .. +3 of row r.  Stores go
+// through a buffer resource (rows past n_rows are dropped by the range);
+// `vec` (uniform): F_out a multiple of 16 with 16-B aligned rows -- one
+// 16-B store per m-tile, no per-lane predicates.
+template <int NTW, bool DROP>
+__device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
+                                         const float *sbias, int r, bool vec, int q) {
+    // relu through a wave-uniform select; dropout (hash per element) only in
+    // the DROP instantiation
+    const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) : 0u;
+    const int obase = r * static_cast<int>(a.ldo) * 4;
+    const bool relu = a.epi.relu;
+#pragma unroll
+    for (int m = 0; m < NTW; ++m) {
+        if (m >= a.NT) continue;  // padded tiles (uniform)
+        const int f = m * 16 + 4 * q;
+        const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
+        v4f v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float y = acc[m][j] + b[j];
+            y = (relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
+            if (DROP)
+                y = a.epi.drop.keep(rk, static_cast<uint32_t>(a.epi.col_base + f + j))
+                        ? y * a.epi.drop.scale
+                        : 0.0f;
+            v[j] = y;
+        }
+        if (a.dbg & 2) {
+            if (v[0] == 12345.f) buf_store1(v[1], orsrc, obase, 0, 0);  // keep the math alive
+        } else if (vec) {
+            buf_store4(v, orsrc, obase + 4 * f, 0, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                buf_store1(v[j], orsrc, f + j < a.Fo ? obase + 4 * (f + j) : kOOB, 0, 0);
+        }
+    }
+}
+
+template <int NTW, int RED, bool WL_LDS>
+__global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
+    constexpr int RT_WAVES = rt_waves(NTW);
+    extern __shared__ __attribute__((aligned(16))) v4f lds[];
+    const int nfr = NTW * a.KG * 64;  // fragments per weight matrix (NTW tiles, zero padded)
+    v4f *swr = lds;
+    v4f *swl = lds + nfr;
+    float *sbias = reinterpret_cast<float *>(lds + (WL_LDS ? 2 : 1) * nfr);
+    const int have_l = a.wl != nullptr;
+    {
+        // weights -> LDS by LDS-DMA, 1 KiB (one n-tile x k-group fragment)
+        // per wave-instruction, all in flight at once; padding tiles zeroed
+        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        const int nch = (a.dbg & 16) ? 0 : a.NT * a.KG;  // valid 1-KiB chunks per matrix
+        for (int c = wv; c < nch; c += RT_WAVES) {
+            const int m = c / a.KG, kg = c - m * a.KG;  // packed [NT][KG] -> LDS [KG][NTW]
+            const int d = (kg * NTW + m) * 64;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(a.wr + c * 64 + ln),
+                (__attribute__((address_space(3))) void *)(swr + d), 16, 0, 0);
+            if (WL_LDS && have_l)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.wl + c * 64 + ln),
+                    (__attribute__((address_space(3))) void *)(swl + d), 16, 0, 0);
+        }
+        const v4f z{0.f, 0.f, 0.f, 0.f};
+        const int npad = (NTW - a.NT) * 64;  // padded tiles of every k-group
+        for (int i = threadIdx.x; i < a.KG * npad; i += RT_WAVES * 64) {
+            const int kg = i / npad, j = i - kg * npad;
+            swr[kg * NTW * 64 + a.NT * 64 + j] = z;
+            if (WL_LDS) swl[kg * NTW * 64 + a.NT * 64 + j] = z;
+        }
+        if (WL_LDS && !have_l)
+            for (int i = threadIdx.x; i < nfr; i += RT_WAVES * 64) swl[i] = z;
+        for (int i = threadIdx.x; i < NTW * 16; i += RT_WAVES * 64)
+            sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] : 0.0f;
+    }
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = lane >> 4, rl = lane & 15;
+    int n_rows = a.n_rows;
+    if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
+    const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
+    const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
+    const int tstride = gridDim.x * RT_WAVES;
+
+    int t = blockIdx.x + gridDim.x * wave;
+    if ((a.dbg & 32) && wave >= RT_WAVES / 2) __builtin_amdgcn_s_sleep(100);  // experiment: stagger SIMD partners
+    // next tile's chunk-0 x fragments and row bounds, loaded one tile ahead,
+    // unconditionally (a tile past the end re-reads tile 0: valid, unused)
+    v4f xn[RT_KC];
+#pragma unroll
+    for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
+    int nbeg = 0, nend = 0;
+    const i32x4 xr = make_rsrc(a.x, a.x_bytes);
+    const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
+    auto prefetch = [&](int tn) {
+        const int rn = (tn < n_tiles ? tn : 0) * RT_ROWS + rl;
+        if (!(a.dbg & 4)) load_x(xn, a, xr, rn, 0, q);
+        if (have_l) {
+            const int mr = lt_mask(rn, n_rows);
+            const int rr = rn & mr;
+            nbeg = a.rowptr[rr];
+            nend = a.rowptr[rr + 1];
+            nend = nbeg + ((nend - nbeg) & mr);  // rows past the end: degree 0
+        }
+    };
+    const bool vec = a.vec_out && (a.Fo == a.NT * 16);
+    prefetch(t);
+    for (; t < n_tiles; t += tstride) {
+        const int r = t * RT_ROWS + rl;
+        const int beg = nbeg, deg = nend - nbeg;
+        const int maxdeg = have_l ? rowgroup_max16(deg) : 0;
+        v4f acc[NTW];
+#pragma unroll
+        for (int m = 0; m < NTW; ++m) acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
+
+        // ---- root term: x[r] . W_r^T, chunk by chunk; chunk c+1 (or, in the
+        // last chunk, the next tile's chunk 0 and row bounds) loads behind
+        // chunk c's MFMAs
+        for (int c = 0; c < nchunk; ++c) {
+            v4f xc[RT_KC];
+            mask_x(xc, xn, a, c * RT_KC * 16, q);
+            const int nkg = min(RT_KC, a.KG - c * RT_KC);
+            if (c + 1 < nchunk) {
+                if (!(a.dbg & 4)) load_x(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
+            } else {
+                prefetch(t + tstride);  // next tile: a whole tile of MFMAs to land
+            }
+            if (!(a.dbg & 1)) mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
+        }
+
+        // ---- neighbour term (tiles with in-edges only)
+        if (maxdeg > 0) {
+            const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
+            for (int c = 0; c < nchunk; ++c) {
+                const int k0 = c * RT_KC * 16;
+                const int nkg = min(RT_KC, a.KG - c * RT_KC);
+                v4f ag[RT_KC];
+                gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q);
+                if (a.agg_out) {
+                    const int kq = a.K - k0 - 4 * q;
+                    const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
+#pragma unroll
+                    for (int g = 0; g < RT_KC; ++g)
+                        if (g < nkg) buf_store4(ag[g], ar, 16 * g < kq ? aoff + 64 * g : kOOB, 0, 0);
+                }
+                if constexpr (WL_LDS)
+                    mfma_chunk_rt<NTW, true>(acc, ag, swl, a.KG, c * RT_KC, nkg, a.NT, lane);
+                else
+                    mfma_chunk_rt<NTW, false>(acc, ag, a.wl, a.KG, c * RT_KC, nkg, a.NT, lane);
+            }
+        }
+
+        // ---- epilogue (bias, relu, dropout and the stores)
+        if (!(a.dbg & 8)) {
+            if (a.epi.drop.thresh)
+                epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q);
+            else
+                epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q);
+        }
+    }
+}
+
+int g_num_cus[64];
+
+int num_cus() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    if (!g_num_cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        g_num_cus[dev] = n;
+    }
+    return g_num_cus[dev];
+}
+
+template <int NTW, int RED, bool WL_LDS>
+int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
+    auto fn = k_sage_rt<NTW, RED, WL_LDS>;
+    static bool attr_set = false;  // benign race: idempotent
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    constexpr int W = rt_waves(NTW);
+    const int grid = static_cast<int>(
+        std::max<int64_t>(1, std::min<int64_t>(num_cus(), ceil_div(n_tiles, W))));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(W * 64), lds_bytes, st, a);
+    return launch_status();
+}
+
+template <int NTW>
+int dispatch_red(const RtArgs &a, int reduce, bool wl_lds, int n_tiles, size_t lds, hipStream_t st) {
+    if (reduce == NGNN_REDUCE_MEAN)
+        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MEAN, true>(a, n_tiles, lds, st)
+                      : launch_rt<NTW, NGNN_REDUCE_MEAN, false>(a, n_tiles, lds, st);
+    if (reduce == NGNN_REDUCE_SUM)
+        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_SUM, true>(a, n_tiles, lds, st)
+                      : launch_rt<NTW, NGNN_REDUCE_SUM, false>(a, n_tiles, lds, st);
+    return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MAX, true>(a, n_tiles, lds, st)
+                  : launch_rt<NTW, NGNN_REDUCE_MAX, false>(a, n_tiles, lds, st);
+}
+
+}  // namespace
+
+// Returns 1 and stores the launch status in *rc when the row-tile kernel
+// takes this call, 0 when the shape is outside its envelope (the caller then
+// runs the 64-row kernel).  Envelope: no input mask, K % 4 == 0 with 16-B
+// aligned rows, packed W_r of one column slice fitting in LDS.  Outputs wider
+// than one slice (<= 256 columns, fewer when K is large) run as one launch
+// per slice; the packed weights are n-tile major, so a slice is a contiguous
+// sub-array.
+int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+                     int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
+                     int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
+                     float *agg_out, int64_t ld_agg, hipStream_t st, int *rc) {
+    static const bool off = getenv("NGNN_NO_ROWTILE") != nullptr;
+    if (off) return 0;
+    if (K % 4 != 0 || ldx % 4 != 0 || !aligned(x, 16)) return 0;
+    if (agg_out && (ld_agg % 4 != 0 || !aligned(agg_out, 16))) return 0;
+    // byte offsets are 32-bit (buffer resources): every buffer < 2 GiB
+    const int64_t lim = (int64_t(1) << 31) - 4096;
+    if (n_rows * ldx * 4 > lim || n_rows * ldo * 4 > lim || (agg_out && n_rows * ld_agg * 4 > lim))
+        return 0;
+    const int KG = static_cast<int>(ceil_div(K, 16));
+    const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one m-tile, all of K
+    const size_t lds_cap = 160 * 1024 - 1024;                          // minus the bias slice
+    // widest supported tile count whose W_r fits
+    int ntw_max = 0;
+    for (int c : {16, 8, 4, 3, 2})
+        if (static_cast<size_t>(c) * frag_kb <= lds_cap) {
+            ntw_max = c;
+            break;
+        }
+    if (ntw_max == 0) return 0;
+    const int64_t slice = 16 * static_cast<int64_t>(ntw_max);
+    const Dropout drop = make_dropout(p_drop, seed);
+    for (int64_t c0 = 0; c0 < Fo; c0 += slice) {
+        const int64_t Fo_c = std::min<int64_t>(slice, Fo - c0);
+        const int NT = static_cast<int>(ceil_div(Fo_c, 16));
+        const int NTW = NT <= 2 ? 2 : NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 8 ? 8 : 16;
+        const size_t wbytes = static_cast<size_t>(NTW) * frag_kb;
+        const size_t bbytes = static_cast<size_t>(NTW) * 16 * sizeof(float);
+        // W_l shares the LDS when both fit; otherwise its fragments stream from L2
+        const bool wl_lds = wl_packed == nullptr || 2 * wbytes + bbytes <= lds_cap + 1024;
+        const size_t lds = (wl_lds ? 2 : 1) * wbytes + bbytes;
+        const int64_t toff = (c0 / 16) * KG * 64;
+        RtArgs a;
+        a.x = x;
+        a.ldx = ldx;
+        a.K = static_cast<int>(K);
+        a.KG = KG;
+        a.n_rows = static_cast<int>(n_rows);
+        a.n_rows_dev = n_rows_dev;
+        a.rowptr = rowptr;
+        a.col = col;
+        a.wl = wl_packed ? static_cast<const v4f *>(wl_packed) + toff : nullptr;
+        a.wr = static_cast<const v4f *>(wr_packed) + toff;
+        a.NT = NT;
+        a.Fo = static_cast<int>(Fo_c);
+        a.out = out + c0;
+        a.ldo = ldo;
+        a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(out + c0, 16);
+        a.agg_out = c0 == 0 ? agg_out : nullptr;
+        a.ld_agg = ld_agg;
+        a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
+        static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
+        a.dbg = dbg;
+        a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
+        a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
+        a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
+        const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
+        switch (NTW) {
+            case 2: *rc = dispatch_red<2>(a, reduce, wl_lds, n_tiles, lds, st); break;
+            case 3: *rc = dispatch_red<3>(a, reduce, wl_lds, n_tiles, lds, st); break;
+            case 4: *rc = dispatch_red<4>(a, reduce, wl_lds, n_tiles, lds, st); break;
+            case 8: *rc = dispatch_red<8>(a, reduce, wl_lds, n_tiles, lds, st); break;
+            default: *rc = dispatch_red<16>(a, reduce, wl_lds, n_tiles, lds, st); break;
+        }
+        if (*rc) return 1;
+    }
+    return 1;
+}
+
+}  // namespace ngnn

@@ -40,8 +40,8 @@ def dropout_keep(seed, n_rows, n_cols, p):
     thresh = math.ceil(float(np.float32(p)) * 16777216.0)
     r = np.arange(n_rows, dtype=np.uint64)[:, None]
     c = np.arange(n_cols, dtype=np.uint64)[None, :]
-    rk = _lowbias32(r ^ s0)
-    h = _lowbias32(_lowbias32((rk + c) & M32) ^ s1)
+    rk = _lowbias32(r ^ s0) ^ s1
+    h = _lowbias32((rk + c) & M32)
     return torch.from_numpy((h >> np.uint64(8)) >= np.uint64(thresh))
 
 
