@@ -53,13 +53,19 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python instead of replaying the captured "
+                         "HIP graph of the step")
+    ap.add_argument("--timer", default="sage_fwd",
+                    help="comma list of kernel spans timed with HIP events in the timed region "
+                         "('all', or 'none' for profiler runs)")
     return ap.parse_args()
 
 
 def train_step(model, opt, reducer, b):
     out = model(b.x, b.edge_index)[:b.batch_size]
     loss = F.cross_entropy(out, b.y[:b.batch_size])
-    opt.zero_grad()
+    opt.zero_grad(set_to_none=False)  # keep the grad tensors (a captured graph owns them)
     loss.backward()
     reducer()
     opt.step()
@@ -110,8 +116,9 @@ def main():
     graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
     torch.manual_seed(1234)  # identical init on every rank
     model = ngnn.SAGE(100, args.hidden, 47, layers, dropout=0.5).to(dev)
-    # torch's single-kernel Adam on the device (same update rule as the reference's Adam)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    # torch's single-kernel Adam on the device (same update rule as the reference's Adam);
+    # capturable: its step count lives on the device, so the HIP graph can replay it
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=not args.eager)
     reducer = GradAllReduce(model.parameters())
     model.train()
 
@@ -128,20 +135,51 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    graph = not args.eager
+    if graph:
+        # the whole step (CSR build .. Adam) as one captured HIP graph over a
+        # static slot sized for any block of this fanout (ngnn/graphs.py)
+        from ngnn.graphs import GraphedTrainStep, slot_size
+        n_cap, e_cap = slot_size(args.batch_size, fanout)
+        gstep = GraphedTrainStep(model, opt, args.batch_size, n_cap, e_cap, batches[0].x.size(1), dev,
+                                 reducer=reducer)
+        gstep.capture(batches[0].x, batches[0].edge_index, batches[0].y)
+
+        def run(b):
+            gstep(b.x, b.edge_index, b.y)
+    else:
+        def run(b):
+            train_step(model, opt, reducer, b)
+
     for i in range(args.warmup):
-        train_step(model, opt, reducer, batches[i % nb])
+        run(batches[i % nb])
     barrier()
-    timer = _timing.KernelTimer()
+    timer_names = None if args.timer == "all" else ([] if args.timer == "none" else args.timer.split(","))
+
+    def new_timer():
+        t = _timing.KernelTimer(only=timer_names or ["-"])
+        t.reserve(8 * args.steps if args.timer != "none" else 0)
+        return t
+    # eager: per-launch events inside the timed region; graph: events cannot be
+    # recorded inside a captured graph on ROCm, so the same kernels on the same
+    # batches are timed in an eager pass right after the timed replays
+    timer = new_timer() if not graph else _timing.KernelTimer(only=["-"])
     edges = 0
     t0 = time.perf_counter()
     with timer:
         for i in range(args.steps):
             b = batches[(args.warmup + i) % nb]
-            train_step(model, opt, reducer, b)
+            run(b)
             edges += layers * b.edge_index.shape[1]
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     dt = time.perf_counter() - t0
+    if graph and args.timer != "none":
+        timer = new_timer()
+        with timer:
+            for i in range(args.steps):
+                train_step(model, opt, reducer, batches[(args.warmup + i) % nb])
+        barrier()
     t = torch.tensor([dt, float(edges)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
@@ -168,6 +206,8 @@ def main():
                     "unit": "GB/s", "frac": round(f_hbm, 4)}
         roof.update({
             "traffic": None, "launches": n, "avg_us": round(1e3 * ms / n, 2),
+            "timed_in": "timed region (eager)" if not graph else
+                        "eager pass over the timed batches, right after the graph replays",
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),
             "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
@@ -181,7 +221,7 @@ def main():
         barrier()
         t1 = time.perf_counter()
         for b in loader:
-            train_step(model, opt, reducer, b)
+            run(b)
         barrier()
         epoch_s = time.perf_counter() - t1
 
@@ -205,6 +245,7 @@ def main():
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
                        "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},
             "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 4),
+            "launch": "eager" if not graph else "hip-graph replay (step captured once)",
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
             "epoch_batches_per_rank": len(loader),
             "roofline": roof,

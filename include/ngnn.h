@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 3
+#define NGNN_ABI_VERSION 4
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -140,7 +140,10 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
  *   agg_out     [n_rows, ld_agg]: workgroups whose 64 rows have in-edges also
  *               store those rows' aggregate (saved for the backward);
  *   xmask       stage x * (xmask > 0 ? xscale : 0) instead of x (ReLU/dropout
- *               backward fused into a dgrad GEMM's input).
+ *               backward fused into a dgrad GEMM's input);
+ *   seed_dev    device uint64 XORed into `seed` when the kernel starts, so a
+ *               captured HIP graph draws a fresh dropout mask per replay (the
+ *               graph increments it); NULL = the host seed alone.
  * Replaces PyG SAGEConv.forward [ext] + relu + F.dropout. */
 size_t ngnn_pack_weight_bytes(int64_t Fo, int64_t K);
 int ngnn_pack_weight(const float *w, int64_t ldw, int64_t Fo, int64_t K, void *packed,
@@ -153,8 +156,9 @@ int ngnn_pack_weight_ex(const float *w0, const float *w1, int64_t ldw, int64_t r
 int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col, int reduce,
                   const void *wl_packed, const void *wr_packed, const float *bias, int64_t Fo,
-                  float *out, int64_t ldo, int relu, float p_drop, uint64_t seed, float *agg_out,
-                  int64_t ld_agg, const float *xmask, int64_t ldm, float xscale, void *stream);
+                  float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
+                  const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, const float *xmask,
+                  int64_t ldm, float xscale, void *stream);
 
 /* ------------------------------------------ backward receptive-field bounds
  * ngnn_row_extent: out[0] = max(out[0], 1 + last row of g[n_rows, F] holding a

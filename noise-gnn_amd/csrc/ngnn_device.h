@@ -42,6 +42,10 @@ struct Dropout {
     __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
         return (lowbias32(rkey + col) >> 8) >= thresh;
     }
+    __device__ __forceinline__ void reseed(uint64_t d) {
+        s0 ^= static_cast<uint32_t>(d);
+        s1 ^= static_cast<uint32_t>(d >> 32);
+    }
 };
 
 // Layer epilogue: bias, optional ReLU, optional dropout; col_base = global
@@ -79,6 +83,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
-                     float *agg_out, int64_t ld_agg, hipStream_t st, int *rc);
+                     const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
+                     int *rc);
 
 }  // namespace ngnn

@@ -54,6 +54,7 @@ struct Extra {
     const float *xmask;
     int64_t ldm;
     float xscale;
+    const uint64_t *seed_dev;  // XORed into the dropout seed (HIP-graph replays)
     int dbg;  // ablation switch for profiling (NGNN_SAGE_ABLATE): 0 in normal runs
 };
 
@@ -284,6 +285,7 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
     if (ex.dbg & 8) return;
     const int q = lane >> 4, cl = lane & 15;
     (void)vec_out;
+    if (ex.seed_dev) epi.drop.reseed(*ex.seed_dev);
     uint32_t rk[MTW][4];
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt)
@@ -462,8 +464,9 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
                              const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                              int reduce, const void *wl_packed, const void *wr_packed,
                              const float *bias, int64_t Fo, float *out, int64_t ldo, int relu,
-                             float p_drop, uint64_t seed, float *agg_out, int64_t ld_agg,
-                             const float *xmask, int64_t ldm, float xscale, void *stream) {
+                             float p_drop, uint64_t seed, const uint64_t *seed_dev,
+                             float *agg_out, int64_t ld_agg, const float *xmask, int64_t ldm,
+                             float xscale, void *stream) {
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
     NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || !wr_packed, NGNN_E_ARG);
     NGNN_RETURN_IF(wl_packed && !rowptr, NGNN_E_ARG);
@@ -477,8 +480,8 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     if (!xmask) {  // default path: the row-tile kernel (ngnn_sage_rt.hip)
         int rc = NGNN_OK;
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl_packed,
-                             wr_packed, bias, Fo, out, ldo, relu, p_drop, seed, agg_out, ld_agg,
-                             as_stream(stream), &rc))
+                             wr_packed, bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out,
+                             ld_agg, as_stream(stream), &rc))
             return rc;
     }
     const int vec_in = (K % 4 == 0) && (ldx % 4 == 0) && aligned(x, 16) &&
@@ -493,7 +496,7 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
         const int64_t Fo_c = std::min<int64_t>(512, Fo - c0);
         const int64_t toff = (c0 / 16) * KG * 64;  // float4 offset of the slice's first n-tile
         static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
-        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, dbg};
+        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, seed_dev, dbg};
         float *of = out + c0;
         const int vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(of, 16);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));

@@ -65,6 +65,7 @@ struct RtArgs {
     int64_t ld_agg;
     Epi epi;
     uint32_t x_bytes, out_bytes, agg_bytes;  // buffer-resource ranges (all < 4 GiB)
+    const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
     int dbg;  // ablation bits (NGNN_SAGE_ABLATE, profiling only): 1 no MFMA, 2 no stores, 4 no x loads,
              // 8 no epilogue, 16 no weight prologue
 };
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
     int nbeg = 0, nend = 0;
+    if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
     const i32x4 xr = make_rsrc(a.x, a.x_bytes);
     const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
     auto prefetch = [&](int tn) {
@@ -498,7 +500,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
-                     float *agg_out, int64_t ld_agg, hipStream_t st, int *rc) {
+                     const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
+                     int *rc) {
     static const bool off = getenv("NGNN_NO_ROWTILE") != nullptr;
     if (off) return 0;
     if (K % 4 != 0 || ldx % 4 != 0 || !aligned(x, 16)) return 0;
@@ -551,6 +554,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
         a.dbg = dbg;
+        a.seed_dev = seed_dev;
         a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
         a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;

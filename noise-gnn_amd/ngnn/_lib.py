@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK = 0
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
@@ -36,7 +36,7 @@ SIGNATURES = {
     "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_pack_weight_ex": (_int, [_p, _p, _i64, _i64, _i64, _i64, _int, _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
-                             _int, ctypes.c_float, ctypes.c_uint64, _p, _i64, _p, _i64,
+                             _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),

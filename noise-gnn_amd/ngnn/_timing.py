@@ -15,6 +15,8 @@ import dataclasses
 import torch
 
 _active = None
+# True while timing inside a HIP-graph capture: events become record nodes
+EXTERNAL = False
 
 
 @dataclasses.dataclass
@@ -27,8 +29,26 @@ class Rec:
 
 
 class KernelTimer:
-    def __init__(self):
+    """only: optional set of span names to time (others cost nothing).  Events
+    come from a pool, created once per timer (event creation is a host API
+    call; recording is a stream command)."""
+
+    def __init__(self, only=None):
         self.recs: list[Rec] = []
+        self.only = set(only) if only else None
+        self._pool: list[torch.cuda.Event] = []
+
+    def _event(self):
+        if EXTERNAL:
+            return torch.cuda.Event(enable_timing=True, external=True)
+        return self._pool.pop() if self._pool else torch.cuda.Event(enable_timing=True)
+
+    def reserve(self, n: int):
+        """Pre-create n events (outside any timed region)."""
+        for _ in range(n):
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # torch creates the HIP event lazily, at the first record
+            self._pool.append(ev)
 
     def __enter__(self):
         global _active
@@ -51,11 +71,10 @@ class KernelTimer:
 @contextlib.contextmanager
 def span(name: str, nbytes: int, flops: int = 0):
     t = _active
-    if t is None:
+    if t is None or (t.only is not None and name not in t.only):
         yield
         return
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
+    s, e = t._event(), t._event()
     s.record()
     yield
     e.record()

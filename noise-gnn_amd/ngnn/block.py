@@ -92,6 +92,9 @@ class Block:
         self.csr = build_csr(edge_index[1], edge_index[0], self.n_dst, self.dst_sorted)
         self._csr_t = None
         self.n_active = None  # leading rows with in-edges, if a producer told us
+        # device int32 scalar: rows >= it are padding (a static HIP-graph slot);
+        # the forward kernels skip them.  None: every row is real.
+        self.n_rows_dev = None
 
     @property
     def rowptr(self):
@@ -132,6 +135,7 @@ class _BlockCache:
             blk = Block(edge_index, num_nodes, validate=False, dst_sorted=hint[0],
                         src_sorted=hint[1])
             blk.n_active = hint[2]
+            blk.n_rows_dev = hint[3]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -155,12 +159,14 @@ _hints_lock = threading.Lock()
 
 
 def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: bool,
-                    n_active: int | None = None) -> None:
+                    n_active: int | None = None, n_rows_dev: torch.Tensor | None = None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
-    later rows have none) -- only used for roofline accounting."""
+    later rows have none) -- only used for roofline accounting.  n_rows_dev:
+    device int32 scalar bounding the real rows of a padded slot."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
-        _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active)
+        _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
+                                  n_rows_dev)
 
 
 def _drop_hint(key):
@@ -173,7 +179,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4]
+    return h[2], h[3], h[4], h[5]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

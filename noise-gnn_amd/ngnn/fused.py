@@ -71,13 +71,15 @@ def pack_dgrad_weight(wl: torch.Tensor, wr: torch.Tensor) -> torch.Tensor:
 
 
 def _gemm_layer(x, K, n_rows, block, reduce, pl, pr, bias, Fo, out, relu, p_drop, seed,
-                agg_out=None, n_rows_dev=None, xmask=None, xscale=1.0):
+                agg_out=None, n_rows_dev=None, xmask=None, xscale=1.0, seed_dev=None):
+    if torch.is_tensor(n_rows_dev):
+        n_rows_dev = _lib.ptr(n_rows_dev)
     rc = _lib.load().ngnn_sage_fwd(
         _lib.ptr(x), x.stride(0), K, n_rows, n_rows_dev,
         _lib.ptr(block.rowptr) if block is not None else None,
         _lib.ptr(block.col) if block is not None else None,
         _lib.REDUCE[reduce], _lib.ptr(pl), _lib.ptr(pr), _lib.ptr(bias), Fo, _lib.ptr(out),
-        out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
+        out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1), _lib.ptr(seed_dev),
         _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
         _lib.ptr(xmask), xmask.stride(0) if xmask is not None else K, float(xscale),
         _lib.stream_handle(x.device))
@@ -85,7 +87,8 @@ def _gemm_layer(x, K, n_rows, block, reduce, pl, pr, bias, Fo, out, relu, p_drop
 
 
 def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu: bool,
-                   p_drop: float, seed: int, agg_out: torch.Tensor | None = None) -> torch.Tensor:
+                   p_drop: float, seed: int, agg_out: torch.Tensor | None = None,
+                   seed_dev: torch.Tensor | None = None) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd."""
     N, K = x.shape
     Fo = wl.shape[0]
@@ -97,13 +100,13 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     flops = 2 * N * K * Fo + 2 * (block.n_active or 0) * K * Fo
     with _timing.span("sage_fwd", nbytes, flops):
         _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
-                    agg_out=agg_out)
+                    agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
     return out
 
 
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, *params):
+    def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, *params):
         L = len(params) // 3
         acts, aggs = [x], []
         h = x
@@ -112,7 +115,8 @@ class _SAGEStack(torch.autograd.Function):
             last = i == L - 1
             agg = torch.empty(h.shape, dtype=torch.float32, device=h.device)
             h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=not last,
-                               p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg)
+                               p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg,
+                               seed_dev=seed_dev)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -206,7 +210,7 @@ class _SAGEStack(torch.autograd.Function):
                 _lib.check(rc, "ngnn_sage_dgrad_scatter")
             dy = dh
         dx = dy if (need_dx and L > 0) else None
-        return (dx, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, *grads)
 
 
 def sage_stack_supported(model, x) -> bool:
@@ -221,11 +225,11 @@ def sage_stack_supported(model, x) -> bool:
     return True
 
 
-def sage_stack(model, x, block: Block, seed: int) -> torch.Tensor:
+def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor:
     params = []
     for conv in model.convs:
         params += [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
     p = model.dropout if model.training else 0.0
     aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
-    return _SAGEStack.apply(xc, block, aggr, float(p), int(seed), *params)
+    return _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, *params)

@@ -1,0 +1,140 @@
+"""HIP-graph replay of the training step (the reference's loop body,
+pipeline.py:152-169: forward on a NeighborLoader block, loss on the seed rows,
+backward, optimizer step) over static, padded input slots.
+
+Every launch of the step -- CSR build, both fused layer kernels, loss,
+backward kernels, Adam -- is captured once into a HIP graph (through
+``torch.cuda.CUDAGraph``) and replayed per batch, so the host issues one
+graph launch instead of ~30 kernel launches and ~100 Python/ATen calls.
+The step is capturable because the ngnn path never reads device values on the
+host: block row bounds, backward receptive-field bounds and the dropout seed
+(``seed_dev``, drawn by torch's graph-safe RNG inside the graph) live on the
+device.
+
+Shapes are static: the slot holds ``n_cap`` node rows and ``e_cap`` edges.
+A batch with N nodes and E edges fills rows ``[0, N)`` and edges ``[0, E)``;
+the padding edges are self-loops spread evenly over the padding rows
+``[N, n_cap)`` (targets stay non-decreasing, no row gets more than a few), so
+padded rows never feed a real row and never receive gradient (the loss reads
+rows < batch_size only).  A device scalar holds N; the forward kernels read it
+and skip the padding rows, so a generous slot costs memory, not time.
+
+The gradient all-reduce of seed-sharded data parallelism (RCCL) runs between
+two graphs (forward+backward, then the optimizer step), outside capture.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .block import block_cache, hint_edge_index
+
+
+class GraphedTrainStep:
+    def __init__(self, model, optimizer, batch_size: int, n_cap: int, e_cap: int, in_dim: int,
+                 device, reducer=None, loss_fn=None, warmup: int = 3):
+        if not optimizer.defaults.get("capturable", False):
+            raise ValueError("GraphedTrainStep needs an optimizer built with capturable=True")
+        self.model, self.opt, self.reducer = model, optimizer, reducer
+        self.B, self.n_cap, self.e_cap = int(batch_size), int(n_cap), int(e_cap)
+        self.loss_fn = loss_fn or F.cross_entropy
+        self.warmup = warmup
+        dev = torch.device(device)
+        self.x = torch.zeros(self.n_cap, in_dim, dtype=torch.float32, device=dev)
+        self.ei = torch.zeros(2, self.e_cap, dtype=torch.int64, device=dev)
+        self.y = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self._ar = torch.arange(self.e_cap, dtype=torch.int64, device=dev)
+        self.n_valid = torch.full((1,), self.n_cap, dtype=torch.int32, device=dev)
+        self.g_fb = self.g_opt = None
+        self.loss = None
+
+    # ---- slot filling (stream-ordered device copies; no host syncs)
+    def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor) -> None:
+        N, E = x.size(0), edge_index.size(1)
+        if N + 1 > self.n_cap or E > self.e_cap:
+            raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
+        self.x[:N].copy_(x)
+        self.ei[:, :E].copy_(edge_index)
+        n_pad = self.e_cap - E
+        if n_pad:
+            # padding self-loops on rows N + floor(j * (n_cap - N) / n_pad): non-decreasing
+            j = self._ar[:n_pad]
+            self.ei[:, E:] = (j * (self.n_cap - N)).div_(n_pad, rounding_mode="floor").add_(N)
+        self.y.copy_(y[:self.B])
+        self.n_valid.fill_(N)  # forward kernels skip the padding rows
+
+    def _fwd_bwd(self):
+        out = self.model(self.x, self.ei)[:self.B]
+        loss = self.loss_fn(out, self.y)
+        loss.backward()
+        return loss
+
+    def capture(self, x, edge_index, y, restore: bool = True) -> None:
+        """Warm up on a side stream (allocates grads, workspaces, optimizer
+        state), then capture.  restore=True puts the parameters and optimizer
+        state back to their pre-warm-up values afterwards, so graph training
+        starts from the same state eager training would."""
+        snap = None
+        if restore:
+            snap = ([p.detach().clone() for p in self.model.parameters()],
+                    {k: {n: (t.clone() if torch.is_tensor(t) else t) for n, t in v.items()}
+                     for k, v in self.opt.state.items()})
+        self.load(x, edge_index, y)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):
+                self.opt.zero_grad(set_to_none=True)
+                self._fwd_bwd()
+                if self.reducer is not None:
+                    self.reducer()
+                self.opt.step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        # the captured Block must be built inside the graph (from the slot's
+        # contents at replay time), never served from the eager cache
+        block_cache.clear()
+        hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid)
+        self.opt.zero_grad(set_to_none=True)
+        self.g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fb):
+            self.loss = self._fwd_bwd()
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
+            self.opt.step()
+        block_cache.clear()
+        torch.cuda.synchronize()
+        if snap is not None:
+            with torch.no_grad():
+                for p, v in zip(self.model.parameters(), snap[0]):
+                    p.copy_(v)
+                for k, st in self.opt.state.items():
+                    old = snap[1].get(k)
+                    for n, t in st.items():
+                        if not torch.is_tensor(t):
+                            continue
+                        if old is not None and torch.is_tensor(old.get(n)):
+                            t.copy_(old[n])
+                        else:
+                            t.zero_()  # state born in the warm-up: a fresh optimizer's zeros
+
+    def __call__(self, x, edge_index, y):
+        """Load one batch into the slot and replay the captured step; returns
+        the (device) loss tensor of this step."""
+        self.load(x, edge_index, y)
+        self.g_fb.replay()
+        if self.reducer is not None:
+            self.reducer()
+        self.g_opt.replay()
+        return self.loss
+
+
+def slot_size(batch_size: int, fanouts, margin_rows: int = 1024):
+    """(n_cap, e_cap) for every NeighborLoader block of this shape: the most
+    edges the sampler can emit (batch x fanout products) and as many node
+    rows plus room for the padding self-loops."""
+    e_cap, frontier = 0, int(batch_size)
+    for k in fanouts:
+        frontier *= int(k)
+        e_cap += frontier
+    return int(batch_size) + e_cap + margin_rows, e_cap

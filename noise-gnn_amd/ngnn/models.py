@@ -47,10 +47,15 @@ class SAGE(nn.Module):
         if fused.sage_stack_supported(self, x):
             # one autograd node for the stack: fused layer kernels forward,
             # receptive-field-bounded backward (ngnn/fused.py)
-            seed = 0
+            seed, seed_dev = 0, None
             if self.training and self.dropout > 0:
-                seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
-            return fused.sage_stack(self, x, block, seed)
+                if torch.cuda.is_current_stream_capturing():
+                    # HIP-graph capture: the seed is drawn on the device by torch's
+                    # graph-safe generator, i.e. afresh at every replay
+                    seed_dev = torch.randint(0, 2**62, (1,), device=x.device)
+                else:
+                    seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
+            return fused.sage_stack(self, x, block, seed, seed_dev)
         if self.use_bn:
             x = self.bn1(x)
         for i, conv in enumerate(self.convs):

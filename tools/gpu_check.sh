@@ -34,7 +34,7 @@ if [ "${SKIP_BENCH:-0}" != 1 ]; then
   tail -2 "$OUT/bench.log"
 fi
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py ${PROF_ARGS:---steps 20 --warmup 5 --no-cpu-baseline --no-epoch} > "$OUT/prof.log" 2>&1
+  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py ${PROF_ARGS:---steps 20 --warmup 5 --no-cpu-baseline --no-epoch --timer none} > "$OUT/prof.log" 2>&1
   stop_on_crash $? rocprof
   find "$OUT/prof" -name "*kernel_stats.csv" -exec head -30 {} \; > "$OUT/kernel_stats_head.txt" 2>/dev/null || true
 fi
