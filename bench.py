@@ -35,7 +35,6 @@ sys.path.insert(0, os.path.join(ROOT, "noise-gnn_amd"))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_*_f32), same table
@@ -63,8 +62,9 @@ def parse():
 
 
 def train_step(model, opt, reducer, b):
-    out = model(b.x, b.edge_index)[:b.batch_size]
-    loss = F.cross_entropy(out, b.y[:b.batch_size])
+    from ngnn.losses import seed_cross_entropy  # == F.cross_entropy(out[:bs], y[:bs])
+    out = model(b.x, b.edge_index)
+    loss = seed_cross_entropy(out, b.y, b.batch_size)
     opt.zero_grad(set_to_none=False)  # keep the grad tensors (a captured graph owns them)
     loss.backward()
     reducer()

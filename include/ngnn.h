@@ -228,6 +228,40 @@ int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t 
                           const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
                           float *dh, int64_t ldd, int zero_tail, void *stream);
 
+/* ------------------------------------------------------ seed-row loss
+ * Mean cross entropy of the first B rows of logits [*, C] (row stride ld)
+ * against labels y[0..B), rows whose label == ignore_index excluded (torch
+ * reduction='mean' semantics):  loss = sum (lse(x_r) - x_r[y_r]) / count.
+ * Writes *loss and *count (device floats).  Deterministic.  The backward
+ * writes dlogits rows < B = g (softmax(x_r) - onehot(y_r)) / count with
+ * g = *grad_scale (0 for ignored rows) and leaves rows >= B untouched.
+ * Replaces F.cross_entropy(out[:batch_size], y[:batch_size]) in the
+ * reference's training loop (pipeline.py:158) and its autograd. */
+size_t ngnn_seed_xent_workspace_bytes(int64_t B);
+/* ws: ngnn_seed_xent_workspace_bytes(B), 16-B aligned, zero-filled before the
+ * FIRST use (its tail holds a self-resetting ticket); calls sharing a ws must
+ * be stream-ordered.  The backward takes the same ws (reserved) and
+ * recomputes the row log-sum-exps. */
+int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
+                       int64_t ignore_index, float *loss, float *count, void *ws,
+                       size_t ws_bytes, void *stream);
+int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
+                       int64_t ignore_index, const void *ws, const float *grad_scale,
+                       const float *count, float *dlogits, int64_t ldd, void *stream);
+
+/* ------------------------------------------------------ HIP-graph slot
+ * Fill the static slot a captured training step reads (ngnn/graphs.py) with
+ * one NeighborLoader block, in one launch: x rows [0, N) (slot rows past N
+ * untouched), edge_index [2, E] (row stride ld_ei) plus padding self-loops
+ * on rows N + floor(j (n_cap - N) / (e_cap - E)) for slot edges E + j, the
+ * first B labels, and *n_valid = N.  Padding needs N < n_cap when E < e_cap.
+ * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
+ * batch.edge_index, batch.y[:batch_size]) for graph replay. */
+int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
+                   int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
+                   int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
+                   int64_t *slot_y, int32_t *n_valid, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,79 @@
+// Static HIP-graph slot filling (ngnn/graphs.py): one launch copies a
+// NeighborLoader block into the slot a captured training step reads.
+//   rows  [0, N)        x copied (16-B vectors when rows allow)
+//   edges [0, E)        copied;  [E, e_cap) padding self-loops on row
+//                       N + floor(j (n_cap - N) / n_pad), j = e - E: targets
+//                       stay non-decreasing (the CSR fast path holds) and no
+//                       padding row gets more than ceil(n_pad / (n_cap - N))
+//   labels [0, B)       copied
+//   *n_valid = N        (the forward kernels skip rows >= N)
+// Replaces the ~8 torch copy / arithmetic launches the slot load took.
+#include "ngnn_internal.h"
+
+namespace ngnn {
+namespace {
+
+__global__ __launch_bounds__(256) void k_slot_load(
+    const float *__restrict__ x, int64_t ldx, int64_t N, int64_t F, const int64_t *__restrict__ ei,
+    int64_t ld_ei, int64_t E, const int64_t *__restrict__ y, int64_t B, float *__restrict__ sx,
+    int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
+    int32_t *__restrict__ n_valid, int vec) {
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    if (vec) {
+        const int64_t f4 = F >> 2, total = N * f4;
+        for (int64_t i = tid; i < total; i += nthr) {
+            const int64_t r = i / f4, c = (i - r * f4) << 2;
+            *reinterpret_cast<float4 *>(sx + r * lds + c) =
+                *reinterpret_cast<const float4 *>(x + r * ldx + c);
+        }
+    } else {
+        const int64_t total = N * F;
+        for (int64_t i = tid; i < total; i += nthr) {
+            const int64_t r = i / F, c = i - r * F;
+            sx[r * lds + c] = x[r * ldx + c];
+        }
+    }
+    const int64_t n_pad = e_cap - E, span = n_cap - N;
+    for (int64_t e = tid; e < e_cap; e += nthr) {
+        int64_t s, d;
+        if (e < E) {
+            s = ei[e];
+            d = ei[ld_ei + e];
+        } else {
+            d = N + ((e - E) * span) / n_pad;
+            s = d;
+        }
+        sei[e] = s;
+        sei[e_cap + e] = d;
+    }
+    for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
+    if (tid == 0) *n_valid = static_cast<int32_t>(N);
+}
+
+}  // namespace
+}  // namespace ngnn
+
+using namespace ngnn;
+
+extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
+                              const int64_t *edge_index, int64_t ld_ei, int64_t E, const int64_t *y,
+                              int64_t B, float *slot_x, int64_t ld_slot, int64_t n_cap,
+                              int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
+                              void *stream) {
+    NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || !slot_x || !slot_ei || !n_valid, NGNN_E_ARG);
+    NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
+                   NGNN_E_ARG);
+    NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E, NGNN_E_SHAPE);
+    // padding needs rows to land on: at least one row past N when edges are padded
+    NGNN_RETURN_IF(N > n_cap || E > e_cap || (E < e_cap && N >= n_cap), NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(N) || !fits_i32(n_cap), NGNN_E_RANGE);
+    const int vec = (F % 4 == 0) && (ldx % 4 == 0) && (ld_slot % 4 == 0) && aligned(x, 16) &&
+                    aligned(slot_x, 16);
+    const int64_t work = std::max<int64_t>({N * F / 4, e_cap, B, 1});
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
+    hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
+                       edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
+                       n_valid, vec);
+    return launch_status();
+}

@@ -138,8 +138,12 @@ class _SAGEStack(torch.autograd.Function):
         # bnd[L] = rows of dout that can be nonzero; bnd[i] = same for d(acts[i])
         bnd = torch.zeros(L + 1, dtype=torch.int32, device=dev)
         bptr = lambda j: bnd.data_ptr() + 4 * j  # noqa: E731
-        _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L), stream),
-                   "ngnn_row_extent")
+        rows_hint = getattr(dout, "_ngnn_nonzero_rows", None)  # set by ngnn.losses
+        if rows_hint is not None:
+            bnd[L:].fill_(int(rows_hint))
+        else:
+            _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
+                                           stream), "ngnn_row_extent")
         # input-gradient scatter: float atomics by default (as the reference's CUDA
         # index_add_); the source-grouped CSR gather when determinism is requested
         deterministic = torch.are_deterministic_algorithms_enabled()

@@ -25,9 +25,10 @@ two graphs (forward+backward, then the optimizer step), outside capture.
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
+from . import _lib
 from .block import block_cache, hint_edge_index
+from .losses import seed_cross_entropy
 
 
 class GraphedTrainStep:
@@ -37,13 +38,13 @@ class GraphedTrainStep:
             raise ValueError("GraphedTrainStep needs an optimizer built with capturable=True")
         self.model, self.opt, self.reducer = model, optimizer, reducer
         self.B, self.n_cap, self.e_cap = int(batch_size), int(n_cap), int(e_cap)
-        self.loss_fn = loss_fn or F.cross_entropy
+        # loss_fn(out, y, batch_size): default == F.cross_entropy(out[:B], y[:B])
+        self.loss_fn = loss_fn or seed_cross_entropy
         self.warmup = warmup
         dev = torch.device(device)
         self.x = torch.zeros(self.n_cap, in_dim, dtype=torch.float32, device=dev)
         self.ei = torch.zeros(2, self.e_cap, dtype=torch.int64, device=dev)
         self.y = torch.zeros(self.B, dtype=torch.int64, device=dev)
-        self._ar = torch.arange(self.e_cap, dtype=torch.int64, device=dev)
         self.n_valid = torch.full((1,), self.n_cap, dtype=torch.int32, device=dev)
         self.g_fb = self.g_opt = None
         self.loss = None
@@ -53,19 +54,21 @@ class GraphedTrainStep:
         N, E = x.size(0), edge_index.size(1)
         if N + 1 > self.n_cap or E > self.e_cap:
             raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
-        self.x[:N].copy_(x)
-        self.ei[:, :E].copy_(edge_index)
-        n_pad = self.e_cap - E
-        if n_pad:
-            # padding self-loops on rows N + floor(j * (n_cap - N) / n_pad): non-decreasing
-            j = self._ar[:n_pad]
-            self.ei[:, E:] = (j * (self.n_cap - N)).div_(n_pad, rounding_mode="floor").add_(N)
-        self.y.copy_(y[:self.B])
-        self.n_valid.fill_(N)  # forward kernels skip the padding rows
+        if x.stride(1) != 1:
+            x = x.contiguous()
+        if edge_index.stride(1) != 1:
+            edge_index = edge_index.contiguous()
+        y = y[:self.B].contiguous()
+        # one launch: x rows, edges + padding self-loops, labels, device row count
+        _lib.check(_lib.load().ngnn_slot_load(
+            _lib.ptr(x), x.stride(0), N, x.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
+            _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
+            _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
+            _lib.stream_handle(self.x.device)), "ngnn_slot_load")
 
     def _fwd_bwd(self):
-        out = self.model(self.x, self.ei)[:self.B]
-        loss = self.loss_fn(out, self.y)
+        out = self.model(self.x, self.ei)
+        loss = self.loss_fn(out, self.y, self.B)
         loss.backward()
         return loss
 
