@@ -160,6 +160,22 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, const float *xmask,
                   int64_t ldm, float xscale, void *stream);
 
+/* Same layer with the RAW PyG Linear weights (W_l, W_r: [Fo, K] row-major,
+ * row stride ldw) through the row-tile kernel: W_r (and W_l when both fit)
+ * go straight from these rows into LDS, no ngnn_pack_weight launch; a W_l
+ * too large to share the LDS is packed into ws (one launch,
+ * ngnn_sage_fwd_raw_workspace_bytes) and streamed from L2.  Returns
+ * NGNN_E_SHAPE, launching nothing, for shapes outside that kernel's envelope
+ * (K % 4 != 0, unaligned rows, W_r slice too large for LDS, buffers >= 2 GiB):
+ * the caller then packs and calls ngnn_sage_fwd. */
+size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo);
+int ngnn_sage_fwd_raw(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                      const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+                      int reduce, const float *wl, const float *wr, int64_t ldw, const float *bias,
+                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
+                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
+                      size_t ws_bytes, void *stream);
+
 /* ------------------------------------------ backward receptive-field bounds
  * ngnn_row_extent: out[0] = max(out[0], 1 + last row of g[n_rows, F] holding a
  * nonzero (or NaN)).  The reference's loss reads only the seed rows
@@ -238,10 +254,9 @@ int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t 
  * Replaces F.cross_entropy(out[:batch_size], y[:batch_size]) in the
  * reference's training loop (pipeline.py:158) and its autograd. */
 size_t ngnn_seed_xent_workspace_bytes(int64_t B);
-/* ws: ngnn_seed_xent_workspace_bytes(B), 16-B aligned, zero-filled before the
- * FIRST use (its tail holds a self-resetting ticket); calls sharing a ws must
- * be stream-ordered.  The backward takes the same ws (reserved) and
- * recomputes the row log-sum-exps. */
+/* ws: ngnn_seed_xent_workspace_bytes(B), 16-B aligned (row losses; calls
+ * sharing a ws must be stream-ordered).  The backward takes the same ws
+ * (reserved) and recomputes the row log-sum-exps. */
 int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
                        int64_t ignore_index, float *loss, float *count, void *ws,
                        size_t ws_bytes, void *stream);

@@ -5,8 +5,8 @@
 // slice-backward / fills.
 //
 // forward : loss = sum_{r<B, y_r != ignore} (lse(x_r) - x_r[y_r]) / #valid
-//           one wave per row; the last workgroup adds the row losses in a
-//           fixed order -> deterministic.
+//           one wave per row, then one workgroup adds the row losses in a
+//           fixed order (second launch) -> deterministic.
 // backward: d x_r[c] = g (softmax(x_r)[c] - [c == y_r]) / #valid for r < B,
 //           0 for ignored rows; rows >= B are not written (the caller keeps
 //           them zero).  One wave per row.
@@ -38,44 +38,37 @@ __device__ __forceinline__ float row_lse(const float *__restrict__ xr, int C, in
     return m + logf(s);
 }
 
-// one wave per row: ws[r] = row loss (0 if ignored), ws[B + r] = 1/0 valid,
-// ws[2B + r] = lse (reused by the backward).  The last block to finish (an
-// atomic ticket, reset by that block) adds the row losses in row order in a
-// fixed tree -> deterministic.
-__global__ __launch_bounds__(256) void k_xent_fwd(const float *__restrict__ x, int64_t ld, int B,
-                                                  int C, const int64_t *__restrict__ y,
-                                                  int64_t ignore, float *__restrict__ ws,
-                                                  unsigned *__restrict__ ticket,
-                                                  float *__restrict__ loss,
-                                                  float *__restrict__ count) {
+// one wave per row: ws[r] = row loss (0 if ignored), ws[B + r] = 1/0 valid
+__global__ __launch_bounds__(256) void k_xent_rows(const float *__restrict__ x, int64_t ld, int B,
+                                                   int C, const int64_t *__restrict__ y,
+                                                   int64_t ignore, float *__restrict__ ws) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r < B) {
-        const int64_t t = y[r];
-        float l = 0.0f, v = 0.0f, lse = 0.0f;
-        if (t != ignore) {
-            const float *xr = x + static_cast<int64_t>(r) * ld;
-            lse = row_lse(xr, C, lane);
-            l = (t >= 0 && t < C) ? lse - xr[t] : NAN;  // out-of-range label: NaN, no OOB read
-            v = 1.0f;
-        }
-        if (lane == 0) {
-            ws[r] = l;
-            ws[B + r] = v;
-            ws[2 * B + r] = lse;
-        }
+    if (r >= B) return;
+    const int64_t t = y[r];
+    float l = 0.0f, v = 0.0f;
+    if (t != ignore) {
+        const float *xr = x + static_cast<int64_t>(r) * ld;
+        const float lse = row_lse(xr, C, lane);
+        l = (t >= 0 && t < C) ? lse - xr[t] : NAN;  // out-of-range label: NaN, no OOB read
+        v = 1.0f;
     }
-    __threadfence();
-    __syncthreads();
-    __shared__ unsigned last;
-    if (threadIdx.x == 0) last = (atomicAdd(ticket, 1u) == gridDim.x - 1);
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
+    if (lane == 0) {
+        ws[r] = l;
+        ws[B + r] = v;
+    }
+}
+
+// one workgroup adds the row losses in a fixed order (strided per thread,
+// then a fixed tree) -> deterministic; a separate launch, so no cross-XCD
+// fences or tickets are needed
+__global__ __launch_bounds__(256) void k_xent_sum(const float *__restrict__ ws, int B,
+                                                  float *__restrict__ loss,
+                                                  float *__restrict__ count) {
     float s = 0.0f, n = 0.0f;
     for (int i = threadIdx.x; i < B; i += 256) {
-        s += __builtin_nontemporal_load(ws + i);
-        n += __builtin_nontemporal_load(ws + B + i);
+        s += ws[i];
+        n += ws[B + i];
     }
     __shared__ float ss[256], sn[256];
     ss[threadIdx.x] = s;
@@ -91,7 +84,6 @@ __global__ __launch_bounds__(256) void k_xent_fwd(const float *__restrict__ x, i
     if (threadIdx.x == 0) {
         *loss = ss[0] / sn[0];  // 0/0 = NaN when every row is ignored, as torch
         *count = sn[0];
-        *ticket = 0u;  // ready for the next launch (stream-ordered)
     }
 }
 
@@ -139,10 +131,11 @@ extern "C" int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, in
     NGNN_RETURN_IF(!fits_i32(B) || !fits_i32(C), NGNN_E_RANGE);
     NGNN_RETURN_IF(ws_bytes < ngnn_seed_xent_workspace_bytes(B) || !aligned(ws, 16), NGNN_E_WORKSPACE);
     float *w = static_cast<float *>(ws);
-    unsigned *ticket = reinterpret_cast<unsigned *>(w + 3 * B);
-    hipLaunchKernelGGL(k_xent_fwd, dim3(static_cast<unsigned>(ceil_div(B, 4))), dim3(256), 0,
-                       as_stream(stream), logits, ld, (int)B, (int)C, y, ignore_index, w, ticket,
-                       loss, count);
+    hipLaunchKernelGGL(k_xent_rows, dim3(static_cast<unsigned>(ceil_div(B, 4))), dim3(256), 0,
+                       as_stream(stream), logits, ld, (int)B, (int)C, y, ignore_index, w);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_xent_sum, dim3(1), dim3(256), 0, as_stream(stream), w, (int)B, loss, count);
     return launch_status();
 }
 

@@ -55,8 +55,10 @@ struct RtArgs {
     const int32_t *n_rows_dev;
     const int32_t *rowptr;
     const int32_t *col;
-    const v4f *wl;  // packed [NT][KG][64] or NULL (no neighbour term)
-    const v4f *wr;  // packed [NT][KG][64]
+    const v4f *wl;  // packed [NT][KG][64] or NULL (no neighbour term); raw (see ldw) only
+                    // when it is staged in LDS -- streamed W_l is always packed
+    const v4f *wr;  // packed [NT][KG][64] or raw (see ldw)
+    int64_t ldw;    // 0: packed;  > 0: raw PyG Linear weights [F_out, K], row stride ldw
     int NT, Fo;
     float *out;
     int64_t ldo;
@@ -117,6 +119,16 @@ __device__ __forceinline__ void mask_x(v4f (&xc)[RT_KC], const v4f (&xf)[RT_KC],
     for (int g = 0; g < RT_KC; ++g) xc[g] = and_mask(xf[g], lt_mask(16 * g, kq));
 }
 
+// Raw (PyG [F_out, K]) weights: fragment (m, kg) lane l is the 16-B run
+// W[m*16 + (l & 15)][kg*16 + 4 (l >> 4) .. +3]; lanes outside F_out x K read
+// row 0 / column 0 and are zeroed.  Returns the float offset; *ok the mask.
+__device__ __forceinline__ int64_t raw_frag_off(int m, int kg, int lane, int64_t ldw, int Fo, int K,
+                                                bool *ok) {
+    const int n = m * 16 + (lane & 15), k = kg * 16 + 4 * (lane >> 4);
+    *ok = n < Fo && k < K;
+    return *ok ? static_cast<int64_t>(n) * ldw + k : 0;
+}
+
 // W fragment loads for k-group kg, m-tiles [p*H, p*H + H).
 // LDS image: k-group major, [KG][NTW][64] v4f, so for a fixed chunk every
 // (g, m) offset is a compile-time immediate off one per-chunk base (no
@@ -130,10 +142,11 @@ __device__ __forceinline__ void load_w(v4f (&w)[H], const v4f *__restrict__ wsrc
 #pragma unroll
     for (int h = 0; h < H; ++h) {
         const int m = p * H + h;
-        if (LDSW)
+        if (LDSW) {
             w[h] = wsrc[(kg * NTW + m) * 64 + lane];
-        else
+        } else {  // streamed from L2: always the packed layout (1 KiB per wave-load)
             w[h] = wsrc[(static_cast<int64_t>(min(m, NT - 1)) * KG + min(kg, KG - 1)) * 64 + lane];
+        }
     }
 }
 
@@ -333,15 +346,35 @@ __global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
         const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
         const int nch = (a.dbg & 16) ? 0 : a.NT * a.KG;  // valid 1-KiB chunks per matrix
         for (int c = wv; c < nch; c += RT_WAVES) {
-            const int m = c / a.KG, kg = c - m * a.KG;  // packed [NT][KG] -> LDS [KG][NTW]
+            const int m = c / a.KG, kg = c - m * a.KG;  // [NT][KG] -> LDS [KG][NTW]
             const int d = (kg * NTW + m) * 64;
+            bool ok = true;
+            const int64_t so = a.ldw ? raw_frag_off(m, kg, ln, a.ldw, a.Fo, a.K, &ok) / 4
+                                     : static_cast<int64_t>(c) * 64 + ln;  // in v4f units
+            // (raw rows are 16-B aligned: K % 4 == 0 and ldw % 4 == 0)
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(a.wr + c * 64 + ln),
+                (const __attribute__((address_space(1))) void *)(a.wr + so),
                 (__attribute__((address_space(3))) void *)(swr + d), 16, 0, 0);
             if (WL_LDS && have_l)
                 __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(a.wl + c * 64 + ln),
+                    (const __attribute__((address_space(1))) void *)(a.wl + so),
                     (__attribute__((address_space(3))) void *)(swl + d), 16, 0, 0);
+        }
+        if (a.ldw) {
+            // raw weights: lanes outside F_out x K loaded row 0 / column 0 --
+            // zero those slots once this wave's LDS-DMAs have landed
+            __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+            const v4f z0{0.f, 0.f, 0.f, 0.f};
+            for (int c = wv; c < nch; c += RT_WAVES) {
+                const int m = c / a.KG, kg = c - m * a.KG;
+                const int d = (kg * NTW + m) * 64;
+                bool ok;
+                (void)raw_frag_off(m, kg, ln, a.ldw, a.Fo, a.K, &ok);
+                if (!ok) {
+                    swr[d + ln] = z0;
+                    if (WL_LDS && have_l) swl[d + ln] = z0;
+                }
+            }
         }
         const v4f z{0.f, 0.f, 0.f, 0.f};
         const int npad = (NTW - a.NT) * 64;  // padded tiles of every k-group
@@ -501,10 +534,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
-                     int *rc) {
+                     int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes) {
     static const bool off = getenv("NGNN_NO_ROWTILE") != nullptr;
     if (off) return 0;
     if (K % 4 != 0 || ldx % 4 != 0 || !aligned(x, 16)) return 0;
+    if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
+        return 0;
     if (agg_out && (ld_agg % 4 != 0 || !aligned(agg_out, 16))) return 0;
     // byte offsets are 32-bit (buffer resources): every buffer < 2 GiB
     const int64_t lim = (int64_t(1) << 31) - 4096;
@@ -542,8 +577,29 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.n_rows_dev = n_rows_dev;
         a.rowptr = rowptr;
         a.col = col;
-        a.wl = wl_packed ? static_cast<const v4f *>(wl_packed) + toff : nullptr;
-        a.wr = static_cast<const v4f *>(wr_packed) + toff;
+        // a slice's weights: packed fragments are n-tile major (contiguous
+        // sub-array); raw weights are rows [c0, c0 + Fo_c)
+        const int64_t woff = ldw ? c0 * ldw / 4 : toff;
+        a.wl = wl_packed ? static_cast<const v4f *>(wl_packed) + woff : nullptr;
+        a.wr = static_cast<const v4f *>(wr_packed) + woff;
+        a.ldw = ldw;
+        if (ldw && wl_packed && !wl_lds) {
+            // raw W_l that must stream from L2: pack it once (all slices) into
+            // the caller's workspace -- fragment-ordered 1-KiB wave loads
+            if (c0 == 0) {
+                if (!wl_ws || wl_ws_bytes < ngnn_pack_weight_bytes(Fo, K)) {
+                    *rc = NGNN_E_WORKSPACE;
+                    return 1;
+                }
+                const int prc = ngnn_pack_weight(static_cast<const float *>(wl_packed), ldw, Fo, K,
+                                                 wl_ws, st);
+                if (prc) {
+                    *rc = prc;
+                    return 1;
+                }
+            }
+            a.wl = static_cast<const v4f *>(wl_ws) + toff;
+        }
         a.NT = NT;
         a.Fo = static_cast<int>(Fo_c);
         a.out = out + c0;
@@ -572,3 +628,33 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
 }
 
 }  // namespace ngnn
+
+using namespace ngnn;
+
+extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo) {
+    return ngnn_pack_weight_bytes(Fo, K);  // a packed W_l, used only when it cannot sit in LDS
+}
+
+extern "C" int ngnn_sage_fwd_raw(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                                 const int32_t *n_rows_dev, const int32_t *rowptr,
+                                 const int32_t *col, int reduce, const float *wl, const float *wr,
+                                 int64_t ldw, const float *bias, int64_t Fo, float *out,
+                                 int64_t ldo, int relu, float p_drop, uint64_t seed,
+                                 const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
+                                 size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
+    NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || !wr, NGNN_E_ARG);
+    NGNN_RETURN_IF(wl && !rowptr, NGNN_E_ARG);
+    NGNN_RETURN_IF(ldx < K || ldo < Fo || ldw < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(agg_out && ld_agg < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(K) || !fits_i32(n_rows) || !fits_i32(Fo), NGNN_E_RANGE);
+    NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
+    if (n_rows == 0) return NGNN_OK;
+    NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
+    int rc = NGNN_OK;
+    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
+                          ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, as_stream(stream), &rc,
+                          ldw, ws, ws_bytes))
+        return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
+    return rc;
+}

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
 ABI_VERSION = 4
 
 OK = 0
+E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
 F32, BF16 = 0, 1
 
@@ -43,6 +44,10 @@ SIGNATURES = {
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
+    "ngnn_sage_fwd_raw_workspace_bytes": (_sz, [_i64, _i64]),
+    "ngnn_sage_fwd_raw": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _i64, _p, _i64,
+                                 _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
+                                 _sz, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),

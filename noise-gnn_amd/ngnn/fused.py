@@ -93,14 +93,30 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     N, K = x.shape
     Fo = wl.shape[0]
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
-    pl, pr = pack_weight(wl), pack_weight(wr)
     # algorithmic bytes: x + gathered rows + col + rowptr + out;  flops: root GEMM on
     # every row + neighbour GEMM on rows with in-edges (0 if not known: conservative)
     nbytes = (N * K + block.E * (K + 1) + N * Fo) * 4 + (N + 1) * 4
     flops = 2 * N * K * Fo + 2 * (block.n_active or 0) * K * Fo
+    wl_, wr_ = wl.detach(), wr.detach()
+    if wl_.stride(1) != 1 or wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0):
+        wl_, wr_ = wl_.contiguous(), wr_.contiguous()
+    nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
+    lib = _lib.load()
+    ws = _workspace(x.device, "wl_pack", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo))
     with _timing.span("sage_fwd", nbytes, flops):
-        _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
-                    agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
+        # raw weights straight into the row-tile kernel; packed fallback otherwise
+        rc = lib.ngnn_sage_fwd_raw(
+            _lib.ptr(x), x.stride(0), K, N, nrd, _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.REDUCE[reduce], _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
+            _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
+            _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
+            _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
+        if rc == _lib.E_SHAPE:
+            pl, pr = pack_weight(wl), pack_weight(wr)
+            _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
+                        agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
+        else:
+            _lib.check(rc, "ngnn_sage_fwd_raw")
     return out
 
 
