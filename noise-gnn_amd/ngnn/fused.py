@@ -34,12 +34,14 @@ from .block import Block
 _ws: dict = {}
 
 
-def _workspace(dev: torch.device, name: str, nbytes: int) -> torch.Tensor:
-    """Per-device scratch buffers, grown on demand and reused across calls."""
+def _workspace(dev: torch.device, name: str, nbytes: int, zero: bool = False) -> torch.Tensor:
+    """Per-device scratch buffers, grown on demand and reused across calls
+    (stream-ordered).  zero: zero-filled when (re)allocated."""
     key = (dev, name)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+        alloc = torch.zeros if zero else torch.empty
+        buf = alloc(max(nbytes, 256), dtype=torch.uint8, device=dev)
         _ws[key] = buf
     return buf
 
@@ -102,7 +104,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         wl_, wr_ = wl_.contiguous(), wr_.contiguous()
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
-    ws = _workspace(x.device, "wl_pack", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo))
+    ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo), zero=True)
     with _timing.span("sage_fwd", nbytes, flops):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         rc = lib.ngnn_sage_fwd_raw(
