@@ -116,9 +116,10 @@ def main():
     graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
     torch.manual_seed(1234)  # identical init on every rank
     model = ngnn.SAGE(100, args.hidden, 47, layers, dropout=0.5).to(dev)
-    # torch's single-kernel Adam on the device (same update rule as the reference's Adam);
-    # capturable: its step count lives on the device, so the HIP graph can replay it
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=not args.eager)
+    # the reference's Adam(lr=1e-3) rule as ngnn's two-launch device Adam; its step count
+    # lives on the device, so the HIP graph can replay it
+    from ngnn.optim import Adam
+    opt = Adam(model.parameters(), lr=1e-3)
     reducer = GradAllReduce(model.parameters())
     model.train()
 
@@ -240,7 +241,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded Chung-Lu graph with ogbn-products sizes; random features)",
             "config": {"workload": f"products-[{args.fanout}]-bs{args.batch_size}",
-                       "model": f"SAGE(100,{args.hidden},47,L={layers}) mean-aggr + Adam",
+                       "model": f"SAGE(100,{args.hidden},47,L={layers}) mean-aggr + Adam(1e-3)",
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
                        "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},

@@ -264,6 +264,18 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
                        int64_t ignore_index, const void *ws, const float *grad_scale,
                        const float *count, float *dlogits, int64_t ldd, void *stream);
 
+/* ------------------------------------------------------------- optimiser
+ * Adam step over n_tensors parameter tensors (host arrays of device
+ * pointers; grads, exp_avgs, exp_avg_sqs like params, numels their sizes),
+ * torch.optim.Adam's rule (amsgrad/maximize off, optional L2 weight decay),
+ * with the step count a device float that this call advances (so a captured
+ * HIP graph replays correctly).  Replaces the reference's
+ * torch.optim.Adam(...).step() (model.py:66-69). */
+int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
+                   float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
+                   float *step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   void *stream);
+
 /* ------------------------------------------------------ HIP-graph slot
  * Fill the static slot a captured training step reads (ngnn/graphs.py) with
  * one NeighborLoader block, in one launch: x rows [0, N) (slot rows past N

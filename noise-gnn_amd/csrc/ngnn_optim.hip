@@ -1,0 +1,91 @@
+// Adam for the training step (the reference's optimiser: torch.optim.Adam,
+// model.py:66-69 [ext: torch]) as one update launch over every parameter
+// tensor plus a one-thread step-count launch, instead of torch's step
+// increment + multi-tensor fused kernel.  Same update rule as torch Adam
+// (amsgrad off, maximize off):
+//   t = step + 1;  g += wd p;  m = m + (1 - b1)(g - m);  v = b2 v + (1 - b2) g^2
+//   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// The step count lives on the device (HIP-graph replays advance it).
+#include "ngnn_internal.h"
+
+namespace ngnn {
+namespace {
+
+constexpr int kMaxT = 16;
+
+struct AdamTensors {
+    float *p[kMaxT];
+    const float *g[kMaxT];
+    float *m[kMaxT];
+    float *v[kMaxT];
+    int64_t off[kMaxT + 1];  // prefix sums of numel
+    int n;
+};
+
+__global__ __launch_bounds__(256) void k_adam(AdamTensors T, const float *__restrict__ step, float lr,
+                                              float b1, float b2, float eps, float wd) {
+    const float t = *step + 1.0f;
+    const float bc1 = 1.0f - powf(b1, t);
+    const float bc2s = sqrtf(1.0f - powf(b2, t));
+    const float step_size = lr / bc1;
+    const int64_t total = T.off[T.n];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int k = 0;
+        while (k + 1 < T.n && i >= T.off[k + 1]) ++k;
+        const int64_t j = i - T.off[k];
+        float g = T.g[k][j];
+        float p = T.p[k][j];
+        if (wd != 0.0f) g = g + wd * p;
+        float m = T.m[k][j];
+        float v = T.v[k][j];
+        m = m + (1.0f - b1) * (g - m);
+        v = b2 * v + (1.0f - b2) * g * g;
+        const float denom = sqrtf(v) / bc2s + eps;
+        p = p - step_size * (m / denom);
+        T.m[k][j] = m;
+        T.v[k][j] = v;
+        T.p[k][j] = p;
+    }
+}
+
+__global__ void k_step_inc(float *step) { *step += 1.0f; }
+
+}  // namespace
+}  // namespace ngnn
+
+using namespace ngnn;
+
+extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
+                              float *const *exp_avgs, float *const *exp_avg_sqs,
+                              const int64_t *numels, float *step, float lr, float beta1,
+                              float beta2, float eps, float weight_decay, void *stream) {
+    NGNN_RETURN_IF(n_tensors < 0 || !step, NGNN_E_ARG);
+    NGNN_RETURN_IF(n_tensors > 0 && (!params || !grads || !exp_avgs || !exp_avg_sqs || !numels),
+                   NGNN_E_ARG);
+    hipStream_t st = as_stream(stream);
+    for (int base = 0; base < n_tensors; base += kMaxT) {
+        AdamTensors T;
+        T.n = std::min(kMaxT, n_tensors - base);
+        T.off[0] = 0;
+        for (int k = 0; k < T.n; ++k) {
+            NGNN_RETURN_IF(numels[base + k] < 0, NGNN_E_ARG);
+            NGNN_RETURN_IF(numels[base + k] > 0 && (!params[base + k] || !grads[base + k] ||
+                                                    !exp_avgs[base + k] || !exp_avg_sqs[base + k]),
+                           NGNN_E_ARG);
+            T.p[k] = params[base + k];
+            T.g[k] = grads[base + k];
+            T.m[k] = exp_avgs[base + k];
+            T.v[k] = exp_avg_sqs[base + k];
+            T.off[k + 1] = T.off[k] + numels[base + k];
+        }
+        if (T.off[T.n] == 0) continue;
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(T.off[T.n], 256), 2048));
+        hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, lr, beta1, beta2, eps,
+                           weight_decay);
+        const int rc = launch_status();
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, st, step);
+    return launch_status();
+}

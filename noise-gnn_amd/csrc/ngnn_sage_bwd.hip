@@ -405,17 +405,37 @@ __global__ __launch_bounds__(256) void k_dgrad_scatter(
 // dh rows < Rn must be zeroed first (k_dh_init with droot = NULL semantics).
 constexpr int FD_MAXF = 512;  // dz row staged per wave: Fo <= 512 on this path
 
-template <int RED>
+// LDS_W: W_r and W_l ([Fo][K] each, row-major as given) are first copied into
+// LDS by the (persistent) workgroup, so the per-row products read LDS
+// (~64-cycle latency, conflict-free: lanes read consecutive columns) instead
+// of chains of L2 loads.  Dynamic LDS: 2 Fo K floats.
+template <int RED, bool LDS_W>
 __global__ __launch_bounds__(256) void k_dgrad_fused(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
-    float yscale, const float *__restrict__ wl, const float *__restrict__ wr, int Fo, int K,
+    float yscale, const float *__restrict__ wl_g, const float *__restrict__ wr_g, int Fo, int K,
     const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int n_rows,
     const int32_t *__restrict__ r_ptr, const float *__restrict__ h, int64_t ldh,
     const float *__restrict__ agg, int64_t ld_agg, float *__restrict__ dh, int64_t ldd) {
     __shared__ __attribute__((aligned(16))) float sdz[4][FD_MAXF];
+    extern __shared__ __attribute__((aligned(16))) float sw[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float *z = sdz[wave];
     const int R = min(n_rows, *r_ptr);
+    const float *wr = wr_g, *wl = wl_g;
+    if (LDS_W) {
+        if (static_cast<int64_t>(blockIdx.x) * 4 >= R) return;  // no rows for this workgroup
+        const int n4 = (Fo * K) >> 2;  // Fo K % 4 == 0 on this path
+        float4 *s4 = reinterpret_cast<float4 *>(sw);
+        const float4 *r4 = reinterpret_cast<const float4 *>(wr_g);
+        const float4 *l4 = reinterpret_cast<const float4 *>(wl_g);
+        for (int i = threadIdx.x; i < n4; i += 256) {
+            s4[i] = r4[i];
+            s4[n4 + i] = l4[i];
+        }
+        __syncthreads();
+        wr = sw;
+        wl = sw + Fo * K;
+    }
     for (int64_t d = blockIdx.x * 4 + wave; d < R; d += gridDim.x * 4) {
         for (int n = lane; n < Fo; n += 64) {
             float v = dy[d * ldy + n];
@@ -644,6 +664,18 @@ extern "C" int ngnn_sage_dgrad_scatter(const float *dagg, int64_t ld_dagg, const
     return launch_status();
 }
 
+static int dgrad_num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        n = v;
+    }
+    return n;
+}
+
 extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
                                      float yscale, const float *wl, const float *wr, int64_t Fo,
                                      int64_t K, const int32_t *rowptr, const int32_t *col,
@@ -665,18 +697,40 @@ extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *
     const unsigned g_init = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows * K, 256), 4096));
     hipLaunchKernelGGL(k_dh_init, dim3(g_init), dim3(256), 0, st, (const float *)nullptr, K,
                        (int)n_rows, r_ptr, rnext_ptr, (int)K, dh, ldd, zero_tail);
-    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows, 4), 1024));
-    if (reduce == NGNN_REDUCE_MEAN)
-        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_MEAN>), dim3(g), dim3(256), 0, st, dy, ldy, y,
-                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
-                           h, ldh, agg, ld_agg, dh, ldd);
-    else if (reduce == NGNN_REDUCE_SUM)
-        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_SUM>), dim3(g), dim3(256), 0, st, dy, ldy, y,
-                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
-                           h, ldh, agg, ld_agg, dh, ldd);
-    else
-        hipLaunchKernelGGL((k_dgrad_fused<NGNN_REDUCE_MAX>), dim3(g), dim3(256), 0, st, dy, ldy, y,
-                           ldyy, yscale, wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr,
-                           h, ldh, agg, ld_agg, dh, ldd);
+    // W in LDS when both fit next to the dz slots (persistent workgroups,
+    // one per CU, rows grid-strided); else the L2-streaming variant
+    const size_t wbytes = 2 * sizeof(float) * static_cast<size_t>(Fo) * static_cast<size_t>(K);
+    const bool lds_w = ((Fo * K) % 4 == 0) && aligned(wl, 16) && aligned(wr, 16) &&
+                       wbytes + sizeof(float) * 4 * FD_MAXF <= 150 * 1024;
+    const unsigned g = static_cast<unsigned>(
+        std::min<int64_t>(ceil_div(n_rows, 4), lds_w ? dgrad_num_cus() : 1024));
+    auto go = [&](auto red_c, auto lds_c) {
+        constexpr int RED_ = decltype(red_c)::value;
+        constexpr bool L_ = decltype(lds_c)::value;
+        auto fn = k_dgrad_fused<RED_, L_>;
+        if (L_) {
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+                attr = true;
+            }
+        }
+        hipLaunchKernelGGL(fn, dim3(g), dim3(256), L_ ? wbytes : 0, st, dy, ldy, y, ldyy, yscale,
+                           wl, wr, (int)Fo, (int)K, rowptr, col, (int)n_rows, r_ptr, h, ldh, agg,
+                           ld_agg, dh, ldd);
+    };
+    using RM = std::integral_constant<int, NGNN_REDUCE_MEAN>;
+    using RS = std::integral_constant<int, NGNN_REDUCE_SUM>;
+    using RX = std::integral_constant<int, NGNN_REDUCE_MAX>;
+    using T = std::true_type;
+    using Fb = std::false_type;
+    if (reduce == NGNN_REDUCE_MEAN) {
+        if (lds_w) go(RM{}, T{}); else go(RM{}, Fb{});
+    } else if (reduce == NGNN_REDUCE_SUM) {
+        if (lds_w) go(RS{}, T{}); else go(RS{}, Fb{});
+    } else {
+        if (lds_w) go(RX{}, T{}); else go(RX{}, Fb{});
+    }
     return launch_status();
 }

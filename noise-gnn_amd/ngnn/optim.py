@@ -1,0 +1,63 @@
+"""Adam on the device in two launches (ngnn_adam_step): the update over every
+parameter tensor, then the step-count increment.
+
+Same rule and hyper-parameters as ``torch.optim.Adam`` (the reference's
+optimiser, model.py:66-69; amsgrad / maximize / foreach variants not
+offered); the step count is a device tensor, so the step is capturable in a
+HIP graph (``ngnn.graphs.GraphedTrainStep``).  State keys follow torch:
+``step``, ``exp_avg``, ``exp_avg_sq``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
+            raise ValueError("invalid Adam hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      capturable=True))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = _lib.load()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            for p in ps:
+                if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
+                    raise RuntimeError("ngnn.optim.Adam: contiguous float32 GPU parameters only")
+                if p.grad.is_sparse:
+                    raise RuntimeError("ngnn.optim.Adam: dense gradients only")
+            st0 = self.state[ps[0]]
+            if "step" not in st0:
+                step = torch.zeros((), dtype=torch.float32, device=ps[0].device)
+                for p in ps:
+                    st = self.state[p]
+                    st["step"] = step  # one device counter per group
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+            step = self.state[ps[0]]["step"]
+            grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
+            n = len(ps)
+            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in ps])
+            G = (ctypes.c_void_p * n)(*[g.data_ptr() for g in grads])
+            M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in ps])
+            V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps])
+            N = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
+            b1, b2 = group["betas"]
+            _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, step.data_ptr(), float(group["lr"]),
+                                          float(b1), float(b2), float(group["eps"]),
+                                          float(group["weight_decay"]),
+                                          _lib.stream_handle(ps[0].device)), "ngnn_adam_step")
+        return loss
