@@ -35,7 +35,11 @@ __host__ __device__ inline size_t slab_floats(int64_t Fo, int64_t K) {
 
 // rows [c0, c0+64) x cols [k0, k0+kc) of src -> LDS (row-major, ld ldl),
 // zero outside [0,R) x [0,K); optional ReLU/dropout mask; optional "deg == 0
-// -> zero row" (saved aggregate).
+// -> zero row" (saved aggregate).  All of a thread's global loads are issued
+// before its first LDS write (up to SR_U 16-B vectors in flight per thread):
+// one memory latency per staged block, not one per loop trip.
+constexpr int SR_U = 4;  // 16-B vectors in flight per thread per batch (register budget)
+
 template <bool VEC>
 __device__ __forceinline__ void stage_rows(float *lds, int ldl, int ncols, const float *__restrict__ src,
                                            int64_t lds_src, int64_t c0, int R, int k0, int K,
@@ -43,40 +47,82 @@ __device__ __forceinline__ void stage_rows(float *lds, int ldl, int ncols, const
                                            const int32_t *__restrict__ rowptr) {
     if (VEC) {
         const int c4 = ncols >> 2;
-        for (int idx = threadIdx.x; idx < WG_BM * c4; idx += 512) {
-            const int r = idx / c4, c = (idx - r * c4) << 2;
-            const int64_t row = c0 + r;
-            const int k = k0 + c;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            bool ok = row < R && k < K;
-            if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
-            if (ok) {
-                v = *reinterpret_cast<const float4 *>(src + row * lds_src + k);
-                if (mask) {
-                    const float4 m = *reinterpret_cast<const float4 *>(mask + row * ldm + k);
-                    v.x = m.x > 0.f ? v.x * mscale : 0.f;
-                    v.y = m.y > 0.f ? v.y * mscale : 0.f;
-                    v.z = m.z > 0.f ? v.z * mscale : 0.f;
-                    v.w = m.w > 0.f ? v.w * mscale : 0.f;
+        const int total = WG_BM * c4;
+        for (int base = 0; base < total; base += 512 * SR_U) {
+            float4 v[SR_U], mv[SR_U];
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) {
+                const int idx = base + threadIdx.x + u * 512;
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                mv[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+                if (idx < total) {
+                    const int r = idx / c4, c = (idx - r * c4) << 2;
+                    const int64_t row = c0 + r;
+                    const int k = k0 + c;
+                    bool ok = row < R && k < K;
+                    if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
+                    if (ok) {
+                        v[u] = *reinterpret_cast<const float4 *>(src + row * lds_src + k);
+                        if (mask) mv[u] = *reinterpret_cast<const float4 *>(mask + row * ldm + k);
+                    }
                 }
             }
-            *reinterpret_cast<float4 *>(lds + r * ldl + c) = v;
+#pragma unroll
+            for (int u = 0; u < SR_U; ++u) {
+                const int idx = base + threadIdx.x + u * 512;
+                if (idx < total) {
+                    const int r = idx / c4, c = (idx - r * c4) << 2;
+                    float4 w = v[u];
+                    if (mask) {
+                        w.x = mv[u].x > 0.f ? w.x * mscale : 0.f;
+                        w.y = mv[u].y > 0.f ? w.y * mscale : 0.f;
+                        w.z = mv[u].z > 0.f ? w.z * mscale : 0.f;
+                        w.w = mv[u].w > 0.f ? w.w * mscale : 0.f;
+                    }
+                    *reinterpret_cast<float4 *>(lds + r * ldl + c) = w;
+                }
+            }
         }
     } else {
-        for (int idx = threadIdx.x; idx < WG_BM * ncols; idx += 512) {
-            const int r = idx / ncols, c = idx - r * ncols;
-            const int64_t row = c0 + r;
-            const int k = k0 + c;
-            float v = 0.0f;
-            bool ok = row < R && k < K;
-            if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
-            if (ok) {
-                v = src[row * lds_src + k];
-                if (mask) v = mask[row * ldm + k] > 0.f ? v * mscale : 0.f;
+        constexpr int U = 2 * SR_U;  // scalar loads in flight per thread per batch (register budget)
+        const int total = WG_BM * ncols;
+        for (int base = 0; base < total; base += 512 * U) {
+            float v[U], mv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = base + threadIdx.x + u * 512;
+                v[u] = 0.0f;
+                mv[u] = 1.0f;
+                if (idx < total) {
+                    const int r = idx / ncols, c = idx - r * ncols;
+                    const int64_t row = c0 + r;
+                    const int k = k0 + c;
+                    bool ok = row < R && k < K;
+                    if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
+                    if (ok) {
+                        v[u] = src[row * lds_src + k];
+                        if (mask) mv[u] = mask[row * ldm + k];
+                    }
+                }
             }
-            lds[r * ldl + c] = v;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int idx = base + threadIdx.x + u * 512;
+                if (idx < total) {
+                    const int r = idx / ncols, c = idx - r * ncols;
+                    lds[r * ldl + c] = mask ? (mv[u] > 0.f ? v[u] * mscale : 0.f) : v[u];
+                }
+            }
         }
     }
+}
+
+// slices actually used for R rows: about WG_CPS 64-row chunks each (fewer
+// partial slabs to write and to reduce), at most the launched S
+constexpr int WG_CPS = 1;
+__device__ __forceinline__ int wgrad_slices(int R, int S) {
+    const int nchunks = (R + WG_BM - 1) / WG_BM;
+    return max(1, min(S, (nchunks + WG_CPS - 1) / WG_CPS));
 }
 
 // NTW n-tiles x KTW k-tiles of 16x16 per wave.  SPLIT_N: the 4 waves of a
@@ -93,9 +139,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     float *sa = sh + WG_BM * LDH;           // [64][LDH]
     const int R = *r_ptr;
     const int nchunks = (R + WG_BM - 1) / WG_BM;
-    const int S = gridDim.x;
+    const int S = wgrad_slices(R, gridDim.x);
     const int s = blockIdx.x;
-    if (s >= nchunks) return;  // no rows for this slice: its slab is never read
+    if (s >= S || s >= nchunks) return;  // no rows for this slice: its slab is never read
     const int k0 = blockIdx.y * WG_KC;
     const int n0 = blockIdx.z * WG_NC;
     const int kc = min(WG_KC, K - k0);
@@ -175,7 +221,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int R = *r_ptr;
-    const int used = min(S, (R + WG_BM - 1) / WG_BM);
+    const int used = min(wgrad_slices(R, S), (R + WG_BM - 1) / WG_BM);
     // loads issued 8 at a time (memory-level parallelism), summed in slab order
     float t = 0.0f;
     int s = 0;
