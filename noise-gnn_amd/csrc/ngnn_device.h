@@ -6,6 +6,29 @@
 namespace ngnn {
 
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// ---- raw buffer access (LLVM intrinsics by name).  A resource covers
+// [base, base + bytes) (word3 = 0x00020000: raw, 32-bit element format for
+// gfx950); loads past the range return 0 and stores past it are dropped, so
+// row/column bounds become one per-lane offset select instead of branches.
+__device__ v4f buf_load4(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ float buf_load1(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+__device__ int buf_load1i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+__device__ void buf_store4(v4f v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
+__device__ void buf_store1(float v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
+
+__device__ __forceinline__ i32x4 make_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    i32x4 r;
+    r.x = static_cast<int>(static_cast<uint32_t>(a));
+    r.y = static_cast<int>(static_cast<uint32_t>(a >> 32));
+    r.z = static_cast<int>(bytes);
+    r.w = 0x00020000;
+    return r;
+}
+// byte offset that is always outside a resource of < 2 GiB
+constexpr int kBufOOB = 0x7fffffff;
 
 // Tile geometry of the fused layer kernels: a 256-thread workgroup owns 64
 // target rows; K is staged through ONE LDS buffer in 128-column chunks.

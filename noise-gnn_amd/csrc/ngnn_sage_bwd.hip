@@ -8,12 +8,16 @@
 // touches rows < R (weight gradients, dgrad GEMM) or rows < R' (gather).
 //
 //   ngnn_sage_wgrad        dW_r = dz^T h, dW_l = dz^T agg, db = sum dz
-//     k_wgrad_partial: 512-thread workgroups, grid (slice, K-chunk, Fo-chunk);
-//       slice s owns 64-row chunks s, s+S, s+2S, ... below R; per chunk dz
-//       [64 x <=256], h and agg [64 x 128] are staged row-major in LDS (16-B
-//       coalesced loads) and v_mfma_f32_16x16x4_f32 reduces over the rows
-//       (A = dz^T read as ds_read_b32 columns, B = h / agg rows); waves 0-3
-//       own dW_r tiles, waves 4-7 dW_l tiles.  Partials -> ws slabs.
+//     k_wgrad_partial: 512-thread workgroups, grid (slice, K-chunk of 128,
+//       Fo-chunk of 64) ~ one workgroup per CU; slice s owns rows [rb, re),
+//       an even 4-row-granular share of R, walked in 64-row chunks.  Per chunk
+//       dz [64 x 64], h and agg [64 x 128] are loaded into registers (the
+//       next chunk's loads overlap this chunk's MFMAs), written row-major to
+//       LDS, and v_mfma_f32_16x16x4_f32 reduces over the rows (A = dz^T read as
+//       ds_read_b32 columns, B = h / agg rows); waves 0-3 own dW_r tiles,
+//       waves 4-7 dW_l tiles.  Partials -> ws slabs.  Splitting Fo (not only
+//       rows) keeps the slab count, hence the slab write + reduce traffic, at
+//       a quarter of a rows-only split for the products hidden layer.
 //     k_wgrad_reduce: fixed-order slab sum => bitwise reproducible.
 //   ngnn_sage_dgrad_gather dh = [j<R] dz W_r + transposed aggregation of dz W_l
 //     over the source-grouped CSR, in edge order, edges into rows >= R skipped.
@@ -24,194 +28,232 @@ namespace {
 
 constexpr int WG_BM = 64;       // rows per chunk
 constexpr int WG_KC = 128;      // K columns per workgroup (grid.y)
-constexpr int WG_NC = 256;      // Fo columns per workgroup (grid.z)
+constexpr int WG_NC = 64;       // Fo columns per workgroup (grid.z)
 constexpr int LDZ = WG_NC + 16; // LDS strides: +16 floats keeps the two 16-lane
 constexpr int LDH = WG_KC + 16; // row groups of a b32 read on disjoint banks
-constexpr int S_MAX = 256;      // slices (partial slabs): one workgroup per CU
+constexpr int S_MAX = 256;      // slices (partial slabs)
 
 __host__ __device__ inline size_t slab_floats(int64_t Fo, int64_t K) {
     return static_cast<size_t>(2 * Fo * K + Fo);
 }
 
-// rows [c0, c0+64) x cols [k0, k0+kc) of src -> LDS (row-major, ld ldl),
-// zero outside [0,R) x [0,K); optional ReLU/dropout mask; optional "deg == 0
-// -> zero row" (saved aggregate).  All of a thread's global loads are issued
-// before its first LDS write (up to SR_U 16-B vectors in flight per thread):
-// one memory latency per staged block, not one per loop trip.
-constexpr int SR_U = 4;  // 16-B vectors in flight per thread per batch (register budget)
+// slices used for R rows: at most the launched S, at least ~64 rows each
+__device__ __forceinline__ int wgrad_slices(int R, int S) {
+    return max(1, min(S, (R + WG_BM - 1) / WG_BM));
+}
 
-template <bool VEC>
-__device__ __forceinline__ void stage_rows(float *lds, int ldl, int ncols, const float *__restrict__ src,
-                                           int64_t lds_src, int64_t c0, int R, int k0, int K,
-                                           const float *__restrict__ mask, int64_t ldm, float mscale,
-                                           const int32_t *__restrict__ rowptr) {
-    if (VEC) {
-        const int c4 = ncols >> 2;
-        const int total = WG_BM * c4;
-        for (int base = 0; base < total; base += 512 * SR_U) {
-            float4 v[SR_U], mv[SR_U];
+// One 64-row chunk of one operand, COLS columns wide, held in registers by
+// the 512 threads of a workgroup (a fixed number of loads per thread), so the
+// next chunk's loads are in flight while the MFMAs of this one run.  Loads go
+// through a buffer resource over rows [c0, re): rows >= re and columns >= K
+// read 0 with no branches (a column past K gets an out-of-range offset).  The
+// optional per-element mask (y > 0: ReLU/dropout of the forward) and per-row
+// "has in-edges" test (rowptr: the saved aggregate of an edgeless row is never
+// written) are applied when the registers are written to LDS, so no load
+// waits on another.  Needs ld * 64 * 4 < 2^31 (host-checked).
+template <int COLS, bool VEC, bool MASK, bool DEG>
+struct Chunk {
+    static constexpr int W = VEC ? 4 : 1;
+    static constexpr int CPR = COLS / W;               // loads per row
+    static constexpr int N = WG_BM * CPR / 512;        // loads per thread
+    static_assert(N >= 1 && (WG_BM * CPR) % 512 == 0, "chunk must tile the workgroup");
+    using T = std::conditional_t<VEC, v4f, float>;
+    T v[N];
+    T m[MASK ? N : 1];
+    int d0[DEG ? N : 1], d1[DEG ? N : 1];
+
+    __device__ __forceinline__ void load(const float *__restrict__ src, int64_t ld,
+                                         const float *__restrict__ mask, int64_t ldm,
+                                         const int32_t *__restrict__ rowptr, int64_t c0, int re,
+                                         int k0, int K) {
+        const uint32_t nr = static_cast<uint32_t>(re - c0);
+        const i32x4 rs = make_rsrc(src + c0 * ld, nr * static_cast<uint32_t>(ld) * 4u);
+        i32x4 rm = rs, rp = rs;
+        if (MASK) rm = make_rsrc(mask + c0 * ldm, nr * static_cast<uint32_t>(ldm) * 4u);
+        if (DEG) rp = make_rsrc(rowptr + c0, (nr + 1u) * 4u);
 #pragma unroll
-            for (int u = 0; u < SR_U; ++u) {
-                const int idx = base + threadIdx.x + u * 512;
-                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                mv[u] = make_float4(1.f, 1.f, 1.f, 1.f);
-                if (idx < total) {
-                    const int r = idx / c4, c = (idx - r * c4) << 2;
-                    const int64_t row = c0 + r;
-                    const int k = k0 + c;
-                    bool ok = row < R && k < K;
-                    if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
-                    if (ok) {
-                        v[u] = *reinterpret_cast<const float4 *>(src + row * lds_src + k);
-                        if (mask) mv[u] = *reinterpret_cast<const float4 *>(mask + row * ldm + k);
-                    }
-                }
+        for (int u = 0; u < N; ++u) {
+            const int idx = static_cast<int>(threadIdx.x) + u * 512;
+            const int r = idx / CPR, c = (idx % CPR) * W;
+            const int k = k0 + c;
+            const bool kok = k < K;
+            const int vo = kok ? (r * static_cast<int>(ld) + k) * 4 : kBufOOB;
+            if constexpr (VEC) v[u] = buf_load4(rs, vo, 0, 0);
+            else v[u] = buf_load1(rs, vo, 0, 0);
+            if (MASK) {
+                const int mo = kok ? (r * static_cast<int>(ldm) + k) * 4 : kBufOOB;
+                if constexpr (VEC) m[u] = buf_load4(rm, mo, 0, 0);
+                else m[u] = buf_load1(rm, mo, 0, 0);
             }
-#pragma unroll
-            for (int u = 0; u < SR_U; ++u) {
-                const int idx = base + threadIdx.x + u * 512;
-                if (idx < total) {
-                    const int r = idx / c4, c = (idx - r * c4) << 2;
-                    float4 w = v[u];
-                    if (mask) {
-                        w.x = mv[u].x > 0.f ? w.x * mscale : 0.f;
-                        w.y = mv[u].y > 0.f ? w.y * mscale : 0.f;
-                        w.z = mv[u].z > 0.f ? w.z * mscale : 0.f;
-                        w.w = mv[u].w > 0.f ? w.w * mscale : 0.f;
-                    }
-                    *reinterpret_cast<float4 *>(lds + r * ldl + c) = w;
-                }
-            }
-        }
-    } else {
-        constexpr int U = 2 * SR_U;  // scalar loads in flight per thread per batch (register budget)
-        const int total = WG_BM * ncols;
-        for (int base = 0; base < total; base += 512 * U) {
-            float v[U], mv[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = base + threadIdx.x + u * 512;
-                v[u] = 0.0f;
-                mv[u] = 1.0f;
-                if (idx < total) {
-                    const int r = idx / ncols, c = idx - r * ncols;
-                    const int64_t row = c0 + r;
-                    const int k = k0 + c;
-                    bool ok = row < R && k < K;
-                    if (ok && rowptr) ok = rowptr[row + 1] > rowptr[row];
-                    if (ok) {
-                        v[u] = src[row * lds_src + k];
-                        if (mask) mv[u] = mask[row * ldm + k];
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = base + threadIdx.x + u * 512;
-                if (idx < total) {
-                    const int r = idx / ncols, c = idx - r * ncols;
-                    lds[r * ldl + c] = mask ? (mv[u] > 0.f ? v[u] * mscale : 0.f) : v[u];
-                }
+            if (DEG) {
+                d0[u] = buf_load1i(rp, r * 4, 0, 0);
+                d1[u] = buf_load1i(rp, r * 4 + 4, 0, 0);
             }
         }
     }
+
+    __device__ __forceinline__ void store(float *lds, int ldl, float mscale) const {
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            const int idx = static_cast<int>(threadIdx.x) + u * 512;
+            const int r = idx / CPR, c = (idx % CPR) * W;
+            T w = v[u];
+            float *wf = reinterpret_cast<float *>(&w);
+            const float *mf = reinterpret_cast<const float *>(&m[MASK ? u : 0]);
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                float x = wf[i];
+                if (MASK) x = mf[i] > 0.f ? x * mscale : 0.f;
+                if (DEG) x = d1[u] > d0[u] ? x : 0.f;
+                wf[i] = x;
+            }
+            *reinterpret_cast<T *>(lds + r * ldl + c) = w;
+        }
+    }
+};
+
+// the MFMAs of one staged chunk: nks 4-row k-steps, KTN (<= KTW) live K tiles
+template <int NTW, int KTW, int KTN>
+__device__ __forceinline__ void wgrad_mfma(v4f (&acc)[NTW][KTW], const float *sz, const float *sb,
+                                           int nks, int nt0, int kt0, int i16, int kk) {
+    // software-pipelined: the LDS reads of k-step ks+1 are issued before the
+    // MFMAs of k-step ks (the last prefetch re-reads a valid row, unused)
+    float a[NTW], b[KTN];
+    auto fetch = [&](int ks, float(&fa)[NTW], float(&fb)[KTN]) {
+        const int rr = ks * 4 + kk;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) fa[t] = sz[rr * LDZ + (nt0 + t) * 16 + i16];
+#pragma unroll
+        for (int t = 0; t < KTN; ++t) fb[t] = sb[rr * LDH + (kt0 + t) * 16 + i16];
+    };
+    fetch(0, a, b);
+    for (int ks = 0; ks < nks; ++ks) {
+        float an[NTW], bn[KTN];
+        fetch(min(ks + 1, WG_BM / 4 - 1), an, bn);
+#pragma unroll
+        for (int ta = 0; ta < NTW; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < KTN; ++tb)
+                acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) a[t] = an[t];
+#pragma unroll
+        for (int t = 0; t < KTN; ++t) b[t] = bn[t];
+    }
 }
 
-// slices actually used for R rows: about WG_CPS 64-row chunks each (fewer
-// partial slabs to write and to reduce), at most the launched S
-constexpr int WG_CPS = 1;
-__device__ __forceinline__ int wgrad_slices(int R, int S) {
-    const int nchunks = (R + WG_BM - 1) / WG_BM;
-    return max(1, min(S, (nchunks + WG_CPS - 1) / WG_CPS));
+template <int NTW, int KTW, int KTN>
+__device__ __forceinline__ void wgrad_mfma_dispatch(int ktn, v4f (&acc)[NTW][KTW], const float *sz,
+                                                    const float *sb, int nks, int nt0, int kt0,
+                                                    int i16, int kk) {
+    if (ktn == KTN) wgrad_mfma<NTW, KTW, KTN>(acc, sz, sb, nks, nt0, kt0, i16, kk);
+    else if constexpr (KTN > 1) wgrad_mfma_dispatch<NTW, KTW, KTN - 1>(ktn, acc, sz, sb, nks, nt0, kt0, i16, kk);
 }
 
 // NTW n-tiles x KTW k-tiles of 16x16 per wave.  SPLIT_N: the 4 waves of a
-// matrix split the Fo tiles (NT >= 4); else they split the K tiles.
-template <int NTW, int KTW, bool SPLIT_N, bool VEC>
+// matrix split the (4) Fo tiles of the workgroup; else they split the K tiles.
+// Slice s owns rows [rb, re) (R split into S ranges on 4-row boundaries, so
+// every used slice gets the same work +-4 rows), walked in 64-row chunks.
+template <int NTW, int KTW, bool SPLIT_N, bool VZ, bool VH, bool MASK>
 __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
     float yscale, const float *__restrict__ h, int64_t ldh, const float *__restrict__ agg,
     int64_t ld_agg, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ r_ptr, int Fo,
     int K, float *__restrict__ ws) {
-    __shared__ __attribute__((aligned(16))) float smem[WG_BM * LDZ + 2 * WG_BM * LDH];  // 140 KB
+    __shared__ __attribute__((aligned(16))) float smem[WG_BM * LDZ + 2 * WG_BM * LDH];  // 94 KB
     float *sz = smem;                       // [64][LDZ]
     float *sh = sz + WG_BM * LDZ;           // [64][LDH]
     float *sa = sh + WG_BM * LDH;           // [64][LDH]
     const int R = *r_ptr;
-    const int nchunks = (R + WG_BM - 1) / WG_BM;
     const int S = wgrad_slices(R, gridDim.x);
     const int s = blockIdx.x;
-    if (s >= S || s >= nchunks) return;  // no rows for this slice: its slab is never read
+    if (s >= S) return;  // slab never read
+    const int R4 = (R + 3) >> 2;
+    const int rb = 4 * static_cast<int>(static_cast<int64_t>(s) * R4 / S);
+    const int re = min(R, 4 * static_cast<int>(static_cast<int64_t>(s + 1) * R4 / S));
     const int k0 = blockIdx.y * WG_KC;
     const int n0 = blockIdx.z * WG_NC;
     const int kc = min(WG_KC, K - k0);
     const int nc = min(WG_NC, Fo - n0);
     const int KT = (kc + 15) >> 4;
-    const int NTc = (nc + 15) >> 4;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int mat = wave >> 2;  // 0: dW_r (B = h), 1: dW_l (B = agg)
     const int w4 = wave & 3;
     const int nt0 = SPLIT_N ? w4 * NTW : 0;
     const int kt0 = SPLIT_N ? 0 : w4 * KTW;
+    const int ktn = max(0, min(KTW, KT - kt0));  // live K tiles of this wave (uniform)
     const int i16 = lane & 15, kk = lane >> 4;
+    const bool do_bias = blockIdx.y == 0;
 
     v4f acc[NTW][KTW];
 #pragma unroll
     for (int a = 0; a < NTW; ++a)
 #pragma unroll
         for (int b = 0; b < KTW; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
-    float dbias = 0.0f;  // column sum of dz for column n0 + threadIdx.x
+    // column sums of dz: thread (row group wave, column lane) over 8 rows/chunk
+    float dbias = 0.0f;
 
-    const int ncp = (nc + 3) & ~3, kcp = (kc + 3) & ~3;
-    for (int c = s; c < nchunks; c += S) {
-        const int64_t c0 = static_cast<int64_t>(c) * WG_BM;
+    Chunk<WG_NC, VZ, MASK, false> cz;
+    Chunk<WG_KC, VH, false, false> ch;
+    Chunk<WG_KC, VH, false, true> ca;
+    if (rb < re) {
+        cz.load(dy, ldy, y, ldyy, nullptr, rb, re, n0, Fo);
+        ch.load(h, ldh, nullptr, 0, nullptr, rb, re, k0, K);
+        ca.load(agg, ld_agg, nullptr, 0, rowptr, rb, re, k0, K);
+    }
+    for (int c0 = rb; c0 < re; c0 += WG_BM) {
+        __syncthreads();  // the previous chunk's MFMAs are done with LDS
+        cz.store(sz, LDZ, yscale);
+        ch.store(sh, LDH, 1.0f);
+        ca.store(sa, LDH, 1.0f);
         __syncthreads();
-        stage_rows<VEC>(sz, LDZ, ncp, dy, ldy, c0, R, n0, Fo, y, ldyy, yscale, nullptr);
-        stage_rows<VEC>(sh, LDH, kcp, h, ldh, c0, R, k0, K, nullptr, 0, 1.0f, nullptr);
-        stage_rows<VEC>(sa, LDH, kcp, agg, ld_agg, c0, R, k0, K, nullptr, 0, 1.0f, rowptr);
-        __syncthreads();
-        if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < nc) {
-            float t = 0.0f;
-            for (int r = 0; r < WG_BM; ++r) t += sz[r * LDZ + threadIdx.x];
-            dbias += t;
+        const int c1 = c0 + WG_BM;
+        if (c1 < re) {  // next chunk's loads overlap this chunk's MFMAs
+            cz.load(dy, ldy, y, ldyy, nullptr, c1, re, n0, Fo);
+            ch.load(h, ldh, nullptr, 0, nullptr, c1, re, k0, K);
+            ca.load(agg, ld_agg, nullptr, 0, rowptr, c1, re, k0, K);
+        }
+        const int nks = min(WG_BM / 4, (re - c0 + 3) >> 2);
+        if (do_bias) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) dbias += sz[(wave * 8 + r) * LDZ + lane];
         }
         const float *sb = mat ? sa : sh;
-        for (int ks = 0; ks < WG_BM / 4; ++ks) {
-            const int rr = ks * 4 + kk;
-            float a[NTW], b[KTW];
-#pragma unroll
-            for (int t = 0; t < NTW; ++t) a[t] = sz[rr * LDZ + (nt0 + t) * 16 + i16];
-#pragma unroll
-            for (int t = 0; t < KTW; ++t) b[t] = sb[rr * LDH + (kt0 + t) * 16 + i16];
-#pragma unroll
-            for (int ta = 0; ta < NTW; ++ta)
-#pragma unroll
-                for (int tb = 0; tb < KTW; ++tb)
-                    acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
-        }
+        // wave-uniform dispatch on the live K tiles (no per-MFMA branches)
+        wgrad_mfma_dispatch<NTW, KTW, KTW>(ktn, acc, sz, sb, nks, nt0, kt0, i16, kk);
     }
-    // ---- partial slab: [Pr Fo x K][Pl Fo x K][Pb Fo]
+    // ---- partial slab: [Pr Fo x K][Pl Fo x K][Pb Fo]; buffer stores, lanes
+    // past Fo / K get an out-of-range offset (dropped)
     float *slab = ws + static_cast<size_t>(s) * slab_floats(Fo, K);
-    float *P = slab + static_cast<size_t>(mat) * Fo * K;
+    const i32x4 prs = make_rsrc(slab + static_cast<size_t>(mat) * Fo * K,
+                                static_cast<uint32_t>(Fo) * static_cast<uint32_t>(K) * 4u);
 #pragma unroll
     for (int ta = 0; ta < NTW; ++ta)
 #pragma unroll
         for (int tb = 0; tb < KTW; ++tb) {
-            const int nt = nt0 + ta, kt = kt0 + tb;
-            if (nt >= NTc || kt >= KT) continue;
-            const int k = k0 + kt * 16 + i16;
-            if (k >= K) continue;
+            const int k = k0 + (kt0 + tb) * 16 + i16;
+            const bool kok = k < K && kt0 + tb < KT;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int n = n0 + nt * 16 + 4 * kk + j;
-                if (n < Fo) P[static_cast<size_t>(n) * K + k] = acc[ta][tb][j];
+                const int n = n0 + (nt0 + ta) * 16 + 4 * kk + j;
+                const int off = (kok && n < n0 + nc) ? (n * K + k) * 4 : kBufOOB;
+                buf_store1(acc[ta][tb][j], prs, off, 0, 0);
             }
         }
-    if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < nc)
-        slab[2 * static_cast<size_t>(Fo) * K + n0 + threadIdx.x] = dbias;
+    if (do_bias) {
+        __syncthreads();  // every wave is past its last LDS read
+        smem[wave * 64 + lane] = dbias;
+        __syncthreads();
+        if (wave == 0 && lane < nc) {
+            float t = 0.0f;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) t += smem[g * 64 + lane];
+            slab[2 * static_cast<size_t>(Fo) * K + n0 + lane] = t;
+        }
+    }
 }
 
-// out[i] = sum over slabs s < min(S, nchunks) of slab[s][i], in slab order
+// out[i] = sum over the used slabs of slab[s][i], in slab order
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ ws,
                                                       const int32_t *__restrict__ r_ptr, int S,
                                                       int Fo, int K, float *__restrict__ dwr,
@@ -220,8 +262,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
     const int64_t total = slab_floats(Fo, K);
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
-    const int R = *r_ptr;
-    const int used = min(wgrad_slices(R, S), (R + WG_BM - 1) / WG_BM);
+    const int used = wgrad_slices(*r_ptr, S);
     // loads issued 8 at a time (memory-level parallelism), summed in slab order
     float t = 0.0f;
     int s = 0;
@@ -552,17 +593,31 @@ extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
     return sizeof(float) * S_MAX * slab_floats(Fo, K);
 }
 
-#define NGNN_WG_LAUNCH(NTW_, KTW_, SPLIT_)                                                        \
-    do {                                                                                       \
-        if (vec)                                                                               \
-            hipLaunchKernelGGL((k_wgrad_partial<NTW_, KTW_, SPLIT_, true>), grid, dim3(512),   \
-                               0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr,   \
-                               r_ptr, (int)Fo, (int)K, wsf);                                   \
-        else                                                                                   \
-            hipLaunchKernelGGL((k_wgrad_partial<NTW_, KTW_, SPLIT_, false>), grid, dim3(512),  \
-                               0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr,   \
-                               r_ptr, (int)Fo, (int)K, wsf);                                   \
-    } while (0)
+template <int NTW, int KTW, bool SPLIT_N>
+static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const float *dy, int64_t ldy,
+                         const float *y, int64_t ldyy, float yscale, const float *h, int64_t ldh,
+                         const float *agg, int64_t ld_agg, const int32_t *rowptr,
+                         const int32_t *r_ptr, int Fo, int K, float *ws) {
+    auto go = [&](auto vz_c, auto vh_c, auto m_c) {
+        hipLaunchKernelGGL((k_wgrad_partial<NTW, KTW, SPLIT_N, decltype(vz_c)::value,
+                                            decltype(vh_c)::value, decltype(m_c)::value>),
+                           grid, dim3(512), 0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg,
+                           rowptr, r_ptr, Fo, K, ws);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    auto with_mask = [&](auto vz_c, auto vh_c) {
+        if (y) go(vz_c, vh_c, T{});
+        else go(vz_c, vh_c, F{});
+    };
+    if (vz) {
+        if (vh) with_mask(T{}, T{});
+        else with_mask(T{}, F{});
+    } else {
+        if (vh) with_mask(F{}, T{});
+        else with_mask(F{}, F{});
+    }
+}
 
 extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
                                float yscale, const float *h, int64_t ldh, const float *agg,
@@ -573,25 +628,32 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     NGNN_RETURN_IF(Fo <= 0 || K <= 0 || n_rows < 0, NGNN_E_ARG);
     NGNN_RETURN_IF(ldy < Fo || ldh < K || ld_agg < K || (y && ldyy < Fo), NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    // 32-bit buffer offsets: a 64-row chunk of every operand and one partial
+    // matrix must stay below 2 GiB
+    NGNN_RETURN_IF(ldy > (1 << 22) || ldh > (1 << 22) || ld_agg > (1 << 22) ||
+                   (y && ldyy > (1 << 22)) || Fo * K > (int64_t{1} << 28), NGNN_E_RANGE);
     NGNN_RETURN_IF(!ws || ws_bytes < ngnn_sage_wgrad_workspace_bytes(Fo, K), NGNN_E_WORKSPACE);
-    const bool vec = (Fo % 4 == 0) && (K % 4 == 0) && (ldy % 4 == 0) && (ldh % 4 == 0) &&
-                     (ld_agg % 4 == 0) && (!y || ldyy % 4 == 0) && aligned(dy, 16) &&
-                     aligned(h, 16) && aligned(agg, 16) && (!y || aligned(y, 16));
+    // 16-B staging per operand pair: dz (+ its mask y) and h / agg
+    const bool vz = (Fo % 4 == 0) && (ldy % 4 == 0) && aligned(dy, 16) &&
+                    (!y || ((ldyy % 4 == 0) && aligned(y, 16)));
+    const bool vh = (K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) && aligned(h, 16) &&
+                    aligned(agg, 16);
     hipStream_t st = as_stream(stream);
     float *wsf = static_cast<float *>(ws);
-    const int S = static_cast<int>(std::min<int64_t>(S_MAX, std::max<int64_t>(1, ceil_div(n_rows, WG_BM))));
-    const dim3 grid(S, static_cast<unsigned>(ceil_div(K, WG_KC)),
-                    static_cast<unsigned>(ceil_div(Fo, WG_NC)));
+    // slices x K-chunks x Fo-chunks ~ one workgroup per CU; the kernel uses
+    // min(S, R/64) slices for the device-side row bound R
+    const int64_t gy = ceil_div(K, WG_KC), gz = ceil_div(Fo, WG_NC);
+    const int S = static_cast<int>(std::max<int64_t>(
+        1, std::min<int64_t>(ceil_div(n_rows, WG_BM), std::max<int64_t>(1, S_MAX / (gy * gz)))));
+    const dim3 grid(S, static_cast<unsigned>(gy), static_cast<unsigned>(gz));
     const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
-    if (NT >= 4) {
-        const int ntw = (NT + 3) / 4;
-        if (ntw == 1) NGNN_WG_LAUNCH(1, 8, true);
-        else if (ntw == 2) NGNN_WG_LAUNCH(2, 8, true);
-        else if (ntw == 3) NGNN_WG_LAUNCH(3, 8, true);
-        else NGNN_WG_LAUNCH(4, 8, true);
-    } else if (NT == 1) NGNN_WG_LAUNCH(1, 2, false);
-    else if (NT == 2) NGNN_WG_LAUNCH(2, 2, false);
-    else NGNN_WG_LAUNCH(3, 2, false);
+#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr, r_ptr, \
+                     (int)Fo, (int)K, wsf
+    if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
+    else if (NT == 1) launch_wgrad<1, 2, false>(NGNN_WG_ARGS);
+    else if (NT == 2) launch_wgrad<2, 2, false>(NGNN_WG_ARGS);
+    else launch_wgrad<3, 2, false>(NGNN_WG_ARGS);
+#undef NGNN_WG_ARGS
     int rc = launch_status();
     if (rc) return rc;
     const int64_t total = static_cast<int64_t>(slab_floats(Fo, K));

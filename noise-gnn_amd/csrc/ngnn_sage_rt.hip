@@ -33,11 +33,6 @@
 #include "ngnn_device.h"
 
 namespace ngnn {
-// raw buffer intrinsics (LLVM names; declared outside the anonymous namespace)
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ v4f buf_load4(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
-__device__ void buf_store4(v4f v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
-__device__ void buf_store1(float v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
 
 namespace {
 
@@ -89,15 +84,6 @@ __device__ __forceinline__ v4f and_mask(v4f v, int m) {
 // beyond n_rows and padded neighbour slots need no lane predicates; the byte
 // offset is one VGPR and the per-k-group step an immediate.
 
-__device__ __forceinline__ i32x4 make_rsrc(const void *p, uint32_t bytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(p);
-    i32x4 r;
-    r.x = static_cast<int>(static_cast<uint32_t>(a));
-    r.y = static_cast<int>(static_cast<uint32_t>(a >> 32));
-    r.z = static_cast<int>(bytes);
-    r.w = 0x00020000;
-    return r;
-}
 constexpr int kOOB = 0x7ffffff0;  // byte offset past every range: load 0 / drop
 
 // x fragments of one 128-column chunk: lane (rl, q) holds
