@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 4
+#define NGNN_ABI_VERSION 5
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -243,6 +243,27 @@ int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *y, int64_t 
                           const int32_t *r_ptr, const int32_t *rnext_ptr, int reduce,
                           const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
                           float *dh, int64_t ldd, int zero_tail, void *stream);
+
+/* Input gradient for MEAN / SUM when Fo < K, aggregating in the narrow
+ * space (the aggregation is linear):
+ *   g[j]  = sum over edges (j -> d), d < R, of dz[d] (MEAN: / deg(d))
+ *           (Fo-wide float atomics; dz = dy (* [y > 0] * yscale))
+ *   dh[j] = [j < R] dz[j] W_r + g[j] W_l   for j < Rn    (one MFMA pass)
+ * = ngnn_sage_dgrad_fused's result up to fp32 summation order, with Fo/K of
+ * its atomics and no zero-fill of dh.  wl / wr: raw PyG weights [Fo, K],
+ * row stride ldw.  ws: ngnn_sage_dgrad_lowdim_workspace_bytes(n_rows, Fo, K)
+ * bytes, 16-B aligned, ZERO-FILLED before its first use and dedicated to one
+ * (Fo, K) pair: [packed W image | g], g = [n_rows][Fo rounded up to 4]
+ * floats; every call leaves g zero again.  Rows >= Rn of dh are zeroed if zero_tail, else untouched.
+ * NGNN_E_SHAPE when the weight image does not fit the LDS budget (callers
+ * use ngnn_sage_dgrad_fused then).  Replaces autograd of lin_l + propagate
+ * (sage.py:34, PyG SAGEConv [ext]). */
+size_t ngnn_sage_dgrad_lowdim_workspace_bytes(int64_t n_rows, int64_t Fo, int64_t K);
+int ngnn_sage_dgrad_lowdim(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
+                           float yscale, const float *wl, const float *wr, int64_t ldw, int64_t Fo,
+                           int64_t K, const int32_t *rowptr, const int32_t *col, int64_t n_rows,
+                           const int32_t *r_ptr, const int32_t *rnext_ptr, int reduce, float *dh,
+                           int64_t ldd, int zero_tail, void *ws, size_t ws_bytes, void *stream);
 
 /* ------------------------------------------------------ seed-row loss
  * Mean cross entropy of the first B rows of logits [*, C] (row stride ld)

@@ -576,6 +576,210 @@ __global__ __launch_bounds__(256) void k_dgrad_fused(
     }
 }
 
+// ---- low-dimensional input gradient (MEAN/SUM, Fo < K).  The aggregation
+// is linear, so  sum_{d <- j} (dz[d] W_l) / deg(d) = (sum_{d <- j} dz[d] /
+// deg(d)) W_l : scatter dz in the Fo-wide space first, then ONE dense MFMA
+// pass  dh[j] = [j < R] dz[j] W_r + g[j] W_l  over rows < Rn.  For the
+// products output layer (Fo = 47, K = 256) that is 5.4x fewer atomics and no
+// zero-fill of dh (every row < Rn is written once).
+//
+// ws = [W image | g]: the image ([KS][NTP][64] floats, MFMA A-operand order:
+// element (ks, t, lane = (i16, kk)) = Wcat[4 ks + kk][16 t + i16], Wcat =
+// [W_r ; W_l] with each half padded to C4 rows) is rebuilt every call by the
+// scatter launch's extra workgroups; g = [n_rows][C4] floats (C4 = Fo rounded
+// up to 4) is zero on entry and the dense pass clears each row as it reads
+// it, so g is zero again on exit.
+constexpr int LD_ROWS = 64;
+__host__ __device__ inline int64_t lowdim_img_floats(int64_t Fo, int ntp) {
+    const int64_t C4 = (Fo + 3) & ~int64_t{3};
+    return (C4 / 2) * ntp * 64;
+}
+
+template <bool MEAN, bool MASK>
+__global__ __launch_bounds__(256) void k_lowdim_scatter(
+    const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
+    float yscale, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ col, int n_rows,
+    const int32_t *__restrict__ r_ptr, int Fo, int C4, float *__restrict__ g, int n_scatter_wg,
+    const float *__restrict__ wl, const float *__restrict__ wr, int64_t ldw, int K, int ntp,
+    float *__restrict__ img) {
+    if (static_cast<int>(blockIdx.x) >= n_scatter_wg) {  // W image packing workgroups
+        const int64_t idx = (static_cast<int64_t>(blockIdx.x) - n_scatter_wg) * 256 + threadIdx.x;
+        if (idx >= lowdim_img_floats(Fo, ntp)) return;
+        const int ln = static_cast<int>(idx & 63);
+        const int t = static_cast<int>((idx >> 6) % ntp), ks = static_cast<int>(idx / (64 * ntp));
+        const int n = t * 16 + (ln & 15), i = ks * 4 + (ln >> 4);
+        float v = 0.0f;
+        if (n < K) {
+            if (i < C4) {
+                if (i < Fo) v = wr[static_cast<int64_t>(i) * ldw + n];
+            } else if (i - C4 < Fo) {
+                v = wl[static_cast<int64_t>(i - C4) * ldw + n];
+            }
+        }
+        img[idx] = v;
+        return;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int R = min(n_rows, *r_ptr);
+    for (int64_t d = blockIdx.x * 4 + wave; d < R; d += n_scatter_wg * 4) {
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        if (beg == end) continue;
+        const float inv = MEAN ? 1.0f / static_cast<float>(end - beg) : 1.0f;
+        for (int f0 = 0; f0 < Fo; f0 += 64) {
+            const int f = f0 + lane;
+            float v = 0.0f;
+            if (f < Fo) {
+                v = dy[d * ldy + f];
+                if (MASK) v = (y[d * ldyy + f] > 0.0f) ? v * yscale : 0.0f;
+                if (MEAN) v *= inv;
+            }
+            // sources preloaded 64 at a time and broadcast, so the atomics of
+            // one row issue back to back (no index load between them)
+            for (int eb = beg; eb < end; eb += 64) {
+                const int ne = min(64, end - eb);
+                const int mycol = lane < ne ? col[eb + lane] : 0;
+                for (int k = 0; k < ne; ++k) {
+                    const int64_t j = __shfl(mycol, k);
+                    if (f < Fo && v != 0.0f) atomicAdd(g + j * C4 + f, v);  // exact 0 adds nothing
+                }
+            }
+        }
+    }
+}
+
+// dense pass.  Workgroup (512 threads) = an even share [rb, re) of rows < Rn
+// on 16-row boundaries, staged 64 rows at a time as X = [dz | g] ([64][2 C4],
+// dz rows >= R and g rows >= Rn read as 0); the W image is copied to LDS once.
+// Wave w: row tile w >> 1, column half w & 1 (NTW tiles); a lane's
+// accumulator holds 4 consecutive output columns of one row -> 16-B stores.
+constexpr int LD_SU = 8;  // loads in flight per thread per staging batch
+template <int NTW, bool VOUT>
+__global__ __launch_bounds__(512, 1) void k_lowdim_gemm(
+    const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
+    float yscale, const float *__restrict__ img, int Fo, int K, int n_rows,
+    const int32_t *__restrict__ r_ptr, const int32_t *__restrict__ rn_ptr, float *__restrict__ g,
+    int C4, float *__restrict__ dh, int64_t ldd) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    constexpr int NTP = 2 * NTW;         // tiles in the image (K <= 16 NTP)
+    const int KS = C4 / 2;               // k-steps: 2 C4 / 4
+    const int LDX = 2 * C4 + 4;          // staged row stride (floats)
+    float *wimg = lsm;                   // [KS][NTP][64]
+    float *xs = lsm + KS * NTP * 64;     // [64][LDX]
+    const int R = min(n_rows, *r_ptr);
+    const int Rn = min(n_rows, *rn_ptr);
+    const int T16 = (Rn + 15) >> 4;      // 16-row tiles below Rn
+    const int G = gridDim.x;
+    const int rb = 16 * static_cast<int>(static_cast<int64_t>(blockIdx.x) * T16 / G);
+    const int re = min(Rn, 16 * static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * T16 / G));
+    if (rb >= re) return;
+    {  // W image -> LDS, LD_SU 16-B loads in flight per thread
+        const int n4 = KS * NTP * 16;
+        const v4f *src = reinterpret_cast<const v4f *>(img);
+        v4f *dst = reinterpret_cast<v4f *>(wimg);
+        for (int base = 0; base < n4; base += 512 * LD_SU) {
+            v4f t[LD_SU];
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int i = base + u * 512 + threadIdx.x;
+                if (i < n4) t[u] = src[i];
+            }
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int i = base + u * 512 + threadIdx.x;
+                if (i < n4) dst[i] = t[u];
+            }
+        }
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int rt = wave >> 1, chf = wave & 1;
+    const int i16 = lane & 15, kk = lane >> 4;
+    const int C44 = C4 >> 2;
+    for (int c0 = rb; c0 < re; c0 += LD_ROWS) {
+        __syncthreads();  // W image written / previous stage's reads done
+        const int nr = min(LD_ROWS, re - c0);
+        // dz half: scalar (Fo need not be a multiple of 4), rows < R only
+        for (int base = 0; base < LD_ROWS * C4; base += 512 * LD_SU) {
+            float t[LD_SU];
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int idx = base + u * 512 + threadIdx.x;
+                const int r = idx / C4, c = idx - r * C4;
+                const int64_t j = c0 + r;
+                t[u] = 0.0f;
+                if (r < nr && c < Fo && j < R) {
+                    float v = dy[j * ldy + c];
+                    if (y) v = (y[j * ldyy + c] > 0.0f) ? v * yscale : 0.0f;
+                    t[u] = v;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int idx = base + u * 512 + threadIdx.x;
+                const int r = idx / C4, c = idx - r * C4;
+                if (r < LD_ROWS) xs[r * LDX + c] = t[u];
+            }
+        }
+        // g half: 16-B loads, each read row cleared behind it
+        for (int base = 0; base < LD_ROWS * C44; base += 512 * LD_SU) {
+            v4f t[LD_SU];
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int idx = base + u * 512 + threadIdx.x;
+                const int r = idx / C44, c = (idx - r * C44) * 4;
+                t[u] = v4f{0.f, 0.f, 0.f, 0.f};
+                if (r < nr) {
+                    v4f *gp = reinterpret_cast<v4f *>(g + (c0 + r) * static_cast<int64_t>(C4) + c);
+                    t[u] = *gp;
+                    *gp = v4f{0.f, 0.f, 0.f, 0.f};  // leave g zero for the next call
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < LD_SU; ++u) {
+                const int idx = base + u * 512 + threadIdx.x;
+                const int r = idx / C44, c = (idx - r * C44) * 4;
+                if (r < LD_ROWS) *reinterpret_cast<v4f *>(xs + r * LDX + C4 + c) = t[u];
+            }
+        }
+        __syncthreads();
+        if (rt * 16 >= nr) continue;  // this wave's row tile is past the stage
+        v4f acc[NTW];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+        const float *xb = xs + (rt * 16 + i16) * LDX + kk;
+        const float *wb = wimg + chf * NTW * 64 + lane;
+        float b = xb[0], a[NTW];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) a[t] = wb[t * 64];
+        for (int ks = 0; ks < KS; ++ks) {  // LDS reads of ks+1 before the MFMAs of ks
+            const int kn = min(ks + 1, KS - 1);
+            const float bn = xb[kn * 4];
+            float an[NTW];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) an[t] = wb[(kn * NTP + t) * 64];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b, acc[t], 0, 0, 0);
+            b = bn;
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) a[t] = an[t];
+        }
+        const int64_t row = c0 + rt * 16 + i16;
+        if (row < re) {
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) {
+                const int f = (chf * NTW + t) * 16 + 4 * kk;
+                float *o = dh + row * ldd + f;
+                if (VOUT) {
+                    if (f < K) *reinterpret_cast<v4f *>(o) = acc[t];
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (f + jj < K) o[jj] = acc[t][jj];
+                }
+            }
+        }
+    }
+}
+
 int lpr_for(int64_t K, int vec) {
     const int64_t chunks = ceil_div(K, vec);
     int l = 4;
@@ -840,5 +1044,94 @@ extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *
     } else {
         if (lds_w) go(RX{}, T{}); else go(RX{}, Fb{});
     }
+    return launch_status();
+}
+
+// ---- low-dimensional input gradient: C ABI
+static int lowdim_ntw(int64_t K) {
+    const int64_t half = ceil_div(ceil_div(K, 16), 2);
+    int t = 1;
+    while (t < half) t <<= 1;
+    return t;
+}
+static size_t lowdim_lds_bytes(int64_t Fo, int ntw) {
+    const int64_t C4 = (Fo + 3) & ~int64_t{3};
+    return sizeof(float) * static_cast<size_t>(lowdim_img_floats(Fo, 2 * ntw) + LD_ROWS * (2 * C4 + 4));
+}
+constexpr size_t LOWDIM_LDS_MAX = 150 * 1024;
+
+extern "C" size_t ngnn_sage_dgrad_lowdim_workspace_bytes(int64_t n_rows, int64_t Fo, int64_t K) {
+    if (n_rows <= 0 || Fo <= 0 || K <= 0) return 0;
+    const size_t img = sizeof(float) * static_cast<size_t>(lowdim_img_floats(Fo, 2 * lowdim_ntw(K)));
+    return ((img + 255) & ~size_t{255}) +
+           sizeof(float) * static_cast<size_t>(n_rows) * static_cast<size_t>((Fo + 3) & ~int64_t{3});
+}
+
+extern "C" int ngnn_sage_dgrad_lowdim(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
+                                      float yscale, const float *wl, const float *wr, int64_t ldw,
+                                      int64_t Fo, int64_t K, const int32_t *rowptr,
+                                      const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
+                                      const int32_t *rnext_ptr, int reduce, float *dh, int64_t ldd,
+                                      int zero_tail, void *ws, size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(reduce != NGNN_REDUCE_SUM && reduce != NGNN_REDUCE_MEAN, NGNN_E_ARG);
+    NGNN_RETURN_IF(!dy || !wl || !wr || !rowptr || !col || !r_ptr || !rnext_ptr || !dh, NGNN_E_ARG);
+    NGNN_RETURN_IF(Fo <= 0 || K <= 0 || n_rows < 0, NGNN_E_ARG);
+    NGNN_RETURN_IF(ldy < Fo || (y && ldyy < Fo) || ldd < K || ldw < K, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
+    const int ntw = lowdim_ntw(K);
+    NGNN_RETURN_IF(ntw > 16 || lowdim_lds_bytes(Fo, ntw) > LOWDIM_LDS_MAX, NGNN_E_SHAPE);
+    if (n_rows == 0) return NGNN_OK;
+    NGNN_RETURN_IF(!ws || ws_bytes < ngnn_sage_dgrad_lowdim_workspace_bytes(n_rows, Fo, K) ||
+                       !aligned(ws, 16), NGNN_E_WORKSPACE);
+    hipStream_t st = as_stream(stream);
+    const int C4 = static_cast<int>((Fo + 3) & ~int64_t{3});
+    const int ntp = 2 * ntw;
+    const int64_t img_n = lowdim_img_floats(Fo, ntp);
+    float *img = static_cast<float *>(ws);
+    float *g = img + (((img_n * 4 + 255) & ~int64_t{255}) >> 2);
+    if (zero_tail) {  // rows >= Rn of the returned gradient
+        const unsigned gi = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows * K, 256), 4096));
+        hipLaunchKernelGGL(k_dh_init, dim3(gi), dim3(256), 0, st, (const float *)nullptr, K,
+                           (int)n_rows, r_ptr, rnext_ptr, (int)K, dh, ldd, 1);
+    }
+    const int gs = static_cast<int>(std::min<int64_t>(ceil_div(n_rows, 4), 2048));
+    const int gp = static_cast<int>(ceil_div(img_n, 256));
+    auto scatter = [&](auto mean_c, auto mask_c) {
+        hipLaunchKernelGGL((k_lowdim_scatter<decltype(mean_c)::value, decltype(mask_c)::value>),
+                           dim3(gs + gp), dim3(256), 0, st, dy, ldy, y, ldyy, yscale, rowptr, col,
+                           (int)n_rows, r_ptr, (int)Fo, C4, g, gs, wl, wr, ldw, (int)K, ntp, img);
+    };
+    using T = std::true_type;
+    using Fb = std::false_type;
+    const bool mean = reduce == NGNN_REDUCE_MEAN;
+    if (mean) { if (y) scatter(T{}, T{}); else scatter(T{}, Fb{}); }
+    else { if (y) scatter(Fb{}, T{}); else scatter(Fb{}, Fb{}); }
+    int rc = launch_status();
+    if (rc) return rc;
+    const bool vout = (K % 4 == 0) && (ldd % 4 == 0) && aligned(dh, 16);
+    const size_t lds = lowdim_lds_bytes(Fo, ntw);
+    const unsigned gg = static_cast<unsigned>(
+        std::max<int64_t>(1, std::min<int64_t>(dgrad_num_cus(), ceil_div(n_rows, 16))));
+    auto gemm = [&](auto ntw_c, auto vout_c) {
+        auto fn = k_lowdim_gemm<decltype(ntw_c)::value, decltype(vout_c)::value>;
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, LOWDIM_LDS_MAX);
+            attr = true;
+        }
+        hipLaunchKernelGGL(fn, dim3(gg), dim3(512), lds, st, dy, ldy, y, ldyy, yscale, img,
+                           (int)Fo, (int)K, (int)n_rows, r_ptr, rnext_ptr, g, C4, dh, ldd);
+    };
+    auto by_ntw = [&](auto vout_c) {
+        switch (ntw) {
+            case 1: gemm(std::integral_constant<int, 1>{}, vout_c); break;
+            case 2: gemm(std::integral_constant<int, 2>{}, vout_c); break;
+            case 4: gemm(std::integral_constant<int, 4>{}, vout_c); break;
+            case 8: gemm(std::integral_constant<int, 8>{}, vout_c); break;
+            default: gemm(std::integral_constant<int, 16>{}, vout_c); break;
+        }
+    };
+    if (vout) by_ntw(T{}); else by_ntw(Fb{});
     return launch_status();
 }

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -63,6 +63,10 @@ SIGNATURES = {
     "ngnn_sage_dgrad_fused": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _i64, _i64, _p,
                                      _p, _i64, _p, _p, _int, _p, _i64, _p, _i64, _p, _i64, _int,
                                      _p]),
+    "ngnn_sage_dgrad_lowdim_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "ngnn_sage_dgrad_lowdim": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _i64, _i64,
+                                      _i64, _p, _p, _i64, _p, _p, _int, _p, _i64, _int, _p, _sz,
+                                      _p]),
 }
 
 _lib = None

@@ -16,6 +16,10 @@ edges into rows < R) for the layer below.  Per layer:
 
 * ``ngnn_sage_wgrad``: dW_r, dW_l, db over rows < R (ReLU/dropout backward
   fused into the staging of dz), fixed-order reduction;
+* input gradient (MEAN/SUM, Fo < K, the default): ``ngnn_sage_dgrad_lowdim``
+  scatters dz in the narrow Fo-wide space, then one MFMA pass writes
+  dh = dz W_r + g W_l for rows < R'; otherwise ``ngnn_sage_dgrad_fused``
+  (per-row products + K-wide atomics), or in deterministic mode
 * ``ngnn_sage_fwd`` in dgrad mode: [dz W_l | dz W_r] for rows < R;
 * ``ngnn_sage_dgrad_gather``: input gradient rows < R' = root term + the
   transposed aggregation over the source-grouped CSR (edges into rows >= R
@@ -191,6 +195,24 @@ class _SAGEStack(torch.autograd.Function):
             _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
                                                    bptr(i + 1), None, bptr(i), block.E, stream),
                        "ngnn_block_prefix_stats")
+            if not deterministic and Fo < K and reduce in ("sum", "mean"):
+                # narrow-space path: scatter dz (Fo wide), then one MFMA pass
+                dh = torch.empty(N, K, dtype=torch.float32, device=dev)
+                wlc, wrc = wl.detach().contiguous(), wr.detach().contiguous()
+                gws = _workspace(dev, ("dgrad_lowdim", Fo, K),  # g stays zero per shape
+                                 lib.ngnn_sage_dgrad_lowdim_workspace_bytes(N, Fo, K), zero=True)
+                with _timing.span("sage_dgrad_lowdim", 0, 0):
+                    rc = lib.ngnn_sage_dgrad_lowdim(
+                        _lib.ptr(dy), dy.stride(0), _lib.ptr(ymask),
+                        ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(wlc),
+                        _lib.ptr(wrc), wlc.stride(0), Fo, K, _lib.ptr(block.rowptr),
+                        _lib.ptr(block.col), N, bptr(i + 1), bptr(i), red, _lib.ptr(dh),
+                        dh.stride(0), int(i == 0), _lib.ptr(gws), gws.numel(), stream)
+                if rc == _lib.OK:
+                    dy = dh
+                    continue
+                if rc != _lib.E_SHAPE:
+                    _lib.check(rc, "ngnn_sage_dgrad_lowdim")
             if not deterministic and Fo <= 512:
                 # atomic path: per-row VALU products + scatter, no dgrad GEMM launch
                 dh = torch.empty(N, K, dtype=torch.float32, device=dev)

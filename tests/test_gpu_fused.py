@@ -217,3 +217,89 @@ def test_zero_gradient_and_no_grad_paths():
     with torch.no_grad():
         o2 = m.eval()(x, ei.to(DEV))
     assert o2.shape == (N, 4)
+
+
+def _dgrad_dense_ref(dy, y, yscale, wl, wr, ei, N, R, reduce):
+    """fp32 torch reference of a layer's input gradient on the rows the
+    bounded backward writes: dz = dy (* [y > 0] * yscale) on rows < R,
+    dh = dz W_r + A^T (dz / deg) W_l  (edges into rows >= R dropped)."""
+    dz = dy.clone()
+    if y is not None:
+        dz = torch.where(y > 0, dz * yscale, torch.zeros_like(dz))
+    dz[R:] = 0
+    src, dst = ei[0], ei[1]
+    deg = torch.bincount(dst, minlength=N).clamp(min=1).float()
+    m = dz[dst] / deg[dst, None] if reduce == "mean" else dz[dst]
+    dagg = torch.zeros_like(dz).index_add_(0, src, m)
+    return dz @ wr + dagg @ wl
+
+
+def _lowdim_img_bytes(Fo, K):
+    """Offset of g in the lowdim workspace (include/ngnn.h: [W image | g])."""
+    c4, half, ntw = (Fo + 3) // 4 * 4, -(-(-(-K // 16)) // 2), 1
+    while ntw < half:
+        ntw *= 2
+    return ((c4 // 2) * 2 * ntw * 64 * 4 + 255) // 256 * 256
+
+
+@pytest.mark.parametrize("Fo,K,reduce,masked", [
+    (47, 256, "mean", False), (47, 256, "sum", True), (10, 48, "mean", True), (5, 30, "sum", False),
+    (8, 300, "mean", True), (12, 100, "mean", False), (3, 17, "mean", True)])
+def test_dgrad_lowdim_abi(Fo, K, reduce, masked):
+    """ngnn_sage_dgrad_lowdim (narrow-space scatter + MFMA pass) against a
+    dense fp32 reference: rows < R' written, rows >= R' untouched, the
+    workspace left zero; a second call gives the same result."""
+    from ngnn import _lib
+    lib = _lib.load()
+    N, E, R = 700, 5000, 150
+    ei = rand_block(Fo * 7 + K, N, E)
+    g = torch.Generator().manual_seed(K)
+    dy = torch.randn(N, Fo, generator=g)
+    y = torch.randn(N, Fo, generator=g) if masked else None
+    wl, wr = torch.randn(Fo, K, generator=g) * 0.2, torch.randn(Fo, K, generator=g) * 0.2
+    yscale = 2.0 if masked else 1.0
+    ref = _dgrad_dense_ref(dy, y, yscale, wl, wr, ei, N, R, reduce)
+    src_into = ei[0][ei[1] < R]
+    Rn = max(R, int(src_into.max()) + 1 if src_into.numel() else 0)
+    blk = Block(ei.to(DEV), N)
+    bnd = torch.tensor([Rn, R], dtype=torch.int32, device=DEV)
+    ws = torch.zeros(lib.ngnn_sage_dgrad_lowdim_workspace_bytes(N, Fo, K), dtype=torch.uint8,
+                     device=DEV)
+    dyd, wld, wrd = dy.to(DEV), wl.to(DEV), wr.to(DEV)
+    yd = y.to(DEV) if masked else None
+    outs = []
+    for _ in range(2):
+        dh = torch.full((N, K), 7.0, device=DEV)
+        rc = lib.ngnn_sage_dgrad_lowdim(
+            _lib.ptr(dyd), Fo, _lib.ptr(yd), Fo, yscale, _lib.ptr(wld), _lib.ptr(wrd), K, Fo, K,
+            _lib.ptr(blk.rowptr), _lib.ptr(blk.col), N, bnd.data_ptr() + 4, bnd.data_ptr(),
+            _lib.REDUCE[reduce], _lib.ptr(dh), K, 0, _lib.ptr(ws), ws.numel(),
+            _lib.stream_handle(DEV))
+        _lib.check(rc, "ngnn_sage_dgrad_lowdim")
+        torch.cuda.synchronize()
+        assert not ws[_lowdim_img_bytes(Fo, K):].any(), "g not left zero"
+        outs.append(dh.cpu())
+    torch.testing.assert_close(outs[0][:Rn], ref[:Rn], **GRAD)
+    assert torch.all(outs[0][Rn:] == 7.0)  # rows >= R' untouched
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-6, atol=1e-6)
+
+
+def test_dgrad_lowdim_shape_envelope():
+    """Weight images past the LDS budget are refused with NGNN_E_SHAPE (the
+    backward then takes ngnn_sage_dgrad_fused)."""
+    from ngnn import _lib
+    lib = _lib.load()
+    N, Fo, K = 64, 47, 500
+    ei = rand_block(1, N, 200)
+    blk = Block(ei.to(DEV), N)
+    bnd = torch.tensor([N, N], dtype=torch.int32, device=DEV)
+    dy = torch.randn(N, Fo, device=DEV)
+    w = torch.randn(Fo, K, device=DEV)
+    dh = torch.empty(N, K, device=DEV)
+    ws = torch.zeros(lib.ngnn_sage_dgrad_lowdim_workspace_bytes(N, Fo, K), dtype=torch.uint8,
+                     device=DEV)
+    rc = lib.ngnn_sage_dgrad_lowdim(
+        _lib.ptr(dy), Fo, None, Fo, 1.0, _lib.ptr(w), _lib.ptr(w), K, Fo, K, _lib.ptr(blk.rowptr),
+        _lib.ptr(blk.col), N, bnd.data_ptr(), bnd.data_ptr() + 4, _lib.REDUCE["mean"],
+        _lib.ptr(dh), K, 0, _lib.ptr(ws), ws.numel(), _lib.stream_handle(DEV))
+    assert rc == _lib.E_SHAPE
