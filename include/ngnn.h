@@ -303,12 +303,17 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * untouched), edge_index [2, E] (row stride ld_ei) plus padding self-loops
  * on rows N + floor(j (n_cap - N) / (e_cap - E)) for slot edges E + j, the
  * first B labels, and *n_valid = N.  Padding needs N < n_cap when E < e_cap.
+ * Optional (NULL to skip): slot_rowptr [n_cap + 1] / slot_col [e_cap] int32
+ * = the target-grouped CSR of the padded edges (both or neither; targets
+ * must be non-decreasing, NeighborLoader's order), and *seed_state advanced
+ * by one splitmix64 step (the dropout seed of the captured step).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
-                   int64_t *slot_y, int32_t *n_valid, void *stream);
+                   int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
+                   uint64_t *seed_state, void *stream);
 
 #ifdef __cplusplus
 }

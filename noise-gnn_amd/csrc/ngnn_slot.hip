@@ -7,7 +7,13 @@
 //                       padding row gets more than ceil(n_pad / (n_cap - N))
 //   labels [0, B)       copied
 //   *n_valid = N        (the forward kernels skip rows >= N)
+//   optional: the target-grouped CSR of the padded edges (rowptr int32
+//   [n_cap + 1] by lower bound over the non-decreasing targets, col int32
+//   [e_cap]), so the captured step needs no CSR-build launches; and the
+//   dropout seed state advanced by one splitmix64 step (a fresh mask per
+//   replay without a device RNG launch).
 // Replaces the ~8 torch copy / arithmetic launches the slot load took.
+// Requires target-sorted edges (NeighborLoader's order), as the CSR fast path.
 #include "ngnn_internal.h"
 
 namespace ngnn {
@@ -17,7 +23,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
     const float *__restrict__ x, int64_t ldx, int64_t N, int64_t F, const int64_t *__restrict__ ei,
     int64_t ld_ei, int64_t E, const int64_t *__restrict__ y, int64_t B, float *__restrict__ sx,
     int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
-    int32_t *__restrict__ n_valid, int vec) {
+    int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
+    uint64_t *__restrict__ seed_state, int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (vec) {
@@ -48,7 +55,39 @@ __global__ __launch_bounds__(256) void k_slot_load(
         sei[e_cap + e] = d;
     }
     for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
-    if (tid == 0) *n_valid = static_cast<int32_t>(N);
+    if (rowptr) {
+        // rowptr[r] = first padded edge with target >= r.  Real edges
+        // (targets < N, sorted): binary search; padding: closed form
+        // (target of padding edge j is N + floor(j span / n_pad)).
+        for (int64_t r = tid; r <= n_cap; r += nthr) {
+            int64_t e;
+            if (r <= N) {
+                int64_t lo = 0, hi = E;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (ei[ld_ei + mid] < r) lo = mid + 1;
+                    else hi = mid;
+                }
+                e = lo;
+            } else if (n_pad > 0) {
+                e = E + min(n_pad, ((r - N) * n_pad + span - 1) / span);
+            } else {
+                e = E;
+            }
+            rowptr[r] = static_cast<int32_t>(r == n_cap ? e_cap : e);
+        }
+        for (int64_t e = tid; e < e_cap; e += nthr)
+            col[e] = static_cast<int32_t>(e < E ? ei[e] : N + ((e - E) * span) / n_pad);
+    }
+    if (tid == 0) {
+        *n_valid = static_cast<int32_t>(N);
+        if (seed_state) {  // splitmix64 step: state <- mix(state + golden gamma)
+            uint64_t z = *seed_state + 0x9e3779b97f4a7c15ULL;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+            *seed_state = z ^ (z >> 31);
+        }
+    }
 }
 
 }  // namespace
@@ -60,6 +99,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               const int64_t *edge_index, int64_t ld_ei, int64_t E, const int64_t *y,
                               int64_t B, float *slot_x, int64_t ld_slot, int64_t n_cap,
                               int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
+                              int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || !slot_x || !slot_ei || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
@@ -67,13 +107,14 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E, NGNN_E_SHAPE);
     // padding needs rows to land on: at least one row past N when edges are padded
     NGNN_RETURN_IF(N > n_cap || E > e_cap || (E < e_cap && N >= n_cap), NGNN_E_SHAPE);
-    NGNN_RETURN_IF(!fits_i32(N) || !fits_i32(n_cap), NGNN_E_RANGE);
+    NGNN_RETURN_IF(!fits_i32(N) || !fits_i32(n_cap) || !fits_i32(e_cap), NGNN_E_RANGE);
+    NGNN_RETURN_IF((slot_rowptr == nullptr) != (slot_col == nullptr), NGNN_E_ARG);
     const int vec = (F % 4 == 0) && (ldx % 4 == 0) && (ld_slot % 4 == 0) && aligned(x, 16) &&
                     aligned(slot_x, 16);
-    const int64_t work = std::max<int64_t>({N * F / 4, e_cap, B, 1});
+    const int64_t work = std::max<int64_t>({N * F / 4, e_cap, n_cap + 1, B, 1});
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
-                       n_valid, vec);
+                       n_valid, slot_rowptr, slot_col, seed_state, vec);
     return launch_status();
 }

@@ -69,7 +69,7 @@ class Block:
 
     def __init__(self, edge_index: torch.Tensor, num_nodes: int, *, n_dst: int | None = None,
                  validate: bool = True, dst_sorted: bool | None = None,
-                 src_sorted: bool | None = None):
+                 src_sorted: bool | None = None, csr: "CSR | None" = None):
         _require_device_index(edge_index)
         edge_index = edge_index.contiguous()
         self.edge_index = edge_index
@@ -89,12 +89,17 @@ class Block:
                 raise IndexError(f"edge_index[1] holds ids outside [0, {self.n_dst})")
             dst_sorted, src_sorted = not s[2], not s[3]
         self.dst_sorted, self.src_sorted = bool(dst_sorted), bool(src_sorted)
-        self.csr = build_csr(edge_index[1], edge_index[0], self.n_dst, self.dst_sorted)
+        # csr: the target-grouped CSR built by a producer (the HIP-graph slot
+        # load writes it with the slot's edges), else built here
+        self.csr = csr if csr is not None else build_csr(edge_index[1], edge_index[0], self.n_dst,
+                                                         self.dst_sorted)
         self._csr_t = None
         self.n_active = None  # leading rows with in-edges, if a producer told us
         # device int32 scalar: rows >= it are padding (a static HIP-graph slot);
         # the forward kernels skip them.  None: every row is real.
         self.n_rows_dev = None
+        # device uint64 dropout seed supplied by a producer (graph slot), or None
+        self.seed_dev = None
 
     @property
     def rowptr(self):
@@ -133,9 +138,10 @@ class _BlockCache:
         hint = _hint_for(edge_index)
         if hint is not None:
             blk = Block(edge_index, num_nodes, validate=False, dst_sorted=hint[0],
-                        src_sorted=hint[1])
+                        src_sorted=hint[1], csr=hint[4])
             blk.n_active = hint[2]
             blk.n_rows_dev = hint[3]
+            blk.seed_dev = hint[5]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -159,14 +165,17 @@ _hints_lock = threading.Lock()
 
 
 def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: bool,
-                    n_active: int | None = None, n_rows_dev: torch.Tensor | None = None) -> None:
+                    n_active: int | None = None, n_rows_dev: torch.Tensor | None = None,
+                    csr: CSR | None = None, seed_dev: torch.Tensor | None = None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
     later rows have none) -- only used for roofline accounting.  n_rows_dev:
-    device int32 scalar bounding the real rows of a padded slot."""
+    device int32 scalar bounding the real rows of a padded slot.  csr: a
+    target-grouped CSR of these edges kept current by the producer.
+    seed_dev: device uint64 dropout seed the producer advances per batch."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
-                                  n_rows_dev)
+                                  n_rows_dev, csr, seed_dev)
 
 
 def _drop_hint(key):
@@ -179,7 +188,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4], h[5]
+    return h[2], h[3], h[4], h[5], h[6], h[7]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

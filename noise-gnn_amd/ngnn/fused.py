@@ -158,12 +158,12 @@ class _SAGEStack(torch.autograd.Function):
         grads = [None] * (3 * L)
         dy = dout if dout.stride(1) == 1 else dout.contiguous()
         # bnd[L] = rows of dout that can be nonzero; bnd[i] = same for d(acts[i])
-        bnd = torch.zeros(L + 1, dtype=torch.int32, device=dev)
-        bptr = lambda j: bnd.data_ptr() + 4 * j  # noqa: E731
+        # (prefix_stats takes max(bnd[i], R, ...), so R is a valid initial bnd[i])
         rows_hint = getattr(dout, "_ngnn_nonzero_rows", None)  # set by ngnn.losses
-        if rows_hint is not None:
-            bnd[L:].fill_(int(rows_hint))
-        else:
+        bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
+                         dtype=torch.int32, device=dev)
+        bptr = lambda j: bnd.data_ptr() + 4 * j  # noqa: E731
+        if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")
         # input-gradient scatter: float atomics by default (as the reference's CUDA

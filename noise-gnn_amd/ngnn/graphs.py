@@ -8,8 +8,10 @@ backward kernels, Adam -- is captured once into a HIP graph (through
 graph launch instead of ~30 kernel launches and ~100 Python/ATen calls.
 The step is capturable because the ngnn path never reads device values on the
 host: block row bounds, backward receptive-field bounds and the dropout seed
-(``seed_dev``, drawn by torch's graph-safe RNG inside the graph) live on the
-device.
+live on the device.  The slot load (one launch before each replay) also
+writes the target-grouped CSR of the padded edges and advances the dropout
+seed, so the graph holds no CSR-build or RNG launches.  Edges must be
+target-sorted (NeighborLoader's order).
 
 Shapes are static: the slot holds ``n_cap`` node rows and ``e_cap`` edges.
 A batch with N nodes and E edges fills rows ``[0, N)`` and edges ``[0, E)``;
@@ -27,7 +29,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .block import block_cache, hint_edge_index
+from .block import CSR, block_cache, hint_edge_index
 from .losses import seed_cross_entropy
 
 
@@ -46,6 +48,11 @@ class GraphedTrainStep:
         self.ei = torch.zeros(2, self.e_cap, dtype=torch.int64, device=dev)
         self.y = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.n_valid = torch.full((1,), self.n_cap, dtype=torch.int32, device=dev)
+        # the slot load also writes the CSR of the padded edges and advances
+        # the dropout seed, so the captured step builds neither
+        self.rowptr = torch.zeros(self.n_cap + 1, dtype=torch.int32, device=dev)
+        self.col = torch.zeros(self.e_cap, dtype=torch.int32, device=dev)
+        self.seed_state = torch.randint(0, 2**62, (1,), dtype=torch.int64).to(dev)
         self.g_fb = self.g_opt = None
         self.loss = None
 
@@ -64,6 +71,7 @@ class GraphedTrainStep:
             _lib.ptr(x), x.stride(0), N, x.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
             _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
             _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
+            _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
             _lib.stream_handle(self.x.device)), "ngnn_slot_load")
 
     def _fwd_bwd(self):
@@ -97,7 +105,8 @@ class GraphedTrainStep:
         # the captured Block must be built inside the graph (from the slot's
         # contents at replay time), never served from the eager cache
         block_cache.clear()
-        hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid)
+        hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
+                        csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state)
         self.opt.zero_grad(set_to_none=True)
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):

@@ -50,9 +50,12 @@ class SAGE(nn.Module):
             seed, seed_dev = 0, None
             if self.training and self.dropout > 0:
                 if torch.cuda.is_current_stream_capturing():
-                    # HIP-graph capture: the seed is drawn on the device by torch's
-                    # graph-safe generator, i.e. afresh at every replay
-                    seed_dev = torch.randint(0, 2**62, (1,), device=x.device)
+                    # HIP-graph capture: a device seed, fresh at every replay --
+                    # the slot's (advanced by each slot load), else drawn by
+                    # torch's graph-safe generator inside the graph
+                    seed_dev = block.seed_dev
+                    if seed_dev is None:
+                        seed_dev = torch.randint(0, 2**62, (1,), device=x.device)
                 else:
                     seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
             return fused.sage_stack(self, x, block, seed, seed_dev)

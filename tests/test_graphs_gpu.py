@@ -84,3 +84,26 @@ def test_slot_padding_rows_inert():
         full = m(step.x, step.ei)[:b.num_nodes]
         ref = m(b.x, b.edge_index)
     torch.testing.assert_close(full, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("tight", [False, True])
+def test_slot_csr_and_seed(tight):
+    """The CSR the slot load writes equals the one the Block builder makes
+    from the slot's padded edges (with and without padding edges), and the
+    dropout seed state moves on every load."""
+    from ngnn.block import build_csr
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    m, batches = _setup(0.0)
+    b = batches[2]
+    N, E = b.x.size(0), b.edge_index.size(1)
+    n_cap, e_cap = (N + 1, E) if tight else slot_size(256, [10, 5])
+    opt = torch.optim.Adam(m.parameters(), lr=0.0, fused=True, capturable=True)
+    step = GraphedTrainStep(m, opt, 256, n_cap, e_cap, b.x.size(1), DEV)
+    seeds = []
+    for _ in range(2):
+        step.load(b.x, b.edge_index, b.y)
+        seeds.append(int(step.seed_state.item()))
+    ref = build_csr(step.ei[1], step.ei[0], n_cap, True)
+    assert torch.equal(step.rowptr, ref.rowptr)
+    assert torch.equal(step.col, ref.col)
+    assert seeds[0] != seeds[1]

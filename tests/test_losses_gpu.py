@@ -10,11 +10,11 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-@pytest.mark.parametrize("C", [47, 10, 130])
-def test_value_and_grad(C):
+@pytest.mark.parametrize("C,B", [(47, 256), (10, 256), (130, 256), (47, 5000)])
+def test_value_and_grad(C, B):
     from ngnn.losses import seed_cross_entropy
     g = torch.Generator().manual_seed(C)
-    N, B = 700, 256
+    N = B + 444
     x = (torch.randn(N, C, generator=g) * 3).to(DEV).requires_grad_(True)
     y = torch.randint(0, C, (N,), generator=g).to(DEV)
     y[5] = -100  # ignored label
