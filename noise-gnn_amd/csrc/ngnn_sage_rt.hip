@@ -40,7 +40,9 @@ constexpr int RT_ROWS = 16;  // rows per wave tile (one MFMA n-tile)
 constexpr int RT_KC = 8;     // k-groups of 16 per chunk (128 columns of K)
 // waves per workgroup: 2 per SIMD (<= 256 VGPRs: accumulators, the current
 // and the prefetched x fragments, two W fragment sets)
-constexpr int rt_waves(int) { return 8; }
+// PRE (aggregate precomputed by k_rt_agg, no gather code): fewer live
+// registers, so narrow outputs run 4 waves per SIMD to hide the x stream
+constexpr int rt_waves(int ntw, bool pre) { return (pre && ntw <= 3) ? 16 : 8; }
 
 struct RtArgs {
     const float *x;
@@ -317,9 +319,9 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     }
 }
 
-template <int NTW, int RED, bool WL_LDS>
-__global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
-    constexpr int RT_WAVES = rt_waves(NTW);
+template <int NTW, int RED, bool WL_LDS, bool PRE>
+__global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
+    constexpr int RT_WAVES = rt_waves(NTW, PRE);
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
     const int nfr = NTW * a.KG * 64;  // fragments per weight matrix (NTW tiles, zero padded)
     v4f *swr = lds;
@@ -432,7 +434,28 @@ __global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
         }
 
         // ---- neighbour term (tiles with in-edges only)
-        if (maxdeg > 0) {
+        if (PRE && maxdeg > 0) {
+            // aggregate rows written by k_rt_agg (rows with in-edges only;
+            // others masked to 0, as the gather's empty-row result)
+            const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
+            const int mrow = lt_mask(0, deg);
+            for (int c = 0; c < nchunk; ++c) {
+                const int k0 = c * RT_KC * 16;
+                const int nkg = min(RT_KC, a.KG - c * RT_KC);
+                const int kq = a.K - k0 - 4 * q;
+                const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
+                v4f ag[RT_KC];
+#pragma unroll
+                for (int g = 0; g < RT_KC; ++g) ag[g] = buf_load4(ar, aoff + 64 * g, 0, 0);
+#pragma unroll
+                for (int g = 0; g < RT_KC; ++g) ag[g] = and_mask(ag[g], mrow & lt_mask(16 * g, kq));
+                if constexpr (WL_LDS)
+                    mfma_chunk_rt<NTW, true>(acc, ag, swl, a.KG, c * RT_KC, nkg, a.NT, lane);
+                else
+                    mfma_chunk_rt<NTW, false>(acc, ag, a.wl, a.KG, c * RT_KC, nkg, a.NT, lane);
+            }
+        }
+        if (!PRE && maxdeg > 0) {
             const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
             for (int c = 0; c < nchunk; ++c) {
                 const int k0 = c * RT_KC * 16;
@@ -463,6 +486,78 @@ __global__ __launch_bounds__(rt_waves(NTW) * 64) void k_sage_rt(RtArgs a) {
     }
 }
 
+// ---- aggregate pre-pass for the PRE kernels: agg[r] = reduce over the CSR
+// row r of x, for rows r < n_rows (and < *n_rows_dev) WITH in-edges only
+// (edgeless rows are never written; the layer kernel masks them to 0).  LPR
+// lanes per row, 16-B loads, RT_AGG_UNR neighbour rows in flight per group,
+// per column in edge order from the identity then / max(deg, 1): the fp32
+// sequence of ngnn_seg_agg_fwd, bit-identical.  Rows are interleaved over
+// the (resident) grid's groups, so a NeighborLoader block's edge rows (a
+// prefix) spread over every CU.
+constexpr int RT_AGG_UNR = 8;
+template <int RED, int LPR>
+__global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x, int64_t ldx, int K,
+                                                const int32_t *__restrict__ rowptr,
+                                                const int32_t *__restrict__ col, int n_rows,
+                                                const int32_t *__restrict__ n_rows_dev,
+                                                float *__restrict__ agg, int64_t ld_agg) {
+    constexpr int GPW = 256 / LPR;
+    const int lane = threadIdx.x % LPR;
+    int nr = n_rows;
+    if (n_rows_dev) nr = min(nr, *n_rows_dev);
+    const int ngroups = gridDim.x * GPW;
+    const int gid = blockIdx.x * GPW + threadIdx.x / LPR;
+    const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
+    // the group's rows gid + j ngroups, LPR of them per round: lane j loads
+    // row j's bounds (one load round for LPR rows, so edgeless rows cost no
+    // latency chain), then the group walks the rows that have in-edges
+    for (int r0 = gid; r0 < nr; r0 += LPR * ngroups) {
+        const int my = r0 + lane * ngroups;
+        int mb = 0, me = 0;
+        if (my < nr) {
+            mb = rowptr[my];
+            me = rowptr[my + 1];
+        }
+        for (int j = 0; j < LPR; ++j) {
+        const int beg = __shfl(mb, j, LPR), end = __shfl(me, j, LPR);
+        if (beg == end) continue;
+        const int row = r0 + j * ngroups;
+        for (int f0 = 0; f0 < K; f0 += 4 * LPR) {
+            const int f = f0 + 4 * lane;
+            const bool act = f < K;
+            const int fc = act ? f : 0;
+            v4f acc{ident, ident, ident, ident};
+            for (int eb = beg; eb < end; eb += LPR) {
+                const int n = min(LPR, end - eb);
+                const int myc = lane < n ? col[eb + lane] : 0;
+                // RT_AGG_UNR rows in flight per batch; a short last batch
+                // re-reads its last row (cached) and skips the extra terms
+                for (int k = 0; k < n; k += RT_AGG_UNR) {
+                    v4f v[RT_AGG_UNR];
+#pragma unroll
+                    for (int u = 0; u < RT_AGG_UNR; ++u) {
+                        const int64_t c = __shfl(myc, min(k + u, n - 1), LPR);
+                        v[u] = *reinterpret_cast<const v4f *>(x + c * ldx + fc);
+                    }
+#pragma unroll
+                    for (int u = 0; u < RT_AGG_UNR; ++u)
+                        if (k + u < n)
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) acc[i] = red_op<RED>(acc[i], v[u][i]);
+                }
+            }
+            if (!act) continue;
+            if (RED == NGNN_REDUCE_MEAN) {
+                const float cnt = static_cast<float>(end - beg);  // deg >= 1 here
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = acc[i] / cnt;
+            }
+            *reinterpret_cast<v4f *>(agg + static_cast<int64_t>(row) * ld_agg + f) = acc;
+        }
+        }
+    }
+}
+
 int g_num_cus[64];
 
 int num_cus() {
@@ -478,32 +573,42 @@ int num_cus() {
     return g_num_cus[dev];
 }
 
-template <int NTW, int RED, bool WL_LDS>
+template <int NTW, int RED, bool WL_LDS, bool PRE>
 int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
-    auto fn = k_sage_rt<NTW, RED, WL_LDS>;
+    auto fn = k_sage_rt<NTW, RED, WL_LDS, PRE>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    constexpr int W = rt_waves(NTW);
+    constexpr int W = rt_waves(NTW, PRE);
     const int grid = static_cast<int>(
         std::max<int64_t>(1, std::min<int64_t>(num_cus(), ceil_div(n_tiles, W))));
     hipLaunchKernelGGL(fn, dim3(grid), dim3(W * 64), lds_bytes, st, a);
     return launch_status();
 }
 
-template <int NTW>
+template <int NTW, bool PRE>
 int dispatch_red(const RtArgs &a, int reduce, bool wl_lds, int n_tiles, size_t lds, hipStream_t st) {
+    if (PRE)  // the reduction happened in k_rt_agg: one instantiation serves all
+        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_SUM, true, true>(a, n_tiles, lds, st)
+                      : launch_rt<NTW, NGNN_REDUCE_SUM, false, true>(a, n_tiles, lds, st);
     if (reduce == NGNN_REDUCE_MEAN)
-        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MEAN, true>(a, n_tiles, lds, st)
-                      : launch_rt<NTW, NGNN_REDUCE_MEAN, false>(a, n_tiles, lds, st);
+        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MEAN, true, false>(a, n_tiles, lds, st)
+                      : launch_rt<NTW, NGNN_REDUCE_MEAN, false, false>(a, n_tiles, lds, st);
     if (reduce == NGNN_REDUCE_SUM)
-        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_SUM, true>(a, n_tiles, lds, st)
-                      : launch_rt<NTW, NGNN_REDUCE_SUM, false>(a, n_tiles, lds, st);
-    return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MAX, true>(a, n_tiles, lds, st)
-                  : launch_rt<NTW, NGNN_REDUCE_MAX, false>(a, n_tiles, lds, st);
+        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_SUM, true, false>(a, n_tiles, lds, st)
+                      : launch_rt<NTW, NGNN_REDUCE_SUM, false, false>(a, n_tiles, lds, st);
+    return wl_lds ? launch_rt<NTW, NGNN_REDUCE_MAX, true, false>(a, n_tiles, lds, st)
+                  : launch_rt<NTW, NGNN_REDUCE_MAX, false, false>(a, n_tiles, lds, st);
+}
+
+template <int NTW>
+int dispatch_pre(const RtArgs &a, int reduce, bool wl_lds, bool pre, int n_tiles, size_t lds,
+                 hipStream_t st) {
+    return pre ? dispatch_red<NTW, true>(a, reduce, wl_lds, n_tiles, lds, st)
+               : dispatch_red<NTW, false>(a, reduce, wl_lds, n_tiles, lds, st);
 }
 
 }  // namespace
@@ -544,6 +649,41 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     if (ntw_max == 0) return 0;
     const int64_t slice = 16 * static_cast<int64_t>(ntw_max);
     const Dropout drop = make_dropout(p_drop, seed);
+    // PRE (NGNN_RT_PRE=1): the aggregate (saved for the backward anyway) is
+    // computed by a separate pass and the layer kernel reads it densely -- no
+    // gather registers, 4 waves per SIMD for narrow outputs.  Measured on the
+    // products block it loses to the in-kernel gather at both layers (the
+    // separate pass re-reads what the gather overlaps: L0 129 + 18 us vs
+    // 141 us, L1 60 + 35 us vs 87 us), so the gather stays the default.
+    const bool use_pre = getenv("NGNN_RT_PRE") != nullptr;  // read per call (tests toggle it)
+    const bool pre = use_pre && agg_out != nullptr && wl_packed != nullptr && rowptr != nullptr;
+    if (pre) {
+        const int64_t k4 = ceil_div(K, 4);
+        const int lpr = k4 <= 8 ? 8 : k4 <= 16 ? 16 : k4 <= 32 ? 32 : 64;
+        const unsigned grid = static_cast<unsigned>(
+            std::max<int64_t>(1, std::min<int64_t>(8 * num_cus(), ceil_div(n_rows, 256 / lpr))));
+        auto go = [&](auto red_c, auto lpr_c) {
+            hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>),
+                               dim3(grid), dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr,
+                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg);
+        };
+        auto by_lpr = [&](auto red_c) {
+            switch (lpr) {
+                case 8: go(red_c, std::integral_constant<int, 8>{}); break;
+                case 16: go(red_c, std::integral_constant<int, 16>{}); break;
+                case 32: go(red_c, std::integral_constant<int, 32>{}); break;
+                default: go(red_c, std::integral_constant<int, 64>{}); break;
+            }
+        };
+        if (reduce == NGNN_REDUCE_MEAN) by_lpr(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
+        else if (reduce == NGNN_REDUCE_SUM) by_lpr(std::integral_constant<int, NGNN_REDUCE_SUM>{});
+        else by_lpr(std::integral_constant<int, NGNN_REDUCE_MAX>{});
+        const int arc = launch_status();
+        if (arc) {
+            *rc = arc;
+            return 1;
+        }
+    }
     for (int64_t c0 = 0; c0 < Fo; c0 += slice) {
         const int64_t Fo_c = std::min<int64_t>(slice, Fo - c0);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));
@@ -591,7 +731,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.out = out + c0;
         a.ldo = ldo;
         a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(out + c0, 16);
-        a.agg_out = c0 == 0 ? agg_out : nullptr;
+        a.agg_out = (pre || c0 == 0) ? agg_out : nullptr;  // PRE: every slice reads it
         a.ld_agg = ld_agg;
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
@@ -602,11 +742,11 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
-            case 2: *rc = dispatch_red<2>(a, reduce, wl_lds, n_tiles, lds, st); break;
-            case 3: *rc = dispatch_red<3>(a, reduce, wl_lds, n_tiles, lds, st); break;
-            case 4: *rc = dispatch_red<4>(a, reduce, wl_lds, n_tiles, lds, st); break;
-            case 8: *rc = dispatch_red<8>(a, reduce, wl_lds, n_tiles, lds, st); break;
-            default: *rc = dispatch_red<16>(a, reduce, wl_lds, n_tiles, lds, st); break;
+            case 2: *rc = dispatch_pre<2>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
+            case 3: *rc = dispatch_pre<3>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
+            case 4: *rc = dispatch_pre<4>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
+            case 8: *rc = dispatch_pre<8>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
+            default: *rc = dispatch_pre<16>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
         }
         if (*rc) return 1;
     }

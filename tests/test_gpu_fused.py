@@ -303,3 +303,27 @@ def test_dgrad_lowdim_shape_envelope():
         _lib.ptr(blk.col), N, bnd.data_ptr(), bnd.data_ptr() + 4, _lib.REDUCE["mean"],
         _lib.ptr(dh), K, 0, _lib.ptr(ws), ws.numel(), _lib.stream_handle(DEV))
     assert rc == _lib.E_SHAPE
+
+
+@pytest.mark.parametrize("aggr", ["mean", "max"])
+def test_stack_precomputed_aggregate_path(aggr, monkeypatch):
+    """NGNN_RT_PRE=1 (aggregate pass + gather-free layer kernel) gives the
+    same outputs and gradients as the oracle."""
+    monkeypatch.setenv("NGNN_RT_PRE", "1")
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.005)
+    b = sample_block(graph, graph.train_idx[:128], [8, 5], seed=2)
+    torch.manual_seed(5)
+    mine = ngnn.SAGE(100, 64, 47, 2, dropout=0.5, aggr=aggr).to(DEV).eval()
+    ref = pyg_ref.SAGE(100, 64, 47, 2, dropout=0.5, aggr=aggr).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    x = b.x.clone().requires_grad_(True)
+    out = mine(x, b.edge_index)
+    F.cross_entropy(out[:b.batch_size], b.y[:b.batch_size]).backward()
+    xr = b.x.cpu().clone().requires_grad_(True)
+    out_r = ref(xr, b.edge_index.cpu())
+    F.cross_entropy(out_r[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
+    torch.testing.assert_close(out.detach().cpu(), out_r.detach(), **OUT)
+    torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
+    for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
