@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 5
+#define NGNN_ABI_VERSION 6
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -167,10 +167,14 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * ngnn_sage_fwd_raw_workspace_bytes) and streamed from L2.  Returns
  * NGNN_E_SHAPE, launching nothing, for shapes outside that kernel's envelope
  * (K % 4 != 0, unaligned rows, W_r slice too large for LDS, buffers >= 2 GiB):
- * the caller then packs and calls ngnn_sage_fwd. */
+ * the caller then packs and calls ngnn_sage_fwd.  x_dev (nullable): a device
+ * word holding x's address, read at run time instead of x (a HIP-graph slot
+ * whose batch stays where the loader put it; 16-B aligned, row stride ldx,
+ * rows < *n_rows_dev). */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo);
-int ngnn_sage_fwd_raw(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                      const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
+                      int64_t n_rows, const int32_t *n_rows_dev, const int32_t *rowptr,
+                      const int32_t *col,
                       int reduce, const float *wl, const float *wr, int64_t ldw, const float *bias,
                       int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                       const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
@@ -198,11 +202,13 @@ int ngnn_block_prefix_stats(const int32_t *rowptr, const int32_t *col, const int
  * reduction => deterministic.  Outputs are overwritten.
  * Replaces autograd of lin_l / lin_r (PyG Linear [ext]) in SAGEConv. */
 size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K);
+/* h_dev (nullable): device word holding h's address, read at run time (as
+ * ngnn_sage_fwd_raw's x_dev). */
 int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy, float yscale,
-                    const float *h, int64_t ldh, const float *agg, int64_t ld_agg,
-                    const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr, int64_t Fo,
-                    int64_t K, float *dwl, float *dbl, float *dwr, void *ws, size_t ws_bytes,
-                    void *stream);
+                    const float *h, const float *const *h_dev, int64_t ldh, const float *agg,
+                    int64_t ld_agg, const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
+                    int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
+                    size_t ws_bytes, void *stream);
 /* Input gradient of one layer, rows j < Rn = *rnext_ptr (R = *r_ptr):
  *   dh[j] = [j < R] droot[j] + sum over edges e with source j and target
  *           d = col_t[e] < R (transposed CSR, edge order) of
@@ -306,14 +312,16 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * Optional (NULL to skip): slot_rowptr [n_cap + 1] / slot_col [e_cap] int32
  * = the target-grouped CSR of the padded edges (both or neither; targets
  * must be non-decreasing, NeighborLoader's order), and *seed_state advanced
- * by one splitmix64 step (the dropout seed of the captured step).
+ * by one splitmix64 step (the dropout seed of the captured step).  x_dev
+ * (nullable): zero-copy -- store x's address there instead of copying the
+ * rows (slot_x may then be NULL; x 16-B aligned with ldx == ld_slot).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
-                   uint64_t *seed_state, void *stream);
+                   uint64_t *seed_state, const float **x_dev, void *stream);
 
 #ifdef __cplusplus
 }

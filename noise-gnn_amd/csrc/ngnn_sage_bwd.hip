@@ -157,10 +157,11 @@ __device__ __forceinline__ void wgrad_mfma_dispatch(int ktn, v4f (&acc)[NTW][KTW
 template <int NTW, int KTW, bool SPLIT_N, bool VZ, bool VH, bool MASK>
 __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
-    float yscale, const float *__restrict__ h, int64_t ldh, const float *__restrict__ agg,
-    int64_t ld_agg, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ r_ptr, int Fo,
-    int K, float *__restrict__ ws) {
+    float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
+    const float *__restrict__ agg, int64_t ld_agg, const int32_t *__restrict__ rowptr,
+    const int32_t *__restrict__ r_ptr, int Fo, int K, float *__restrict__ ws) {
     __shared__ __attribute__((aligned(16))) float smem[WG_BM * LDZ + 2 * WG_BM * LDH];  // 94 KB
+    const float *__restrict__ h = h_dev ? *h_dev : h_arg;  // run-time address (graph slot)
     float *sz = smem;                       // [64][LDZ]
     float *sh = sz + WG_BM * LDZ;           // [64][LDH]
     float *sa = sh + WG_BM * LDH;           // [64][LDH]
@@ -799,14 +800,14 @@ extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
 
 template <int NTW, int KTW, bool SPLIT_N>
 static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const float *dy, int64_t ldy,
-                         const float *y, int64_t ldyy, float yscale, const float *h, int64_t ldh,
-                         const float *agg, int64_t ld_agg, const int32_t *rowptr,
-                         const int32_t *r_ptr, int Fo, int K, float *ws) {
+                         const float *y, int64_t ldyy, float yscale, const float *h,
+                         const float *const *h_dev, int64_t ldh, const float *agg, int64_t ld_agg,
+                         const int32_t *rowptr, const int32_t *r_ptr, int Fo, int K, float *ws) {
     auto go = [&](auto vz_c, auto vh_c, auto m_c) {
         hipLaunchKernelGGL((k_wgrad_partial<NTW, KTW, SPLIT_N, decltype(vz_c)::value,
                                             decltype(vh_c)::value, decltype(m_c)::value>),
-                           grid, dim3(512), 0, st, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg,
-                           rowptr, r_ptr, Fo, K, ws);
+                           grid, dim3(512), 0, st, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, agg,
+                           ld_agg, rowptr, r_ptr, Fo, K, ws);
     };
     using T = std::true_type;
     using F = std::false_type;
@@ -824,11 +825,13 @@ static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const floa
 }
 
 extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
-                               float yscale, const float *h, int64_t ldh, const float *agg,
-                               int64_t ld_agg, const int32_t *rowptr, int64_t n_rows,
-                               const int32_t *r_ptr, int64_t Fo, int64_t K, float *dwl, float *dbl,
-                               float *dwr, void *ws, size_t ws_bytes, void *stream) {
-    NGNN_RETURN_IF(!dy || !h || !agg || !rowptr || !r_ptr || !dwl || !dbl || !dwr, NGNN_E_ARG);
+                               float yscale, const float *h, const float *const *h_dev,
+                               int64_t ldh, const float *agg, int64_t ld_agg,
+                               const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
+                               int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
+                               size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(!dy || (!h && !h_dev) || !agg || !rowptr || !r_ptr || !dwl || !dbl || !dwr,
+                   NGNN_E_ARG);
     NGNN_RETURN_IF(Fo <= 0 || K <= 0 || n_rows < 0, NGNN_E_ARG);
     NGNN_RETURN_IF(ldy < Fo || ldh < K || ld_agg < K || (y && ldyy < Fo), NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(K), NGNN_E_RANGE);
@@ -840,8 +843,8 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     // 16-B staging per operand pair: dz (+ its mask y) and h / agg
     const bool vz = (Fo % 4 == 0) && (ldy % 4 == 0) && aligned(dy, 16) &&
                     (!y || ((ldyy % 4 == 0) && aligned(y, 16)));
-    const bool vh = (K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) && aligned(h, 16) &&
-                    aligned(agg, 16);
+    const bool vh = (K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) &&
+                    (h_dev || aligned(h, 16)) && aligned(agg, 16);  // h_dev: 16-B aligned by contract
     hipStream_t st = as_stream(stream);
     float *wsf = static_cast<float *>(ws);
     // slices x K-chunks x Fo-chunks ~ one workgroup per CU; the kernel uses
@@ -851,8 +854,8 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
         1, std::min<int64_t>(ceil_div(n_rows, WG_BM), std::max<int64_t>(1, S_MAX / (gy * gz)))));
     const dim3 grid(S, static_cast<unsigned>(gy), static_cast<unsigned>(gz));
     const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
-#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, ldh, agg, ld_agg, rowptr, r_ptr, \
-                     (int)Fo, (int)K, wsf
+#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, agg, ld_agg, rowptr, \
+                     r_ptr, (int)Fo, (int)K, wsf
     if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
     else if (NT == 1) launch_wgrad<1, 2, false>(NGNN_WG_ARGS);
     else if (NT == 2) launch_wgrad<2, 2, false>(NGNN_WG_ARGS);

@@ -65,6 +65,7 @@ struct RtArgs {
     Epi epi;
     uint32_t x_bytes, out_bytes, agg_bytes;  // buffer-resource ranges (all < 4 GiB)
     const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
+    const float *const *x_dev;                // non-null: x's address read at run time (graph slot)
     int dbg;  // ablation bits (NGNN_SAGE_ABLATE, profiling only): 1 no MFMA, 2 no stores, 4 no x loads,
              // 8 no epilogue, 16 no weight prologue
 };
@@ -395,7 +396,11 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
     int nbeg = 0, nend = 0;
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
-    const i32x4 xr = make_rsrc(a.x, a.x_bytes);
+    // x: the address given at launch, or (graph replay of a changing batch)
+    // the one the slot load stored, ranged by the device row count
+    const i32x4 xr = a.x_dev ? make_rsrc(*a.x_dev, static_cast<uint32_t>(
+                                             ((n_rows - 1) * a.ldx + a.K) * 4 * (n_rows > 0)))
+                             : make_rsrc(a.x, a.x_bytes);
     const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
     auto prefetch = [&](int tn) {
         const int rn = (tn < n_tiles ? tn : 0) * RT_ROWS + rl;
@@ -496,11 +501,13 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
 // prefix) spread over every CU.
 constexpr int RT_AGG_UNR = 8;
 template <int RED, int LPR>
-__global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x, int64_t ldx, int K,
+__global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x_arg, int64_t ldx, int K,
                                                 const int32_t *__restrict__ rowptr,
                                                 const int32_t *__restrict__ col, int n_rows,
                                                 const int32_t *__restrict__ n_rows_dev,
-                                                float *__restrict__ agg, int64_t ld_agg) {
+                                                float *__restrict__ agg, int64_t ld_agg,
+                                                const float *const *x_dev) {
+    const float *__restrict__ x = x_dev ? *x_dev : x_arg;
     constexpr int GPW = 256 / LPR;
     const int lane = threadIdx.x % LPR;
     int nr = n_rows;
@@ -625,10 +632,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
-                     int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes) {
+                     int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
+                     const float *const *x_dev) {
     static const bool off = getenv("NGNN_NO_ROWTILE") != nullptr;
     if (off) return 0;
-    if (K % 4 != 0 || ldx % 4 != 0 || !aligned(x, 16)) return 0;
+    // (with x_dev the run-time address must be 16-B aligned, as torch's are)
+    if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
         return 0;
     if (agg_out && (ld_agg % 4 != 0 || !aligned(agg_out, 16))) return 0;
@@ -665,7 +674,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         auto go = [&](auto red_c, auto lpr_c) {
             hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>),
                                dim3(grid), dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr,
-                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg);
+                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg, x_dev);
         };
         auto by_lpr = [&](auto red_c) {
             switch (lpr) {
@@ -737,6 +746,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
         a.dbg = dbg;
         a.seed_dev = seed_dev;
+        a.x_dev = x_dev;
         a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
         a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
@@ -761,8 +771,9 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo) {
     return ngnn_pack_weight_bytes(Fo, K);  // a packed W_l, used only when it cannot sit in LDS
 }
 
-extern "C" int ngnn_sage_fwd_raw(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                                 const int32_t *n_rows_dev, const int32_t *rowptr,
+extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx,
+                                 int64_t K, int64_t n_rows, const int32_t *n_rows_dev,
+                                 const int32_t *rowptr,
                                  const int32_t *col, int reduce, const float *wl, const float *wr,
                                  int64_t ldw, const float *bias, int64_t Fo, float *out,
                                  int64_t ldo, int relu, float p_drop, uint64_t seed,
@@ -776,11 +787,11 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, int64_t ldx, int64_t K, int64_t
     NGNN_RETURN_IF(!fits_i32(K) || !fits_i32(n_rows) || !fits_i32(Fo), NGNN_E_RANGE);
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
     if (n_rows == 0) return NGNN_OK;
-    NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
+    NGNN_RETURN_IF((!x && !x_dev) || !out, NGNN_E_ARG);
     int rc = NGNN_OK;
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, as_stream(stream), &rc,
-                          ldw, ws, ws_bytes))
+                          ldw, ws, ws_bytes, x_dev))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

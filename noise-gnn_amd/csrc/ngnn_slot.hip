@@ -1,6 +1,7 @@
 // Static HIP-graph slot filling (ngnn/graphs.py): one launch copies a
 // NeighborLoader block into the slot a captured training step reads.
-//   rows  [0, N)        x copied (16-B vectors when rows allow)
+//   rows  [0, N)        x copied (16-B vectors when rows allow), or with
+//                       x_dev only its address stored (zero-copy)
 //   edges [0, E)        copied;  [E, e_cap) padding self-loops on row
 //                       N + floor(j (n_cap - N) / n_pad), j = e - E: targets
 //                       stay non-decreasing (the CSR fast path holds) and no
@@ -24,10 +25,12 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int64_t ld_ei, int64_t E, const int64_t *__restrict__ y, int64_t B, float *__restrict__ sx,
     int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
-    uint64_t *__restrict__ seed_state, int vec) {
+    uint64_t *__restrict__ seed_state, const float **x_dev, int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-    if (vec) {
+    if (x_dev) {  // zero-copy: the captured kernels read x where it is
+        if (tid == 0) *x_dev = x;
+    } else if (vec) {
         const int64_t f4 = F >> 2, total = N * f4;
         for (int64_t i = tid; i < total; i += nthr) {
             const int64_t r = i / f4, c = (i - r * f4) << 2;
@@ -100,8 +103,10 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int64_t B, float *slot_x, int64_t ld_slot, int64_t n_cap,
                               int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
-                              void *stream) {
-    NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || !slot_x || !slot_ei || !n_valid, NGNN_E_ARG);
+                              const float **x_dev, void *stream) {
+    NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !slot_ei || !n_valid,
+                   NGNN_E_ARG);
+    NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
                    NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E, NGNN_E_SHAPE);
@@ -111,10 +116,10 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     NGNN_RETURN_IF((slot_rowptr == nullptr) != (slot_col == nullptr), NGNN_E_ARG);
     const int vec = (F % 4 == 0) && (ldx % 4 == 0) && (ld_slot % 4 == 0) && aligned(x, 16) &&
                     aligned(slot_x, 16);
-    const int64_t work = std::max<int64_t>({N * F / 4, e_cap, n_cap + 1, B, 1});
+    const int64_t work = std::max<int64_t>({x_dev ? 0 : N * F / 4, e_cap, n_cap + 1, B, 1});
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
-                       n_valid, slot_rowptr, slot_col, seed_state, vec);
+                       n_valid, slot_rowptr, slot_col, seed_state, x_dev, vec);
     return launch_status();
 }

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -42,18 +42,18 @@ SIGNATURES = {
     "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
-                              _p, _i64, _p, _p, _p, _p, _p, _p]),
+                              _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
     "ngnn_sage_fwd_raw_workspace_bytes": (_sz, [_i64, _i64]),
-    "ngnn_sage_fwd_raw": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _i64, _p, _i64,
+    "ngnn_sage_fwd_raw": (_int, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
-    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _i64, _p, _i64, _p, _i64,
+    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _i64, _p, _i64, _p, _i64,
                                _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
     "ngnn_sage_dgrad_workspace_bytes": (_sz, [_i64, _i64, _int]),
     "ngnn_sage_dgrad_gather": (_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p, _p, _i64,

@@ -94,8 +94,11 @@ def _gemm_layer(x, K, n_rows, block, reduce, pl, pr, bias, Fo, out, relu, p_drop
 
 def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu: bool,
                    p_drop: float, seed: int, agg_out: torch.Tensor | None = None,
-                   seed_dev: torch.Tensor | None = None) -> torch.Tensor:
-    """One fused SAGEConv(+relu+dropout) layer, no autograd."""
+                   seed_dev: torch.Tensor | None = None,
+                   x_dev: torch.Tensor | None = None) -> torch.Tensor:
+    """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
+    word holding the address of x's rows (zero-copy graph slot); x then only
+    supplies the shape."""
     N, K = x.shape
     Fo = wl.shape[0]
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
@@ -112,12 +115,14 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     with _timing.span("sage_fwd", nbytes, flops):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         rc = lib.ngnn_sage_fwd_raw(
-            _lib.ptr(x), x.stride(0), K, N, nrd, _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, _lib.ptr(block.rowptr), _lib.ptr(block.col),
             _lib.REDUCE[reduce], _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
         if rc == _lib.E_SHAPE:
+            if x_dev is not None:
+                raise _lib.NGNNError("zero-copy input outside the row-tile kernel's envelope")
             pl, pr = pack_weight(wl), pack_weight(wr)
             _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
                         agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
@@ -138,7 +143,7 @@ class _SAGEStack(torch.autograd.Function):
             agg = torch.empty(h.shape, dtype=torch.float32, device=h.device)
             h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=not last,
                                p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg,
-                               seed_dev=seed_dev)
+                               seed_dev=seed_dev, x_dev=block.x_dev if i == 0 else None)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -154,6 +159,8 @@ class _SAGEStack(torch.autograd.Function):
         dev = dout.device
         stream = _lib.stream_handle(dev)
         need_dx = ctx.needs_input_grad[0]
+        if need_dx and block.x_dev is not None:
+            raise _lib.NGNNError("input gradient of a zero-copy slot input is not supported")
         N = block.n_dst
         grads = [None] * (3 * L)
         dy = dout if dout.stride(1) == 1 else dout.contiguous()
@@ -185,6 +192,7 @@ class _SAGEStack(torch.autograd.Function):
                 rc = lib.ngnn_sage_wgrad(
                     _lib.ptr(dy), dy.stride(0), _lib.ptr(ymask),
                     ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(h_in),
+                    _lib.ptr(block.x_dev) if i == 0 else None,
                     h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
                     bptr(i + 1), Fo, K, _lib.ptr(dwl), _lib.ptr(dbl), _lib.ptr(dwr),
                     _lib.ptr(ws), ws.numel(), stream)

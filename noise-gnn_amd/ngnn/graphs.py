@@ -14,6 +14,10 @@ seed, so the graph holds no CSR-build or RNG launches.  Edges must be
 target-sorted (NeighborLoader's order).
 
 Shapes are static: the slot holds ``n_cap`` node rows and ``e_cap`` edges.
+The feature rows are not copied for a replay: the slot load stores the
+batch's address in a device word the captured layer-0 kernels read
+(zero-copy), so the batch tensor must stay alive until the step completes
+(the step keeps a reference until the next load).
 A batch with N nodes and E edges fills rows ``[0, N)`` and edges ``[0, E)``;
 the padding edges are self-loops spread evenly over the padding rows
 ``[N, n_cap)`` (targets stay non-decreasing, no row gets more than a few), so
@@ -53,16 +57,24 @@ class GraphedTrainStep:
         self.rowptr = torch.zeros(self.n_cap + 1, dtype=torch.int32, device=dev)
         self.col = torch.zeros(self.e_cap, dtype=torch.int32, device=dev)
         self.seed_state = torch.randint(0, 2**62, (1,), dtype=torch.int64).to(dev)
+        # zero-copy input: the slot load stores the batch's feature address
+        # here and the captured layer-0 kernels read the rows in place
+        self.x_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
         self.loss = None
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
-    def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor) -> None:
+    def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
+             zero_copy: bool = False) -> None:
+        """zero_copy: store x's address for the captured kernels instead of
+        copying its rows into the slot (replays); the copy serves eager use
+        of the slot (warm-up, tests)."""
         N, E = x.size(0), edge_index.size(1)
         if N + 1 > self.n_cap or E > self.e_cap:
             raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
-        if x.stride(1) != 1:
-            x = x.contiguous()
+        if x.stride(1) != 1 or x.stride(0) != self.x.stride(0) or x.data_ptr() % 16:
+            x = x.clone(memory_format=torch.contiguous_format)
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
         y = y[:self.B].contiguous()
@@ -72,7 +84,9 @@ class GraphedTrainStep:
             _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
             _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
-            _lib.stream_handle(self.x.device)), "ngnn_slot_load")
+            _lib.ptr(self.x_dev) if zero_copy else None, _lib.stream_handle(self.x.device)),
+            "ngnn_slot_load")
+        self._x_live = x if zero_copy else None
 
     def _fwd_bwd(self):
         out = self.model(self.x, self.ei)
@@ -106,7 +120,8 @@ class GraphedTrainStep:
         # contents at replay time), never served from the eager cache
         block_cache.clear()
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
-                        csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state)
+                        csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
+                        x_dev=self.x_dev)
         self.opt.zero_grad(set_to_none=True)
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
@@ -133,7 +148,7 @@ class GraphedTrainStep:
     def __call__(self, x, edge_index, y):
         """Load one batch into the slot and replay the captured step; returns
         the (device) loss tensor of this step."""
-        self.load(x, edge_index, y)
+        self.load(x, edge_index, y, zero_copy=True)
         self.g_fb.replay()
         if self.reducer is not None:
             self.reducer()
