@@ -55,10 +55,25 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python instead of replaying the captured "
                          "HIP graph of the step")
-    ap.add_argument("--timer", default="sage_fwd",
+    ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1",
                     help="comma list of kernel spans timed with HIP events in the timed region "
                          "('all', or 'none' for profiler runs)")
     return ap.parse_args()
+
+
+def pmc_traffic(span):
+    """HBM bytes per launch of the kernel behind `span` from the committed PMC
+    summary (tools/gpu_pmc.sh + tools/pmc_traffic.py: FETCH_SIZE x 2 on gfx950
+    plus WRITE_SIZE, separate passes), or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(span)
+    except (OSError, ValueError):
+        return None, None
+    if not rec:
+        return None, None
+    return int(rec["traffic_bytes"]), f"profiles/pmc_traffic.json ({rec.get('source', '?')})"
 
 
 def train_step(model, opt, reducer, b):
@@ -158,7 +173,7 @@ def main():
     timer_names = None if args.timer == "all" else ([] if args.timer == "none" else args.timer.split(","))
 
     def new_timer():
-        t = _timing.KernelTimer(only=timer_names or ["-"])
+        t = _timing.KernelTimer(only=None if args.timer == "all" else (timer_names or ["-"]))
         t.reserve(8 * args.steps if args.timer != "none" else 0)
         return t
     # eager: per-launch events inside the timed region; graph: events cannot be
@@ -205,8 +220,10 @@ def main():
         else:
             roof = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(f_hbm, 4)}
+        traffic, traffic_src = pmc_traffic(name)
         roof.update({
-            "traffic": None, "launches": n, "avg_us": round(1e3 * ms / n, 2),
+            "traffic": traffic, "traffic_src": traffic_src, "launches": n,
+            "avg_us": round(1e3 * ms / n, 2),
             "timed_in": "timed region (eager)" if not graph else
                         "eager pass over the timed batches, right after the graph replays",
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),

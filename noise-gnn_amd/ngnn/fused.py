@@ -95,7 +95,7 @@ def _gemm_layer(x, K, n_rows, block, reduce, pl, pr, bias, Fo, out, relu, p_drop
 def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu: bool,
                    p_drop: float, seed: int, agg_out: torch.Tensor | None = None,
                    seed_dev: torch.Tensor | None = None,
-                   x_dev: torch.Tensor | None = None) -> torch.Tensor:
+                   x_dev: torch.Tensor | None = None, span: str = "sage_fwd") -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
     supplies the shape."""
@@ -112,7 +112,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo), zero=True)
-    with _timing.span("sage_fwd", nbytes, flops):
+    with _timing.span(span, nbytes, flops):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         rc = lib.ngnn_sage_fwd_raw(
             _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, _lib.ptr(block.rowptr), _lib.ptr(block.col),
@@ -143,7 +143,8 @@ class _SAGEStack(torch.autograd.Function):
             agg = torch.empty(h.shape, dtype=torch.float32, device=h.device)
             h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=not last,
                                p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg,
-                               seed_dev=seed_dev, x_dev=block.x_dev if i == 0 else None)
+                               seed_dev=seed_dev, x_dev=block.x_dev if i == 0 else None,
+                               span=f"sage_fwd_l{i}")
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L

@@ -1,0 +1,58 @@
+"""HBM traffic per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3
+passes (tools/gpu_pmc.sh), mapped to bench.py's timer spans, written to
+profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+
+FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section), so it is
+doubled; WRITE_SIZE is exact for 16-B stores.
+
+    python tools/pmc_traffic.py gpurun_out/TAG --map sage_fwd_l0='k_sage_rt<16,' \
+        --map sage_fwd_l1='k_sage_rt<3,' [--out profiles/pmc_traffic.json]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--map", action="append", default=[], help="span=kernel-name-substring")
+    ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    a = ap.parse_args()
+    spans = dict(m.split("=", 1) for m in a.map)
+    # (span, counter) -> {dispatch: summed value}
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for f in sorted(glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].replace(" ", "")
+            for span, sub in spans.items():
+                if sub.replace(" ", "") in k:
+                    acc[(span, r["Counter_Name"])][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+                    names[span] = r["Kernel_Name"].split("(")[0]
+    out = {}
+    if os.path.exists(a.out):
+        out = json.load(open(a.out))
+    for span in spans:
+        fv = list(acc[(span, "FETCH_SIZE")].values())
+        wv = list(acc[(span, "WRITE_SIZE")].values())
+        if not fv or not wv:
+            print(f"{span}: no FETCH_SIZE/WRITE_SIZE rows")
+            continue
+        fetch = 2 * 1024 * statistics.mean(fv)
+        write = 1024 * statistics.mean(wv)
+        out[span] = {"kernel": names[span], "fetch_bytes": int(fetch), "write_bytes": int(write),
+                     "traffic_bytes": int(fetch + write), "dispatches": [len(fv), len(wv)],
+                     "source": os.path.basename(os.path.normpath(a.dir))}
+        print(span, out[span])
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
