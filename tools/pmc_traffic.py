@@ -34,7 +34,7 @@ def main():
             for span, sub in spans.items():
                 if sub.replace(" ", "") in k:
                     acc[(span, r["Counter_Name"])][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
-                    names[span] = r["Kernel_Name"].split("(")[0]
+                    names[span] = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     out = {}
     if os.path.exists(a.out):
         out = json.load(open(a.out))
