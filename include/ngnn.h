@@ -123,6 +123,43 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
                     int64_t n_frontier, int fanout, uint64_t seed, int64_t *out_nbr,
                     int32_t *out_cnt, void *stream);
 
+/* ------------------------------------------------- whole-block sampling
+ * The whole NeighborLoader mini-batch on the device: every hop of
+ * ngnn_sample_hop's sampler (hop h uses seed*1000003 + h), the relabelling
+ * of sampled global ids to block-local ids and the block's edge list --
+ * what PyG's NeighborLoader (pipeline.py:75-83, pyg-lib neighbor_sample
+ * [ext]) builds in its worker process plus the batch.to(device) of
+ * pipeline.py:153.  Local ids: seeds first (seeds must be distinct), then
+ * each hop's newly reached nodes in order of first appearance in the hop's
+ * (frontier position, draw) sequence.  Edges: row 0 = local source (the
+ * sampled neighbour), row 1 = local target, grouped by target in frontier
+ * order (targets non-decreasing).
+ *
+ * Two calls.  ngnn_sample_block runs the hops and writes
+ * counts (device int32[4]) = {n_nodes, n_edges, n_active, 0}, n_active =
+ * rows that received in-edges (the frontiers of hops < last); the caller
+ * reads them (one device->host copy), allocates the outputs and calls
+ * ngnn_sample_block_finish with the same fanouts / seeds count / workspace,
+ * which writes n_id int64[n_nodes], edge_index int64[2, n_edges]
+ * (contiguous), optionally y = y_all[n_id] and x = x_all[n_id] (fp32 rows),
+ * and restores node_map.
+ *   node_map: int32[2 * n_graph], caller-owned, all -1 before the first call
+ *             and again after every finish (one map per stream at a time).
+ *   ws:       ngnn_sample_block_workspace_bytes(batch, fanouts, n_hops);
+ *             holds the block between the two calls.
+ *   fanouts:  HOST int32[n_hops], each 0..64. */
+size_t ngnn_sample_block_workspace_bytes(int64_t batch, const int32_t *fanouts, int n_hops);
+int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, int64_t n_graph,
+                      const int64_t *seeds, int64_t n_seeds, const int32_t *fanouts, int n_hops,
+                      uint64_t seed, int32_t *node_map, void *ws, size_t ws_bytes,
+                      int32_t *counts, void *stream);
+int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int64_t n_seeds,
+                             int64_t n_nodes, int64_t n_edges, int32_t *node_map,
+                             int64_t n_graph, const void *ws, size_t ws_bytes, int64_t *n_id,
+                             int64_t *edge_index, const int64_t *y_all, int64_t *y,
+                             const float *x_all, int64_t ldx, int64_t F, float *x, int64_t ldo,
+                             void *stream);
+
 /* ------------------------------------------------------- fused SAGE layer
  * One SAGEConv layer of SAGE.forward (sage.py:33-39) in one launch:
  *   out[r] = act( b + x[r] . W_r^T + [deg(r)>0] agg(r) . W_l^T ),   r < n_rows

@@ -33,6 +33,11 @@ SIGNATURES = {
     "ngnn_seg_agg_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _i64, _int, _int,
                                 _p, _i64, _p, _i64, _p, _i64, _p, _sz, _p]),
     "ngnn_sample_hop": (_int, [_p, _p, _p, _i64, _int, ctypes.c_uint64, _p, _p, _p]),
+    "ngnn_sample_block_workspace_bytes": (_sz, [_i64, _p, _int]),
+    "ngnn_sample_block": (_int, [_p, _p, _i64, _p, _i64, _p, _int, ctypes.c_uint64, _p, _p, _sz, _p,
+                                 _p]),
+    "ngnn_sample_block_finish": (_int, [_p, _int, _i64, _i64, _i64, _p, _i64, _p, _sz, _p, _p, _p,
+                                        _p, _p, _i64, _i64, _p, _i64, _p]),
     "ngnn_pack_weight_bytes": (_sz, [_i64, _i64]),
     "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_pack_weight_ex": (_int, [_p, _p, _i64, _i64, _i64, _i64, _int, _p, _p]),

@@ -4,8 +4,10 @@ The reference builds ``torch_geometric.loader.NeighborLoader`` over an
 OGB / PyG dataset (``pipeline.py:75-92``, ``pipeline_s.py:72-89``) whose
 sampler (pyg-lib / torch-sparse, C++ [ext]) runs in a worker process and
 ships every batch host->device (``pipeline.py:153``).  Here the graph CSR and
-the feature table stay resident in HBM and every hop is sampled on the GPU
-by ``ngnn_sample_hop`` (uniform, without replacement, Floyd's algorithm).
+the feature table stay resident in HBM and the whole block -- every hop
+(uniform, without replacement, Floyd's algorithm), the relabelling to local
+ids, the edge list and the x / y gathers -- is built on the GPU by
+``ngnn_sample_block``.
 
 Batch layout follows what NeighborLoader hands the model (the contract of
 ``pipeline.py:152-160``):
@@ -136,43 +138,84 @@ def sample_hop(graph: Graph, frontier: torch.Tensor, fanout: int, seed: int):
     return out, cnt
 
 
+class _SamplerCache:
+    """Per-graph device state of ngnn_sample_block: the node map (int32
+    [2 N], all -1 between calls) and one workspace per (batch, fanouts)."""
+
+    def __init__(self, n: int, device):
+        self.node_map = torch.full((2 * n,), -1, dtype=torch.int32, device=device)
+        self.ws: dict = {}
+        self.counts = torch.empty(4, dtype=torch.int32, device=device)
+        self.counts_host = torch.empty(4, dtype=torch.int32).pin_memory()
+
+    def workspace(self, lib, batch: int, fan, n_hops: int) -> torch.Tensor:
+        key = (batch, tuple(fan[:n_hops]))
+        buf = self.ws.get(key)
+        if buf is None:
+            n = lib.ngnn_sample_block_workspace_bytes(batch, fan, n_hops)
+            if n == 0:
+                raise ValueError(f"unsupported sampling shape: batch {batch}, "
+                                 f"fanouts {list(fan[:n_hops])} (each 0..64, at most 8 hops)")
+            buf = torch.empty(n, dtype=torch.uint8, device=self.node_map.device)
+            self.ws[key] = buf
+        return buf
+
+
+_sampler_caches: dict = {}
+
+
+def _sampler_cache(graph: Graph) -> _SamplerCache:
+    key = (graph.col.data_ptr(), graph.num_nodes, graph.col.device)
+    c = _sampler_caches.get(key)
+    if c is None:
+        c = _SamplerCache(graph.num_nodes, graph.col.device)
+        _sampler_caches[key] = c
+    return c
+
+
 def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
                  gather_features: bool = True) -> Batch:
+    """One NeighborLoader mini-batch (pipeline.py:152-160 contract) sampled,
+    relabelled and gathered on the device by ngnn_sample_block (+ _finish):
+    about a dozen launches and ONE device->host read (the block's node and
+    edge counts, needed to size the outputs).  Seeds must be distinct."""
+    import ctypes
+    lib = _lib.load()
     dev = seeds.device
-    n_id = seeds.to(torch.int64)
-    frontier = n_id
-    frontier_local = torch.arange(n_id.numel(), device=dev)
-    srcs, dsts = [], []
-    n_active = n_id.numel()
-    for hop, k in enumerate(fanouts):
-        nbr, _ = sample_hop(graph, frontier, int(k), seed * 1_000_003 + hop)
-        mask = nbr >= 0
-        dst_local = frontier_local.unsqueeze(1).expand(-1, int(k))[mask]
-        cand = nbr[mask]
-        n_old = n_id.numel()
-        n_active = n_old  # rows that received in-edges so far (all frontiers up to this hop)
-        all_ids = torch.cat([n_id, cand])
-        uniq, inv = torch.unique(all_ids, return_inverse=True)
-        pos = torch.arange(all_ids.numel(), device=dev)
-        first = torch.full((uniq.numel(),), all_ids.numel(), dtype=torch.int64, device=dev)
-        first.scatter_reduce_(0, inv, pos, reduce="amin")
-        order = torch.argsort(first)
-        rank = torch.empty_like(order)
-        rank[order] = torch.arange(order.numel(), device=dev)
-        local_all = rank[inv]
-        srcs.append(local_all[n_old:])
-        dsts.append(dst_local)
-        new_nodes = uniq[order[n_old:]]
-        frontier_local = torch.arange(n_old, n_old + new_nodes.numel(), device=dev)
-        n_id = torch.cat([n_id, new_nodes])
-        frontier = new_nodes
-    edge_index = torch.stack([torch.cat(srcs), torch.cat(dsts)]) if srcs else \
-        torch.empty(2, 0, dtype=torch.int64, device=dev)
+    if not seeds.is_cuda:
+        raise RuntimeError("ngnn.loader.sample_block: GPU only (no CPU fallback)")
+    if graph.y.dtype != torch.int64 or not graph.y.is_contiguous():
+        raise TypeError("graph.y must be a contiguous int64 vector")
+    if gather_features and (graph.x.dtype != torch.float32 or graph.x.stride(1) != 1):
+        raise TypeError("graph.x must be a row-major float32 matrix")
+    s64 = seeds.to(torch.int64).contiguous()
+    B = s64.numel()
+    fan = (ctypes.c_int32 * max(len(fanouts), 1))(*[int(k) for k in fanouts])
+    H = len(fanouts)
+    cache = _sampler_cache(graph)
+    ws = cache.workspace(lib, B, fan, H)
+    st = _lib.stream_handle(dev)
+    _lib.check(lib.ngnn_sample_block(
+        _lib.ptr(graph.rowptr), _lib.ptr(graph.col), graph.num_nodes, _lib.ptr(s64), B, fan, H,
+        int(seed) & (2**64 - 1), _lib.ptr(cache.node_map), _lib.ptr(ws), ws.numel(),
+        _lib.ptr(cache.counts), st), "ngnn_sample_block")
+    cache.counts_host.copy_(cache.counts, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    n, e, n_active = (int(v) for v in cache.counts_host[:3])
+    n_id = torch.empty(n, dtype=torch.int64, device=dev)
+    edge_index = torch.empty(2, e, dtype=torch.int64, device=dev)
+    y = torch.empty(n, dtype=torch.int64, device=dev)
+    x = None
+    if gather_features:
+        x = torch.empty(n, graph.x.size(1), dtype=torch.float32, device=dev)
+    _lib.check(lib.ngnn_sample_block_finish(
+        fan, H, B, n, e, _lib.ptr(cache.node_map), graph.num_nodes, _lib.ptr(ws), ws.numel(),
+        _lib.ptr(n_id), _lib.ptr(edge_index), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(graph.x),
+        graph.x.stride(0), graph.x.size(1), _lib.ptr(x), x.stride(0) if x is not None else 0, st),
+        "ngnn_sample_block_finish")
     # built here: ids are in range and targets non-decreasing -> no probe needed
     hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active)
-    x = graph.x.index_select(0, n_id) if gather_features else None
-    y = graph.y.index_select(0, n_id)
-    return Batch(x, y, edge_index, n_id, int(seeds.numel()))
+    return Batch(x, y, edge_index, n_id, B)
 
 
 class NeighborLoader:

@@ -54,6 +54,18 @@ def test_argument_errors_return_before_launch():
     assert lib.ngnn_sample_hop(1, 1, 1, 4, 65, 0, 1, 1, None) == -3
     assert lib.ngnn_seg_agg_bwd_workspace_bytes(10, 4, 1) == 0
     assert lib.ngnn_seg_agg_bwd_workspace_bytes(10, 4, 2) == 160
+    # whole-block sampler: workspace sizing and argument checks (no launch)
+    import ctypes
+    fan = (ctypes.c_int32 * 2)(15, 10)
+    ws = lib.ngnn_sample_block_workspace_bytes(1024, fan, 2)
+    assert ws >= 4 * (1024 * 166 + 2 * 1024 * 165)  # n_id + both edge rows, int32
+    bad = (ctypes.c_int32 * 2)(15, 65)
+    assert lib.ngnn_sample_block_workspace_bytes(1024, bad, 2) == 0
+    assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, bad, 2, 0, 1, 1, 1 << 30, 1, None) == -3
+    assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, 1, 1, ws - 1, 1, None) == -6
+    assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, None, 1, ws, 1, None) == -1
+    assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1023, 0, 1, 100, 1, ws, 1, 1, None, None,
+                                        None, 0, 0, None, 0, None) == -3
     # zero-size work is a no-op success
     assert lib.ngnn_seg_agg_fwd(None, 4, 4, 1, None, 0, 1, 0, None, 4, None) == 0
 

@@ -105,3 +105,67 @@ def test_loader_epoch_and_sharding(graph):
     both = torch.cat(parts)
     assert both.numel() == graph.train_idx.numel()
     assert torch.equal(both.sort().values, graph.train_idx.sort().values)
+
+
+# ---- native whole-block sampler (ngnn_sample_block) vs the torch restatement
+
+from sampler_ref import sample_block_ref  # noqa: E402
+
+
+def _assert_same_block(b, ref):
+    assert torch.equal(b.n_id, ref.n_id)
+    assert torch.equal(b.edge_index, ref.edge_index)
+    assert torch.equal(b.y, ref.y)
+    assert torch.equal(b.x, ref.x)
+    assert b.batch_size == ref.batch_size
+
+
+@pytest.mark.parametrize("fanouts,bs", [([15, 10], 300), ([5], 64), ([20, 15, 10], 128),
+                                        ([3, 0, 2], 50), ([64], 17), ([], 10)])
+def test_sample_block_matches_reference(graph, fanouts, bs):
+    from ngnn.loader import _sampler_cache
+    seeds = graph.train_idx[:bs]
+    for s in (1, 99):
+        b = sample_block(graph, seeds, fanouts, seed=s)
+        ref, n_active = sample_block_ref(graph, seeds, fanouts, s)
+        _assert_same_block(b, ref)
+        from ngnn.block import _hint_for
+        assert _hint_for(b.edge_index)[2] == n_active
+    # the node map is restored after every block
+    assert bool((_sampler_cache(graph).node_map == -1).all())
+
+
+def test_sample_block_multigraph_and_isolated():
+    """duplicate edges (the same neighbour at two CSR positions), a seed with
+    no in-edges, degree < fanout, and a self loop."""
+    from ngnn.loader import Graph
+    # node: in-neighbours
+    adj = {0: [1, 1, 2, 3, 4, 5, 6, 1], 1: [], 2: [2, 0], 3: [0, 1, 2, 4, 5, 6, 7, 8, 9],
+           4: [9], 5: [0, 0, 0], 6: [], 7: [3], 8: [8, 8], 9: [1, 2, 3, 4]}
+    N = 10
+    rowptr = [0]
+    col = []
+    for v in range(N):
+        col += adj[v]
+        rowptr.append(len(col))
+    g = Graph(torch.tensor(rowptr, device=DEV), torch.tensor(col, dtype=torch.int32, device=DEV),
+              torch.randn(N, 12, device=DEV), torch.arange(N, device=DEV) % 3,
+              torch.arange(N, device=DEV), 3)
+    for seeds in ([0, 1, 3], [6, 1], [9, 8, 7, 5]):
+        s = torch.tensor(seeds, device=DEV)
+        for fan in ([4, 3], [2, 2, 2], [10]):
+            for sd in range(4):
+                b = sample_block(g, s, fan, seed=sd)
+                ref, _ = sample_block_ref(g, s, fan, sd)
+                _assert_same_block(b, ref)
+
+
+def test_sample_block_full_products_size():
+    """a products-shaped [15,10] bs=1024 block at full graph size: the native
+    block equals the restatement and respects the capacity bounds."""
+    g = synthetic_graph("ogbn-products", DEV, seed=0, scale=0.25)
+    seeds = g.train_idx[:1024]
+    b = sample_block(g, seeds, [15, 10], seed=12345)
+    ref, _ = sample_block_ref(g, seeds, [15, 10], 12345)
+    _assert_same_block(b, ref)
+    assert b.num_nodes <= 1024 * (1 + 15 + 150) and b.edge_index.size(1) <= 1024 * 165
