@@ -160,6 +160,34 @@ int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int64_t n_seeds
                              const float *x_all, int64_t ldx, int64_t F, float *x, int64_t ldo,
                              void *stream);
 
+/* ------------------------------------------------------ co-teaching loss
+ * CTLoss.forward (src/utils/losses.py:19-49) without its two host argsorts:
+ * for models m = 1, 2 with logits y_m [B, C] (row stride ld_m) and noisy
+ * labels y_noise int64[B]:
+ *   l_m[r]       = cross_entropy(y_m[r], y_noise[r])  (0 if ignore_index)
+ *   ind_m_sorted = argsort(l_m) ascending, ties by row index, NaN last
+ *                  (np.argsort(loss_m) of losses.py:22,26)
+ *   out[0] = mean_{r in ind_2_sorted[:R]} l_1[r]   (loss_1_update, :44)
+ *   out[1] = mean_{r in ind_1_sorted[:R]} l_2[r]   (loss_2_update, :45)
+ *   out[2] = sum noise_or_not[ind[ind_1_sorted[:R]]] / R  (pure_ratio_1, :33)
+ *   out[3] = same for model 2 (NaN when noise_or_not is NULL)
+ * with R = num_remember (losses.py:31), ind = the batch's n_id (NULL = row
+ * ids), noise_or_not bool (uint8) [n_noise]; an index outside it sets *err
+ * (device int, caller-zeroed) and contributes nothing.  B <= 8192.
+ * ngnn_ct_loss_bwd: d y_m = grad_m / #valid (softmax - onehot) on the rows
+ * the other model kept, 0 on every other row of [0, B) -- the autograd of
+ * out[m-1]; model = 0 or 1.  ws: ngnn_ct_loss_workspace_bytes(B), kept
+ * between the forward and both backwards. */
+size_t ngnn_ct_loss_workspace_bytes(int64_t B);
+int ngnn_ct_loss_fwd(const float *y1, int64_t ld1, const float *y2, int64_t ld2, int64_t B,
+                     int64_t C, const int64_t *y_noise, int64_t ignore_index, int64_t num_remember,
+                     const int64_t *ind, const uint8_t *noise_or_not, int64_t n_noise, float *out,
+                     int64_t *ind1_sorted, int64_t *ind2_sorted, void *ws, size_t ws_bytes,
+                     int *err, void *stream);
+int ngnn_ct_loss_bwd(int model, const float *y, int64_t ld, int64_t B, int64_t C,
+                     const int64_t *y_noise, int64_t ignore_index, const void *ws,
+                     const float *grad, float *dy, int64_t ldd, void *stream);
+
 /* ------------------------------------------------------- fused SAGE layer
  * One SAGEConv layer of SAGE.forward (sage.py:33-39) in one launch:
  *   out[r] = act( b + x[r] . W_r^T + [deg(r)>0] agg(r) . W_l^T ),   r < n_rows

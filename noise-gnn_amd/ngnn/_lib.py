@@ -44,6 +44,10 @@ SIGNATURES = {
     "ngnn_seed_xent_workspace_bytes": (_sz, [_i64]),
     "ngnn_seed_xent_fwd": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _sz, _p]),
     "ngnn_seed_xent_bwd": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p]),
+    "ngnn_ct_loss_workspace_bytes": (_sz, [_i64]),
+    "ngnn_ct_loss_fwd": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _i64, _p,
+                                _p, _p, _p, _sz, _p, _p]),
+    "ngnn_ct_loss_bwd": (_int, [_int, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _p]),
     "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,

@@ -255,10 +255,25 @@ class NeighborLoader:
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
+        """Batches are sampled on a side stream: batch b+1 is built while the
+        consumer's step on batch b (already enqueued on the current stream
+        when the generator resumes) runs, so sampling overlaps training the
+        way the reference's worker process overlaps it (pipeline.py:81-82)."""
         seeds = self._seeds()
         ep = self.epoch
         self.epoch += 1
+        dev = seeds.device
+        main = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)  # seeds (randperm) were made on the main stream
         for b in range(len(self)):
             s = seeds[b * self.batch_size:(b + 1) * self.batch_size]
-            yield sample_block(self.graph, s, self.num_neighbors,
-                               seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size + self.rank)
+            with torch.cuda.stream(side):
+                blk = sample_block(self.graph, s, self.num_neighbors,
+                                   seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size
+                                   + self.rank)
+            main.wait_stream(side)
+            for t in (blk.x, blk.y, blk.edge_index, blk.n_id):
+                if t is not None:
+                    t.record_stream(main)  # consumed on the main stream
+            yield blk

@@ -83,3 +83,104 @@ def seed_cross_entropy(logits: torch.Tensor, y: torch.Tensor, batch_size: int,
     if batch_size <= 0 or batch_size > logits.size(0) or y.numel() < batch_size:
         raise ValueError("batch_size out of range")
     return _SeedXent.apply(logits, y, batch_size, ignore_index)
+
+
+# ---------------------------------------------------------------------------
+# Co-teaching loss (CTLoss, src/utils/losses.py:10-49) on the device
+
+class _CTState:
+    """Outputs of one ngnn_ct_loss_fwd launch pair, shared by the two
+    per-model autograd nodes (each model's backward reads the rows the other
+    model kept from the workspace)."""
+    __slots__ = ("ws", "out", "y_noise", "ignore", "B", "C")
+
+
+class _CTPick(torch.autograd.Function):
+    """loss_m (already computed by the shared forward) as a differentiable
+    function of y_m alone, so that loss_1.backward() and loss_2.backward()
+    each run only their own model's graph, as in pipeline.py:125-131."""
+
+    @staticmethod
+    def forward(ctx, y, state: _CTState, m: int):
+        ctx.state, ctx.m = state, m
+        ctx.save_for_backward(y)
+        return state.out[m].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        st = ctx.state
+        dy = torch.empty(st.B, st.C, dtype=torch.float32, device=y.device)
+        g = g.reshape(1).to(torch.float32).contiguous()
+        _lib.check(_lib.load().ngnn_ct_loss_bwd(
+            ctx.m, _lib.ptr(y), y.stride(0), st.B, st.C, _lib.ptr(st.y_noise), st.ignore,
+            _lib.ptr(st.ws), _lib.ptr(g), _lib.ptr(dy), dy.stride(0),
+            _lib.stream_handle(y.device)), "ngnn_ct_loss_bwd")
+        return dy, None, None
+
+
+class CTLoss(torch.nn.Module):
+    """Drop-in for the reference's ``CTLoss(device)`` (losses.py:10-49).
+
+    ``forward(y_1, y_2, y_noise, forget_rate, ind, noise_or_not)`` returns the
+    same 8-tuple ``(loss_1_update, loss_2_update, pure_ratio_1, pure_ratio_2,
+    ind_1_update, ind_2_update, ind_noisy_1, ind_noisy_2)`` with no host
+    round trip: the per-row cross entropies, both argsorts, the exchange
+    selection and the pure ratios are two device launches
+    (``ngnn_ct_loss_fwd``), each loss's backward one launch.
+
+    Differences from the reference, all documented in DESIGN.md: the index
+    outputs are device int64 tensors instead of numpy arrays (the pipelines
+    discard them, pipeline.py:116); tied losses are ordered by row index
+    (np.argsort's quicksort leaves ties unspecified); ``noise_or_not`` is
+    best passed as a device bool tensor (a CPU one is copied per call);
+    batches of at most 8192 rows.
+    """
+
+    def __init__(self, device=None, ignore_index: int = -100):
+        super().__init__()
+        self.device = device
+        self.ignore_index = ignore_index
+        # device int32: nonzero once an `ind` entry fell outside noise_or_not
+        # (the reference raises IndexError there; checking it needs a sync)
+        self.index_error = None
+
+    def forward(self, y_1, y_2, y_noise, forget_rate, ind, noise_or_not):
+        if not (y_1.is_cuda and y_2.is_cuda):
+            raise RuntimeError("ngnn.losses.CTLoss: GPU only (no CPU fallback)")
+        if y_1.dim() != 2 or y_1.shape != y_2.shape or y_1.dtype != torch.float32 \
+                or y_2.dtype != torch.float32:
+            raise ValueError("y_1, y_2 must be float32 [B, C] tensors of the same shape")
+        B, C = y_1.shape
+        dev = y_1.device
+        remember_rate = 1 - forget_rate
+        num_remember = int(remember_rate * B)  # losses.py:29-30, same float arithmetic
+        if not 0 <= num_remember <= B:
+            raise ValueError(f"forget_rate {forget_rate} gives num_remember {num_remember}")
+        a = y_1 if y_1.stride(1) == 1 else y_1.contiguous()
+        b = y_2 if y_2.stride(1) == 1 else y_2.contiguous()
+        yn = y_noise.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        if yn.numel() != B:
+            raise ValueError("y_noise must hold one label per row")
+        idx = None if ind is None else ind.to(device=dev, dtype=torch.int64).contiguous()
+        clean = None
+        if noise_or_not is not None:
+            clean = noise_or_not.to(device=dev, dtype=torch.bool).contiguous()
+        # per call (caching allocator, no sync): both backwards read it later
+        ws = torch.empty(_lib.load().ngnn_ct_loss_workspace_bytes(B), dtype=torch.uint8, device=dev)
+        out = torch.empty(4, dtype=torch.float32, device=dev)
+        i1 = torch.empty(B, dtype=torch.int64, device=dev)
+        i2 = torch.empty(B, dtype=torch.int64, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(_lib.load().ngnn_ct_loss_fwd(
+            _lib.ptr(a), a.stride(0), _lib.ptr(b), b.stride(0), B, C, _lib.ptr(yn),
+            int(self.ignore_index), num_remember, _lib.ptr(idx), _lib.ptr(clean),
+            0 if clean is None else clean.numel(), _lib.ptr(out), _lib.ptr(i1), _lib.ptr(i2),
+            _lib.ptr(ws), ws.numel(), _lib.ptr(err), _lib.stream_handle(dev)), "ngnn_ct_loss_fwd")
+        self.index_error = err
+        st = _CTState()
+        st.ws, st.out, st.y_noise, st.ignore, st.B, st.C = ws, out, yn, int(self.ignore_index), B, C
+        loss_1 = _CTPick.apply(a, st, 0)
+        loss_2 = _CTPick.apply(b, st, 1)
+        return (loss_1, loss_2, out[2], out[3], i1[:num_remember], i2[:num_remember],
+                i1[num_remember:], i2[num_remember:])

@@ -119,9 +119,39 @@ def run_model_case(model, x, ei, seed, train=False):
     return rec
 
 
+def ct_loss_cases(ref: str):
+    if ref not in sys.path:
+        sys.path.insert(0, ref)
+    import importlib
+    losses = importlib.import_module("src.utils.losses")
+    out = {}
+    for name, B, C, n_graph, forget, seed in [("ct_loss_b300", 300, 47, 1000, 0.2, 1000),
+                                              ("ct_loss_b1024", 1024, 40, 5000, 0.45, 1001)]:
+        g = torch.Generator().manual_seed(seed)
+        y1 = (2 * torch.randn(B, C, generator=g)).requires_grad_(True)
+        y2 = (2 * torch.randn(B, C, generator=g)).requires_grad_(True)
+        yn = torch.randint(0, C, (B,), generator=g)
+        ind = torch.randperm(n_graph, generator=g)[:B]
+        clean = torch.rand(n_graph, generator=g) < 0.7
+        crit = losses.CTLoss("cpu")
+        l1, l2, p1, p2, i1, i2, n1, n2 = crit(y1, y2, yn, forget, ind, clean)
+        l1.backward()
+        l2.backward()
+        out[name] = {"y1": y1.detach().numpy(), "y2": y2.detach().numpy(), "y_noise": yn.numpy(),
+                     "ind": ind.numpy(), "noise_or_not": clean.numpy(),
+                     "forget_rate": np.array(forget), "loss_1": l1.detach().numpy(),
+                     "loss_2": l2.detach().numpy(), "pure_ratio_1": np.asarray(p1, dtype=np.float32),
+                     "pure_ratio_2": np.asarray(p2, dtype=np.float32),
+                     "ind_1_update": np.asarray(i1), "ind_2_update": np.asarray(i2),
+                     "ind_noisy_1": np.asarray(n1), "ind_noisy_2": np.asarray(n2),
+                     "grad_y1": y1.grad.numpy(), "grad_y2": y2.grad.numpy(), "meta/seed": np.array(seed)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="comma list of case names to (re)write")
     args = ap.parse_args()
     out_dir = HERE
     cases = {}
@@ -212,6 +242,14 @@ def main():
         rec["param/" + k] = v.numpy().copy()
     cases["sage_inference"] = rec
 
+    # 8. co-teaching loss (src/utils/losses.py:19-49, imported from the checkout):
+    #    tie-free continuous logits; forward outputs, kept indices, and the
+    #    gradients of each model's loss
+    cases.update(ct_loss_cases(args.ref))
+
+    if args.only:
+        keep = set(args.only.split(","))
+        cases = {k: v for k, v in cases.items() if k in keep}
     total = 0
     for name, rec in cases.items():
         path = os.path.join(out_dir, name + ".npz")

@@ -48,3 +48,118 @@ def test_cpu_raises():
     from ngnn.losses import seed_cross_entropy
     with pytest.raises(RuntimeError):
         seed_cross_entropy(torch.zeros(4, 3), torch.zeros(4, dtype=torch.long), 2)
+
+
+# ---- co-teaching loss (CTLoss, losses.py:19-49) on the device
+
+import os  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from ngnn.losses import CTLoss  # noqa: E402
+from oracle import losses_ref  # noqa: E402
+
+
+def _run_ct(y1, y2, yn, forget, ind, clean):
+    a = y1.cuda().requires_grad_(True)
+    b = y2.cuda().requires_grad_(True)
+    out = CTLoss("cuda")(a, b, yn.cuda(), forget, None if ind is None else ind.cuda(),
+                         None if clean is None else clean.cuda())
+    out[0].backward()
+    out[1].backward()
+    return out, a.grad, b.grad
+
+
+@pytest.mark.parametrize("name", ["ct_loss_b300", "ct_loss_b1024"])
+def test_ct_loss_vs_reference_fixture(golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    y1, y2 = torch.from_numpy(g["y1"]), torch.from_numpy(g["y2"])
+    yn = torch.from_numpy(g["y_noise"])
+    (l1, l2, p1, p2, i1, i2, n1, n2), g1, g2 = _run_ct(
+        y1, y2, yn, float(g["forget_rate"]), torch.from_numpy(g["ind"]),
+        torch.from_numpy(g["noise_or_not"]))
+    R = len(g["ind_1_update"])
+    assert i1.numel() == R and n1.numel() == len(y1) - R
+    for m, (y, ik, nk, dev_sorted) in enumerate(((y1, "ind_1_update", "ind_noisy_1", torch.cat([i1, n1])),
+                                                 (y2, "ind_2_update", "ind_noisy_2", torch.cat([i2, n2])))):
+        lref = F.cross_entropy(y, yn, reduction="none")
+        ref_sorted = torch.from_numpy(np.concatenate([g[ik], g[nk]]))
+        # a valid ascending order of the same losses (fp32 row losses may differ by an ulp,
+        # so near-ties may swap); identical positions wherever the gap is clear
+        torch.testing.assert_close(lref[dev_sorted.cpu()], lref[ref_sorted], rtol=0, atol=2e-6)
+        gap = (lref[ref_sorted][R] - lref[ref_sorted][R - 1]).item()
+        if gap > 1e-5:
+            assert set(dev_sorted[:R].tolist()) == set(ref_sorted[:R].tolist())
+    torch.testing.assert_close(l1.detach().cpu(), torch.from_numpy(g["loss_1"]), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(l2.detach().cpu(), torch.from_numpy(g["loss_2"]), rtol=1e-5, atol=1e-6)
+    assert abs(float(p1) - float(g["pure_ratio_1"])) < 1e-6
+    assert abs(float(p2) - float(g["pure_ratio_2"])) < 1e-6
+    torch.testing.assert_close(g1.cpu(), torch.from_numpy(g["grad_y1"]), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(g2.cpu(), torch.from_numpy(g["grad_y2"]), rtol=1e-5, atol=1e-7)
+
+
+def _separated_logits(B, C, seed):
+    """rows whose losses are far apart (well-defined order): label 0 and a
+    first logit stepping by 0.01 per (shuffled) row"""
+    gen = torch.Generator().manual_seed(seed)
+    y = torch.randn(B, C, generator=gen) * 0.1
+    y[:, 0] = torch.linspace(-3, 3, B)[torch.randperm(B, generator=gen)]
+    return y
+
+
+@pytest.mark.parametrize("B,C,forget", [(1024, 47, 0.2), (17, 3, 0.5), (4096, 10, 0.0),
+                                        (8192, 40, 0.9), (5, 2, 1.0)])
+def test_ct_loss_vs_oracle_separated(B, C, forget):
+    y1, y2 = _separated_logits(B, C, 1), _separated_logits(B, C, 2)
+    yn = torch.zeros(B, dtype=torch.long)
+    ind = torch.randperm(3 * B)[:B]
+    clean = torch.rand(3 * B) < 0.5
+    dev_out, g1, g2 = _run_ct(y1, y2, yn, forget, ind, clean)
+    a, b = y1.clone().requires_grad_(True), y2.clone().requires_grad_(True)
+    ref = losses_ref.ct_loss(a, b, yn, forget, ind, clean)
+    R = ref[4].numel()
+    for k in (4, 5, 6, 7):  # index outputs: bitwise
+        assert torch.equal(dev_out[k].cpu(), ref[k]), k
+    if R == 0:  # empty selection: NaN, as torch's mean of nothing
+        assert torch.isnan(dev_out[0]).item() and torch.isnan(dev_out[2]).item()
+        return
+    for k in (0, 1, 2, 3):
+        torch.testing.assert_close(dev_out[k].detach().cpu().float(), ref[k].detach().float(),
+                                   rtol=1e-5, atol=1e-6)
+    ref[0].backward()
+    ref[1].backward()
+    torch.testing.assert_close(g1.cpu(), a.grad, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(g2.cpu(), b.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_ct_loss_ties_and_ignore_index():
+    B, C = 64, 5
+    y1 = torch.zeros(B, C)  # every loss ties: order by row index
+    y2 = _separated_logits(B, C, 3)
+    yn = torch.zeros(B, dtype=torch.long)
+    yn[::7] = -100  # ignored rows: loss 0 -> sorted first, excluded from the means
+    dev_out, g1, g2 = _run_ct(y1, y2, yn, 0.25, None, torch.ones(B, dtype=torch.bool))
+    a, b = y1.clone().requires_grad_(True), y2.clone().requires_grad_(True)
+    ref = losses_ref.ct_loss(a, b, yn, 0.25, torch.arange(B), torch.ones(B, dtype=torch.bool))
+    for k in (4, 5, 6, 7):
+        assert torch.equal(dev_out[k].cpu(), ref[k]), k
+    for k in (0, 1, 2, 3):
+        torch.testing.assert_close(dev_out[k].detach().cpu().float(), ref[k].detach().float(),
+                                   rtol=1e-5, atol=1e-6)
+    ref[0].backward()
+    ref[1].backward()
+    torch.testing.assert_close(g1.cpu(), a.grad, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(g2.cpu(), b.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_ct_loss_backwards_are_independent():
+    """loss_1.backward() touches only model 1's graph (pipeline.py:125-131)."""
+    w1 = torch.randn(8, 4, device="cuda", requires_grad=True)
+    w2 = torch.randn(8, 4, device="cuda", requires_grad=True)
+    x = torch.randn(32, 8, device="cuda")
+    out = CTLoss("cuda")(x @ w1, x @ w2, torch.randint(0, 4, (32,), device="cuda"), 0.3, None, None)
+    out[0].backward()
+    assert w1.grad is not None and w2.grad is None
+    out[1].backward()
+    assert w2.grad is not None

@@ -172,3 +172,26 @@ def test_c_oracle_on_golden_block(golden_dir):
     got = c_agg.agg_fwd(x, ei, x.shape[0], "mean")
     want = pyg_ref.propagate(torch.from_numpy(x), torch.from_numpy(ei), "mean").numpy()
     assert np.array_equal(got, want)
+
+
+# ---- co-teaching loss restatement vs the reference's own CTLoss (fixtures)
+
+@pytest.mark.parametrize("name", ["ct_loss_b300", "ct_loss_b1024"])
+def test_ct_loss_oracle_matches_reference(golden_dir, name):
+    from oracle import losses_ref
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    y1 = torch.from_numpy(g["y1"]).requires_grad_(True)
+    y2 = torch.from_numpy(g["y2"]).requires_grad_(True)
+    out = losses_ref.ct_loss(y1, y2, torch.from_numpy(g["y_noise"]), float(g["forget_rate"]),
+                             torch.from_numpy(g["ind"]), torch.from_numpy(g["noise_or_not"]))
+    l1, l2, p1, p2, i1, i2, n1, n2 = out
+    assert torch.equal(l1.detach(), torch.from_numpy(g["loss_1"]))
+    assert torch.equal(l2.detach(), torch.from_numpy(g["loss_2"]))
+    assert float(p1) == float(g["pure_ratio_1"]) and float(p2) == float(g["pure_ratio_2"])
+    for got, key in ((i1, "ind_1_update"), (i2, "ind_2_update"), (n1, "ind_noisy_1"),
+                     (n2, "ind_noisy_2")):
+        assert np.array_equal(got.numpy(), g[key]), key
+    l1.backward()
+    l2.backward()
+    assert torch.equal(y1.grad, torch.from_numpy(g["grad_y1"]))
+    assert torch.equal(y2.grad, torch.from_numpy(g["grad_y2"]))
