@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 6
+#define NGNN_ABI_VERSION 7
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -361,12 +361,15 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * pointers; grads, exp_avgs, exp_avg_sqs like params, numels their sizes),
  * torch.optim.Adam's rule (amsgrad/maximize off, optional L2 weight decay),
  * with the step count a device float that this call advances (so a captured
- * HIP graph replays correctly).  Replaces the reference's
- * torch.optim.Adam(...).step() (model.py:66-69). */
+ * HIP graph replays correctly).  ticket (nullable): a device uint32, zero
+ * before the first call, that the update's workgroups count themselves on;
+ * the last one advances *step and re-zeroes it (one launch per call instead
+ * of an update + increment pair; up to 16 tensors).  Replaces the
+ * reference's torch.optim.Adam(...).step() (model.py:66-69). */
 int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
-                   float *step, float lr, float beta1, float beta2, float eps, float weight_decay,
-                   void *stream);
+                   float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, void *stream);
 
 /* ------------------------------------------------------ HIP-graph slot
  * Fill the static slot a captured training step reads (ngnn/graphs.py) with
@@ -380,13 +383,16 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * by one splitmix64 step (the dropout seed of the captured step).  x_dev
  * (nullable): zero-copy -- store x's address there instead of copying the
  * rows (slot_x may then be NULL; x 16-B aligned with ldx == ld_slot).
- * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
+ * r_next (nullable): *r_next = max(B, 1 + max source of the edges into rows
+ * < B) -- ngnn_block_prefix_stats for R = B, the input-gradient row bound of
+ * the top layer's backward (computed here so the captured step has no
+ * bound launch).  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
-                   uint64_t *seed_state, const float **x_dev, void *stream);
+                   uint64_t *seed_state, const float **x_dev, int32_t *r_next, void *stream);
 
 #ifdef __cplusplus
 }

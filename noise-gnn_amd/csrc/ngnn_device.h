@@ -43,7 +43,9 @@ __device__ __forceinline__ float nanmax(float acc, float v) {
 }
 
 // ---- dropout RNG: counter-based, keyed by (seed, row, col); the keep mask is
-// never stored.  keep <=> (hash >> 8) >= thresh, thresh = ceil(p * 2^24).
+// never stored.  One 32-bit hash per column PAIR (2c, 2c+1): its low half
+// decides column 2c, its high half 2c+1; keep <=> half >= thresh,
+// thresh = ceil(p * 2^16) (p resolved to 1/65536; p = 0.5 exactly).
 // Host replica: tests/test_gpu_fused.py::dropout_keep.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;
@@ -55,15 +57,21 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 }
 
 struct Dropout {
-    uint32_t s0, s1, thresh;  // thresh == 0: no dropout; > 2^24: drop all
+    uint32_t s0, s1, thresh;  // thresh == 0: no dropout; > 2^16: drop all
     float scale;
-    // one hash per row (seed-mixed), one per element: rkey + col are distinct
-    // within a row and lowbias32 is a bijection
+    // one hash per row (seed-mixed), one per column pair: rkey + col/2 are
+    // distinct within a row and lowbias32 is a bijection
     __device__ __forceinline__ uint32_t row_key(uint32_t row) const {
         return lowbias32(row ^ s0) ^ s1;
     }
+    __device__ __forceinline__ uint32_t pair_hash(uint32_t rkey, uint32_t col) const {
+        return lowbias32(rkey + (col >> 1));
+    }
+    __device__ __forceinline__ bool keep_half(uint32_t h, uint32_t col) const {
+        return ((col & 1u) ? (h >> 16) : (h & 0xffffu)) >= thresh;
+    }
     __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
-        return (lowbias32(rkey + col) >> 8) >= thresh;
+        return keep_half(pair_hash(rkey, col), col);
     }
     __device__ __forceinline__ void reseed(uint64_t d) {
         s0 ^= static_cast<uint32_t>(d);
@@ -88,10 +96,10 @@ inline Dropout make_dropout(float p, uint64_t seed) {
         d.thresh = 0;
         d.scale = 1.0f;
     } else if (p >= 1.0f) {
-        d.thresh = (1u << 24) + 1;  // nothing kept
+        d.thresh = (1u << 16) + 1;  // nothing kept
         d.scale = 0.0f;
     } else {
-        const double t = static_cast<double>(p) * 16777216.0;
+        const double t = static_cast<double>(p) * 65536.0;
         uint32_t ti = static_cast<uint32_t>(t);
         if (static_cast<double>(ti) < t) ++ti;  // ceil
         d.thresh = ti;

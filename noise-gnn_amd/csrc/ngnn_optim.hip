@@ -1,7 +1,7 @@
 // Adam for the training step (the reference's optimiser: torch.optim.Adam,
-// model.py:66-69 [ext: torch]) as one update launch over every parameter
-// tensor plus a one-thread step-count launch, instead of torch's step
-// increment + multi-tensor fused kernel.  Same update rule as torch Adam
+// model.py:66-69 [ext: torch]) as ONE launch over every parameter tensor:
+// the last workgroup to finish (a device ticket) advances the step count,
+// instead of torch's step increment + multi-tensor fused kernel.  Same update rule as torch Adam
 // (amsgrad off, maximize off):
 //   t = step + 1;  g += wd p;  m = m + (1 - b1)(g - m);  v = b2 v + (1 - b2) g^2
 //   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
@@ -22,8 +22,9 @@ struct AdamTensors {
     int n;
 };
 
-__global__ __launch_bounds__(256) void k_adam(AdamTensors T, const float *__restrict__ step, float lr,
-                                              float b1, float b2, float eps, float wd) {
+__global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__ step,
+                                              uint32_t *__restrict__ ticket, float lr, float b1,
+                                              float b2, float eps, float wd) {
     const float t = *step + 1.0f;
     const float bc1 = 1.0f - powf(b1, t);
     const float bc2s = sqrtf(1.0f - powf(b2, t));
@@ -47,6 +48,15 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, const float *__rest
         T.v[k][j] = v;
         T.p[k][j] = p;
     }
+    if (ticket) {
+        // every workgroup has read *step (its value fed the loop above) before
+        // it takes a ticket; the last one advances the count for the next call
+        __syncthreads();
+        if (threadIdx.x == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {
+            *step = t;
+            *ticket = 0u;
+        }
+    }
 }
 
 __global__ void k_step_inc(float *step) { *step += 1.0f; }
@@ -58,12 +68,16 @@ using namespace ngnn;
 
 extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                               float *const *exp_avgs, float *const *exp_avg_sqs,
-                              const int64_t *numels, float *step, float lr, float beta1,
-                              float beta2, float eps, float weight_decay, void *stream) {
+                              const int64_t *numels, float *step, uint32_t *ticket, float lr,
+                              float beta1, float beta2, float eps, float weight_decay,
+                              void *stream) {
     NGNN_RETURN_IF(n_tensors < 0 || !step, NGNN_E_ARG);
     NGNN_RETURN_IF(n_tensors > 0 && (!params || !grads || !exp_avgs || !exp_avg_sqs || !numels),
                    NGNN_E_ARG);
     hipStream_t st = as_stream(stream);
+    // the ticket path needs every tensor in one launch (one reader set of *step)
+    if (n_tensors > kMaxT) ticket = nullptr;
+    bool launched = false;
     for (int base = 0; base < n_tensors; base += kMaxT) {
         AdamTensors T;
         T.n = std::min(kMaxT, n_tensors - base);
@@ -81,11 +95,13 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         }
         if (T.off[T.n] == 0) continue;
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(T.off[T.n], 256), 2048));
-        hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, lr, beta1, beta2, eps,
-                           weight_decay);
+        hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
+                           eps, weight_decay);
         const int rc = launch_status();
         if (rc) return rc;
+        launched = true;
     }
+    if (ticket && launched) return NGNN_OK;
     hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, st, step);
     return launch_status();
 }

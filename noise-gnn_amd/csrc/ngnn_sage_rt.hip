@@ -297,15 +297,17 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
         if (m >= a.NT) continue;  // padded tiles (uniform)
         const int f = m * 16 + 4 * q;
         const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
+        // two pair hashes cover the lane's 4 columns (col_base + f is even)
+        const uint32_t c0 = static_cast<uint32_t>(a.epi.col_base + f);
+        const uint32_t h0 = DROP ? a.epi.drop.pair_hash(rk, c0) : 0u;
+        const uint32_t h1 = DROP ? a.epi.drop.pair_hash(rk, c0 + 2) : 0u;
         v4f v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             float y = acc[m][j] + b[j];
             y = (relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
             if (DROP)
-                y = a.epi.drop.keep(rk, static_cast<uint32_t>(a.epi.col_base + f + j))
-                        ? y * a.epi.drop.scale
-                        : 0.0f;
+                y = a.epi.drop.keep_half(j < 2 ? h0 : h1, c0 + j) ? y * a.epi.drop.scale : 0.0f;
             v[j] = y;
         }
         if (a.dbg & 2) {

@@ -170,7 +170,13 @@ class _SAGEStack(torch.autograd.Function):
         rows_hint = getattr(dout, "_ngnn_nonzero_rows", None)  # set by ngnn.losses
         bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
                          dtype=torch.int32, device=dev)
-        bptr = lambda j: bnd.data_ptr() + 4 * j  # noqa: E731
+        bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
+        # the producer's precomputed top-layer bound (graph slot): no prefix-stats launch
+        pre_top = (L > 0 and block.r_next is not None and rows_hint is not None
+                   and int(rows_hint) == block.r_next[1])
+        if pre_top:
+            bp[L - 1] = block.r_next[0].data_ptr()
+        bptr = lambda j: bp[j]  # noqa: E731
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")
@@ -201,9 +207,10 @@ class _SAGEStack(torch.autograd.Function):
             grads[3 * i:3 * i + 3] = [dwl, dbl, dwr]
             if i == 0 and not need_dx:
                 break
-            _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
-                                                   bptr(i + 1), None, bptr(i), block.E, stream),
-                       "ngnn_block_prefix_stats")
+            if not (pre_top and i == L - 1):
+                _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
+                                                       bptr(i + 1), None, bptr(i), block.E, stream),
+                           "ngnn_block_prefix_stats")
             if not deterministic and Fo < K and reduce in ("sum", "mean"):
                 # narrow-space path: scatter dz (Fo wide), then one MFMA pass
                 dh = torch.empty(N, K, dtype=torch.float32, device=dev)

@@ -60,6 +60,9 @@ class GraphedTrainStep:
         # zero-copy input: the slot load stores the batch's feature address
         # here and the captured layer-0 kernels read the rows in place
         self.x_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        # input-gradient row bound of the top layer (prefix stats for R = B),
+        # written by the slot load so the captured backward needs no bound launch
+        self.r_next = torch.zeros(1, dtype=torch.int32, device=dev)
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
         self.loss = None
@@ -84,7 +87,8 @@ class GraphedTrainStep:
             _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
             _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
-            _lib.ptr(self.x_dev) if zero_copy else None, _lib.stream_handle(self.x.device)),
+            _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next),
+            _lib.stream_handle(self.x.device)),
             "ngnn_slot_load")
         self._x_live = x if zero_copy else None
 
@@ -121,7 +125,7 @@ class GraphedTrainStep:
         block_cache.clear()
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
-                        x_dev=self.x_dev)
+                        x_dev=self.x_dev, r_next=(self.r_next, self.B))
         self.opt.zero_grad(set_to_none=True)
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):

@@ -1,5 +1,5 @@
-"""Adam on the device in two launches (ngnn_adam_step): the update over every
-parameter tensor, then the step-count increment.
+"""Adam on the device in one launch (ngnn_adam_step): the update over every
+parameter tensor; its last workgroup advances the step count.
 
 Same rule and hyper-parameters as ``torch.optim.Adam`` (the reference's
 optimiser, model.py:66-69; amsgrad / maximize / foreach variants not
@@ -22,6 +22,7 @@ class Adam(torch.optim.Optimizer):
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       capturable=True))
+        self._tickets: dict = {}  # step tensor address -> device ticket
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -48,6 +49,10 @@ class Adam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
             step = self.state[ps[0]]["step"]
+            ticket = self._tickets.get(step.data_ptr())
+            if ticket is None:  # zero once; the kernel re-zeroes it after every use
+                ticket = torch.zeros(1, dtype=torch.int32, device=step.device)
+                self._tickets[step.data_ptr()] = ticket
             grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
             n = len(ps)
             P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in ps])
@@ -56,7 +61,8 @@ class Adam(torch.optim.Optimizer):
             V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps])
             N = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
             b1, b2 = group["betas"]
-            _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, step.data_ptr(), float(group["lr"]),
+            _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, step.data_ptr(), ticket.data_ptr(),
+                                          float(group["lr"]),
                                           float(b1), float(b2), float(group["eps"]),
                                           float(group["weight_decay"]),
                                           _lib.stream_handle(ps[0].device)), "ngnn_adam_step")

@@ -34,15 +34,18 @@ def _lowbias32(x):
 
 
 def dropout_keep(seed, n_rows, n_cols, p):
-    """Host replica of ngnn_device.h::Dropout: keep <=> (hash >> 8) >= ceil(p * 2^24)."""
+    """Host replica of ngnn_device.h::Dropout: one hash per column pair,
+    keep <=> 16-bit half >= ceil(p * 2^16)."""
     import math
     s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
-    thresh = math.ceil(float(np.float32(p)) * 16777216.0)
+    pf = float(np.float32(p))
+    thresh = 0 if pf <= 0 else (65537 if pf >= 1 else math.ceil(pf * 65536.0))
     r = np.arange(n_rows, dtype=np.uint64)[:, None]
     c = np.arange(n_cols, dtype=np.uint64)[None, :]
     rk = _lowbias32(r ^ s0) ^ s1
-    h = _lowbias32((rk + c) & M32)
-    return torch.from_numpy((h >> np.uint64(8)) >= np.uint64(thresh))
+    h = _lowbias32((rk + (c >> np.uint64(1))) & M32)
+    half = np.where((c & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    return torch.from_numpy(half >= np.uint64(thresh))
 
 
 def rand_block(seed, N, E, order="dst"):
