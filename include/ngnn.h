@@ -383,16 +383,18 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * by one splitmix64 step (the dropout seed of the captured step).  x_dev
  * (nullable): zero-copy -- store x's address there instead of copying the
  * rows (slot_x may then be NULL; x 16-B aligned with ldx == ld_slot).
- * r_next (nullable): *r_next = max(B, 1 + max source of the edges into rows
- * < B) -- ngnn_block_prefix_stats for R = B, the input-gradient row bound of
- * the top layer's backward (computed here so the captured step has no
- * bound launch).  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
+ * r_next (nullable, 8-B aligned): its low 32 bits become max(B, 1 + max
+ * source of the edges into rows < B) -- ngnn_block_prefix_stats for R = B,
+ * the input-gradient row bound of the top layer's backward (computed here
+ * so the captured step has no bound launch).  Kept by a 64-bit atomicMax of
+ * (gen << 32 | value): gen must grow with every load (no reset launch).  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
-                   uint64_t *seed_state, const float **x_dev, int32_t *r_next, void *stream);
+                   uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
+                   void *stream);
 
 #ifdef __cplusplus
 }

@@ -114,7 +114,38 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_init(const int64_t *__restrict_
     }
 }
 
+// Floyd draws with the fanout bounded at compile time (KF >= fanout): the
+// selections stay in registers (fully unrolled), so a node's column and map
+// loads issue back to back instead of as one dependent chain through
+// scratch.  Same draws as floyd_sample.
+template <int KF>
+__device__ __forceinline__ int floyd_sample_r(int64_t d, int fanout, uint64_t seed, int64_t i,
+                                              int32_t (&sel)[KF]) {
+    const int k = d < fanout ? static_cast<int>(d) : fanout;
+    if (d <= fanout) {
+#pragma unroll
+        for (int j = 0; j < KF; ++j) sel[j] = j;
+        return k;
+    }
+    const uint64_t base = mix64(seed ^ mix64(static_cast<uint64_t>(i) + 0x632BE59BD9B4E019ull));
+#pragma unroll
+    for (int jj = 0; jj < KF; ++jj) {
+        if (jj < k) {
+            const int64_t j = d - k + jj;
+            const uint64_t r = mix64(base + static_cast<uint64_t>(j));
+            const int64_t t = static_cast<int64_t>(
+                (static_cast<unsigned __int128>(r) * static_cast<uint64_t>(j + 1)) >> 64);
+            bool dup = false;
+#pragma unroll
+            for (int q = 0; q < jj; ++q) dup |= sel[q] == t;
+            sel[jj] = static_cast<int32_t>(dup ? j : t);
+        }
+    }
+    return k;
+}
+
 // draws of frontier node i -> cand[i*f + j]; claims first appearances
+template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ gcol, int64_t n_graph,
     const int32_t *__restrict__ hs, const int32_t *__restrict__ nid, int fanout, uint64_t seed,
@@ -124,26 +155,45 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     if (i >= hi - lo) return;
     const int64_t v = nid[lo + i];
     const int64_t b = rowptr[v];
-    int64_t sel[kMaxFanout];
-    const int k = floyd_sample(rowptr[v + 1] - b, fanout, seed, i, sel);
+    int32_t sel[KF];
+    const int k = floyd_sample_r<KF>(rowptr[v + 1] - b, fanout, seed, i, sel);
+    int32_t u[KF], mp[KF];
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k) u[j] = gcol[b + sel[j]];
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k) {
+            cand[i * fanout + j] = u[j];
+            mp[j] = map[u[j]];
+        }
     int32_t *claim = map + n_graph;
-    for (int j = 0; j < k; ++j) {
-        const int32_t u = gcol[b + sel[j]];
-        cand[i * fanout + j] = u;
-        if (map[u] < 0) atomicMax(claim + u, INT32_MAX - (i * fanout + j));
-    }
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k && mp[j] < 0) atomicMax(claim + u[j], INT32_MAX - (i * fanout + j));
     cnt[i] = k;
 }
 
-// number of first appearances among frontier node i's draws
-__device__ __forceinline__ int sb_new_count(const int32_t *cand, const int32_t *map,
-                                            const int32_t *claim, int i, int fanout, int k) {
-    int n = 0;
-    for (int j = 0; j < k; ++j) {
-        const int32_t u = cand[i * fanout + j];
-        n += (claim[u] == INT32_MAX - (i * fanout + j)) & (map[u] < 0);
-    }
-    return n;
+// first-appearance flags of frontier node i's draws (bit j), and the draws
+template <int KF>
+__device__ __forceinline__ uint64_t sb_new_flags(const int32_t *cand, const int32_t *map,
+                                                 const int32_t *claim, int i, int fanout, int k,
+                                                 int32_t (&u)[KF]) {
+    int32_t c[KF], m[KF];
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k) u[j] = cand[i * fanout + j];
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k) {
+            c[j] = claim[u[j]];
+            m[j] = map[u[j]];
+        }
+    uint64_t f = 0;
+#pragma unroll
+    for (int j = 0; j < KF; ++j)
+        if (j < k && c[j] == INT32_MAX - (i * fanout + j) && m[j] < 0) f |= 1ull << j;
+    return f;
 }
 
 __device__ __forceinline__ int block_sum(int v, int *red) {
@@ -157,6 +207,7 @@ __device__ __forceinline__ int block_sum(int v, int *red) {
     return t;
 }
 
+template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_count(const int32_t *__restrict__ hs,
                                                        const int32_t *__restrict__ cand,
                                                        const int32_t *__restrict__ cnt,
@@ -169,7 +220,8 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_count(const int32_t *__restrict
     int e = 0, n = 0;
     if (i < nf) {
         e = cnt[i];
-        n = sb_new_count(cand, map, map + n_graph, i, fanout, e);
+        int32_t u[KF];
+        n = __popcll(sb_new_flags<KF>(cand, map, map + n_graph, i, fanout, e, u));
     }
     e = block_sum(e, red);
     n = block_sum(n, red);
@@ -234,6 +286,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int *sh) {
 
 // new local ids (first appearances, in order) and the hop's edges
 // (global source ids for now, local targets)
+template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_assign(
     const int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
     int32_t *__restrict__ map, int64_t n_graph, int fanout, const int32_t *__restrict__ bsum,
@@ -242,23 +295,27 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_assign(
     const int i = blockIdx.x * kSbBlock + threadIdx.x;
     const int lo = hs[0], hi = hs[1], e0 = hs[2];
     const int nf = hi - lo;
-    const int32_t *claim = map + n_graph;
-    int k = 0, nn = 0;
+    int k = 0;
+    uint64_t fl = 0;
+    int32_t u[KF];
     if (i < nf) {
         k = cnt[i];
-        nn = sb_new_count(cand, map, claim, i, fanout, k);
+        // only the owner of u's claim ever writes map[u], and every flag is
+        // read before this thread writes: the test is race-free
+        fl = sb_new_flags<KF>(cand, map, map + n_graph, i, fanout, k, u);
     }
     int e = e0 + bsum[blockIdx.x] + block_excl_scan(k, sh);
-    int n = hi + bsum[nblk + blockIdx.x] + block_excl_scan(nn, sh);
-    for (int j = 0; j < k; ++j, ++e) {
-        const int32_t u = cand[i * fanout + j];
-        // only the owner of u's claim ever writes map[u]: the test is race-free
-        if (claim[u] == INT32_MAX - (i * fanout + j) && map[u] < 0) {
-            map[u] = n;
-            nid[n++] = u;
+    int n = hi + bsum[nblk + blockIdx.x] + block_excl_scan(__popcll(fl), sh);
+#pragma unroll
+    for (int j = 0; j < KF; ++j) {
+        if (j < k) {
+            if ((fl >> j) & 1) {
+                map[u[j]] = n;
+                nid[n++] = u[j];
+            }
+            esrc[e + j] = u[j];
+            edst[e + j] = lo + i;
         }
-        esrc[e] = u;
-        edst[e] = lo + i;
     }
 }
 
@@ -291,16 +348,29 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_finish(
     }
 }
 
-// x[i] = x_all[n_id[i]], 16-B vectors (F % 4 == 0, aligned rows)
+// x[i] = x_all[n_id[i]], 16-B vectors (F % 4 == 0, aligned rows); 32-bit
+// item indices (n * F/4 < 2^31 checked by the caller), 4 vectors in flight
 __global__ __launch_bounds__(kSbBlock) void k_gather_rows4(const float *__restrict__ x_all,
                                                            int64_t ldx, const int32_t *__restrict__ nid,
-                                                           int64_t n, int64_t f4,
-                                                           float *__restrict__ x, int64_t ldo) {
-    const int64_t stride = (int64_t)gridDim.x * kSbBlock;
-    for (int64_t t = blockIdx.x * (int64_t)kSbBlock + threadIdx.x; t < n * f4; t += stride) {
-        const int64_t r = t / f4, c = (t - r * f4) * 4;
-        *reinterpret_cast<float4 *>(x + r * ldo + c) =
-            *reinterpret_cast<const float4 *>(x_all + nid[r] * ldx + c);
+                                                           int n, int f4, float *__restrict__ x,
+                                                           int64_t ldo) {
+    const int total = n * f4;
+    const int stride = gridDim.x * kSbBlock;
+    for (int t0 = blockIdx.x * kSbBlock + threadIdx.x; t0 < total; t0 += 4 * stride) {
+        float4 v[4];
+        int r[4], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + u * stride;
+            r[u] = t / f4;
+            c[u] = (t - r[u] * f4) * 4;
+            if (t < total)
+                v[u] = *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(nid[r[u]]) * ldx + c[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (t0 + u * stride < total)
+                *reinterpret_cast<float4 *>(x + static_cast<int64_t>(r[u]) * ldo + c[u]) = v[u];
     }
 }
 
@@ -419,6 +489,7 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
                        w.state);
     for (int h = 0; h < n_hops; ++h) {
         const int f = fanouts[h];
+        const int kf = f <= 8 ? 8 : f <= 16 ? 16 : f <= 32 ? 32 : 64;
         int32_t *hs = w.state + 4 * h;
         const int64_t nf = p.nf_cap[h];
         const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf, kSbBlock)));
@@ -426,17 +497,35 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
         // the per-hop seed of ngnn_sample_hop's callers (loader.sample_block)
         const uint64_t hseed = seed * 1000003ull + static_cast<uint64_t>(h);
         if (f > 0) {
-            hipLaunchKernelGGL(k_sb_sample, dim3(nblk), dim3(kSbBlock), 0, st, g_rowptr, g_col,
-                               n_graph, hs, w.nid, f, hseed, cand, cnt, node_map);
-            hipLaunchKernelGGL(k_sb_count, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt, node_map,
-                               n_graph, f, w.bsum, nblk);
+            auto sample = [&](auto kf_c) {
+                constexpr int KF = decltype(kf_c)::value;
+                hipLaunchKernelGGL(k_sb_sample<KF>, dim3(nblk), dim3(kSbBlock), 0, st, g_rowptr, g_col,
+                                   n_graph, hs, w.nid, f, hseed, cand, cnt, node_map);
+                hipLaunchKernelGGL(k_sb_count<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt,
+                                   node_map, n_graph, f, w.bsum, nblk);
+            };
+            switch (kf) {
+                case 8: sample(std::integral_constant<int, 8>{}); break;
+                case 16: sample(std::integral_constant<int, 16>{}); break;
+                case 32: sample(std::integral_constant<int, 32>{}); break;
+                default: sample(std::integral_constant<int, 64>{}); break;
+            }
         } else {
             (void)hipMemsetAsync(w.bsum, 0, 2 * nblk * sizeof(int32_t), st);
         }
         hipLaunchKernelGGL(k_sb_scan, dim3(1), dim3(1024), 0, st, hs, w.bsum, nblk);
         if (f > 0) {
-            hipLaunchKernelGGL(k_sb_assign, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt,
-                               node_map, n_graph, f, w.bsum, nblk, w.nid, w.esrc, w.edst);
+            auto assign = [&](auto kf_c) {
+                constexpr int KF = decltype(kf_c)::value;
+                hipLaunchKernelGGL(k_sb_assign<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt,
+                                   node_map, n_graph, f, w.bsum, nblk, w.nid, w.esrc, w.edst);
+            };
+            switch (kf) {
+                case 8: assign(std::integral_constant<int, 8>{}); break;
+                case 16: assign(std::integral_constant<int, 16>{}); break;
+                case 32: assign(std::integral_constant<int, 32>{}); break;
+                default: assign(std::integral_constant<int, 64>{}); break;
+            }
             hipLaunchKernelGGL(k_sb_relabel, dim3(std::max<int64_t>(1, ceil_div(nf * f, kSbBlock))),
                                dim3(kSbBlock), 0, st, hs, node_map, w.esrc);
         }
@@ -465,12 +554,13 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
     const int64_t work = std::max<int64_t>(std::max<int64_t>(n_nodes, n_edges), 1);
     if (x && n_nodes > 0) {  // gather before the map reset (order irrelevant: reads nid only)
         const bool vec = F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&
-                         aligned(x, 16);
+                         aligned(x, 16) && n_nodes * (F / 4) < INT32_MAX;
         const int64_t items = vec ? n_nodes * (F / 4) : n_nodes * F;
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(items, kSbBlock), 8192));
         if (vec)
-            hipLaunchKernelGGL(k_gather_rows4, dim3(grid), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
-                               n_nodes, F / 4, x, ldo);
+            hipLaunchKernelGGL(k_gather_rows4, dim3(std::min(grid, 2048u)), dim3(kSbBlock), 0, st,
+                               x_all, ldx, w.nid, static_cast<int>(n_nodes),
+                               static_cast<int>(F / 4), x, ldo);
         else
             hipLaunchKernelGGL(k_gather_rows1, dim3(grid), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
                                n_nodes, F, x, ldo);

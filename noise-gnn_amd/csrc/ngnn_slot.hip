@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int64_t ld_ei, int64_t E, const int64_t *__restrict__ y, int64_t B, float *__restrict__ sx,
     int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
-    uint64_t *__restrict__ seed_state, const float **x_dev, int32_t *__restrict__ r_next, int vec) {
+    uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
+    uint32_t gen, int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
@@ -87,21 +88,19 @@ __global__ __launch_bounds__(256) void k_slot_load(
         for (int64_t e = tid; e < e_cap; e += nthr)
             col[e] = static_cast<int32_t>(e < E ? ei[e] : N + ((e - E) * span) / n_pad);
     }
-    if (r_next && blockIdx.x == 0) {
-        // max source over the edges into rows < B: a prefix of the sorted edges
-        int64_t m = -1;
-        for (int64_t e = threadIdx.x; e < E; e += blockDim.x) {
-            if (ei[ld_ei + e] >= B) break;
-            m = max(m, ei[e]);
+    if (r_next) {
+        // max(B, 1 + max source over the edges into rows < B), as a 64-bit
+        // atomicMax of (gen << 32 | value): this load's generation outranks
+        // every stale value, so the word needs no reset launch; consumers
+        // read its low 32 bits
+        const uint64_t g = static_cast<uint64_t>(gen) << 32;
+        uint64_t m = tid == 0 ? (g | static_cast<uint64_t>(B)) : 0;
+        for (int64_t e = tid; e < E; e += nthr) {
+            if (ei[ld_ei + e] >= B) break;  // targets sorted: the rest are >= B too
+            m = max(m, g | static_cast<uint64_t>(ei[e] + 1));
         }
-        __shared__ int64_t red[256];
-        red[threadIdx.x] = m;
-        __syncthreads();
-        for (int h = 128; h > 0; h >>= 1) {
-            if (static_cast<int>(threadIdx.x) < h) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + h]);
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) *r_next = static_cast<int32_t>(max<int64_t>(B, red[0] + 1));
+        if (m) atomicMax(reinterpret_cast<unsigned long long *>(r_next),
+                         static_cast<unsigned long long>(m));
     }
     if (tid == 0) {
         *n_valid = static_cast<int32_t>(N);
@@ -124,7 +123,8 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int64_t B, float *slot_x, int64_t ld_slot, int64_t n_cap,
                               int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
-                              const float **x_dev, int32_t *r_next, void *stream) {
+                              const float **x_dev, int64_t *r_next, uint32_t gen,
+                              void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !slot_ei || !n_valid,
                    NGNN_E_ARG);
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
@@ -141,6 +141,6 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
-                       n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, vec);
+                       n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, vec);
     return launch_status();
 }

@@ -62,7 +62,9 @@ class GraphedTrainStep:
         self.x_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         # input-gradient row bound of the top layer (prefix stats for R = B),
         # written by the slot load so the captured backward needs no bound launch
-        self.r_next = torch.zeros(1, dtype=torch.int32, device=dev)
+        # (int64 word: generation << 32 | bound; consumers read the low half)
+        self.r_next = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._gen = 0
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
         self.loss = None
@@ -87,10 +89,17 @@ class GraphedTrainStep:
             _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
             _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
-            _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next),
+            _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
             _lib.stream_handle(self.x.device)),
             "ngnn_slot_load")
         self._x_live = x if zero_copy else None
+
+    def _next_gen(self) -> int:
+        self._gen += 1
+        if self._gen >= 2**32:  # wrapped: restart the generations from a zeroed word
+            self.r_next.zero_()
+            self._gen = 1
+        return self._gen
 
     def _fwd_bwd(self):
         out = self.model(self.x, self.ei)
