@@ -349,28 +349,16 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_finish(
 }
 
 // x[i] = x_all[n_id[i]], 16-B vectors (F % 4 == 0, aligned rows); 32-bit
-// item indices (n * F/4 < 2^31 checked by the caller), 4 vectors in flight
+// item indices (n * F/4 < 2^31 checked by the caller), one vector per thread
 __global__ __launch_bounds__(kSbBlock) void k_gather_rows4(const float *__restrict__ x_all,
                                                            int64_t ldx, const int32_t *__restrict__ nid,
                                                            int n, int f4, float *__restrict__ x,
                                                            int64_t ldo) {
     const int total = n * f4;
-    const int stride = gridDim.x * kSbBlock;
-    for (int t0 = blockIdx.x * kSbBlock + threadIdx.x; t0 < total; t0 += 4 * stride) {
-        float4 v[4];
-        int r[4], c[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = t0 + u * stride;
-            r[u] = t / f4;
-            c[u] = (t - r[u] * f4) * 4;
-            if (t < total)
-                v[u] = *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(nid[r[u]]) * ldx + c[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (t0 + u * stride < total)
-                *reinterpret_cast<float4 *>(x + static_cast<int64_t>(r[u]) * ldo + c[u]) = v[u];
+    for (int t = blockIdx.x * kSbBlock + threadIdx.x; t < total; t += gridDim.x * kSbBlock) {
+        const int r = t / f4, c = (t - r * f4) * 4;
+        *reinterpret_cast<float4 *>(x + static_cast<int64_t>(r) * ldo + c) =
+            *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(nid[r]) * ldx + c);
     }
 }
 
@@ -556,9 +544,9 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
         const bool vec = F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&
                          aligned(x, 16) && n_nodes * (F / 4) < INT32_MAX;
         const int64_t items = vec ? n_nodes * (F / 4) : n_nodes * F;
-        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(items, kSbBlock), 8192));
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(items, kSbBlock), 65536));
         if (vec)
-            hipLaunchKernelGGL(k_gather_rows4, dim3(std::min(grid, 2048u)), dim3(kSbBlock), 0, st,
+            hipLaunchKernelGGL(k_gather_rows4, dim3(grid), dim3(kSbBlock), 0, st,
                                x_all, ldx, w.nid, static_cast<int>(n_nodes),
                                static_cast<int>(F / 4), x, ldo);
         else

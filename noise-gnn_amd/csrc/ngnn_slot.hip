@@ -99,8 +99,16 @@ __global__ __launch_bounds__(256) void k_slot_load(
             if (ei[ld_ei + e] >= B) break;  // targets sorted: the rest are >= B too
             m = max(m, g | static_cast<uint64_t>(ei[e] + 1));
         }
-        if (m) atomicMax(reinterpret_cast<unsigned long long *>(r_next),
-                         static_cast<unsigned long long>(m));
+        // one atomic per wave (same-address atomics serialise)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t other = (static_cast<uint64_t>(static_cast<uint32_t>(
+                                        __shfl_xor(static_cast<int>(m >> 32), o))) << 32) |
+                                   static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o));
+            m = max(m, other);
+        }
+        if (m && (threadIdx.x & 63) == 0)
+            atomicMax(reinterpret_cast<unsigned long long *>(r_next), static_cast<unsigned long long>(m));
     }
     if (tid == 0) {
         *n_valid = static_cast<int32_t>(N);
