@@ -238,7 +238,8 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * rows < *n_rows_dev). */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
-                      int64_t n_rows, const int32_t *n_rows_dev, const int32_t *rowptr,
+                      int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
+                      const int32_t *n_edge_rows_dev, const int32_t *rowptr,
                       const int32_t *col,
                       int reduce, const float *wl, const float *wr, int64_t ldw, const float *bias,
                       int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
@@ -387,14 +388,16 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * source of the edges into rows < B) -- ngnn_block_prefix_stats for R = B,
  * the input-gradient row bound of the top layer's backward (computed here
  * so the captured step has no bound launch).  Kept by a 64-bit atomicMax of
- * (gen << 32 | value): gen must grow with every load (no reset launch).  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
+ * (gen << 32 | value): gen must grow with every load (no reset launch).
+ * n_edge_rows (nullable): 1 + the last target (0 without edges) = the split
+ * of ngnn_sage_fwd_raw's n_edge_rows_dev.  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
-                   void *stream);
+                   int32_t *n_edge_rows, void *stream);
 
 #ifdef __cplusplus
 }

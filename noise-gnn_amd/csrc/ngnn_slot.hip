@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
-    uint32_t gen, int vec) {
+    uint32_t gen, int32_t *__restrict__ n_edge_rows, int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
@@ -112,6 +112,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
     }
     if (tid == 0) {
         *n_valid = static_cast<int32_t>(N);
+        if (n_edge_rows)  // rows past the last target have no in-edges
+            *n_edge_rows = E > 0 ? static_cast<int32_t>(ei[ld_ei + E - 1] + 1) : 0;
         if (seed_state) {  // splitmix64 step: state <- mix(state + golden gamma)
             uint64_t z = *seed_state + 0x9e3779b97f4a7c15ULL;
             z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -132,7 +134,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
-                              void *stream) {
+                              int32_t *n_edge_rows, void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !slot_ei || !n_valid,
                    NGNN_E_ARG);
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
@@ -149,6 +151,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
-                       n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, vec);
+                       n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
+                       vec);
     return launch_status();
 }

@@ -106,6 +106,8 @@ class Block:
         # (device int32, R): the input-gradient row bound for output rows < R,
         # kept by a producer (graph slot), or None
         self.r_next = None
+        # device int32: rows at or past it have no in-edges (graph slot), or None
+        self.n_edge_rows_dev = None
 
     @property
     def rowptr(self):
@@ -150,6 +152,7 @@ class _BlockCache:
             blk.seed_dev = hint[5]
             blk.x_dev = hint[6]
             blk.r_next = hint[7]
+            blk.n_edge_rows_dev = hint[8]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -175,7 +178,8 @@ _hints_lock = threading.Lock()
 def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: bool,
                     n_active: int | None = None, n_rows_dev: torch.Tensor | None = None,
                     csr: CSR | None = None, seed_dev: torch.Tensor | None = None,
-                    x_dev: torch.Tensor | None = None, r_next=None) -> None:
+                    x_dev: torch.Tensor | None = None, r_next=None,
+                    n_edge_rows_dev: torch.Tensor | None = None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
     later rows have none) -- only used for roofline accounting.  n_rows_dev:
     device int32 scalar bounding the real rows of a padded slot.  csr: a
@@ -183,11 +187,12 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     seed_dev: device uint64 dropout seed the producer advances per batch.
     x_dev: device word the producer fills with the address of the feature
     rows the layer-0 kernels must read (zero-copy slot).  r_next: (device int32,
-    R): the producer keeps ngnn_block_prefix_stats' bound for R there."""
+    R): the producer keeps ngnn_block_prefix_stats' bound for R there.
+    n_edge_rows_dev: device int32 holding n_active for a changing batch."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
-                                  n_rows_dev, csr, seed_dev, x_dev, r_next)
+                                  n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev)
 
 
 def _drop_hint(key):
@@ -200,7 +205,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]
+    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

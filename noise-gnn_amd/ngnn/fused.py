@@ -114,8 +114,11 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo), zero=True)
     with _timing.span(span, nbytes, flops):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
+        # rows >= n_active have no in-edges (a sampler-built block): dense kernel
+        n_edge = N if block.n_active is None else min(int(block.n_active), N)
         rc = lib.ngnn_sage_fwd_raw(
-            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, n_edge,
+            _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
             _lib.REDUCE[reduce], _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,

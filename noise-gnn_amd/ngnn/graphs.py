@@ -64,6 +64,8 @@ class GraphedTrainStep:
         # written by the slot load so the captured backward needs no bound launch
         # (int64 word: generation << 32 | bound; consumers read the low half)
         self.r_next = torch.zeros(1, dtype=torch.int64, device=dev)
+        # rows past the batch's last target have no in-edges (dense forward kernel)
+        self.n_edge_rows = torch.zeros(1, dtype=torch.int32, device=dev)
         self._gen = 0
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
@@ -90,7 +92,7 @@ class GraphedTrainStep:
             _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
             _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
-            _lib.stream_handle(self.x.device)),
+            _lib.ptr(self.n_edge_rows), _lib.stream_handle(self.x.device)),
             "ngnn_slot_load")
         self._x_live = x if zero_copy else None
 
@@ -134,7 +136,8 @@ class GraphedTrainStep:
         block_cache.clear()
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
-                        x_dev=self.x_dev, r_next=(self.r_next, self.B))
+                        x_dev=self.x_dev, r_next=(self.r_next, self.B),
+                        n_edge_rows_dev=self.n_edge_rows)
         self.opt.zero_grad(set_to_none=True)
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):

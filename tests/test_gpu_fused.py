@@ -99,6 +99,33 @@ def test_fused_layer_dropout_mask_and_scale():
     assert torch.equal(got, again)
 
 
+@pytest.mark.parametrize("K,Fo", [(100, 256), (256, 47), (128, 40), (52, 100), (200, 129),
+                                  (64, 16), (240, 250)])
+@pytest.mark.parametrize("split", [0, 1, 333, 700])
+def test_dense_split_matches_oracle(K, Fo, split):
+    """Rows at or past the block's n_active (no in-edges) run through the dense
+    kernel, the rows below through the fused gather kernel: the union equals
+    the oracle layer, with ReLU and the host-replicated dropout mask."""
+    N, p, seed = 700, 0.5, 777
+    g = torch.Generator().manual_seed(K * 7 + Fo + split)
+    ei = rand_block(K + Fo + split, N, 4000)
+    ei = ei[:, ei[1] < split]  # only rows < split receive edges
+    x = torch.randn(N, K, generator=g)
+    conv = pyg_ref.SAGEConv(K, Fo)
+    with torch.no_grad():
+        pre = conv(x, ei).relu()
+    blk = Block(ei.to(DEV), N)
+    blk.n_active = split
+    args = (x.to(DEV), blk, "mean", conv.lin_l.weight.to(DEV), conv.lin_l.bias.to(DEV),
+            conv.lin_r.weight.to(DEV))
+    got = sage_layer_fwd(*args, relu=True, p_drop=p, seed=seed).cpu()
+    keep = dropout_keep(seed, N, Fo, p)
+    torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)
+    got = sage_layer_fwd(*args, relu=False, p_drop=0.0, seed=seed).cpu()
+    with torch.no_grad():
+        torch.testing.assert_close(got, conv(x, ei), **OUT)
+
+
 class _MaskedSAGE(pyg_ref.SAGE):
     """Oracle SAGE whose dropout uses given keep masks (one per hidden layer)."""
 

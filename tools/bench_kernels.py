@@ -72,6 +72,7 @@ def main():
         res[tag + "_full"] = timeit(layer(blk, True, 0.0, agg), a.reps)
         res[tag + "_noagg_out"] = timeit(layer(blk, True, 0.0, None), a.reps)
         res[tag + "_root_only"] = timeit(layer(empty, False, 0.0, None), a.reps)
+        res[tag + "_root_only_drop"] = timeit(layer(empty, True, 0.5, None), a.reps)
         res[tag + "_pack2"] = timeit(lambda: (pack_weight(wl), pack_weight(wr)), a.reps)
         # pure-copy roofline reference: read x + write out
         res[tag + "_torch_copy_x"] = timeit(lambda: x.clone(), a.reps)
