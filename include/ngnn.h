@@ -236,7 +236,7 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * word holding x's address, read at run time instead of x (a HIP-graph slot
  * whose batch stays where the loader put it; 16-B aligned, row stride ldx,
  * rows < *n_rows_dev). */
-size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo);
+size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                       const int32_t *n_edge_rows_dev, const int32_t *rowptr,

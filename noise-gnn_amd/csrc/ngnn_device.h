@@ -27,6 +27,19 @@ __device__ __forceinline__ i32x4 make_rsrc(const void *p, uint32_t bytes) {
     r.w = 0x00020000;
     return r;
 }
+// The same for a resource the compiler cannot prove wave-uniform (derived
+// from a loaded value: a graph slot's x address, a device row count) but that
+// is: readfirstlane puts it in SGPRs, else every buffer access is wrapped in a
+// waterfall loop behind an s_waitcnt vmcnt(0) that drains the prefetches.
+__device__ __forceinline__ i32x4 make_rsrc_u(const void *p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(a)));
+    r.y = __builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(a >> 32)));
+    r.z = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+    r.w = 0x00020000;
+    return r;
+}
 // byte offset that is always outside a resource of < 2 GiB
 constexpr int kBufOOB = 0x7fffffff;
 
@@ -120,12 +133,14 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const float *const *x_dev = nullptr);
 
 // Dense (edge-free rows) forward, ngnn_sage_dense.hip: rows [row_begin (or
-// *row_begin_dev), min(n_rows, *n_rows_dev)).  Returns 1 (status in *rc) when
+// *row_begin_dev), min(n_rows, *n_rows_dev)); optional addend z (rows <
+// min(z_rows, *z_rows_dev) add z[r] before the epilogue).  Returns 1 (status in *rc) when
 // it takes the call, 0 (nothing launched) outside its envelope.
 int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
                    int64_t row_begin, const int32_t *row_begin_dev, int64_t n_rows,
                    const int32_t *n_rows_dev, const float *wr, int64_t ldw, const float *bias,
                    int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
-                   const uint64_t *seed_dev, hipStream_t st, int *rc);
+                   const uint64_t *seed_dev, hipStream_t st, int *rc, const float *z = nullptr,
+                   int64_t ldz = 0, int64_t z_rows = 0, const int32_t *z_rows_dev = nullptr);
 
 }  // namespace ngnn

@@ -13,13 +13,14 @@
 //   * one 256-thread workgroup per CU -- ONE wave per SIMD -- persistent;
 //     W_r (raw PyG [F_out, K] rows) DMA'd once into LDS in MFMA fragment order
 //     [k-group][n-tile][lane] (1 KiB per fragment), bias too;
-//   * a wave owns 16-row tiles; B = x (16 rows straight from HBM into
-//     registers, the next tile's loads issued before this tile's MFMAs),
+//   * a wave owns 32-row tiles (two 16-row MFMA sub-tiles sharing every W
+//     fragment read); B = x (straight from HBM into registers, the next
+//     tile's loads issued before this tile's MFMAs),
 //     A = W from LDS, v_mfma_f32_16x16x4_f32, so each lane ends with 4
 //     consecutive output features of one row -> 16-B stores;
 //   * software pipeline: the epilogue of tile t-1 (bias, ReLU, hash
-//     dropout, stores) is spread over the MFMAs of the first k-groups of
-//     tile t in one basic block, so its VALU work and stores issue in the
+//     dropout, stores) is spread over the MFMA steps of tile t in one basic
+//     block (K is a template constant: no branches in the tile body), so its VALU work and stores issue in the
 //     matrix pipe's shadow instead of after it (the fused kernel runs two
 //     waves per SIMD whose epilogues do not overlap their partner's MFMAs:
 //     tools/ablate.sh measured +26 % over its MFMA-only time on L0).
@@ -34,7 +35,10 @@ namespace ngnn {
 namespace {
 
 constexpr int DN_WAVES = 4;  // one wave per SIMD
-constexpr int DN_ROWS = 16;  // rows per tile (the MFMA n dimension)
+// 16-row MFMA sub-tiles per tile (each W fragment feeds 4 RS MFMAs): two for
+// the wide (MFMA-bound) outputs, one for narrow outputs, where the x stream
+// dominates and lower register use buys more waves per SIMD
+constexpr int dn_rs(int ntw) { return ntw >= 32 ? 2 : 1; }
 
 struct DenseArgs {
     const float *x;
@@ -55,6 +59,12 @@ struct DenseArgs {
     int64_t ldo;
     int vec_out;
     uint32_t x_bytes, out_bytes;
+    // optional addend (pre-activation partial sums, e.g. agg . W_l^T of the
+    // rows that have in-edges): rows < its range add z[r]; rows past it read 0
+    const float *z;
+    int64_t ldz;  // multiple of 4, >= NTW * 16 (padded n-tiles read it)
+    int z_rows;
+    const int32_t *z_rows_dev;
 };
 
 __device__ __forceinline__ int dn_lt_mask(int a, int b) { return (a - b) >> 31; }
@@ -96,21 +106,29 @@ __device__ __forceinline__ void dn_epi_tile(const v4f &acc, const DenseArgs &a, 
 }
 
 // NTW: n-tiles (16 output columns each, >= NT, padded tiles hold zero W);
-// KGM: k-groups (16 columns of K each) unrolled, with KGM/2 < KG <= KGM so
-// the first KGM/2 groups run unconditionally (one basic block with the
-// pending epilogue).
-template <int NTW, int KGM, bool DROP>
+// KG: k-groups of 16 columns of K, exact, so the whole tile body is one basic
+// block: the MFMAs run in steps of MB n-tiles (W fragments of the next step
+// read from LDS while the current step's 4*RS*MB MFMAs issue; RS*MB
+// independent accumulators between dependent MFMAs) and the pending tile's
+// epilogue is spread over the first steps, interleaved MFMA by MFMA
+// (sched_group_barrier).
+template <int NTW, int KG, bool DROP, bool ADD>
 __global__ __launch_bounds__(DN_WAVES * 64) void k_dense(DenseArgs a) {
+    constexpr int RS = dn_rs(NTW);
+    constexpr int DN_TROWS = 16 * RS;
+    constexpr int MB = NTW >= 4 ? 4 : NTW;  // n-tiles per MFMA step
+    constexpr int NB = NTW / MB;            // steps per k-group
+    constexpr int NS = KG * NB;             // steps per tile
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
     v4f *sw = lds;
-    float *sbias = reinterpret_cast<float *>(lds + a.KG * NTW * 64);
+    float *sbias = reinterpret_cast<float *>(lds + KG * NTW * 64);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     {
         // W -> LDS by LDS-DMA, one 1-KiB fragment (n-tile m, k-group kg) per
         // wave-instruction: lane l brings W[m*16 + (l & 15)][kg*16 + 4 (l >> 4) .. +3]
-        const int nch = a.NT * a.KG;
+        const int nch = a.NT * KG;
         for (int c = wv; c < nch; c += DN_WAVES) {
-            const int m = c / a.KG, kg = c - m * a.KG;
+            const int m = c / KG, kg = c - m * KG;
             const int n = m * 16 + (ln & 15), k = kg * 16 + 4 * (ln >> 4);
             const int64_t so = (n < a.Fo && k < a.K) ? static_cast<int64_t>(n) * a.ldw + k : 0;
             __builtin_amdgcn_global_load_lds(
@@ -120,12 +138,12 @@ __global__ __launch_bounds__(DN_WAVES * 64) void k_dense(DenseArgs a) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's LDS-DMAs have landed
         const v4f z{0.f, 0.f, 0.f, 0.f};
         for (int c = wv; c < nch; c += DN_WAVES) {  // lanes outside F_out x K -> 0
-            const int m = c / a.KG, kg = c - m * a.KG;
+            const int m = c / KG, kg = c - m * KG;
             const int n = m * 16 + (ln & 15), k = kg * 16 + 4 * (ln >> 4);
             if (!(n < a.Fo && k < a.K)) sw[(kg * NTW + m) * 64 + ln] = z;
         }
         const int npad = (NTW - a.NT) * 64;  // padded n-tiles of every k-group
-        for (int i = threadIdx.x; i < a.KG * npad; i += DN_WAVES * 64) {
+        for (int i = threadIdx.x; i < KG * npad; i += DN_WAVES * 64) {
             const int kg = i / npad, j = i - kg * npad;
             sw[kg * NTW * 64 + a.NT * 64 + j] = z;
         }
@@ -139,94 +157,137 @@ __global__ __launch_bounds__(DN_WAVES * 64) void k_dense(DenseArgs a) {
     if (a.row_begin_dev) rb = *a.row_begin_dev;
     int nr = a.n_rows;
     if (a.n_rows_dev) nr = min(nr, *a.n_rows_dev);
-    const int n_tiles = nr > rb ? (nr - rb + DN_ROWS - 1) / DN_ROWS : 0;
+    rb = __builtin_amdgcn_readfirstlane(rb);
+    nr = __builtin_amdgcn_readfirstlane(nr);
+    const int n_tiles = nr > rb ? (nr - rb + DN_TROWS - 1) / DN_TROWS : 0;
     const int tstride = gridDim.x * DN_WAVES;
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
-    const i32x4 xr = a.x_dev ? make_rsrc(*a.x_dev, static_cast<uint32_t>(
-                                             ((nr - 1) * a.ldx + a.K) * 4 * (nr > 0)))
-                             : make_rsrc(a.x, a.x_bytes);
-    const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
+    const i32x4 xr = a.x_dev ? make_rsrc_u(*a.x_dev, static_cast<uint32_t>(
+                                               ((nr - 1) * a.ldx + a.K) * 4 * (nr > 0)))
+                             : make_rsrc_u(a.x, a.x_bytes);
+    const i32x4 orsrc = make_rsrc_u(a.out, a.out_bytes);
+    i32x4 zr{0, 0, 0, 0};
+    if constexpr (ADD) {  // z rows < the addend's row count (device or host), the rest read 0
+        int zrows = a.z_rows;
+        if (a.z_rows_dev) zrows = min(zrows, *a.z_rows_dev);
+        zrows = __builtin_amdgcn_readfirstlane(zrows);
+        zr = make_rsrc_u(a.z, static_cast<uint32_t>(zrows > 0 ? zrows * a.ldz * 4 : 0));
+    }
     const bool vec = a.vec_out && (a.Fo == a.NT * 16);
     const int kq = a.K - 4 * q;  // group g's 4 columns of this lane are valid iff 16 g < kq
 
     // x fragments of a tile: lane (rl, q) holds x[r][16 g + 4 q .. +3];
     // rows past nr read 0 (buffer range); a tile past the end re-reads the
     // first tile (valid addresses, never used)
-    auto load_x = [&](v4f (&xf)[KGM], int tt) {
-        const int r = rb + (tt < n_tiles ? tt : 0) * DN_ROWS + rl;
+    auto load_x = [&](v4f (&xf)[KG], int tt, int u) {
+        const int r = rb + (tt < n_tiles ? tt : 0) * DN_TROWS + 16 * u + rl;
         const int voff = (r * static_cast<int>(a.ldx) + 4 * q) * 4;
 #pragma unroll
-        for (int g = 0; g < KGM; ++g)
-            if (g < KGM / 2 || g < a.KG) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+        for (int g = 0; g < KG; ++g) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+    };
+    // addend fragments of a tile in the accumulator layout: lane (rl, q)
+    // holds z[r][16 m + 4 q .. +3]
+    auto load_z = [&](v4f (&zf)[NTW], int tt, int u) {
+        const int r = rb + (tt < n_tiles ? tt : 0) * DN_TROWS + 16 * u + rl;
+        const int voff = (r * static_cast<int>(a.ldz) + 4 * q) * 4;
+#pragma unroll
+        for (int m = 0; m < NTW; ++m) zf[m] = buf_load4(zr, voff + 64 * m, 0, 0);
+    };
+    auto load_w = [&](v4f (&w)[MB], int s) {
+        const int g = s / NB, b = s % NB;
+#pragma unroll
+        for (int h = 0; h < MB; ++h) w[h] = sw[(g * NTW + b * MB + h) * 64 + lane];
     };
 
     int t = blockIdx.x + gridDim.x * wv;  // consecutive tiles spread over the CUs
-    v4f xn[KGM];
+    v4f xn[RS][KG];
+    v4f zn[RS][ADD ? NTW : 1];
 #pragma unroll
-    for (int g = 0; g < KGM; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
-    load_x(xn, t);
+    for (int u = 0; u < RS; ++u) {
+        load_x(xn[u], t, u);
+        if constexpr (ADD) load_z(zn[u], t, u);
+    }
 
-    // the pending (previous) tile: accumulators + its row; the first
+    // the pending (previous) tile: accumulators + its rows; the first
     // iteration's "pending" tile is a dummy whose stores fall past the range
-    v4f pend[NTW];
+    v4f pend[RS][NTW];
 #pragma unroll
-    for (int m = 0; m < NTW; ++m) pend[m] = v4f{0.f, 0.f, 0.f, 0.f};
-    int prow = nr;
-    constexpr int G0 = KGM / 2 > 0 ? KGM / 2 : 1;             // unconditional k-groups
-    constexpr int EPG = (NTW + G0 - 1) / G0;                  // pending n-tiles per group
+    for (int u = 0; u < RS; ++u)
+#pragma unroll
+        for (int m = 0; m < NTW; ++m) pend[u][m] = v4f{0.f, 0.f, 0.f, 0.f};
+    int prow = nr;  // first row of the pending tile (lane's rows: prow + 16 u + rl)
+    // pending epilogue: EPS (sub-tile, n-tile) pieces after each of the first steps
+    constexpr int NPIECE = RS * NTW;
+    constexpr int EPS = (NPIECE + NS - 1) / NS;
 
     for (; t < n_tiles; t += tstride) {
-        const int r = rb + t * DN_ROWS + rl;
-        v4f xc[KGM];
+        const int r0 = rb + t * DN_TROWS;
+        v4f xc[RS][KG];
 #pragma unroll
-        for (int g = 0; g < KGM; ++g) xc[g] = dn_and_mask(xn[g], dn_lt_mask(16 * g, kq));
-        load_x(xn, t + tstride);
-
-        const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(prow)) : 0u;
-        const int obase = prow * static_cast<int>(a.ldo) * 4;
-        v4f acc[NTW];
+        for (int u = 0; u < RS; ++u)
 #pragma unroll
-        for (int m = 0; m < NTW; ++m) acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
-        // k-groups [0, G0): MFMAs + the pending tile's epilogue, one block
+            for (int g = 0; g < KG; ++g) xc[u][g] = dn_and_mask(xn[u][g], dn_lt_mask(16 * g, kq));
+        v4f acc[RS][NTW];
 #pragma unroll
-        for (int g = 0; g < G0; ++g) {
+        for (int u = 0; u < RS; ++u)
 #pragma unroll
             for (int m = 0; m < NTW; ++m) {
-                const v4f wf = sw[(g * NTW + m) * 64 + lane];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[i], xc[g][i], acc[m], 0, 0, 0);
+                if constexpr (ADD) acc[u][m] = zn[u][m];
+                else acc[u][m] = v4f{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
-            for (int e = 0; e < EPG; ++e) {
-                const int m = g * EPG + e;  // (padded n-tiles: every store dropped)
-                if (m < NTW) dn_epi_tile<DROP>(pend[m], a, orsrc, sbias, m, q, obase, rk, vec);
-            }
+        for (int u = 0; u < RS; ++u) {
+            load_x(xn[u], t + tstride, u);
+            if constexpr (ADD) load_z(zn[u], t + tstride, u);
         }
-        // remaining k-groups (present only when K needs them)
+
+        uint32_t rk[RS];
+        int obase[RS];
 #pragma unroll
-        for (int g = G0; g < KGM; ++g) {
-            if (g < a.KG) {
+        for (int u = 0; u < RS; ++u) {
+            const int pr = prow + 16 * u + rl;
+            rk[u] = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(pr)) : 0u;
+            obase[u] = pr < nr ? pr * static_cast<int>(a.ldo) * 4 : kBufOOB;
+        }
+        v4f wb[2][MB];
+        load_w(wb[0], 0);
 #pragma unroll
-                for (int m = 0; m < NTW; ++m) {
-                    const v4f wf = sw[(g * NTW + m) * 64 + lane];
+        for (int s = 0; s < NS; ++s) {
+            if (s + 1 < NS) load_w(wb[(s + 1) & 1], s + 1);
+            const int g = s / NB, b = s % NB;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[i], xc[g][i], acc[m], 0, 0,
-                                                                      0);
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int u = 0; u < RS; ++u)
+#pragma unroll
+                    for (int h = 0; h < MB; ++h)
+                        acc[u][b * MB + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            wb[s & 1][h][i], xc[u][g][i], acc[u][b * MB + h], 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < EPS; ++e) {
+                const int piece = s * EPS + e;  // (padded n-tiles: every store dropped)
+                if (piece < NPIECE) {
+                    const int u = piece / NTW, m = piece % NTW;
+                    dn_epi_tile<DROP>(pend[u][m], a, orsrc, sbias, m, q, obase[u], rk[u], vec);
                 }
             }
         }
 #pragma unroll
-        for (int m = 0; m < NTW; ++m) pend[m] = acc[m];
-        prow = r;
+        for (int u = 0; u < RS; ++u)
+#pragma unroll
+            for (int m = 0; m < NTW; ++m) pend[u][m] = acc[u][m];
+        prow = r0;
     }
     {  // drain: the last tile's epilogue
-        const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(prow)) : 0u;
-        const int obase = prow * static_cast<int>(a.ldo) * 4;
 #pragma unroll
-        for (int m = 0; m < NTW; ++m)
-            if (m < a.NT) dn_epi_tile<DROP>(pend[m], a, orsrc, sbias, m, q, obase, rk, vec);
+        for (int u = 0; u < RS; ++u) {
+            const int pr = prow + 16 * u + rl;
+            const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(pr)) : 0u;
+            const int obase = pr < nr ? pr * static_cast<int>(a.ldo) * 4 : kBufOOB;
+#pragma unroll
+            for (int m = 0; m < NTW; ++m)
+                if (m < a.NT) dn_epi_tile<DROP>(pend[u][m], a, orsrc, sbias, m, q, obase, rk, vec);
+        }
     }
 }
 
@@ -245,9 +306,9 @@ int dn_num_cus() {
     return g_dn_cus[dev];
 }
 
-template <int NTW, int KGM, bool DROP>
+template <int NTW, int KG, bool DROP, bool ADD>
 int dn_launch(const DenseArgs &a, int max_tiles, size_t lds, hipStream_t st) {
-    auto fn = k_dense<NTW, KGM, DROP>;
+    auto fn = k_dense<NTW, KG, DROP, ADD>;
     static int per_cu = 0;  // benign race: idempotent
     if (!per_cu) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
@@ -266,17 +327,24 @@ int dn_launch(const DenseArgs &a, int max_tiles, size_t lds, hipStream_t st) {
     return launch_status();
 }
 
-template <int NTW, int KGM>
+template <int NTW, int KG>
 int dn_drop(const DenseArgs &a, int max_tiles, size_t lds, hipStream_t st) {
-    return a.epi.drop.thresh ? dn_launch<NTW, KGM, true>(a, max_tiles, lds, st)
-                             : dn_launch<NTW, KGM, false>(a, max_tiles, lds, st);
+    return a.epi.drop.thresh ? dn_launch<NTW, KG, true, false>(a, max_tiles, lds, st)
+                             : dn_launch<NTW, KG, false, false>(a, max_tiles, lds, st);
 }
 
-template <int NTW>
-int dn_kgm(const DenseArgs &a, int max_tiles, size_t lds, hipStream_t st) {
-    if (a.KG <= 4) return dn_drop<NTW, 4>(a, max_tiles, lds, st);
-    if (a.KG <= 8) return dn_drop<NTW, 8>(a, max_tiles, lds, st);
-    return dn_drop<NTW, 16>(a, max_tiles, lds, st);
+template <int NTW, int KG>
+int dn_drop_add(const DenseArgs &a, int max_tiles, size_t lds, hipStream_t st) {
+    if (!a.z) return dn_drop<NTW, KG>(a, max_tiles, lds, st);
+    return a.epi.drop.thresh ? dn_launch<NTW, KG, true, true>(a, max_tiles, lds, st)
+                             : dn_launch<NTW, KG, false, true>(a, max_tiles, lds, st);
+}
+
+// instantiated (n-tiles, k-groups): the products / arxiv layer shapes --
+// K in (96, 128] -> F_out in (240, 256], and K in (240, 256] -> F_out <= 64 or
+// in (112, 128]; other shapes take the fused kernel
+constexpr bool dn_shape_ok(int ntw, int kg) {
+    return (ntw == 16 && (kg == 7 || kg == 8)) || (kg == 16 && (ntw == 3 || ntw == 4 || ntw == 8));
 }
 
 }  // namespace
@@ -289,7 +357,8 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
                    int64_t row_begin, const int32_t *row_begin_dev, int64_t n_rows,
                    const int32_t *n_rows_dev, const float *wr, int64_t ldw, const float *bias,
                    int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
-                   const uint64_t *seed_dev, hipStream_t st, int *rc) {
+                   const uint64_t *seed_dev, hipStream_t st, int *rc, const float *z,
+                   int64_t ldz, int64_t z_rows, const int32_t *z_rows_dev) {
     if (getenv("NGNN_NO_DENSE")) return 0;
     if (K % 4 != 0 || ldx % 4 != 0 || ldw % 4 != 0 || K <= 48 || K > 256 || Fo > 256) return 0;
     if ((!x_dev && !aligned(x, 16)) || !aligned(wr, 16)) return 0;
@@ -297,7 +366,11 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
     if (n_rows * ldx * 4 > lim || (n_rows + 1) * ldo * 4 > lim) return 0;
     const int KG = static_cast<int>(ceil_div(K, 16));
     const int NT = static_cast<int>(ceil_div(Fo, 16));
-    const int NTW = NT <= 2 ? 2 : NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 8 ? 8 : 16;
+    const int NTW = NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 8 ? 8 : 16;
+    if (!dn_shape_ok(NTW, KG)) return 0;
+    if (z && (NTW != 16 || ldz % 4 != 0 || ldz < NTW * 16 || !aligned(z, 16) ||
+              (z_rows + 1) * ldz * 4 > lim))
+        return 0;  // (the addend is only instantiated for the wide layers)
     const size_t lds = static_cast<size_t>(KG) * NTW * 64 * sizeof(v4f) + NTW * 16 * sizeof(float);
     if (lds > 160 * 1024) return 0;
     DenseArgs a;
@@ -322,15 +395,21 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
     a.vec_out = (Fo % 4 == 0) && (ldo % 4 == 0) && aligned(out, 16);
     a.x_bytes = static_cast<uint32_t>(n_rows > 0 ? ((n_rows - 1) * ldx + K) * 4 : 0);
     a.out_bytes = static_cast<uint32_t>(n_rows > 0 ? ((n_rows - 1) * ldo + Fo) * 4 : 0);
+    a.z = z;
+    a.ldz = ldz;
+    a.z_rows = static_cast<int>(z_rows);
+    a.z_rows_dev = z_rows_dev;
     const int max_tiles = static_cast<int>(ceil_div(std::max<int64_t>(n_rows - (row_begin_dev ? 0 : row_begin), 0),
-                                                    DN_ROWS));
-    switch (NTW) {
-        case 2: *rc = dn_kgm<2>(a, max_tiles, lds, st); break;
-        case 3: *rc = dn_kgm<3>(a, max_tiles, lds, st); break;
-        case 4: *rc = dn_kgm<4>(a, max_tiles, lds, st); break;
-        case 8: *rc = dn_kgm<8>(a, max_tiles, lds, st); break;
-        default: *rc = dn_kgm<16>(a, max_tiles, lds, st); break;
-    }
+                                                    16 * dn_rs(NTW)));
+    if (NTW == 16)
+        *rc = KG == 7 ? dn_drop_add<16, 7>(a, max_tiles, lds, st)
+                      : dn_drop_add<16, 8>(a, max_tiles, lds, st);
+    else if (NTW == 3)
+        *rc = dn_drop<3, 16>(a, max_tiles, lds, st);
+    else if (NTW == 4)
+        *rc = dn_drop<4, 16>(a, max_tiles, lds, st);
+    else
+        *rc = dn_drop<8, 16>(a, max_tiles, lds, st);
     return 1;
 }
 

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x_arg,
                                                 const int32_t *__restrict__ col, int n_rows,
                                                 const int32_t *__restrict__ n_rows_dev,
                                                 float *__restrict__ agg, int64_t ld_agg,
-                                                const float *const *x_dev) {
+                                                const float *const *x_dev, int zero_empty) {
     const float *__restrict__ x = x_dev ? *x_dev : x_arg;
     constexpr int GPW = 256 / LPR;
     const int lane = threadIdx.x % LPR;
@@ -536,8 +536,16 @@ __global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x_arg,
         }
         for (int j = 0; j < LPR; ++j) {
         const int beg = __shfl(mb, j, LPR), end = __shfl(me, j, LPR);
-        if (beg == end) continue;
         const int row = r0 + j * ngroups;
+        if (beg == end) {
+            // edgeless row: left unwritten, or zeroed when the caller needs
+            // every row (the dense split's agg . W_l^T pass)
+            if (zero_empty && row < nr)
+                for (int f = 4 * lane; f < K; f += 4 * LPR)
+                    *reinterpret_cast<v4f *>(agg + static_cast<int64_t>(row) * ld_agg + f) =
+                        v4f{0.f, 0.f, 0.f, 0.f};
+            continue;
+        }
         for (int f0 = 0; f0 < K; f0 += 4 * LPR) {
             const int f = f0 + 4 * lane;
             const bool act = f < K;
@@ -627,6 +635,35 @@ int dispatch_pre(const RtArgs &a, int reduce, bool wl_lds, bool pre, int n_tiles
                : dispatch_red<NTW, false>(a, reduce, wl_lds, n_tiles, lds, st);
 }
 
+// aggregate of rows [0, min(n_rows, *n_rows_dev)) into agg (edgeless rows
+// zeroed), the fp32 sequence of ngnn_seg_agg_fwd
+int launch_rt_agg(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
+                  const int32_t *rowptr, const int32_t *col, int64_t n_rows,
+                  const int32_t *n_rows_dev, int reduce, float *agg, int64_t ld_agg,
+                  hipStream_t st) {
+    const int64_t k4 = ceil_div(K, 4);
+    const int lpr = k4 <= 8 ? 8 : k4 <= 16 ? 16 : k4 <= 32 ? 32 : 64;
+    const unsigned grid = static_cast<unsigned>(
+        std::max<int64_t>(1, std::min<int64_t>(8 * num_cus(), ceil_div(n_rows, 256 / lpr))));
+    auto go = [&](auto red_c, auto lpr_c) {
+        hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>), dim3(grid),
+                           dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
+                           static_cast<int>(n_rows), n_rows_dev, agg, ld_agg, x_dev, 1);
+    };
+    auto by_lpr = [&](auto red_c) {
+        switch (lpr) {
+            case 8: go(red_c, std::integral_constant<int, 8>{}); break;
+            case 16: go(red_c, std::integral_constant<int, 16>{}); break;
+            case 32: go(red_c, std::integral_constant<int, 32>{}); break;
+            default: go(red_c, std::integral_constant<int, 64>{}); break;
+        }
+    };
+    if (reduce == NGNN_REDUCE_MEAN) by_lpr(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
+    else if (reduce == NGNN_REDUCE_SUM) by_lpr(std::integral_constant<int, NGNN_REDUCE_SUM>{});
+    else by_lpr(std::integral_constant<int, NGNN_REDUCE_MAX>{});
+    return launch_status();
+}
+
 }  // namespace
 
 // Returns 1 and stores the launch status in *rc when the row-tile kernel
@@ -684,7 +721,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         auto go = [&](auto red_c, auto lpr_c) {
             hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>),
                                dim3(grid), dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr,
-                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg, x_dev);
+                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg, x_dev, 0);
         };
         auto by_lpr = [&](auto red_c) {
             switch (lpr) {
@@ -779,8 +816,15 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
 
 using namespace ngnn;
 
-extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo) {
-    return ngnn_pack_weight_bytes(Fo, K);  // a packed W_l, used only when it cannot sit in LDS
+// padded row stride of the split path's agg . W_l^T rows
+static int64_t split_ldz(int64_t Fo) { return ceil_div(Fo, 16) * 16; }
+
+extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows) {
+    // a packed W_l (fused path, when it cannot sit in LDS), or the split
+    // path's agg . W_l^T rows
+    const size_t pack = ngnn_pack_weight_bytes(Fo, K);
+    const size_t z = static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * split_ldz(Fo) * sizeof(float);
+    return std::max(pack, z);
 }
 
 extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx,
@@ -803,19 +847,48 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     NGNN_RETURN_IF((!x && !x_dev) || !out, NGNN_E_ARG);
     hipStream_t st = as_stream(stream);
     int rc = NGNN_OK;
-    // rows >= the edge-row bound have no in-edges: the dense kernel takes
-    // them (no neighbour term at all: every row) and the fused gather kernel
-    // only the rows below
-    int64_t split = wl ? std::max<int64_t>(0, std::min(n_edge_rows, n_rows)) : 0;
-    const int32_t *split_dev = wl ? n_edge_rows_dev : nullptr;
-    const bool want = !wl || split < n_rows || split_dev;
-    if (want && sage_fwd_dense(x, x_dev, ldx, K, split, split_dev, n_rows, n_rows_dev, wr, ldw, bias,
-                               Fo, out, ldo, relu, p_drop, seed, seed_dev, st, &rc)) {
-        if (rc || !wl || (!split_dev && split == 0)) return rc;
-    } else {
-        split = n_rows;
-        split_dev = nullptr;
+    // rows >= the edge-row bound have no in-edges.  No neighbour term: the
+    // dense kernel takes every row.  Wide outputs (MFMA-bound) with a known
+    // bound: three launches -- the aggregate of the edge rows (saved for the
+    // backward anyway), z = agg . W_l^T on those rows (dense kernel, no
+    // epilogue), then the dense kernel over every row with z added to the
+    // edge rows.  Otherwise the fused gather kernel takes the layer.
+    int64_t split = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
+    const int32_t *split_dev = n_edge_rows_dev;
+    // opt-in (NGNN_SPLIT=1): measured on products [15,10] L0 the three
+    // launches (agg 16 k rows + z + dense 153 k rows) tie the fused kernel
+    // (159 vs 155 us): the one-wave-per-SIMD dense kernel reaches ~60 % of the
+    // fp32 MFMA rate, not enough to pay for the separate aggregate pass
+    const bool no_split = getenv("NGNN_SPLIT") == nullptr;  // read per call (tests toggle it)
+    if (!wl) {
+        if (sage_fwd_dense(x, x_dev, ldx, K, 0, nullptr, n_rows, n_rows_dev, wr, ldw, bias, Fo, out,
+                           ldo, relu, p_drop, seed, seed_dev, st, &rc))
+            return rc;
+    } else if (!no_split && Fo > 128 && (split < n_rows || split_dev) && agg_out &&
+               ws_bytes >= ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) && aligned(ws, 16) &&
+               ld_agg % 4 == 0 && aligned(agg_out, 16)) {
+        const int64_t zrows = split_dev ? n_rows : split;  // host bound of the z rows
+        float *z = static_cast<float *>(ws);
+        const int64_t ldz = split_ldz(Fo);
+        const int32_t *zdev = split_dev;
+        // the dense kernel's envelope check launches nothing when it refuses,
+        // so probe the cheap pass shapes first: z pass and main pass share it
+        int rz = NGNN_OK;
+        if (zrows > 0 || split_dev) {
+            rc = launch_rt_agg(x, x_dev, ldx, K, rowptr, col, zrows, zdev, reduce, agg_out, ld_agg, st);
+            if (rc) return rc;
+            if (!sage_fwd_dense(agg_out, nullptr, ld_agg, K, 0, nullptr, zrows, zdev, wl, ldw,
+                                nullptr, Fo, z, ldz, 0, 0.0f, 0, nullptr, st, &rz))
+                goto fused;  // (the agg pass already ran: harmless, the fused kernel rewrites it)
+            if (rz) return rz;
+        }
+        if (sage_fwd_dense(x, x_dev, ldx, K, 0, nullptr, n_rows, n_rows_dev, wr, ldw, bias, Fo, out,
+                           ldo, relu, p_drop, seed, seed_dev, st, &rc, z, ldz, zrows, zdev))
+            return rc;
     }
+fused:
+    split = n_rows;
+    split_dev = nullptr;
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, split, split_dev, rowptr, col, reduce, wl, wr,
                           bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc,
                           ldw, ws, ws_bytes, x_dev))

@@ -111,7 +111,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         wl_, wr_ = wl_.contiguous(), wr_.contiguous()
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
-    ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo), zero=True)
+    ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
     with _timing.span(span, nbytes, flops):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel

@@ -100,7 +100,7 @@ def test_fused_layer_dropout_mask_and_scale():
 
 
 @pytest.mark.parametrize("K,Fo", [(100, 256), (256, 47), (128, 40), (52, 100), (200, 129),
-                                  (64, 16), (240, 250)])
+                                  (64, 16), (240, 250), (128, 200), (112, 144)])
 @pytest.mark.parametrize("split", [0, 1, 333, 700])
 def test_dense_split_matches_oracle(K, Fo, split):
     """Rows at or past the block's n_active (no in-edges) run through the dense
@@ -118,12 +118,19 @@ def test_dense_split_matches_oracle(K, Fo, split):
     blk.n_active = split
     args = (x.to(DEV), blk, "mean", conv.lin_l.weight.to(DEV), conv.lin_l.bias.to(DEV),
             conv.lin_r.weight.to(DEV))
-    got = sage_layer_fwd(*args, relu=True, p_drop=p, seed=seed).cpu()
     keep = dropout_keep(seed, N, Fo, p)
-    torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)
-    got = sage_layer_fwd(*args, relu=False, p_drop=0.0, seed=seed).cpu()
-    with torch.no_grad():
-        torch.testing.assert_close(got, conv(x, ei), **OUT)
+    agg_ref = torch.from_numpy(c_agg.agg_fwd(x, ei, N, "mean"))
+    has_edges = torch.bincount(ei[1], minlength=N) > 0
+    # with agg_out (the model's call: wide layers take the agg / z / dense split)
+    for with_agg in (False, True):
+        agg = torch.full((N, K), float("nan"), device=DEV) if with_agg else None
+        got = sage_layer_fwd(*args, relu=True, p_drop=p, seed=seed, agg_out=agg).cpu()
+        torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)
+        if with_agg:  # saved aggregate of the rows with edges: bitwise
+            assert torch.equal(agg.cpu()[has_edges], agg_ref[has_edges])
+        got = sage_layer_fwd(*args, relu=False, p_drop=0.0, seed=seed, agg_out=agg).cpu()
+        with torch.no_grad():
+            torch.testing.assert_close(got, conv(x, ei), **OUT)
 
 
 class _MaskedSAGE(pyg_ref.SAGE):

@@ -73,6 +73,23 @@ def main():
         res[tag + "_noagg_out"] = timeit(layer(blk, True, 0.0, None), a.reps)
         res[tag + "_root_only"] = timeit(layer(empty, False, 0.0, None), a.reps)
         res[tag + "_root_only_drop"] = timeit(layer(empty, True, 0.5, None), a.reps)
+        # raw-weight entry (the model's path): split at n_active (dense kernel
+        # for the edge-free rows) vs no split, and the dense kernel alone
+        from ngnn.fused import sage_layer_fwd
+        n_act = int(b.edge_index[1].max().item()) + 1
+        blk_s = Block(b.edge_index, N)
+        blk_s.n_active = n_act
+
+        def raw(block, p):
+            return lambda: sage_layer_fwd(x, block, "mean", wl, bl, wr, relu=True, p_drop=p,
+                                          seed=7, agg_out=agg)
+        res[tag + "_raw_drop_nosplit"] = timeit(raw(blk, 0.5), a.reps)
+        res[tag + "_raw_drop_split"] = timeit(raw(blk_s, 0.5), a.reps)
+        blk_e = Block(torch.empty(2, 0, dtype=torch.long, device=dev), N)
+        blk_e.n_active = 0
+        res[tag + "_dense_only_drop"] = timeit(raw(blk_e, 0.5), a.reps)
+        res[tag + "_dense_only"] = timeit(raw(blk_e, 0.0), a.reps)
+        res["n_active"] = n_act
         res[tag + "_pack2"] = timeit(lambda: (pack_weight(wl), pack_weight(wr)), a.reps)
         # pure-copy roofline reference: read x + write out
         res[tag + "_torch_copy_x"] = timeit(lambda: x.clone(), a.reps)
