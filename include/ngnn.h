@@ -235,7 +235,16 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * the caller then packs and calls ngnn_sage_fwd.  x_dev (nullable): a device
  * word holding x's address, read at run time instead of x (a HIP-graph slot
  * whose batch stays where the loader put it; 16-B aligned, row stride ldx,
- * rows < *n_rows_dev). */
+ * rows < *n_rows_dev).  n_edge_rows / n_edge_rows_dev (device int, nullable,
+ * overrides): rows at or past it have no in-edges (NeighborLoader numbers
+ * the rows that receive edges first).  With NGNN_SPLIT=1 in the environment
+ * (opt-in; the fused kernel is the default), F_out > 128 and agg_out given,
+ * the layer runs as three launches: the aggregate of the rows below the
+ * bound (into agg_out, edgeless rows zeroed), z = agg . W_l^T on them (into
+ * ws), and a gather-free dense kernel over every row (one wave per SIMD, W_r
+ * in LDS, epilogue software-pipelined under the MFMAs) adding z to the edge
+ * rows.  Pass n_edge_rows = n_rows, NULL when unknown.
+ * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes. */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
@@ -390,7 +399,8 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * so the captured step has no bound launch).  Kept by a 64-bit atomicMax of
  * (gen << 32 | value): gen must grow with every load (no reset launch).
  * n_edge_rows (nullable): 1 + the last target (0 without edges) = the split
- * of ngnn_sage_fwd_raw's n_edge_rows_dev.  Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
+ * of ngnn_sage_fwd_raw's n_edge_rows_dev.
+ * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,

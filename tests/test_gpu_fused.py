@@ -102,7 +102,7 @@ def test_fused_layer_dropout_mask_and_scale():
 @pytest.mark.parametrize("K,Fo", [(100, 256), (256, 47), (128, 40), (52, 100), (200, 129),
                                   (64, 16), (240, 250), (128, 200), (112, 144)])
 @pytest.mark.parametrize("split", [0, 1, 333, 700])
-def test_dense_split_matches_oracle(K, Fo, split):
+def test_dense_split_matches_oracle(K, Fo, split, monkeypatch):
     """Rows at or past the block's n_active (no in-edges) run through the dense
     kernel, the rows below through the fused gather kernel: the union equals
     the oracle layer, with ReLU and the host-replicated dropout mask."""
@@ -121,7 +121,9 @@ def test_dense_split_matches_oracle(K, Fo, split):
     keep = dropout_keep(seed, N, Fo, p)
     agg_ref = torch.from_numpy(c_agg.agg_fwd(x, ei, N, "mean"))
     has_edges = torch.bincount(ei[1], minlength=N) > 0
-    # with agg_out (the model's call: wide layers take the agg / z / dense split)
+    # with agg_out (the model's call: wide layers take the agg / z / dense split,
+    # opted in here) and without (fused kernel on the edge rows only)
+    monkeypatch.setenv("NGNN_SPLIT", "1")
     for with_agg in (False, True):
         agg = torch.full((N, K), float("nan"), device=DEV) if with_agg else None
         got = sage_layer_fwd(*args, relu=True, p_drop=p, seed=seed, agg_out=agg).cpu()
