@@ -83,6 +83,11 @@ struct Dropout {
     __device__ __forceinline__ bool keep_half(uint32_t h, uint32_t col) const {
         return ((col & 1u) ? (h >> 16) : (h & 0xffffu)) >= thresh;
     }
+    // the same with the column's parity known at compile time
+    template <int ODD>
+    __device__ __forceinline__ bool keep_par(uint32_t h) const {
+        return (ODD ? (h >> 16) : (h & 0xffffu)) >= thresh;
+    }
     __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
         return keep_half(pair_hash(rkey, col), col);
     }
@@ -124,8 +129,7 @@ inline Dropout make_dropout(float p, uint64_t seed) {
 // Row-tile forward (ngnn_sage_rt.hip): returns 1 (launch status in *rc) when
 // it takes the call, 0 when the shape is outside its envelope.
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, int64_t row_end, const int32_t *row_end_dev,
-                     const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,

@@ -93,7 +93,10 @@ __device__ __forceinline__ void dn_epi_tile(const v4f &acc, const DenseArgs &a, 
     for (int j = 0; j < 4; ++j) {
         float y = acc[j] + b[j];
         y = (a.epi.relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
-        if (DROP) y = a.epi.drop.keep_half(j < 2 ? h0 : h1, c0 + j) ? y * a.epi.drop.scale : 0.0f;
+        if (DROP)
+            y = ((j & 1) ? a.epi.drop.keep_par<1>(j < 2 ? h0 : h1) : a.epi.drop.keep_par<0>(j < 2 ? h0 : h1))
+                    ? y * a.epi.drop.scale
+                    : 0.0f;
         v[j] = y;
     }
     if (vec) {  // (F_out % 16 == 0: padded n-tiles start at f >= F_out and are dropped)

@@ -50,10 +50,6 @@ struct RtArgs {
     int K, KG;  // KG = ceil(K / 16)
     int n_rows;
     const int32_t *n_rows_dev;
-    // rows [row_end, n_rows) belong to the dense kernel (ngnn_sage_dense.hip):
-    // no tiles start there and their stores are dropped; x keeps the full range
-    int row_end;
-    const int32_t *row_end_dev;
     const int32_t *rowptr;
     const int32_t *col;
     const v4f *wl;  // packed [NT][KG][64] or NULL (no neighbour term); raw (see ldw) only
@@ -290,12 +286,11 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 // 16-B store per m-tile, no per-lane predicates.
 template <int NTW, bool DROP>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
-                                         const float *sbias, int r, bool vec, int q, int row_end) {
+                                         const float *sbias, int r, bool vec, int q) {
     // relu through a wave-uniform select; dropout (hash per element) only in
     // the DROP instantiation
     const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) : 0u;
-    // rows at or past row_end: every offset lands past the range (dropped)
-    const int obase = r < row_end ? r * static_cast<int>(a.ldo) * 4 : kOOB;
+    const int obase = r * static_cast<int>(a.ldo) * 4;
     const bool relu = a.epi.relu;
 #pragma unroll
     for (int m = 0; m < NTW; ++m) {
@@ -304,16 +299,17 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
         const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
         // two pair hashes cover the lane's 4 columns (col_base + f is even)
         const uint32_t c0 = static_cast<uint32_t>(a.epi.col_base + f);
-        const uint32_t h0 = DROP ? a.epi.drop.pair_hash(rk, c0) : 0u;
-        const uint32_t h1 = DROP ? a.epi.drop.pair_hash(rk, c0 + 2) : 0u;
         v4f v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float y = acc[m][j] + b[j];
-            y = (relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
-            if (DROP)
-                y = a.epi.drop.keep_half(j < 2 ? h0 : h1, c0 + j) ? y * a.epi.drop.scale : 0.0f;
-            v[j] = y;
+        for (int j = 0; j < 4; j += 2) {
+            const uint32_t h = DROP ? a.epi.drop.pair_hash(rk, c0 + j) : 0u;
+#pragma unroll
+            for (int jj = j; jj < j + 2; ++jj) {
+                float y = acc[m][jj] + b[jj];
+                y = (relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
+                if (DROP) y = a.epi.drop.keep_half(h, c0 + jj) ? y * a.epi.drop.scale : 0.0f;
+                v[jj] = y;
+            }
         }
         if (a.dbg & 2) {
             if (v[0] == 12345.f) buf_store1(v[1], orsrc, obase, 0, 0);  // keep the math alive
@@ -390,9 +386,7 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     const int q = lane >> 4, rl = lane & 15;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
-    int row_end = min(n_rows, a.row_end);
-    if (a.row_end_dev) row_end = min(row_end, *a.row_end_dev);
-    const int n_tiles = (row_end + RT_ROWS - 1) / RT_ROWS;
+    const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
     const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
     const int tstride = gridDim.x * RT_WAVES;
 
@@ -493,9 +487,9 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
         // ---- epilogue (bias, relu, dropout and the stores)
         if (!(a.dbg & 8)) {
             if (a.epi.drop.thresh)
-                epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q, row_end);
+                epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q);
             else
-                epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q, row_end);
+                epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q);
         }
     }
 }
@@ -674,8 +668,7 @@ int launch_rt_agg(const float *x, const float *const *x_dev, int64_t ldx, int64_
 // per slice; the packed weights are n-tile major, so a slice is a contiguous
 // sub-array.
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, int64_t row_end, const int32_t *row_end_dev,
-                     const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
@@ -757,8 +750,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.KG = KG;
         a.n_rows = static_cast<int>(n_rows);
         a.n_rows_dev = n_rows_dev;
-        a.row_end = static_cast<int>(std::min(row_end, n_rows));
-        a.row_end_dev = row_end_dev;
         a.rowptr = rowptr;
         a.col = col;
         // a slice's weights: packed fragments are n-tile major (contiguous
@@ -799,7 +790,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
         a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
-        const int n_tiles = static_cast<int>(ceil_div(std::min(row_end, n_rows), RT_ROWS));
+        const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_pre<2>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
             case 3: *rc = dispatch_pre<3>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
@@ -887,9 +878,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
             return rc;
     }
 fused:
-    split = n_rows;
-    split_dev = nullptr;
-    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, split, split_dev, rowptr, col, reduce, wl, wr,
+    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr,
                           bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc,
                           ldw, ws, ws_bytes, x_dev))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
