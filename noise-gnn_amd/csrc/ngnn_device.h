@@ -129,7 +129,8 @@ inline Dropout make_dropout(float p, uint64_t seed) {
 // Row-tile forward (ngnn_sage_rt.hip): returns 1 (launch status in *rc) when
 // it takes the call, 0 when the shape is outside its envelope.
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, int64_t tile_end, const int32_t *tile_end_dev,
+                     bool prefer_wl_lds, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
@@ -145,6 +146,7 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
                    const int32_t *n_rows_dev, const float *wr, int64_t ldw, const float *bias,
                    int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                    const uint64_t *seed_dev, hipStream_t st, int *rc, const float *z = nullptr,
-                   int64_t ldz = 0, int64_t z_rows = 0, const int32_t *z_rows_dev = nullptr);
+                   int64_t ldz = 0, int64_t z_rows = 0, const int32_t *z_rows_dev = nullptr,
+                   bool round_begin16 = false);
 
 }  // namespace ngnn

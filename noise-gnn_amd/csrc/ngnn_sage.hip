@@ -479,7 +479,7 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
     if (!xmask) {  // default path: the row-tile kernel (ngnn_sage_rt.hip)
         int rc = NGNN_OK;
-        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl_packed,
+        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, n_rows, nullptr, false, rowptr, col, reduce, wl_packed,
                              wr_packed, bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out,
                              ld_agg, as_stream(stream), &rc))
             return rc;

@@ -47,6 +47,7 @@ struct DenseArgs {
     int K, KG;
     int row_begin;
     const int32_t *row_begin_dev;  // non-null: first row read at run time
+    int round16;                   // first row rounded up to a multiple of 16
     int n_rows;
     const int32_t *n_rows_dev;
     const float *w;  // raw PyG weights [F_out, K], row stride ldw
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(DN_WAVES * 64) void k_dense(DenseArgs a) {
     const int lane = ln, q = lane >> 4, rl = lane & 15;
     int rb = a.row_begin;
     if (a.row_begin_dev) rb = *a.row_begin_dev;
+    if (a.round16) rb = (rb + 15) & ~15;
     int nr = a.n_rows;
     if (a.n_rows_dev) nr = min(nr, *a.n_rows_dev);
     rb = __builtin_amdgcn_readfirstlane(rb);
@@ -361,7 +363,7 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
                    const int32_t *n_rows_dev, const float *wr, int64_t ldw, const float *bias,
                    int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                    const uint64_t *seed_dev, hipStream_t st, int *rc, const float *z,
-                   int64_t ldz, int64_t z_rows, const int32_t *z_rows_dev) {
+                   int64_t ldz, int64_t z_rows, const int32_t *z_rows_dev, bool round_begin16) {
     if (getenv("NGNN_NO_DENSE")) return 0;
     if (K % 4 != 0 || ldx % 4 != 0 || ldw % 4 != 0 || K <= 48 || K > 256 || Fo > 256) return 0;
     if ((!x_dev && !aligned(x, 16)) || !aligned(wr, 16)) return 0;
@@ -384,6 +386,7 @@ int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64
     a.KG = KG;
     a.row_begin = static_cast<int>(row_begin);
     a.row_begin_dev = row_begin_dev;
+    a.round16 = round_begin16;
     a.n_rows = static_cast<int>(n_rows);
     a.n_rows_dev = n_rows_dev;
     a.w = wr;

@@ -50,6 +50,7 @@ struct RtArgs {
     int K, KG;  // KG = ceil(K / 16)
     int n_rows;
     const int32_t *n_rows_dev;
+    const int32_t *tile_end_dev;  // non-null: tiles only below ceil16(*tile_end_dev) (split mode)
     const int32_t *rowptr;
     const int32_t *col;
     const v4f *wl;  // packed [NT][KG][64] or NULL (no neighbour term); raw (see ldw) only
@@ -390,7 +391,8 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     const int q = lane >> 4, rl = lane & 15;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
-    const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
+    int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
+    if (a.tile_end_dev) n_tiles = min(n_tiles, (*a.tile_end_dev + RT_ROWS - 1) / RT_ROWS);
     const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
     const int tstride = gridDim.x * RT_WAVES;
 
@@ -672,7 +674,8 @@ int launch_rt_agg(const float *x, const float *const *x_dev, int64_t ldx, int64_
 // per slice; the packed weights are n-tile major, so a slice is a contiguous
 // sub-array.
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, int64_t tile_end, const int32_t *tile_end_dev,
+                     bool prefer_wl_lds, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
@@ -694,8 +697,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     const size_t lds_cap = 160 * 1024 - 1024;                          // minus the bias slice
     // widest supported tile count whose W_r fits
     int ntw_max = 0;
-    for (int c : {16, 8, 4, 3, 2})
-        if (static_cast<size_t>(c) * frag_kb <= lds_cap) {
+    for (int c : {16, 8, 4, 3, 2})  // prefer_wl_lds: narrower slices whose W_r AND W_l fit
+        if (static_cast<size_t>(c) * frag_kb * ((prefer_wl_lds && wl_packed) ? 2 : 1) <= lds_cap) {
             ntw_max = c;
             break;
         }
@@ -754,6 +757,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.KG = KG;
         a.n_rows = static_cast<int>(n_rows);
         a.n_rows_dev = n_rows_dev;
+        a.tile_end_dev = tile_end_dev;
         a.rowptr = rowptr;
         a.col = col;
         // a slice's weights: packed fragments are n-tile major (contiguous
@@ -794,7 +798,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
         a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
-        const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
+        const int n_tiles = static_cast<int>(ceil_div(std::min(tile_end, n_rows), RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_pre<2>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
             case 3: *rc = dispatch_pre<3>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
@@ -854,12 +858,13 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     // launches (agg 16 k rows + z + dense 153 k rows) tie the fused kernel
     // (159 vs 155 us): the one-wave-per-SIMD dense kernel reaches ~60 % of the
     // fp32 MFMA rate, not enough to pay for the separate aggregate pass
-    const bool no_split = getenv("NGNN_SPLIT") == nullptr;  // read per call (tests toggle it)
+    const char *split_env = getenv("NGNN_SPLIT");  // read per call (tests toggle it)
+    const int split_mode = split_env ? atoi(split_env) : 0;
     if (!wl) {
         if (sage_fwd_dense(x, x_dev, ldx, K, 0, nullptr, n_rows, n_rows_dev, wr, ldw, bias, Fo, out,
                            ldo, relu, p_drop, seed, seed_dev, st, &rc))
             return rc;
-    } else if (!no_split && Fo > 128 && (split < n_rows || split_dev) && agg_out &&
+    } else if (split_mode == 1 && Fo > 128 && (split < n_rows || split_dev) && agg_out &&
                ws_bytes >= ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) && aligned(ws, 16) &&
                ld_agg % 4 == 0 && aligned(agg_out, 16)) {
         const int64_t zrows = split_dev ? n_rows : split;  // host bound of the z rows
@@ -882,7 +887,25 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
             return rc;
     }
 fused:
-    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr,
+    if (wl && split_mode == 2 && (split < n_rows || split_dev)) {
+        // split mode 2: the fused gather kernel on the tiles below the split
+        // (output slices narrow enough for W_r and W_l to share the LDS),
+        // the dense kernel from the next 16-row boundary up
+        const int64_t s16 = std::min(n_rows, ceil_div(split, 16) * 16);
+        int rd = NGNN_OK;
+        if (sage_fwd_dense(x, x_dev, ldx, K, split_dev ? 0 : s16, split_dev, n_rows, n_rows_dev, wr,
+                           ldw, bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, st, &rd, nullptr, 0,
+                           0, nullptr, /*round_begin16=*/true)) {
+            if (rd) return rd;
+            if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, split_dev ? n_rows : s16, split_dev,
+                                  true, rowptr, col, reduce, wl, wr, bias, Fo, out, ldo, relu, p_drop,
+                                  seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws, ws_bytes, x_dev))
+                return NGNN_E_SHAPE;
+            return rc;
+        }
+    }
+    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, n_rows, nullptr, false, rowptr, col, reduce,
+                          wl, wr,
                           bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc,
                           ldw, ws, ws_bytes, x_dev))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd

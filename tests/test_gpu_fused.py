@@ -123,8 +123,8 @@ def test_dense_split_matches_oracle(K, Fo, split, monkeypatch):
     has_edges = torch.bincount(ei[1], minlength=N) > 0
     # with agg_out (the model's call: wide layers take the agg / z / dense split,
     # opted in here) and without (fused kernel on the edge rows only)
-    monkeypatch.setenv("NGNN_SPLIT", "1")
-    for with_agg in (False, True):
+    for mode, with_agg in (("1", False), ("1", True), ("2", True)):
+        monkeypatch.setenv("NGNN_SPLIT", mode)
         agg = torch.full((N, K), float("nan"), device=DEV) if with_agg else None
         got = sage_layer_fwd(*args, relu=True, p_drop=p, seed=seed, agg_out=agg).cpu()
         torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)

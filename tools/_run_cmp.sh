@@ -5,7 +5,7 @@ mkdir -p gpurun_out/$T
 timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py tests/test_graphs_gpu.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/$T/pytest.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-for v in "" "NGNN_PACK_WL=1"; do
-  env $v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-epoch > gpurun_out/$T/bench_${v:-raw}.log 2>&1
-  echo "bench $v rc=$?"; tail -1 gpurun_out/$T/bench_${v:-raw}.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['all_kernels'])"
+for v in ${VARIANTS:-X=0 NGNN_SPLIT=2 NGNN_SPLIT=1 X=1}; do
+  env $v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-epoch > gpurun_out/$T/bench_$v.log 2>&1
+  echo "bench $v rc=$?"; tail -1 gpurun_out/$T/bench_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], {k: v['avg_us'] for k, v in d['roofline']['all_kernels'].items()})"
 done
