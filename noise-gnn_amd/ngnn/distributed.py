@@ -65,10 +65,11 @@ class GradAllReduce:
         dev = self.params[0].device
         self.bucket = torch.empty(n, dtype=torch.float32, device=dev)
 
-    def __call__(self):
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
-            return
-        world = dist.get_world_size(self.group)
+    def active(self) -> bool:
+        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def pack(self):
+        """grads -> bucket (stream-ordered copies; capturable in a HIP graph)."""
         off = 0
         for p in self.params:
             n = p.numel()
@@ -77,7 +78,14 @@ class GradAllReduce:
             else:
                 self.bucket[off:off + n].copy_(p.grad.reshape(-1))
             off += n
+
+    def allreduce(self):
+        """The one collective: SUM over ranks (RCCL over xGMI with nccl)."""
         dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=self.group)
+
+    def unpack(self):
+        """bucket / world -> grads (capturable)."""
+        world = dist.get_world_size(self.group)
         self.bucket.div_(world)
         off = 0
         for p in self.params:
@@ -86,3 +94,10 @@ class GradAllReduce:
                 p.grad = torch.empty_like(p)
             p.grad.copy_(self.bucket[off:off + n].view_as(p))
             off += n
+
+    def __call__(self):
+        if not self.active():
+            return
+        self.pack()
+        self.allreduce()
+        self.unpack()

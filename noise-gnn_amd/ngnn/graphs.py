@@ -26,7 +26,8 @@ rows < batch_size only).  A device scalar holds N; the forward kernels read it
 and skip the padding rows, so a generous slot costs memory, not time.
 
 The gradient all-reduce of seed-sharded data parallelism (RCCL) runs between
-two graphs (forward+backward, then the optimizer step), outside capture.
+two graphs (forward+backward+bucket pack, then bucket unpack+optimizer step),
+outside capture: one collective call per step on the host.
 """
 from __future__ import annotations
 
@@ -70,6 +71,7 @@ class GraphedTrainStep:
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
         self.loss = None
+        self._split_reduce = False
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -139,11 +141,21 @@ class GraphedTrainStep:
                         x_dev=self.x_dev, r_next=(self.r_next, self.B),
                         n_edge_rows_dev=self.n_edge_rows)
         self.opt.zero_grad(set_to_none=True)
+        # data parallel: the bucket pack is the tail of the first graph and the
+        # unpack (/ world) the head of the second, so between the replays the
+        # host issues only the one all-reduce
+        red = self.reducer if (self.reducer is not None and hasattr(self.reducer, "active")
+                               and self.reducer.active()) else None
+        self._split_reduce = red is not None
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
             self.loss = self._fwd_bwd()
+            if red is not None:
+                red.pack()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
+            if red is not None:
+                red.unpack()
             self.opt.step()
         block_cache.clear()
         torch.cuda.synchronize()
@@ -166,7 +178,9 @@ class GraphedTrainStep:
         the (device) loss tensor of this step."""
         self.load(x, edge_index, y, zero_copy=True)
         self.g_fb.replay()
-        if self.reducer is not None:
+        if self._split_reduce:
+            self.reducer.allreduce()
+        elif self.reducer is not None:
             self.reducer()
         self.g_opt.replay()
         return self.loss
