@@ -400,6 +400,8 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * (gen << 32 | value): gen must grow with every load (no reset launch).
  * n_edge_rows (nullable): 1 + the last target (0 without edges) = the split
  * of ngnn_sage_fwd_raw's n_edge_rows_dev.
+ * slot_ei may be NULL when the CSR is written (a captured step that reads
+ * only the CSR).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,

@@ -55,8 +55,10 @@ __global__ __launch_bounds__(256) void k_slot_load(
             d = N + ((e - E) * span) / n_pad;
             s = d;
         }
-        sei[e] = s;
-        sei[e_cap + e] = d;
+        if (sei) {
+            sei[e] = s;
+            sei[e_cap + e] = d;
+        }
     }
     for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
     if (rowptr) {
@@ -135,8 +137,8 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
                               int32_t *n_edge_rows, void *stream) {
-    NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !slot_ei || !n_valid,
-                   NGNN_E_ARG);
+    NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
+    NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
                    NGNN_E_ARG);

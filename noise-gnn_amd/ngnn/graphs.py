@@ -91,7 +91,10 @@ class GraphedTrainStep:
         _lib.check(_lib.load().ngnn_slot_load(
             _lib.ptr(x), x.stride(0), N, x.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
             _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
-            _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
+            # replays read only the slot's CSR (the int64 edge copy serves eager
+            # use and the deterministic mode's transposed CSR)
+            None if (zero_copy and not torch.are_deterministic_algorithms_enabled())
+            else _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
             _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
             _lib.ptr(self.n_edge_rows), _lib.stream_handle(self.x.device)),
