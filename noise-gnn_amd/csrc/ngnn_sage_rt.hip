@@ -396,7 +396,15 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
     const int tstride = gridDim.x * RT_WAVES;
 
-    int t = blockIdx.x + gridDim.x * wave;
+    // tile k of this wave: k = 0 -> w0; later rounds, with bit 64, in reverse
+    // wave order, so the partial last round lands on the waves that did NOT
+    // start with a (heavier) edge tile -- NeighborLoader puts the rows with
+    // in-edges first
+    const int w0 = blockIdx.x + gridDim.x * wave;
+    const bool rev = (a.dbg & 64) != 0;
+    auto tile_of = [&](int k) { return (k == 0 || !rev) ? w0 + k * tstride : k * tstride + (tstride - 1 - w0); };
+    int kt = 0;
+    int t = w0;
     if ((a.dbg & 32) && wave >= RT_WAVES / 2) __builtin_amdgcn_s_sleep(100);  // experiment: stagger SIMD partners
     // next tile's chunk-0 x fragments and row bounds, loaded one tile ahead,
     // unconditionally (a tile past the end re-reads tile 0: valid, unused)
@@ -424,7 +432,7 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     };
     const bool vec = a.vec_out && (a.Fo == a.NT * 16);
     prefetch(t);
-    for (; t < n_tiles; t += tstride) {
+    for (; t < n_tiles; t = tile_of(++kt)) {
         const int r = t * RT_ROWS + rl;
         const int beg = nbeg, deg = nend - nbeg;
         const int maxdeg = have_l ? rowgroup_max16(deg) : 0;
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
             if (c + 1 < nchunk) {
                 if (!(a.dbg & 4)) load_x(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
             } else {
-                prefetch(t + tstride);  // next tile: a whole tile of MFMAs to land
+                prefetch(tile_of(kt + 1));  // next tile: a whole tile of MFMAs to land
             }
             if (!(a.dbg & 1)) mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
         }

@@ -171,12 +171,23 @@ class _SAGEStack(torch.autograd.Function):
         # bnd[L] = rows of dout that can be nonzero; bnd[i] = same for d(acts[i])
         # (prefix_stats takes max(bnd[i], R, ...), so R is a valid initial bnd[i])
         rows_hint = getattr(dout, "_ngnn_nonzero_rows", None)  # set by ngnn.losses
-        bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
-                         dtype=torch.int32, device=dev)
-        bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
         # the producer's precomputed top-layer bound (graph slot): no prefix-stats launch
         pre_top = (L > 0 and block.r_next is not None and rows_hint is not None
                    and int(rows_hint) == block.r_next[1])
+        # bound entries some launch below writes: row_extent (bnd[L]) without a
+        # hint, prefix stats for layers L-1 .. 1 (and 0 when dx is needed)
+        written = rows_hint is None or any(
+            not (pre_top and i == L - 1) for i in range(L - 1, -1 if need_dx else 0, -1))
+        if written:
+            bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
+                             dtype=torch.int32, device=dev)
+        else:  # read-only: a cached constant (no fill launch per step)
+            key = (dev, "bnd", L, int(rows_hint))
+            bnd = _ws.get(key)
+            if bnd is None:
+                bnd = torch.full((L + 1,), int(rows_hint), dtype=torch.int32, device=dev)
+                _ws[key] = bnd
+        bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
         if pre_top:
             bp[L - 1] = block.r_next[0].data_ptr()
         bptr = lambda j: bp[j]  # noqa: E731

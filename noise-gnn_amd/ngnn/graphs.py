@@ -72,6 +72,7 @@ class GraphedTrainStep:
         self.g_fb = self.g_opt = None
         self.loss = None
         self._split_reduce = False
+        self._one = None
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -111,7 +112,10 @@ class GraphedTrainStep:
     def _fwd_bwd(self):
         out = self.model(self.x, self.ei)
         loss = self.loss_fn(out, self.y, self.B)
-        loss.backward()
+        # a persistent d(loss) = 1 instead of backward()'s ones_like fill launch
+        if self._one is None or self._one.shape != loss.shape:
+            self._one = torch.ones_like(loss)
+        loss.backward(self._one)
         return loss
 
     def capture(self, x, edge_index, y, restore: bool = True) -> None:
