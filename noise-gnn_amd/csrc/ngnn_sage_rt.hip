@@ -396,12 +396,12 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
     const int tstride = gridDim.x * RT_WAVES;
 
-    // tile k of this wave: k = 0 -> w0; later rounds, with bit 64, in reverse
-    // wave order, so the partial last round lands on the waves that did NOT
-    // start with a (heavier) edge tile -- NeighborLoader puts the rows with
-    // in-edges first
+    // tile k of this wave: k = 0 -> w0; later rounds in reverse wave order,
+    // so the partial last round lands on the waves that did NOT start with a
+    // (heavier) edge tile -- NeighborLoader puts the rows with in-edges
+    // first (ablation bit 64 restores the plain order; -0.3..0.4 % step time)
     const int w0 = blockIdx.x + gridDim.x * wave;
-    const bool rev = (a.dbg & 64) != 0;
+    const bool rev = (a.dbg & 64) == 0;
     auto tile_of = [&](int k) { return (k == 0 || !rev) ? w0 + k * tstride : k * tstride + (tstride - 1 - w0); };
     int kt = 0;
     int t = w0;

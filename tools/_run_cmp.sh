@@ -9,3 +9,8 @@ for v in ${VARIANTS:-X=0 NGNN_SPLIT=2 NGNN_SPLIT=1 X=1}; do
   env $v timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-epoch > gpurun_out/$T/bench_$v.log 2>&1
   echo "bench $v rc=$?"; tail -1 gpurun_out/$T/bench_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], {k: v['avg_us'] for k, v in d['roofline']['all_kernels'].items()})"
 done
+if [ "${PROF:-0}" = 1 ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$T/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-epoch --timer none > gpurun_out/$T/prof.log 2>&1
+  echo "prof rc=$?"
+fi
