@@ -287,8 +287,13 @@ class _SAGEStack(torch.autograd.Function):
         return (dx, None, None, None, None, None, *grads)
 
 
+_IO_DTYPES = (torch.float32, torch.bfloat16)
+
+
 def sage_stack_supported(model, x) -> bool:
-    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2:
+    if not x.is_cuda or x.dtype not in _IO_DTYPES or x.dim() != 2:
+        return False
+    if any(p.dtype not in _IO_DTYPES for p in model.parameters()):
         return False
     if getattr(model, "use_bn", False):
         return False
@@ -300,10 +305,19 @@ def sage_stack_supported(model, x) -> bool:
 
 
 def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor:
+    """bf16 models (config #3 of BASELINE.json) run with bf16 storage at the
+    module boundary: inputs and parameters are widened to fp32 for the fused
+    fp32 kernels (autograd narrows the gradients back) and the logits are
+    returned in x's dtype -- fp32 arithmetic inside, no bf16 MFMA path."""
     params = []
     for conv in model.convs:
         params += [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
+    out_dtype = x.dtype
+    if out_dtype != torch.float32 or any(q.dtype != torch.float32 for q in params):
+        x = x.float()
+        params = [q.float() for q in params]
     p = model.dropout if model.training else 0.0
     aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
-    return _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, *params)
+    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, *params)
+    return out if out_dtype == torch.float32 else out.to(out_dtype)

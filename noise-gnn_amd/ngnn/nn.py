@@ -78,6 +78,12 @@ class SAGEConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         block = get_block(edge_index, x.size(0))
+        if x.dtype == torch.bfloat16 or self.lin_l.weight.dtype == torch.bfloat16:
+            # bf16 storage, fp32 arithmetic (the kernels are fp32)
+            out = (F.linear(segment_aggregate(x.float(), block, self.aggr), self.lin_l.weight.float(),
+                            self.lin_l.bias.float())
+                   + F.linear(x.float(), self.lin_r.weight.float()))
+            return out.to(x.dtype)
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p.requires_grad for p in self.parameters()))
         if not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2:
@@ -112,6 +118,10 @@ class GCNConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         block = get_block(edge_index, x.size(0))
+        if x.dtype == torch.bfloat16 or self.lin.weight.dtype == torch.bfloat16:
+            # bf16 storage, fp32 arithmetic (the kernels are fp32)
+            h = F.linear(x.float(), self.lin.weight.float())
+            return (segment_aggregate(h, block, "sum") + self.bias.float()).to(x.dtype)
         h = self.lin(x)
         return segment_aggregate(h, block, "sum") + self.bias
 

@@ -227,3 +227,33 @@ def test_training_step_matches_oracle():
         assert abs(float(l_ref) - float(l_mine)) < 1e-5
     for (k, p), (_, q) in zip(mine.state_dict().items(), ref.state_dict().items()):
         torch.testing.assert_close(p.cpu(), q, rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.parametrize("module", ["sage", "gcn"])
+def test_bf16_model_matches_fp32_oracle(module):
+    """A bf16 model (BASELINE config #3 asks for bf16): bf16 inputs and
+    parameters, fp32 arithmetic inside -- equal to the fp32 oracle run on the
+    same bf16-rounded values up to the bf16 rounding of the logits (rtol 1e-2,
+    the bar SURVEY §8c sets for bf16), gradients in bf16."""
+    import ngnn
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=5, scale=0.005)
+    b = sample_block(graph, graph.train_idx[:64], [6, 4, 3], seed=2)
+    torch.manual_seed(3)
+    if module == "sage":
+        mine = ngnn.SAGE(100, 64, 47, 3, dropout=0.5).eval()
+        ref = pyg_ref.SAGE(100, 64, 47, 3, dropout=0.5).eval()
+    else:
+        mine = ngnn.SimpleGCN(100, 64, 47, 3, dropout=0.5).eval()
+        ref = pyg_ref.SimpleGCN(100, 64, 47, 3, dropout=0.5).eval()
+    mine = mine.to(DEV).to(torch.bfloat16)
+    ref.load_state_dict({k: v.float().cpu() for k, v in mine.state_dict().items()})
+    xb = b.x.to(torch.bfloat16).requires_grad_(True)
+    out = mine(xb, b.edge_index)
+    assert out.dtype == torch.bfloat16
+    out.float().square().sum().backward()
+    assert xb.grad.dtype == torch.bfloat16
+    assert all(p.grad.dtype == torch.bfloat16 for p in mine.parameters())
+    xr = xb.detach().float().cpu().requires_grad_(True)
+    want = ref(xr, b.edge_index.cpu())
+    torch.testing.assert_close(out.float().cpu(), want.detach(), rtol=1e-2, atol=1e-2)
