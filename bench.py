@@ -49,6 +49,11 @@ def parse():
     ap.add_argument("--fanout", type=str, default="15,10")
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--scale", type=float, default=1.0, help="graph size scale (tests)")
+    ap.add_argument("--dataset", default="ogbn-products",
+                    help="synthetic graph shape (ngnn.loader.DATASETS); the headline is ogbn-products")
+    ap.add_argument("--aggr", default="mean", choices=["mean", "max", "sum"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="model / feature storage dtype (bf16: fp32 kernels inside)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -94,7 +99,9 @@ def cpu_baseline(batch, args, layers):
     from oracle import pyg_ref
     torch.manual_seed(0)
     threads = torch.get_num_threads()
-    m = pyg_ref.SAGE(100, args.hidden, 47, layers, dropout=0.5)
+    from ngnn.loader import DATASETS
+    _, _, F_in, C, _ = DATASETS[args.dataset]
+    m = pyg_ref.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     x, ei, y = batch.x.cpu(), batch.edge_index.cpu(), batch.y.cpu()
     E = ei.shape[1]
@@ -108,7 +115,8 @@ def cpu_baseline(batch, args, layers):
             break
     return {"value": layers * E * n / dt, "unit": "edges/s", "cores": threads, "kind": "port",
             "ms_per_step": 1e3 * dt / n,
-            "sample": f"{n} training steps (fwd+bwd+Adam) on one products-[15,10] bs=1024 block "
+            "sample": f"{n} training steps (fwd+bwd+Adam) on one {args.dataset}-[{args.fanout}] "
+                      f"bs={args.batch_size} block "
                       f"(E={E}, N={batch.num_nodes}), torch {torch.__version__} CPU, "
                       f"{threads} threads, PyG 2.5.1 op sequence restated in oracle/pyg_ref.py"}
 
@@ -128,9 +136,14 @@ def main():
     fanout = [int(v) for v in args.fanout.split(",")]
     layers = len(fanout)
 
-    graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
+    from ngnn.loader import DATASETS
+    _, _, F_in, C, _ = DATASETS[args.dataset]
+    graph = synthetic_graph(args.dataset, dev, seed=0, scale=args.scale)
     torch.manual_seed(1234)  # identical init on every rank
-    model = ngnn.SAGE(100, args.hidden, 47, layers, dropout=0.5).to(dev)
+    model = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
+    if args.dtype == "bf16":
+        model = model.to(torch.bfloat16)
+        graph.x = graph.x.to(torch.bfloat16)
     # the reference's Adam(lr=1e-3) rule as ngnn's two-launch device Adam; its step count
     # lives on the device, so the HIP graph can replay it
     from ngnn.optim import Adam
@@ -251,14 +264,17 @@ def main():
         E_avg = sum(b.edge_index.shape[1] for b in batches) / nb
         N_avg = sum(b.num_nodes for b in batches) / nb
         line = {
-            "metric": "aggregated edges/sec (GraphSAGE train step), ogbn-products fanout=[15,10] bs=1024",
+            "metric": "aggregated edges/sec (GraphSAGE train step), ogbn-products fanout=[15,10] bs=1024"
+                      if (args.dataset, args.fanout, args.batch_size) == ("ogbn-products", "15,10", 1024)
+                      else f"aggregated edges/sec (GraphSAGE train step), {args.dataset} "
+                           f"fanout=[{args.fanout}] bs={args.batch_size}",
             "value": round(edges / dt, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded Chung-Lu graph with ogbn-products sizes; random features)",
-            "config": {"workload": f"products-[{args.fanout}]-bs{args.batch_size}",
-                       "model": f"SAGE(100,{args.hidden},47,L={layers}) mean-aggr + Adam(1e-3)",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": f"synthetic (seeded Chung-Lu graph with {args.dataset} sizes; random features)",
+            "config": {"workload": f"{args.dataset.replace('ogbn-', '')}-[{args.fanout}]-bs{args.batch_size}",
+                       "model": f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)",
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
                        "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},

@@ -83,6 +83,8 @@ class GraphedTrainStep:
         N, E = x.size(0), edge_index.size(1)
         if N + 1 > self.n_cap or E > self.e_cap:
             raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
+        if x.dtype != torch.float32:  # bf16 batches: the captured kernels read fp32 rows
+            x = x.float()
         if x.stride(1) != 1 or x.stride(0) != self.x.stride(0) or x.data_ptr() % 16:
             x = x.clone(memory_format=torch.contiguous_format)
         if edge_index.stride(1) != 1:

@@ -186,8 +186,10 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
         raise RuntimeError("ngnn.loader.sample_block: GPU only (no CPU fallback)")
     if graph.y.dtype != torch.int64 or not graph.y.is_contiguous():
         raise TypeError("graph.y must be a contiguous int64 vector")
-    if gather_features and (graph.x.dtype != torch.float32 or graph.x.stride(1) != 1):
-        raise TypeError("graph.x must be a row-major float32 matrix")
+    if gather_features and (graph.x.dtype not in (torch.float32, torch.bfloat16)
+                            or graph.x.stride(1) != 1
+                            or (graph.x.dtype == torch.bfloat16 and graph.x.size(1) % 2)):
+        raise TypeError("graph.x must be a row-major float32 matrix (or bf16 with an even width)")
     s64 = seeds.to(torch.int64).contiguous()
     B = s64.numel()
     fan = (ctypes.c_int32 * max(len(fanouts), 1))(*[int(k) for k in fanouts])
@@ -205,13 +207,17 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
     n_id = torch.empty(n, dtype=torch.int64, device=dev)
     edge_index = torch.empty(2, e, dtype=torch.int64, device=dev)
     y = torch.empty(n, dtype=torch.int64, device=dev)
-    x = None
+    x = xw = None
+    xa = graph.x
     if gather_features:
-        x = torch.empty(n, graph.x.size(1), dtype=torch.float32, device=dev)
+        x = torch.empty(n, graph.x.size(1), dtype=graph.x.dtype, device=dev)
+        # the row gather copies 32-bit words: bf16 rows are viewed as float32 pairs
+        xa = graph.x.view(torch.float32) if graph.x.dtype == torch.bfloat16 else graph.x
+        xw = x.view(torch.float32) if x.dtype == torch.bfloat16 else x
     _lib.check(lib.ngnn_sample_block_finish(
         fan, H, B, n, e, _lib.ptr(cache.node_map), graph.num_nodes, _lib.ptr(ws), ws.numel(),
-        _lib.ptr(n_id), _lib.ptr(edge_index), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(graph.x),
-        graph.x.stride(0), graph.x.size(1), _lib.ptr(x), x.stride(0) if x is not None else 0, st),
+        _lib.ptr(n_id), _lib.ptr(edge_index), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(xa),
+        xa.stride(0), xa.size(1), _lib.ptr(xw), xw.stride(0) if xw is not None else 0, st),
         "ngnn_sample_block_finish")
     # built here: ids are in range and targets non-decreasing -> no probe needed
     hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active)
