@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 7
+#define NGNN_ABI_VERSION 8
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -374,11 +374,13 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * HIP graph replays correctly).  ticket (nullable): a device uint32, zero
  * before the first call, that the update's workgroups count themselves on;
  * the last one advances *step and re-zeroes it (one launch per call instead
- * of an update + increment pair; up to 16 tensors).  Replaces the
- * reference's torch.optim.Adam(...).step() (model.py:66-69). */
+ * of an update + increment pair; up to 16 tensors).  dtypes (host, nullable
+ * = all NGNN_F32): per tensor NGNN_F32 or NGNN_BF16 (params and grads in that
+ * dtype; exp_avgs / exp_avg_sqs always fp32).  Replaces the reference's
+ * torch.optim.Adam(...).step() (model.py:66-69). */
 int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
-                   float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,
+                   const int32_t *dtypes, float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,
                    float weight_decay, void *stream);
 
 /* ------------------------------------------------------ HIP-graph slot

@@ -2,10 +2,13 @@
 // model.py:66-69 [ext: torch]) as ONE launch over every parameter tensor:
 // the last workgroup to finish (a device ticket) advances the step count,
 // instead of torch's step increment + multi-tensor fused kernel.  Same update rule as torch Adam
-// (amsgrad off, maximize off):
+// (amsgrad off, maximize off); bf16 parameters/gradients are widened, updated
+// in fp32 against fp32 moments and rounded to nearest on store:
 //   t = step + 1;  g += wd p;  m = m + (1 - b1)(g - m);  v = b2 v + (1 - b2) g^2
 //   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // The step count lives on the device (HIP-graph replays advance it).
+#include <hip/hip_bf16.h>
+
 #include "ngnn_internal.h"
 
 namespace ngnn {
@@ -14,8 +17,9 @@ namespace {
 constexpr int kMaxT = 16;
 
 struct AdamTensors {
-    float *p[kMaxT];
+    float *p[kMaxT];  // fp32, or bf16 when bf[k] (update in fp32, stored rounded)
     const float *g[kMaxT];
+    int bf[kMaxT];
     float *m[kMaxT];
     float *v[kMaxT];
     int64_t off[kMaxT + 1];  // prefix sums of numel
@@ -35,8 +39,14 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
         int k = 0;
         while (k + 1 < T.n && i >= T.off[k + 1]) ++k;
         const int64_t j = i - T.off[k];
-        float g = T.g[k][j];
-        float p = T.p[k][j];
+        float g, p;
+        if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
+            g = __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(T.g[k])[j]);
+            p = __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(T.p[k])[j]);
+        } else {
+            g = T.g[k][j];
+            p = T.p[k][j];
+        }
         if (wd != 0.0f) g = g + wd * p;
         float m = T.m[k][j];
         float v = T.v[k][j];
@@ -46,7 +56,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
         p = p - step_size * (m / denom);
         T.m[k][j] = m;
         T.v[k][j] = v;
-        T.p[k][j] = p;
+        if (T.bf[k]) reinterpret_cast<__hip_bfloat16 *>(T.p[k])[j] = __float2bfloat16(p);
+        else T.p[k][j] = p;
     }
     if (ticket) {
         // every workgroup has read *step (its value fed the loop above) before
@@ -68,7 +79,8 @@ using namespace ngnn;
 
 extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                               float *const *exp_avgs, float *const *exp_avg_sqs,
-                              const int64_t *numels, float *step, uint32_t *ticket, float lr,
+                              const int64_t *numels, const int32_t *dtypes, float *step,
+                              uint32_t *ticket, float lr,
                               float beta1, float beta2, float eps, float weight_decay,
                               void *stream) {
     NGNN_RETURN_IF(n_tensors < 0 || !step, NGNN_E_ARG);
@@ -90,6 +102,9 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
             T.p[k] = params[base + k];
             T.g[k] = grads[base + k];
             T.m[k] = exp_avgs[base + k];
+            T.bf[k] = dtypes ? (dtypes[base + k] == NGNN_BF16) : 0;
+            NGNN_RETURN_IF(dtypes && dtypes[base + k] != NGNN_F32 && dtypes[base + k] != NGNN_BF16,
+                           NGNN_E_DTYPE);
             T.v[k] = exp_avg_sqs[base + k];
             T.off[k + 1] = T.off[k] + numels[base + k];
         }

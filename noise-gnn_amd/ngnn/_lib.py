@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -48,7 +48,7 @@ SIGNATURES = {
     "ngnn_ct_loss_fwd": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _i64, _p,
                                 _p, _p, _p, _sz, _p, _p]),
     "ngnn_ct_loss_bwd": (_int, [_int, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _p]),
-    "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
+    "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                               _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p]),

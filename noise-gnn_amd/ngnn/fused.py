@@ -304,6 +304,23 @@ def sage_stack_supported(model, x) -> bool:
     return True
 
 
+def zero_copy_ok(model, n_rows: int, in_dim: int) -> bool:
+    """Can a HIP-graph slot hand this model's layer 0 the batch's feature rows
+    in place (ngnn_sage_fwd_raw's x_dev)?  Only the fused SAGE stack reads
+    x_dev, and only the row-tile kernel accepts it: K % 4 == 0 and 32-bit
+    buffer offsets over the slot's rows (x, the output, the saved aggregate)."""
+    if not isinstance(getattr(model, "convs", None), torch.nn.ModuleList):
+        return False
+    if getattr(model, "use_bn", False) or not hasattr(model.convs[0], "lin_r"):
+        return False
+    if len({c.aggr for c in model.convs}) != 1:
+        return False
+    fo = model.convs[0].lin_r.weight.shape[0]
+    lim = (1 << 31) - 4096
+    return (in_dim % 4 == 0 and n_rows * in_dim * 4 <= lim and n_rows * fo * 4 <= lim
+            and -(-in_dim // 16) <= 79)
+
+
 def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor:
     """bf16 models (config #3 of BASELINE.json) run with bf16 storage at the
     module boundary: inputs and parameters are widened to fp32 for the fused

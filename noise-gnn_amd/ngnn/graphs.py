@@ -73,6 +73,7 @@ class GraphedTrainStep:
         self.loss = None
         self._split_reduce = False
         self._one = None
+        self.zero_copy = True
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -145,9 +146,13 @@ class GraphedTrainStep:
         # the captured Block must be built inside the graph (from the slot's
         # contents at replay time), never served from the eager cache
         block_cache.clear()
+        # zero-copy features only where the layer-0 kernel can take them
+        # (otherwise every replay copies the rows into the slot)
+        from .fused import zero_copy_ok
+        self.zero_copy = zero_copy_ok(self.model, self.n_cap, self.x.size(1))
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
-                        x_dev=self.x_dev, r_next=(self.r_next, self.B),
+                        x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B),
                         n_edge_rows_dev=self.n_edge_rows)
         self.opt.zero_grad(set_to_none=True)
         # data parallel: the bucket pack is the tail of the first graph and the
@@ -185,7 +190,7 @@ class GraphedTrainStep:
     def __call__(self, x, edge_index, y):
         """Load one batch into the slot and replay the captured step; returns
         the (device) loss tensor of this step."""
-        self.load(x, edge_index, y, zero_copy=True)
+        self.load(x, edge_index, y, zero_copy=self.zero_copy)
         self.g_fb.replay()
         if self._split_reduce:
             self.reducer.allreduce()

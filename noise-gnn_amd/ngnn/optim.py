@@ -36,8 +36,12 @@ class Adam(torch.optim.Optimizer):
             if not ps:
                 continue
             for p in ps:
-                if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
-                    raise RuntimeError("ngnn.optim.Adam: contiguous float32 GPU parameters only")
+                if not p.is_cuda or p.dtype not in (torch.float32, torch.bfloat16) \
+                        or not p.is_contiguous():
+                    raise RuntimeError("ngnn.optim.Adam: contiguous float32 / bfloat16 GPU "
+                                       "parameters only")
+                if p.grad.dtype != p.dtype:
+                    raise RuntimeError("ngnn.optim.Adam: gradient dtype differs from the parameter")
                 if p.grad.is_sparse:
                     raise RuntimeError("ngnn.optim.Adam: dense gradients only")
             st0 = self.state[ps[0]]
@@ -46,8 +50,8 @@ class Adam(torch.optim.Optimizer):
                 for p in ps:
                     st = self.state[p]
                     st["step"] = step  # one device counter per group
-                    st["exp_avg"] = torch.zeros_like(p)
-                    st["exp_avg_sq"] = torch.zeros_like(p)
+                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32)
+                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
             step = self.state[ps[0]]["step"]
             ticket = self._tickets.get(step.data_ptr())
             if ticket is None:  # zero once; the kernel re-zeroes it after every use
@@ -60,8 +64,10 @@ class Adam(torch.optim.Optimizer):
             M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in ps])
             V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps])
             N = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
+            D = (ctypes.c_int32 * n)(*[_lib.BF16 if p.dtype == torch.bfloat16 else _lib.F32
+                                       for p in ps])
             b1, b2 = group["betas"]
-            _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, step.data_ptr(), ticket.data_ptr(),
+            _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, D, step.data_ptr(), ticket.data_ptr(),
                                           float(group["lr"]),
                                           float(b1), float(b2), float(group["eps"]),
                                           float(group["weight_decay"]),

@@ -256,4 +256,7 @@ def test_bf16_model_matches_fp32_oracle(module):
     assert all(p.grad.dtype == torch.bfloat16 for p in mine.parameters())
     xr = xb.detach().float().cpu().requires_grad_(True)
     want = ref(xr, b.edge_index.cpu())
-    torch.testing.assert_close(out.float().cpu(), want.detach(), rtol=1e-2, atol=1e-2)
+    # bf16 logits (and, through the per-conv GCN path, bf16 activations between
+    # layers): compare in norm, 1e-2 relative
+    err = (out.float().cpu() - want.detach()).norm() / want.detach().norm()
+    assert err < 1e-2, float(err)

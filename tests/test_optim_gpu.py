@@ -48,3 +48,31 @@ def test_graph_capturable():
         oref.step()
     torch.cuda.synchronize()
     torch.testing.assert_close(p, ref, rtol=2e-6, atol=2e-7)
+
+
+def test_bf16_params_match_rounded_fp32_adam():
+    """bf16 parameters (BASELINE config #3): the update runs in fp32 against
+    fp32 moments and is rounded to bf16 on store -- equal to torch's fp32 Adam
+    whose parameters are rounded to bf16 after every step (within one bf16
+    ulp)."""
+    from ngnn.optim import Adam
+    g = torch.Generator().manual_seed(5)
+    shapes = [(256, 100), (256,), (47, 256)]
+    base = [torch.randn(s, generator=g).to(DEV).to(torch.bfloat16) for s in shapes]
+    pb = [b.clone().requires_grad_(True) for b in base]
+    pf = [b.float().clone().requires_grad_(True) for b in base]
+    ob, of = Adam(pb, lr=1e-2), torch.optim.Adam(pf, lr=1e-2)
+    for it in range(4):
+        for a, c in zip(pb, pf):
+            gr = torch.randn(a.shape, generator=g).to(DEV).to(torch.bfloat16)
+            a.grad = gr.clone()
+            c.grad = gr.float()
+        ob.step()
+        of.step()
+        with torch.no_grad():
+            for c in pf:
+                c.copy_(c.to(torch.bfloat16).float())
+    for a, c in zip(pb, pf):
+        assert a.dtype == torch.bfloat16
+        torch.testing.assert_close(a.float(), c, rtol=8e-3, atol=1e-6)
+    assert ob.state[pb[0]]["exp_avg"].dtype == torch.float32
