@@ -78,8 +78,10 @@ def seed_cross_entropy(logits: torch.Tensor, y: torch.Tensor, batch_size: int,
     """Mean cross entropy of ``logits[:batch_size]`` against ``y[:batch_size]``."""
     if not logits.is_cuda:
         raise RuntimeError("ngnn.losses.seed_cross_entropy: GPU only (no CPU fallback)")
+    if logits.dtype == torch.bfloat16:  # bf16 models: the loss is taken in fp32
+        logits = logits.float()
     if logits.dim() != 2 or logits.dtype != torch.float32:
-        raise ValueError("logits must be a 2-D float32 tensor")
+        raise ValueError("logits must be a 2-D float32 (or bf16) tensor")
     if batch_size <= 0 or batch_size > logits.size(0) or y.numel() < batch_size:
         raise ValueError("batch_size out of range")
     return _SeedXent.apply(logits, y, batch_size, ignore_index)
