@@ -131,7 +131,8 @@ def main():
     from ngnn.loader import NeighborLoader, sample_block, synthetic_graph
 
     rank, world, local = init()
-    dev = torch.device("cuda", local)
+    # (one GPU per rank; modulo only matters when rehearsing N ranks on fewer GPUs)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     fanout = [int(v) for v in args.fanout.split(",")]
     layers = len(fanout)

@@ -29,8 +29,9 @@ def init(backend: str | None = None):
     """Initialise the default process group from torchrun's env (no-op at world 1)."""
     rank, world, local = env_world()
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # NGNN_DIST_BACKEND=gloo: rehearse N ranks on fewer GPUs
+            backend = os.environ.get("NGNN_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = {}
