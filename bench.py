@@ -121,6 +121,14 @@ def cpu_baseline(batch, args, layers):
                       f"{threads} threads, PyG 2.5.1 op sequence restated in oracle/pyg_ref.py"}
 
 
+def _allreduce_name(world: int) -> str:
+    """Which collective carries the gradient all-reduce (gloo only in rehearsals)."""
+    import torch.distributed as dist
+    if world <= 1 or not dist.is_initialized():
+        return "RCCL"
+    return "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+
+
 def main():
     args = parse()
     import torch.distributed as dist
@@ -278,7 +286,7 @@ def main():
                        "model": f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)",
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
-                       "parallelism": f"dp{world} (seed-sharded, RCCL grad all-reduce)"},
+                       "parallelism": f"dp{world} (seed-sharded, {_allreduce_name(world)} grad all-reduce)"},
             "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 4),
             "launch": "eager" if not graph else "hip-graph replay (step captured once)",
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
