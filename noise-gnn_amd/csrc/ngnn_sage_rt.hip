@@ -704,9 +704,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one m-tile, all of K
     const size_t lds_cap = 160 * 1024 - 1024;                          // minus the bias slice
     // widest supported tile count whose W_r fits
+    // NGNN_RT_MAXNTW caps the slice width (column tiles per wave) -- tuning experiments
+    static const int ntw_cap = getenv("NGNN_RT_MAXNTW") ? atoi(getenv("NGNN_RT_MAXNTW")) : 16;
     int ntw_max = 0;
     for (int c : {16, 8, 4, 3, 2})  // prefer_wl_lds: narrower slices whose W_r AND W_l fit
-        if (static_cast<size_t>(c) * frag_kb * ((prefer_wl_lds && wl_packed) ? 2 : 1) <= lds_cap) {
+        if (c <= ntw_cap &&
+            static_cast<size_t>(c) * frag_kb * ((prefer_wl_lds && wl_packed) ? 2 : 1) <= lds_cap) {
             ntw_max = c;
             break;
         }
