@@ -66,14 +66,16 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(span):
-    """HBM bytes per launch of the kernel behind `span` from the committed PMC
-    summary (tools/gpu_pmc.sh + tools/pmc_traffic.py: FETCH_SIZE x 2 on gfx950
-    plus WRITE_SIZE, separate passes), or (None, None)."""
+def pmc_traffic(span, workload, dtype):
+    """HBM bytes per launch of the kernel behind `span` ON THIS WORKLOAD AND
+    DTYPE from the committed PMC summary (tools/gpu_pmc.sh +
+    tools/pmc_traffic.py: FETCH_SIZE x 2 on gfx950 plus WRITE_SIZE, separate
+    passes; records keyed "span|workload|dtype"), or (None, None) when that
+    combination was never profiled -- never another workload's number."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            rec = json.load(f).get(span)
+            rec = json.load(f).get(f"{span}|{workload}|{dtype}")
     except (OSError, ValueError):
         return None, None
     if not rec:
@@ -92,33 +94,75 @@ def train_step(model, opt, reducer, b):
     return loss
 
 
-def cpu_baseline(batch, args, layers):
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads() -> int:
+    """Every CPU this process may run on: the affinity mask (the GPU box gives
+    each GPU's job a share of the host, OMP_NUM_THREADS = that share), capped
+    by os.cpu_count()."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
+
+
+def cpu_baseline(batches, args, layers):
     """The reference's CPU path: the PyG 2.5.1 op sequence restated in torch
-    (oracle/pyg_ref.py), one training step (fwd + bwd + Adam) on ONE sampled
-    block of the same workload, repeated for ~args.cpu_seconds."""
+    (oracle/pyg_ref.py), full training steps (fwd + bwd + Adam) over the
+    bench's own sampled blocks of the same workload (cycled), for about
+    args.cpu_seconds at every available thread, then a bounded 1-thread run
+    (all cores and 1 thread, CPU model named)."""
     from oracle import pyg_ref
-    torch.manual_seed(0)
-    threads = torch.get_num_threads()
     from ngnn.loader import DATASETS
     _, _, F_in, C, _ = DATASETS[args.dataset]
-    m = pyg_ref.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr)
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-    x, ei, y = batch.x.cpu(), batch.edge_index.cpu(), batch.y.cpu()
-    E = ei.shape[1]
-    pyg_ref.train_step(m, opt, x, ei, y, batch.batch_size)  # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        pyg_ref.train_step(m, opt, x, ei, y, batch.batch_size)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds or n >= 50:
-            break
-    return {"value": layers * E * n / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "ms_per_step": 1e3 * dt / n,
-            "sample": f"{n} training steps (fwd+bwd+Adam) on one {args.dataset}-[{args.fanout}] "
-                      f"bs={args.batch_size} block "
-                      f"(E={E}, N={batch.num_nodes}), torch {torch.__version__} CPU, "
-                      f"{threads} threads, PyG 2.5.1 op sequence restated in oracle/pyg_ref.py"}
+    host = [(b.x.cpu(), b.edge_index.cpu(), b.y.cpu(), b.batch_size) for b in batches]
+
+    def run(threads, seconds, max_steps):
+        torch.set_num_threads(threads)
+        torch.manual_seed(0)
+        m = pyg_ref.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        x, ei, y, bs = host[0]
+        pyg_ref.train_step(m, opt, x, ei, y, bs)  # warm
+        n, edges, t0 = 0, 0, time.perf_counter()
+        while True:
+            x, ei, y, bs = host[n % len(host)]
+            pyg_ref.train_step(m, opt, x, ei, y, bs)
+            n += 1
+            edges += layers * ei.shape[1]
+            dt = time.perf_counter() - t0
+            if dt >= seconds or n >= max_steps:
+                break
+        return edges / dt, 1e3 * dt / n, n
+
+    threads0 = torch.get_num_threads()
+    threads = _cpu_threads()
+    rate, ms, n = run(threads, args.cpu_seconds, 50)
+    rate1, ms1, n1 = run(1, max(args.cpu_seconds / 3, 1.0), 3)
+    torch.set_num_threads(threads0)
+    E = sum(ei.shape[1] for _, ei, _, _ in host[:n]) / min(n, len(host))
+    return {"value": rate, "unit": "edges/s", "cores": threads, "kind": "port",
+            "ms_per_step": ms, "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "single_thread": {"value": rate1, "unit": "edges/s", "ms_per_step": ms1, "steps": n1},
+            "sample": f"{n} training steps (fwd+bwd+Adam) over {min(n, len(host))} sampled "
+                      f"{args.dataset}-[{args.fanout}] bs={args.batch_size} blocks "
+                      f"(avg E={E:.0f}) at {threads} threads, then {n1} at 1 thread; "
+                      f"torch {torch.__version__} CPU; PyG 2.5.1 op sequence restated in "
+                      f"oracle/pyg_ref.py"}
 
 
 def _allreduce_name(world: int) -> str:
@@ -184,7 +228,7 @@ def main():
         gstep.capture(batches[0].x, batches[0].edge_index, batches[0].y)
 
         def run(b):
-            gstep(b.x, b.edge_index, b.y)
+            gstep(b.x, b.edge_index, b.y, b.batch_size)
     else:
         def run(b):
             train_step(model, opt, reducer, b)
@@ -227,6 +271,9 @@ def main():
     else:
         dt, edges = float(t[0]), float(t[1])
 
+    workload = f"{args.dataset.replace('ogbn-', '')}-[{args.fanout}]-bs{args.batch_size}"
+    if args.aggr != "mean":
+        workload += f"-{args.aggr}"
     # dominant kernel roofline from the live events of the timed region
     summ = timer.summary()
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
@@ -242,7 +289,7 @@ def main():
         else:
             roof = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(f_hbm, 4)}
-        traffic, traffic_src = pmc_traffic(name)
+        traffic, traffic_src = pmc_traffic(name, workload, args.dtype)
         roof.update({
             "traffic": traffic, "traffic_src": traffic_src, "launches": n,
             "avg_us": round(1e3 * ms / n, 2),
@@ -267,7 +314,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(batches[0], args, layers)
+        cpu = cpu_baseline(batches, args, layers)
 
     if rank == 0:
         E_avg = sum(b.edge_index.shape[1] for b in batches) / nb
@@ -282,7 +329,7 @@ def main():
             "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic (seeded Chung-Lu graph with {args.dataset} sizes; random features)",
-            "config": {"workload": f"{args.dataset.replace('ogbn-', '')}-[{args.fanout}]-bs{args.batch_size}",
+            "config": {"workload": workload,
                        "model": f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)",
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 8
+#define NGNN_ABI_VERSION 9
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -47,6 +47,10 @@ extern "C" {
 #define NGNN_REDUCE_SUM 0  /* GCNConv aggr='add'                             */
 #define NGNN_REDUCE_MEAN 1 /* SAGEConv default aggr='mean' (sage.py:16-19)   */
 #define NGNN_REDUCE_MAX 2  /* SAGEConv(aggr='max'): build extension          */
+/* math-mode flag OR-ed into ngnn_sage_fwd_raw's `reduce`: the root term
+ * x . W_r^T on exact fp32 MFMA (v_mfma_f32_16x16x4_f32, a fmaf chain) instead
+ * of the default fp32-accurate 3 x bf16 split. */
+#define NGNN_MATH_EXACT_F32 0x100
 
 /* dtypes */
 #define NGNN_F32 0
@@ -226,24 +230,22 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   int64_t ldm, float xscale, void *stream);
 
 /* Same layer with the RAW PyG Linear weights (W_l, W_r: [Fo, K] row-major,
- * row stride ldw) through the row-tile kernel: W_r (and W_l when both fit)
- * go straight from these rows into LDS, no ngnn_pack_weight launch; a W_l
- * too large to share the LDS is packed into ws (one launch,
- * ngnn_sage_fwd_raw_workspace_bytes) and streamed from L2.  Returns
- * NGNN_E_SHAPE, launching nothing, for shapes outside that kernel's envelope
- * (K % 4 != 0, unaligned rows, W_r slice too large for LDS, buffers >= 2 GiB):
- * the caller then packs and calls ngnn_sage_fwd.  x_dev (nullable): a device
- * word holding x's address, read at run time instead of x (a HIP-graph slot
- * whose batch stays where the loader put it; 16-B aligned, row stride ldx,
- * rows < *n_rows_dev).  n_edge_rows / n_edge_rows_dev (device int, nullable,
- * overrides): rows at or past it have no in-edges (NeighborLoader numbers
- * the rows that receive edges first).  With NGNN_SPLIT=1 in the environment
- * (opt-in; the fused kernel is the default), F_out > 128 and agg_out given,
- * the layer runs as three launches: the aggregate of the rows below the
- * bound (into agg_out, edgeless rows zeroed), z = agg . W_l^T on them (into
- * ws), and a gather-free dense kernel over every row (one wave per SIMD, W_r
- * in LDS, epilogue software-pipelined under the MFMAs) adding z to the edge
- * rows.  Pass n_edge_rows = n_rows, NULL when unknown.
+ * row stride ldw) through the row-tile kernel (ngnn_sage_rt.hip, the model's
+ * path).  Root term x . W_r^T: by default fp32-accurate 3 x bf16 split MFMA
+ * (each operand split v = v1 + v2 + v3 in bf16, the six products down to
+ * 2^-18 of the leading one accumulated in fp32; error below the fp32
+ * rounding of the reference GEMM); `reduce | NGNN_MATH_EXACT_F32` runs it on
+ * exact fp32 MFMA.  The W_r image is built in LDS from these rows in the
+ * kernel prologue (no pack launch); W_l (fp32, neighbour term of rows with
+ * in-edges) shares the LDS when it fits, else it is packed into ws (one
+ * launch) and streamed from L2.  Returns NGNN_E_SHAPE, launching nothing,
+ * for shapes outside that kernel's envelope (K % 4 != 0, unaligned rows, W_r
+ * slice too large for LDS, buffers >= 2 GiB): the caller then packs and calls
+ * ngnn_sage_fwd.  x_dev (nullable): a device word holding x's address, read
+ * at run time instead of x (a HIP-graph slot whose batch stays where the
+ * loader put it; 16-B aligned, row stride ldx, rows < *n_rows_dev).
+ * n_edge_rows / n_edge_rows_dev: accepted and unused (row hints of a retired
+ * split path).
  * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes. */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,

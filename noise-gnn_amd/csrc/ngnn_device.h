@@ -127,26 +127,14 @@ inline Dropout make_dropout(float p, uint64_t seed) {
 }
 
 // Row-tile forward (ngnn_sage_rt.hip): returns 1 (launch status in *rc) when
-// it takes the call, 0 when the shape is outside its envelope.
+// it takes the call, 0 when the shape is outside its envelope.  exact: root
+// term on fp32 MFMA (else the 3 x bf16 split when the weights are raw rows).
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, int64_t tile_end, const int32_t *tile_end_dev,
-                     bool prefer_wl_lds, const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
                      int *rc, int64_t ldw = 0, void *wl_ws = nullptr, size_t wl_ws_bytes = 0,
-                     const float *const *x_dev = nullptr);
-
-// Dense (edge-free rows) forward, ngnn_sage_dense.hip: rows [row_begin (or
-// *row_begin_dev), min(n_rows, *n_rows_dev)); optional addend z (rows <
-// min(z_rows, *z_rows_dev) add z[r] before the epilogue).  Returns 1 (status in *rc) when
-// it takes the call, 0 (nothing launched) outside its envelope.
-int sage_fwd_dense(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
-                   int64_t row_begin, const int32_t *row_begin_dev, int64_t n_rows,
-                   const int32_t *n_rows_dev, const float *wr, int64_t ldw, const float *bias,
-                   int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
-                   const uint64_t *seed_dev, hipStream_t st, int *rc, const float *z = nullptr,
-                   int64_t ldz = 0, int64_t z_rows = 0, const int32_t *z_rows_dev = nullptr,
-                   bool round_begin16 = false);
+                     const float *const *x_dev = nullptr, bool exact = true);
 
 }  // namespace ngnn

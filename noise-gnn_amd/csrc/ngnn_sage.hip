@@ -479,7 +479,7 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
     if (!xmask) {  // default path: the row-tile kernel (ngnn_sage_rt.hip)
         int rc = NGNN_OK;
-        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, n_rows, nullptr, false, rowptr, col, reduce, wl_packed,
+        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl_packed,
                              wr_packed, bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out,
                              ld_agg, as_stream(stream), &rc))
             return rc;
@@ -495,8 +495,7 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     for (int64_t c0 = 0; c0 < Fo; c0 += 512) {
         const int64_t Fo_c = std::min<int64_t>(512, Fo - c0);
         const int64_t toff = (c0 / 16) * KG * 64;  // float4 offset of the slice's first n-tile
-        static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
-        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, seed_dev, dbg};
+        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, seed_dev, 0};
         float *of = out + c0;
         const int vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(of, 16);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));

@@ -25,6 +25,20 @@
 //     fp32 sequence of ngnn_seg_agg_fwd, so the aggregate is bit-identical),
 //     neighbour indices preloaded 16 per row and broadcast by ds_bpermute.
 //
+// Root-term arithmetic (X3, the default): fp32-accurate 3 x bf16 split MFMA.
+// x and W_r are each split v = v1 + v2 + v3 (bf16, round to nearest: |v -
+// v1 - v2 - v3| <= 2^-27 |v|) and x.W_r^T is accumulated in fp32 from the six
+// products whose magnitude reaches 2^-18 of the leading term (v1w1, v1w2,
+// v2w1, v2w2, v1w3, v3w1; each bf16 x bf16 product is exact in fp32; the
+// three dropped terms are <= 2^-26 relative) on v_mfma_f32_16x16x32_bf16:
+// 6 bf16 MFMAs at 16 cycles = 96 cycles per 32-deep k-chunk vs 8 fp32
+// 16x16x4 MFMAs at 32 = 256.  The error is below the fp32 rounding of the
+// reference's own GEMM.  A tail of K % 32 <= 12 columns
+// runs on exact fp32 MFMA steps (cheaper than a padded bf16 chunk).  With
+// NGNN_MATH_EXACT_F32 OR-ed into `reduce`, every product is exact-fp32
+// v_mfma_f32_16x16x4_f32 (a fmaf chain).  The neighbour term (edge tiles)
+// stays on exact fp32 MFMA with W_l fp32.
+//
 // Bytes per launch: 4*(N*K + E*K + E + N + 1 + N*F_out) (x, gathered rows,
 // col, rowptr, out) + the optional saved aggregate; flops 2*N*K*F_out +
 // 2*N_edge_rows*K*F_out.
@@ -40,9 +54,27 @@ constexpr int RT_ROWS = 16;  // rows per wave tile (one MFMA n-tile)
 constexpr int RT_KC = 8;     // k-groups of 16 per chunk (128 columns of K)
 // waves per workgroup: 2 per SIMD (<= 256 VGPRs: accumulators, the current
 // and the prefetched x fragments, two W fragment sets)
-// PRE (aggregate precomputed by k_rt_agg, no gather code): fewer live
-// registers, so narrow outputs run 4 waves per SIMD to hide the x stream
-constexpr int rt_waves(int ntw, bool pre) { return (pre && ntw <= 3) ? 16 : 8; }
+constexpr int RT_WAVES = 8;
+constexpr int X3_TAIL_MAX = 3;  // fp32 tail steps (K % 32 <= 12); more: a padded bf16 chunk
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// v = p1 + p2 + p3 in bf16 (round to nearest even); an infinite v gives
+// (v, 0, 0) instead of the NaN residual inf - inf, a NaN gives NaNs
+__device__ __forceinline__ void split3(v4f a, v4f b, bf16x8 &p1, bf16x8 &p2, bf16x8 &p3) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = j < 4 ? a[j] : b[j - 4];
+        const __bf16 h = static_cast<__bf16>(v);
+        const float fh = static_cast<float>(h);
+        const float r = (fh == v) ? 0.0f : v - fh;
+        const __bf16 m = static_cast<__bf16>(r);
+        const float r2 = r - static_cast<float>(m);
+        p1[j] = h;
+        p2[j] = m;
+        p3[j] = static_cast<__bf16>(r2);
+    }
+}
 
 struct RtArgs {
     const float *x;
@@ -67,8 +99,10 @@ struct RtArgs {
     uint32_t x_bytes, out_bytes, agg_bytes;  // buffer-resource ranges (all < 4 GiB)
     const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
     const float *const *x_dev;                // non-null: x's address read at run time (graph slot)
-    int dbg;  // ablation bits (NGNN_SAGE_ABLATE, profiling only): 1 no MFMA, 2 no stores, 4 no x loads,
-             // 8 no epilogue, 16 no weight prologue
+    // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
+    // when kpad), then T4 exact-fp32 steps of 4 columns
+    int C, T4, kpad;
+    const float *wr_raw;  // X3: raw W_r rows of this slice [Fo, K], stride ldw
 };
 
 // -1 (all ones) when a < b, else 0: a lane mask held in a VGPR, built without
@@ -95,11 +129,68 @@ constexpr int kOOB = 0x7ffffff0;  // byte offset past every range: load 0 / drop
 // Columns past K (which read the next row) are masked by mask_x at the point
 // of USE, not here: masking right after the loads would make the compiler
 // wait for a prefetch the moment it is issued.
+// X3 layout instead: lane (rl, q) holds x[r][k0 + 32 c + 8 q + 4 h .. +3] in
+// xf[2 c + h] (the B fragment of 16x16x32 bf16: 8 consecutive k per lane);
+// 32-chunks past the root term's C read nothing (offset past the range).
+template <bool X3>
 __device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], const RtArgs &a, i32x4 xr, int r, int k0,
                                        int q) {
-    const int voff = (r * static_cast<int>(a.ldx) + k0 + 4 * q) * 4;
+    if (X3) {
+        const int voff = (r * static_cast<int>(a.ldx) + k0 + 8 * q) * 4;
+        const int ncc = a.C - k0 / 32;  // chunks of this group inside the root term
 #pragma unroll
-    for (int g = 0; g < RT_KC; ++g) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+        for (int g = 0; g < RT_KC; ++g)
+            xf[g] = buf_load4(xr, (g >> 1) < ncc ? voff + 4 * (32 * (g >> 1) + 4 * (g & 1)) : kOOB, 0, 0);
+    } else {
+        const int voff = (r * static_cast<int>(a.ldx) + k0 + 4 * q) * 4;
+#pragma unroll
+        for (int g = 0; g < RT_KC; ++g) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+    }
+}
+
+// X3 fp32 tail: lane (rl, q) holds x[r][32 C + 4 s + q] (the B operand of
+// 16x16x4 f32 step s)
+__device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &a, i32x4 xr, int r,
+                                        int q) {
+    const int voff = (r * static_cast<int>(a.ldx) + 32 * a.C + q) * 4;
+#pragma unroll
+    for (int s = 0; s < X3_TAIL_MAX; ++s) xt[s] = buf_load1(xr, s < a.T4 ? voff + 16 * s : kOOB, 0, 0);
+}
+
+// root term of one 128-column group in the X3 layout: per 32-chunk, split x
+// into three bf16 parts and issue the six products per output tile (W parts
+// from the LDS image [3][C][NTW][64] bf16x8, piece stride pst)
+template <int NTW>
+__device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[RT_KC],
+                                              const bf16x8 *__restrict__ sw3, int pst, int cc0,
+                                              int ncc, int mask_last, int kq8, int lane) {
+#pragma unroll
+    for (int c = 0; c < RT_KC / 2; ++c) {
+        if (c < ncc) {
+            v4f lo = xf[2 * c], hi = xf[2 * c + 1];
+            if (mask_last && c == ncc - 1) {  // padded last chunk: columns past K read the next row
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    lo[i] = i < kq8 ? lo[i] : 0.0f;
+                    hi[i] = 4 + i < kq8 ? hi[i] : 0.0f;
+                }
+            }
+            bf16x8 x1, x2, x3;
+            split3(lo, hi, x1, x2, x3);
+            const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
+#pragma unroll
+            for (int m = 0; m < NTW; ++m) {
+                const bf16x8 w1 = w[m * 64], w2 = w[pst + m * 64], w3 = w[2 * pst + m * 64];
+                v4f t = acc[m];
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3, x1, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x3, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x2, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x1, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x2, t, 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, t, 0, 0, 0);
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ void mask_x(v4f (&xc)[RT_KC], const v4f (&xf)[RT_KC], const RtArgs &a,
@@ -312,9 +403,7 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
                 v[jj] = y;
             }
         }
-        if (a.dbg & 2) {
-            if (v[0] == 12345.f) buf_store1(v[1], orsrc, obase, 0, 0);  // keep the math alive
-        } else if (vec) {
+        if (vec) {
             buf_store4(v, orsrc, obase + 4 * f, 0, 0);
         } else {
 #pragma unroll
@@ -327,21 +416,63 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
 // WLM: W_l source -- 0 streamed from L2 (packed fragments), 1 in LDS.  (A
 // raw-layout L2 stream that saves the pack launch measured slower: 0.373 vs
 // 0.355 ms/step on products, the extra address VALU spills the L0 kernel.)
-template <int NTW, int RED, int WLM, bool PRE>
-__global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
+// X3: root term on the 3 x bf16 split (LDS image of W_r split in the
+// prologue from the raw rows); otherwise exact fp32 MFMA.
+template <int NTW, int RED, int WLM, bool X3>
+__global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     constexpr bool WL_LDS = WLM == 1;
-    constexpr int RT_WAVES = rt_waves(NTW, PRE);
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
-    const int nfr = NTW * a.KG * 64;  // fragments per weight matrix (NTW tiles, zero padded)
-    v4f *swr = lds;
-    v4f *swl = lds + nfr;
-    float *sbias = reinterpret_cast<float *>(lds + (WL_LDS ? 2 : 1) * nfr);
+    const int nfr = NTW * a.KG * 64;  // fragments per fp32 weight matrix (NTW tiles, zero padded)
+    // X3 image: [3][C][NTW][64] bf16x8 (16 B each) + fp32 tail [T4][NTW][64]
+    const int pst = a.C * NTW * 64;                        // bf16x8 per piece
+    const int x3_v4f = X3 ? 3 * pst + (a.T4 * NTW * 64) / 4 : 0;
+    bf16x8 *sw3 = reinterpret_cast<bf16x8 *>(lds);
+    float *swt = reinterpret_cast<float *>(lds + 3 * pst);
+    v4f *swr = lds;                                        // fp32 W_r image (X3 == false)
+    v4f *swl = lds + (X3 ? x3_v4f : nfr);
+    float *sbias = reinterpret_cast<float *>(swl + (WL_LDS ? nfr : 0));
     const int have_l = a.wl != nullptr;
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     {
-        // weights -> LDS by LDS-DMA, 1 KiB (one n-tile x k-group fragment)
-        // per wave-instruction, all in flight at once; padding tiles zeroed
-        const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-        const int nch = (a.dbg & 16) ? 0 : a.NT * a.KG;  // valid 1-KiB chunks per matrix
+        const int nch = a.NT * a.KG;  // valid 1-KiB fp32 fragments per matrix
+        if (X3) {
+            // W_r split into three bf16 parts, one lane fragment (8 consecutive
+            // k of one output row) per slot; rows past F_out / columns past K
+            // are zero
+            const int nslot = pst;
+            for (int sl = threadIdx.x; sl < nslot; sl += RT_WAVES * 64) {
+                const int l = sl & 63, mt = (sl >> 6) % NTW, cc = (sl >> 6) / NTW;
+                const int n = mt * 16 + (l & 15), k = 32 * cc + 8 * (l >> 4);
+                v4f lo{0.f, 0.f, 0.f, 0.f}, hi{0.f, 0.f, 0.f, 0.f};
+                if (n < a.Fo) {
+                    const float *src = a.wr_raw + static_cast<int64_t>(n) * a.ldw + k;
+                    if (k + 8 <= a.K) {
+                        lo = *reinterpret_cast<const v4f *>(src);
+                        hi = *reinterpret_cast<const v4f *>(src + 4);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            lo[j] = k + j < a.K ? src[j] : 0.0f;
+                            hi[j] = k + 4 + j < a.K ? src[4 + j] : 0.0f;
+                        }
+                    }
+                }
+                bf16x8 p1, p2, p3;
+                split3(lo, hi, p1, p2, p3);
+                sw3[sl] = p1;
+                sw3[pst + sl] = p2;
+                sw3[2 * pst + sl] = p3;
+            }
+            const int ntail = a.T4 * NTW * 64;
+            for (int sl = threadIdx.x; sl < ntail; sl += RT_WAVES * 64) {
+                const int l = sl & 63, mt = (sl >> 6) % NTW, st = (sl >> 6) / NTW;
+                const int n = mt * 16 + (l & 15), k = 32 * a.C + 4 * st + (l >> 4);
+                swt[sl] = (n < a.Fo && k < a.K) ? a.wr_raw[static_cast<int64_t>(n) * a.ldw + k] : 0.0f;
+            }
+        }
+        // fp32 images by LDS-DMA, 1 KiB (one n-tile x k-group fragment) per
+        // wave-instruction, all in flight at once; padding tiles zeroed.
+        // X3: only W_l (when it lives in LDS); otherwise W_r and W_l.
         for (int c = wv; c < nch; c += RT_WAVES) {
             const int m = c / a.KG, kg = c - m * a.KG;  // [NT][KG] -> LDS [KG][NTW]
             const int d = (kg * NTW + m) * 64;
@@ -349,15 +480,16 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
             const int64_t so = a.ldw ? raw_frag_off(m, kg, ln, a.ldw, a.Fo, a.K, &ok) / 4
                                      : static_cast<int64_t>(c) * 64 + ln;  // in v4f units
             // (raw rows are 16-B aligned: K % 4 == 0 and ldw % 4 == 0)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(a.wr + so),
-                (__attribute__((address_space(3))) void *)(swr + d), 16, 0, 0);
+            if (!X3)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.wr + so),
+                    (__attribute__((address_space(3))) void *)(swr + d), 16, 0, 0);
             if (WL_LDS && have_l)
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void *)(a.wl + so),
                     (__attribute__((address_space(3))) void *)(swl + d), 16, 0, 0);
         }
-        if (a.ldw) {
+        if (a.ldw && (!X3 || (WL_LDS && have_l))) {
             // raw weights: lanes outside F_out x K loaded row 0 / column 0 --
             // zero those slots once this wave's LDS-DMAs have landed
             __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
@@ -368,7 +500,7 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
                 bool ok;
                 (void)raw_frag_off(m, kg, ln, a.ldw, a.Fo, a.K, &ok);
                 if (!ok) {
-                    swr[d + ln] = z0;
+                    if (!X3) swr[d + ln] = z0;
                     if (WL_LDS && have_l) swl[d + ln] = z0;
                 }
             }
@@ -377,7 +509,7 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
         const int npad = (NTW - a.NT) * 64;  // padded tiles of every k-group
         for (int i = threadIdx.x; i < a.KG * npad; i += RT_WAVES * 64) {
             const int kg = i / npad, j = i - kg * npad;
-            swr[kg * NTW * 64 + a.NT * 64 + j] = z;
+            if (!X3) swr[kg * NTW * 64 + a.NT * 64 + j] = z;
             if (WL_LDS) swl[kg * NTW * 64 + a.NT * 64 + j] = z;
         }
         if (WL_LDS && !have_l)
@@ -387,30 +519,31 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     }
     __syncthreads();
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wv, lane = ln;
     const int q = lane >> 4, rl = lane & 15;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
-    int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
-    if (a.tile_end_dev) n_tiles = min(n_tiles, (*a.tile_end_dev + RT_ROWS - 1) / RT_ROWS);
-    const int nchunk = (a.KG + RT_KC - 1) / RT_KC;
+    const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
+    // 128-column groups of the root term: X3 covers 32 C columns (at least
+    // one group, which also carries the next tile's prefetch); fp32 all of K
+    const int nchunk = X3 ? max(1, (a.C + 3) / 4) : (a.KG + RT_KC - 1) / RT_KC;
+    const int nchunk_l = (a.KG + RT_KC - 1) / RT_KC;  // neighbour term (fp32 layout)
     const int tstride = gridDim.x * RT_WAVES;
 
     // tile k of this wave: k = 0 -> w0; later rounds in reverse wave order,
     // so the partial last round lands on the waves that did NOT start with a
     // (heavier) edge tile -- NeighborLoader puts the rows with in-edges
-    // first (ablation bit 64 restores the plain order; -0.3..0.4 % step time)
+    // first (measured: -0.3..0.4 % step time)
     const int w0 = blockIdx.x + gridDim.x * wave;
-    const bool rev = (a.dbg & 64) == 0;
-    auto tile_of = [&](int k) { return (k == 0 || !rev) ? w0 + k * tstride : k * tstride + (tstride - 1 - w0); };
+    auto tile_of = [&](int k) { return k == 0 ? w0 : k * tstride + (tstride - 1 - w0); };
     int kt = 0;
     int t = w0;
-    if ((a.dbg & 32) && wave >= RT_WAVES / 2) __builtin_amdgcn_s_sleep(100);  // experiment: stagger SIMD partners
     // next tile's chunk-0 x fragments and row bounds, loaded one tile ahead,
     // unconditionally (a tile past the end re-reads tile 0: valid, unused)
     v4f xn[RT_KC];
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
+    float xtn[X3_TAIL_MAX] = {0.f, 0.f, 0.f};
     int nbeg = 0, nend = 0;
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
     // x: the address given at launch, or (graph replay of a changing batch)
@@ -421,7 +554,8 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
     const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
     auto prefetch = [&](int tn) {
         const int rn = (tn < n_tiles ? tn : 0) * RT_ROWS + rl;
-        if (!(a.dbg & 4)) load_x(xn, a, xr, rn, 0, q);
+        load_x<X3>(xn, a, xr, rn, 0, q);
+        if (X3) load_xt(xtn, a, xr, rn, q);
         if (have_l) {
             const int mr = lt_mask(rn, n_rows);
             const int rr = rn & mr;
@@ -431,6 +565,8 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
         }
     };
     const bool vec = a.vec_out && (a.Fo == a.NT * 16);
+    // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
+    const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
     prefetch(t);
     for (; t < n_tiles; t = tile_of(++kt)) {
         const int r = t * RT_ROWS + rl;
@@ -439,51 +575,60 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
         v4f acc[NTW];
 #pragma unroll
         for (int m = 0; m < NTW; ++m) acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
+        float xt[X3_TAIL_MAX];
+#pragma unroll
+        for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) xt[s2] = xtn[s2];
 
         // ---- root term: x[r] . W_r^T, chunk by chunk; chunk c+1 (or, in the
         // last chunk, the next tile's chunk 0 and row bounds) loads behind
         // chunk c's MFMAs
         for (int c = 0; c < nchunk; ++c) {
             v4f xc[RT_KC];
-            mask_x(xc, xn, a, c * RT_KC * 16, q);
+            if (X3) {
+#pragma unroll
+                for (int g = 0; g < RT_KC; ++g) xc[g] = xn[g];
+            } else {
+                mask_x(xc, xn, a, c * RT_KC * 16, q);
+            }
             const int nkg = min(RT_KC, a.KG - c * RT_KC);
             if (c + 1 < nchunk) {
-                if (!(a.dbg & 4)) load_x(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
-            } else {
+                load_x<X3>(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
+            } else if (maxdeg == 0) {
                 prefetch(tile_of(kt + 1));  // next tile: a whole tile of MFMAs to land
             }
-            if (!(a.dbg & 1)) mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
+            if (X3) {
+                const int ncc = min(4, a.C - 4 * c);
+                mfma_group_x3<NTW>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
+            } else {
+                mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
+            }
+        }
+        if (X3) {
+            // fp32 tail steps (K % 32 columns past the bf16 chunks)
+#pragma unroll
+            for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) {
+                if (s2 < a.T4) {
+                    const float xv = __int_as_float(__float_as_int(xt[s2]) &
+                                                    lt_mask(32 * a.C + 4 * s2 + q, a.K));
+#pragma unroll
+                    for (int m = 0; m < NTW; ++m)
+                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(swt[(s2 * NTW + m) * 64 + lane], xv,
+                                                                      acc[m], 0, 0, 0);
+                }
+            }
         }
 
         // ---- neighbour term (tiles with in-edges only)
-        if (PRE && maxdeg > 0) {
-            // aggregate rows written by k_rt_agg (rows with in-edges only;
-            // others masked to 0, as the gather's empty-row result)
+        if (maxdeg > 0) {
             const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
-            const int mrow = lt_mask(0, deg);
-            for (int c = 0; c < nchunk; ++c) {
-                const int k0 = c * RT_KC * 16;
-                const int nkg = min(RT_KC, a.KG - c * RT_KC);
-                const int kq = a.K - k0 - 4 * q;
-                const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
-                v4f ag[RT_KC];
-#pragma unroll
-                for (int g = 0; g < RT_KC; ++g) ag[g] = buf_load4(ar, aoff + 64 * g, 0, 0);
-#pragma unroll
-                for (int g = 0; g < RT_KC; ++g) ag[g] = and_mask(ag[g], mrow & lt_mask(16 * g, kq));
-                if constexpr (WL_LDS)
-                    mfma_chunk_rt<NTW, true>(acc, ag, swl, a.KG, c * RT_KC, nkg, a.NT, lane);
-                else
-                    mfma_chunk_rt<NTW, false>(acc, ag, a.wl, a.KG, c * RT_KC, nkg, a.NT, lane);
-            }
-        }
-        if (!PRE && maxdeg > 0) {
-            const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
-            for (int c = 0; c < nchunk; ++c) {
+            for (int c = 0; c < nchunk_l; ++c) {
                 const int k0 = c * RT_KC * 16;
                 const int nkg = min(RT_KC, a.KG - c * RT_KC);
                 v4f ag[RT_KC];
                 gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q);
+                // edge tiles prefetch the next tile only now: its x fragments
+                // are not live across the gather (register budget)
+                if (c == nchunk_l - 1) prefetch(tile_of(kt + 1));
                 if (a.agg_out) {
                     const int kq = a.K - k0 - 4 * q;
                     const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
@@ -499,94 +644,10 @@ __global__ __launch_bounds__(rt_waves(NTW, PRE) * 64) void k_sage_rt(RtArgs a) {
         }
 
         // ---- epilogue (bias, relu, dropout and the stores)
-        if (!(a.dbg & 8)) {
-            if (a.epi.drop.thresh)
-                epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q);
-            else
-                epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q);
-        }
-    }
-}
-
-// ---- aggregate pre-pass for the PRE kernels: agg[r] = reduce over the CSR
-// row r of x, for rows r < n_rows (and < *n_rows_dev) WITH in-edges only
-// (edgeless rows are never written; the layer kernel masks them to 0).  LPR
-// lanes per row, 16-B loads, RT_AGG_UNR neighbour rows in flight per group,
-// per column in edge order from the identity then / max(deg, 1): the fp32
-// sequence of ngnn_seg_agg_fwd, bit-identical.  Rows are interleaved over
-// the (resident) grid's groups, so a NeighborLoader block's edge rows (a
-// prefix) spread over every CU.
-constexpr int RT_AGG_UNR = 8;
-template <int RED, int LPR>
-__global__ __launch_bounds__(256) void k_rt_agg(const float *__restrict__ x_arg, int64_t ldx, int K,
-                                                const int32_t *__restrict__ rowptr,
-                                                const int32_t *__restrict__ col, int n_rows,
-                                                const int32_t *__restrict__ n_rows_dev,
-                                                float *__restrict__ agg, int64_t ld_agg,
-                                                const float *const *x_dev, int zero_empty) {
-    const float *__restrict__ x = x_dev ? *x_dev : x_arg;
-    constexpr int GPW = 256 / LPR;
-    const int lane = threadIdx.x % LPR;
-    int nr = n_rows;
-    if (n_rows_dev) nr = min(nr, *n_rows_dev);
-    const int ngroups = gridDim.x * GPW;
-    const int gid = blockIdx.x * GPW + threadIdx.x / LPR;
-    const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
-    // the group's rows gid + j ngroups, LPR of them per round: lane j loads
-    // row j's bounds (one load round for LPR rows, so edgeless rows cost no
-    // latency chain), then the group walks the rows that have in-edges
-    for (int r0 = gid; r0 < nr; r0 += LPR * ngroups) {
-        const int my = r0 + lane * ngroups;
-        int mb = 0, me = 0;
-        if (my < nr) {
-            mb = rowptr[my];
-            me = rowptr[my + 1];
-        }
-        for (int j = 0; j < LPR; ++j) {
-        const int beg = __shfl(mb, j, LPR), end = __shfl(me, j, LPR);
-        const int row = r0 + j * ngroups;
-        if (beg == end) {
-            // edgeless row: left unwritten, or zeroed when the caller needs
-            // every row (the dense split's agg . W_l^T pass)
-            if (zero_empty && row < nr)
-                for (int f = 4 * lane; f < K; f += 4 * LPR)
-                    *reinterpret_cast<v4f *>(agg + static_cast<int64_t>(row) * ld_agg + f) =
-                        v4f{0.f, 0.f, 0.f, 0.f};
-            continue;
-        }
-        for (int f0 = 0; f0 < K; f0 += 4 * LPR) {
-            const int f = f0 + 4 * lane;
-            const bool act = f < K;
-            const int fc = act ? f : 0;
-            v4f acc{ident, ident, ident, ident};
-            for (int eb = beg; eb < end; eb += LPR) {
-                const int n = min(LPR, end - eb);
-                const int myc = lane < n ? col[eb + lane] : 0;
-                // RT_AGG_UNR rows in flight per batch; a short last batch
-                // re-reads its last row (cached) and skips the extra terms
-                for (int k = 0; k < n; k += RT_AGG_UNR) {
-                    v4f v[RT_AGG_UNR];
-#pragma unroll
-                    for (int u = 0; u < RT_AGG_UNR; ++u) {
-                        const int64_t c = __shfl(myc, min(k + u, n - 1), LPR);
-                        v[u] = *reinterpret_cast<const v4f *>(x + c * ldx + fc);
-                    }
-#pragma unroll
-                    for (int u = 0; u < RT_AGG_UNR; ++u)
-                        if (k + u < n)
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) acc[i] = red_op<RED>(acc[i], v[u][i]);
-                }
-            }
-            if (!act) continue;
-            if (RED == NGNN_REDUCE_MEAN) {
-                const float cnt = static_cast<float>(end - beg);  // deg >= 1 here
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[i] = acc[i] / cnt;
-            }
-            *reinterpret_cast<v4f *>(agg + static_cast<int64_t>(row) * ld_agg + f) = acc;
-        }
-        }
+        if (a.epi.drop.thresh)
+            epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q);
+        else
+            epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q);
     }
 }
 
@@ -605,29 +666,29 @@ int num_cus() {
     return g_num_cus[dev];
 }
 
-template <int NTW, int RED, int WLM, bool PRE>
+template <int NTW, int RED, int WLM, bool X3>
 int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
-    auto fn = k_sage_rt<NTW, RED, WLM, PRE>;
+    auto fn = k_sage_rt<NTW, RED, WLM, X3>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    constexpr int W = rt_waves(NTW, PRE);
     const int grid = static_cast<int>(
-        std::max<int64_t>(1, std::min<int64_t>(num_cus(), ceil_div(n_tiles, W))));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(W * 64), lds_bytes, st, a);
+        std::max<int64_t>(1, std::min<int64_t>(num_cus(), ceil_div(n_tiles, RT_WAVES))));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(RT_WAVES * 64), lds_bytes, st, a);
     return launch_status();
 }
 
-template <int NTW, bool PRE>
-int dispatch_red(const RtArgs &a, int reduce, bool wl_lds, int n_tiles, size_t lds, hipStream_t st) {
-    if (PRE)  // the reduction happened in k_rt_agg: one instantiation serves all
-        return wl_lds ? launch_rt<NTW, NGNN_REDUCE_SUM, 1, true>(a, n_tiles, lds, st)
-                      : launch_rt<NTW, NGNN_REDUCE_SUM, 0, true>(a, n_tiles, lds, st);
+template <int NTW>
+int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, size_t lds,
+                hipStream_t st) {
     auto by_red = [&](auto red_c) {
         constexpr int RED = decltype(red_c)::value;
+        if (x3)
+            return wl_lds ? launch_rt<NTW, RED, 1, true>(a, n_tiles, lds, st)
+                          : launch_rt<NTW, RED, 0, true>(a, n_tiles, lds, st);
         return wl_lds ? launch_rt<NTW, RED, 1, false>(a, n_tiles, lds, st)
                       : launch_rt<NTW, RED, 0, false>(a, n_tiles, lds, st);
     };
@@ -636,61 +697,23 @@ int dispatch_red(const RtArgs &a, int reduce, bool wl_lds, int n_tiles, size_t l
     return by_red(std::integral_constant<int, NGNN_REDUCE_MAX>{});
 }
 
-template <int NTW>
-int dispatch_pre(const RtArgs &a, int reduce, bool wl_lds, bool pre, int n_tiles, size_t lds,
-                 hipStream_t st) {
-    return pre ? dispatch_red<NTW, true>(a, reduce, wl_lds, n_tiles, lds, st)
-               : dispatch_red<NTW, false>(a, reduce, wl_lds, n_tiles, lds, st);
-}
-
-// aggregate of rows [0, min(n_rows, *n_rows_dev)) into agg (edgeless rows
-// zeroed), the fp32 sequence of ngnn_seg_agg_fwd
-int launch_rt_agg(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
-                  const int32_t *rowptr, const int32_t *col, int64_t n_rows,
-                  const int32_t *n_rows_dev, int reduce, float *agg, int64_t ld_agg,
-                  hipStream_t st) {
-    const int64_t k4 = ceil_div(K, 4);
-    const int lpr = k4 <= 8 ? 8 : k4 <= 16 ? 16 : k4 <= 32 ? 32 : 64;
-    const unsigned grid = static_cast<unsigned>(
-        std::max<int64_t>(1, std::min<int64_t>(8 * num_cus(), ceil_div(n_rows, 256 / lpr))));
-    auto go = [&](auto red_c, auto lpr_c) {
-        hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>), dim3(grid),
-                           dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
-                           static_cast<int>(n_rows), n_rows_dev, agg, ld_agg, x_dev, 1);
-    };
-    auto by_lpr = [&](auto red_c) {
-        switch (lpr) {
-            case 8: go(red_c, std::integral_constant<int, 8>{}); break;
-            case 16: go(red_c, std::integral_constant<int, 16>{}); break;
-            case 32: go(red_c, std::integral_constant<int, 32>{}); break;
-            default: go(red_c, std::integral_constant<int, 64>{}); break;
-        }
-    };
-    if (reduce == NGNN_REDUCE_MEAN) by_lpr(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
-    else if (reduce == NGNN_REDUCE_SUM) by_lpr(std::integral_constant<int, NGNN_REDUCE_SUM>{});
-    else by_lpr(std::integral_constant<int, NGNN_REDUCE_MAX>{});
-    return launch_status();
-}
-
 }  // namespace
 
 // Returns 1 and stores the launch status in *rc when the row-tile kernel
 // takes this call, 0 when the shape is outside its envelope (the caller then
 // runs the 64-row kernel).  Envelope: no input mask, K % 4 == 0 with 16-B
-// aligned rows, packed W_r of one column slice fitting in LDS.  Outputs wider
-// than one slice (<= 256 columns, fewer when K is large) run as one launch
-// per slice; the packed weights are n-tile major, so a slice is a contiguous
-// sub-array.
+// aligned rows, the W_r image of one column slice fitting in LDS.  Outputs
+// wider than one slice (<= 256 columns, fewer when K is large) run as one
+// launch per slice; the packed weights are n-tile major, so a slice is a
+// contiguous sub-array.  exact: fp32 MFMA for the root term (else the 3 x
+// bf16 split, raw weights only).
 int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
-                     const int32_t *n_rows_dev, int64_t tile_end, const int32_t *tile_end_dev,
-                     bool prefer_wl_lds, const int32_t *rowptr, const int32_t *col,
+                     const int32_t *n_rows_dev, const int32_t *rowptr, const int32_t *col,
                      int reduce, const void *wl_packed, const void *wr_packed, const float *bias,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
-                     const float *const *x_dev) {
-    static const bool off = getenv("NGNN_NO_ROWTILE") != nullptr;
-    if (off) return 0;
+                     const float *const *x_dev, bool exact) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -701,65 +724,39 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     if (n_rows * ldx * 4 > lim || n_rows * ldo * 4 > lim || (agg_out && n_rows * ld_agg * 4 > lim))
         return 0;
     const int KG = static_cast<int>(ceil_div(K, 16));
-    const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one m-tile, all of K
-    const size_t lds_cap = 160 * 1024 - 1024;                          // minus the bias slice
-    // widest supported tile count whose W_r fits
-    // NGNN_RT_MAXNTW caps the slice width (column tiles per wave) -- tuning experiments
-    static const int ntw_cap = getenv("NGNN_RT_MAXNTW") ? atoi(getenv("NGNN_RT_MAXNTW")) : 16;
+    // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
+    // columns become one zero-padded bf16 chunk)
+    const bool x3 = !exact && ldw > 0;
+    int C = static_cast<int>(K / 32), T4 = static_cast<int>(ceil_div(K % 32, 4)), kpad = 0;
+    if (T4 > X3_TAIL_MAX) {
+        C += 1;
+        T4 = 0;
+        kpad = 1;
+    }
+    const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one fp32 m-tile, all of K
+    // one m-tile of the root image: X3 3 parts x C chunks x 1 KiB + the tail
+    const size_t root_kb = x3 ? (static_cast<size_t>(3 * C) * 64 * 16 + static_cast<size_t>(T4) * 64 * 4)
+                              : frag_kb;
+    const size_t lds_cap = 160 * 1024 - 1024;  // minus the bias slice
     int ntw_max = 0;
-    for (int c : {16, 8, 4, 3, 2})  // prefer_wl_lds: narrower slices whose W_r AND W_l fit
-        if (c <= ntw_cap &&
-            static_cast<size_t>(c) * frag_kb * ((prefer_wl_lds && wl_packed) ? 2 : 1) <= lds_cap) {
+    for (int c : {16, 8, 4, 3, 2})
+        if (static_cast<size_t>(c) * root_kb <= lds_cap) {
             ntw_max = c;
             break;
         }
     if (ntw_max == 0) return 0;
     const int64_t slice = 16 * static_cast<int64_t>(ntw_max);
     const Dropout drop = make_dropout(p_drop, seed);
-    // PRE (NGNN_RT_PRE=1): the aggregate (saved for the backward anyway) is
-    // computed by a separate pass and the layer kernel reads it densely -- no
-    // gather registers, 4 waves per SIMD for narrow outputs.  Measured on the
-    // products block it loses to the in-kernel gather at both layers (the
-    // separate pass re-reads what the gather overlaps: L0 129 + 18 us vs
-    // 141 us, L1 60 + 35 us vs 87 us), so the gather stays the default.
-    const bool use_pre = getenv("NGNN_RT_PRE") != nullptr;  // read per call (tests toggle it)
-    const bool pre = use_pre && agg_out != nullptr && wl_packed != nullptr && rowptr != nullptr;
-    if (pre) {
-        const int64_t k4 = ceil_div(K, 4);
-        const int lpr = k4 <= 8 ? 8 : k4 <= 16 ? 16 : k4 <= 32 ? 32 : 64;
-        const unsigned grid = static_cast<unsigned>(
-            std::max<int64_t>(1, std::min<int64_t>(8 * num_cus(), ceil_div(n_rows, 256 / lpr))));
-        auto go = [&](auto red_c, auto lpr_c) {
-            hipLaunchKernelGGL((k_rt_agg<decltype(red_c)::value, decltype(lpr_c)::value>),
-                               dim3(grid), dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr,
-                               col, static_cast<int>(n_rows), n_rows_dev, agg_out, ld_agg, x_dev, 0);
-        };
-        auto by_lpr = [&](auto red_c) {
-            switch (lpr) {
-                case 8: go(red_c, std::integral_constant<int, 8>{}); break;
-                case 16: go(red_c, std::integral_constant<int, 16>{}); break;
-                case 32: go(red_c, std::integral_constant<int, 32>{}); break;
-                default: go(red_c, std::integral_constant<int, 64>{}); break;
-            }
-        };
-        if (reduce == NGNN_REDUCE_MEAN) by_lpr(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
-        else if (reduce == NGNN_REDUCE_SUM) by_lpr(std::integral_constant<int, NGNN_REDUCE_SUM>{});
-        else by_lpr(std::integral_constant<int, NGNN_REDUCE_MAX>{});
-        const int arc = launch_status();
-        if (arc) {
-            *rc = arc;
-            return 1;
-        }
-    }
     for (int64_t c0 = 0; c0 < Fo; c0 += slice) {
         const int64_t Fo_c = std::min<int64_t>(slice, Fo - c0);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));
         const int NTW = NT <= 2 ? 2 : NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 8 ? 8 : 16;
+        const size_t rbytes = static_cast<size_t>(NTW) * root_kb;
         const size_t wbytes = static_cast<size_t>(NTW) * frag_kb;
         const size_t bbytes = static_cast<size_t>(NTW) * 16 * sizeof(float);
-        // W_l shares the LDS when both fit; otherwise its fragments stream from L2
-        const bool wl_lds = wl_packed == nullptr || 2 * wbytes + bbytes <= lds_cap + 1024;
-        const size_t lds = (wl_lds ? 2 : 1) * wbytes + bbytes;
+        // W_l (fp32) shares the LDS when both fit; otherwise its fragments stream from L2
+        const bool wl_lds = wl_packed == nullptr || rbytes + wbytes + bbytes <= lds_cap + 1024;
+        const size_t lds = rbytes + (wl_lds ? wbytes : 0) + bbytes;
         const int64_t toff = (c0 / 16) * KG * 64;
         RtArgs a;
         a.x = x;
@@ -768,7 +765,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.KG = KG;
         a.n_rows = static_cast<int>(n_rows);
         a.n_rows_dev = n_rows_dev;
-        a.tile_end_dev = tile_end_dev;
         a.rowptr = rowptr;
         a.col = col;
         // a slice's weights: packed fragments are n-tile major (contiguous
@@ -776,7 +772,11 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         const int64_t woff = ldw ? c0 * ldw / 4 : toff;
         a.wl = wl_packed ? static_cast<const v4f *>(wl_packed) + woff : nullptr;
         a.wr = static_cast<const v4f *>(wr_packed) + woff;
+        a.wr_raw = ldw ? static_cast<const float *>(wr_packed) + c0 * ldw : nullptr;
         a.ldw = ldw;
+        a.C = C;
+        a.T4 = T4;
+        a.kpad = kpad;
         if (ldw && wl_packed && !wl_lds) {
             // raw W_l that must stream from L2: pack it once (all slices) into
             // the caller's workspace -- fragment-ordered 1-KiB wave loads
@@ -799,23 +799,21 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.out = out + c0;
         a.ldo = ldo;
         a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(out + c0, 16);
-        a.agg_out = (pre || c0 == 0) ? agg_out : nullptr;  // PRE: every slice reads it
+        a.agg_out = c0 == 0 ? agg_out : nullptr;
         a.ld_agg = ld_agg;
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
-        static const int dbg = getenv("NGNN_SAGE_ABLATE") ? atoi(getenv("NGNN_SAGE_ABLATE")) : 0;
-        a.dbg = dbg;
         a.seed_dev = seed_dev;
         a.x_dev = x_dev;
         a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
         a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
         a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
-        const int n_tiles = static_cast<int>(ceil_div(std::min(tile_end, n_rows), RT_ROWS));
+        const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
-            case 2: *rc = dispatch_pre<2>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
-            case 3: *rc = dispatch_pre<3>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
-            case 4: *rc = dispatch_pre<4>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
-            case 8: *rc = dispatch_pre<8>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
-            default: *rc = dispatch_pre<16>(a, reduce, wl_lds, pre, n_tiles, lds, st); break;
+            case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
+            case 3: *rc = dispatch_rt<3>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
+            case 4: *rc = dispatch_rt<4>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
+            case 8: *rc = dispatch_rt<8>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
+            default: *rc = dispatch_rt<16>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
         }
         if (*rc) return 1;
     }
@@ -826,15 +824,9 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
 
 using namespace ngnn;
 
-// padded row stride of the split path's agg . W_l^T rows
-static int64_t split_ldz(int64_t Fo) { return ceil_div(Fo, 16) * 16; }
-
 extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows) {
-    // a packed W_l (fused path, when it cannot sit in LDS), or the split
-    // path's agg . W_l^T rows
-    const size_t pack = ngnn_pack_weight_bytes(Fo, K);
-    const size_t z = static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * split_ldz(Fo) * sizeof(float);
-    return std::max(pack, z);
+    (void)n_rows;  // a packed W_l (when it cannot sit in LDS)
+    return ngnn_pack_weight_bytes(Fo, K);
 }
 
 extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx,
@@ -846,6 +838,10 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
                                  int64_t ldo, int relu, float p_drop, uint64_t seed,
                                  const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
                                  size_t ws_bytes, void *stream) {
+    (void)n_edge_rows;  // (row hints of the retired split path; kept for the ABI)
+    (void)n_edge_rows_dev;
+    const bool exact = (reduce & NGNN_MATH_EXACT_F32) != 0;
+    reduce &= ~NGNN_MATH_EXACT_F32;
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
     NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || !wr, NGNN_E_ARG);
     NGNN_RETURN_IF(wl && !rowptr, NGNN_E_ARG);
@@ -857,68 +853,9 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     NGNN_RETURN_IF((!x && !x_dev) || !out, NGNN_E_ARG);
     hipStream_t st = as_stream(stream);
     int rc = NGNN_OK;
-    // rows >= the edge-row bound have no in-edges.  No neighbour term: the
-    // dense kernel takes every row.  Wide outputs (MFMA-bound) with a known
-    // bound: three launches -- the aggregate of the edge rows (saved for the
-    // backward anyway), z = agg . W_l^T on those rows (dense kernel, no
-    // epilogue), then the dense kernel over every row with z added to the
-    // edge rows.  Otherwise the fused gather kernel takes the layer.
-    int64_t split = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
-    const int32_t *split_dev = n_edge_rows_dev;
-    // opt-in (NGNN_SPLIT=1): measured on products [15,10] L0 the three
-    // launches (agg 16 k rows + z + dense 153 k rows) tie the fused kernel
-    // (159 vs 155 us): the one-wave-per-SIMD dense kernel reaches ~60 % of the
-    // fp32 MFMA rate, not enough to pay for the separate aggregate pass
-    const char *split_env = getenv("NGNN_SPLIT");  // read per call (tests toggle it)
-    const int split_mode = split_env ? atoi(split_env) : 0;
-    if (!wl) {
-        if (sage_fwd_dense(x, x_dev, ldx, K, 0, nullptr, n_rows, n_rows_dev, wr, ldw, bias, Fo, out,
-                           ldo, relu, p_drop, seed, seed_dev, st, &rc))
-            return rc;
-    } else if (split_mode == 1 && Fo > 128 && (split < n_rows || split_dev) && agg_out &&
-               ws_bytes >= ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) && aligned(ws, 16) &&
-               ld_agg % 4 == 0 && aligned(agg_out, 16)) {
-        const int64_t zrows = split_dev ? n_rows : split;  // host bound of the z rows
-        float *z = static_cast<float *>(ws);
-        const int64_t ldz = split_ldz(Fo);
-        const int32_t *zdev = split_dev;
-        // the dense kernel's envelope check launches nothing when it refuses,
-        // so probe the cheap pass shapes first: z pass and main pass share it
-        int rz = NGNN_OK;
-        if (zrows > 0 || split_dev) {
-            rc = launch_rt_agg(x, x_dev, ldx, K, rowptr, col, zrows, zdev, reduce, agg_out, ld_agg, st);
-            if (rc) return rc;
-            if (!sage_fwd_dense(agg_out, nullptr, ld_agg, K, 0, nullptr, zrows, zdev, wl, ldw,
-                                nullptr, Fo, z, ldz, 0, 0.0f, 0, nullptr, st, &rz))
-                goto fused;  // (the agg pass already ran: harmless, the fused kernel rewrites it)
-            if (rz) return rz;
-        }
-        if (sage_fwd_dense(x, x_dev, ldx, K, 0, nullptr, n_rows, n_rows_dev, wr, ldw, bias, Fo, out,
-                           ldo, relu, p_drop, seed, seed_dev, st, &rc, z, ldz, zrows, zdev))
-            return rc;
-    }
-fused:
-    if (wl && split_mode == 2 && (split < n_rows || split_dev)) {
-        // split mode 2: the fused gather kernel on the tiles below the split
-        // (output slices narrow enough for W_r and W_l to share the LDS),
-        // the dense kernel from the next 16-row boundary up
-        const int64_t s16 = std::min(n_rows, ceil_div(split, 16) * 16);
-        int rd = NGNN_OK;
-        if (sage_fwd_dense(x, x_dev, ldx, K, split_dev ? 0 : s16, split_dev, n_rows, n_rows_dev, wr,
-                           ldw, bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, st, &rd, nullptr, 0,
-                           0, nullptr, /*round_begin16=*/true)) {
-            if (rd) return rd;
-            if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, split_dev ? n_rows : s16, split_dev,
-                                  true, rowptr, col, reduce, wl, wr, bias, Fo, out, ldo, relu, p_drop,
-                                  seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws, ws_bytes, x_dev))
-                return NGNN_E_SHAPE;
-            return rc;
-        }
-    }
-    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, n_rows, nullptr, false, rowptr, col, reduce,
-                          wl, wr,
-                          bias, Fo, out, ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc,
-                          ldw, ws, ws_bytes, x_dev))
+    if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
+                          ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
+                          ws_bytes, x_dev, exact))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

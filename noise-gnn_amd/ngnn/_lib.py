@@ -13,11 +13,12 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
+MATH_EXACT_F32 = 0x100  # OR-ed into ngnn_sage_fwd_raw's reduce (include/ngnn.h)
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one

@@ -43,20 +43,44 @@ def init(backend: str | None = None):
     return rank, world, local
 
 
+def shard_len(n: int, world: int) -> int:
+    """Seeds per rank: ceil(n / world) on EVERY rank (see shard_seeds)."""
+    return -(-int(n) // max(int(world), 1))
+
+
 def shard_seeds(nodes: torch.Tensor, rank: int, world: int, epoch: int, seed: int,
                 shuffle: bool = True) -> torch.Tensor:
-    """Same permutation on every rank (shared seed), strided slice per rank."""
+    """Same permutation on every rank (shared seed), strided slice per rank.
+
+    Every rank gets exactly ``shard_len(n, world)`` seeds: when ``world`` does
+    not divide ``n`` the permutation is padded cyclically with its own head
+    (as torch's DistributedSampler does), so all ranks run the same number of
+    batches -- and therefore the same number of gradient all-reduces -- per
+    epoch.  Unequal shards would leave the ranks with more batches waiting in
+    a collective the others never join."""
     if shuffle:
         g = torch.Generator(device=nodes.device).manual_seed(seed + 1000 + epoch)
         nodes = nodes[torch.randperm(nodes.numel(), device=nodes.device, generator=g)]
+    n = nodes.numel()
+    pad = shard_len(n, world) * world - n
+    if pad and n:
+        reps = -(-pad // n)
+        nodes = torch.cat([nodes] + [nodes] * reps)[:n + pad]
     return nodes[rank::world]
 
 
 class GradAllReduce:
     """Average gradients across ranks with ONE flat bucket all-reduce.
 
-    The bucket is allocated once; ``__call__`` packs every parameter's grad,
-    runs ``all_reduce(SUM)`` and unpacks ``bucket / world``.
+    The bucket is allocated once and every fp32 parameter gets a view of it
+    (``p._ngnn_grad_out``).  The fused SAGE backward writes its weight
+    gradients straight into those views whenever ``p.grad`` is None at
+    backward time (``optimizer.zero_grad(set_to_none=True)``, as the graph
+    step does), and autograd adopts the view as ``p.grad``: the bucket then
+    IS the gradients and ``pack`` / ``unpack`` copy nothing -- one
+    ``all_reduce(SUM)`` and one scale by 1/world per step.  Gradients that
+    live elsewhere (other modules, accumulation into existing ``.grad``) are
+    copied in and out as before.
     """
 
     def __init__(self, params, group=None):
@@ -64,21 +88,31 @@ class GradAllReduce:
         self.group = group
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
-        self.bucket = torch.empty(n, dtype=torch.float32, device=dev)
+        self.bucket = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            v = self.bucket[off:off + p.numel()].view(p.shape)
+            self.views.append(v)
+            if p.dtype == torch.float32:
+                p._ngnn_grad_out = v
+            off += p.numel()
 
     def active(self) -> bool:
         return dist.is_initialized() and dist.get_world_size(self.group) > 1
 
+    @staticmethod
+    def _aliased(p, v) -> bool:
+        return p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+
     def pack(self):
-        """grads -> bucket (stream-ordered copies; capturable in a HIP graph)."""
-        off = 0
-        for p in self.params:
-            n = p.numel()
+        """grads -> bucket (stream-ordered copies, none for gradients that are
+        already bucket views; capturable in a HIP graph)."""
+        for p, v in zip(self.params, self.views):
             if p.grad is None:
-                self.bucket[off:off + n].zero_()
-            else:
-                self.bucket[off:off + n].copy_(p.grad.reshape(-1))
-            off += n
+                v.zero_()
+            elif not self._aliased(p, v):
+                v.copy_(p.grad)
 
     def allreduce(self):
         """The one collective: SUM over ranks (RCCL over xGMI with nccl)."""
@@ -88,13 +122,11 @@ class GradAllReduce:
         """bucket / world -> grads (capturable)."""
         world = dist.get_world_size(self.group)
         self.bucket.div_(world)
-        off = 0
-        for p in self.params:
-            n = p.numel()
+        for p, v in zip(self.params, self.views):
             if p.grad is None:
-                p.grad = torch.empty_like(p)
-            p.grad.copy_(self.bucket[off:off + n].view_as(p))
-            off += n
+                p.grad = v if p.dtype == v.dtype else v.to(p.dtype)
+            elif not self._aliased(p, v):
+                p.grad.copy_(v)
 
     def __call__(self):
         if not self.active():

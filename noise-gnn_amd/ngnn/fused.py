@@ -37,6 +37,35 @@ from .block import Block
 
 _ws: dict = {}
 
+# Root-term arithmetic of the fused layer forward (include/ngnn.h,
+# NGNN_MATH_EXACT_F32).  False (default): fp32-accurate 3 x bf16 split MFMA --
+# error below the fp32 rounding of the reference's own GEMM (DESIGN.md
+# section 3).  True: exact fp32 MFMA (a fmaf chain), like torch.backends'
+# allow_tf32 = False.
+_exact_f32 = False
+
+
+def set_exact_f32(flag: bool) -> None:
+    global _exact_f32
+    _exact_f32 = bool(flag)
+
+
+class exact_f32:
+    """Context manager: exact fp32 MFMA for the layer forward inside it."""
+
+    def __init__(self, flag: bool = True):
+        self.flag = flag
+
+    def __enter__(self):
+        global _exact_f32
+        self.prev, _exact_f32 = _exact_f32, self.flag
+        return self
+
+    def __exit__(self, *exc):
+        global _exact_f32
+        _exact_f32 = self.prev
+        return False
+
 
 def _workspace(dev: torch.device, name: str, nbytes: int, zero: bool = False) -> torch.Tensor:
     """Per-device scratch buffers, grown on demand and reused across calls
@@ -119,7 +148,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         rc = lib.ngnn_sage_fwd_raw(
             _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, n_edge,
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
-            _lib.REDUCE[reduce], _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
+            _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
+            _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
@@ -136,7 +166,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
 
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, *params):
+    def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
+                *params):
         L = len(params) // 3
         acts, aggs = [x], []
         h = x
@@ -151,6 +182,7 @@ class _SAGEStack(torch.autograd.Function):
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
+        ctx.gouts = gouts  # per parameter: a buffer the weight gradient is written into, or None
         ctx.save_for_backward(*acts, *aggs, *params)
         return h
 
@@ -206,7 +238,12 @@ class _SAGEStack(torch.autograd.Function):
             hidden = i != L - 1
             ymask = y_out if hidden else None
             yscale = (1.0 / (1.0 - p)) if (hidden and p > 0.0) else 1.0
-            dwl, dbl, dwr = torch.empty_like(wl), torch.empty_like(bl), torch.empty_like(wr)
+            # gradient buffers: the data-parallel bucket's views when the caller
+            # registered them (a fresh view each time, so autograd adopts it as
+            # .grad instead of copying it), else new tensors
+            dwl, dbl, dwr = (
+                (g.view(q.shape) if g is not None else torch.empty_like(q))
+                for g, q in zip(ctx.gouts[3 * i:3 * i + 3], (wl, bl, wr)))
             wsb = lib.ngnn_sage_wgrad_workspace_bytes(Fo, K)
             ws = _workspace(dev, "wgrad", wsb)
             with _timing.span("sage_wgrad", 0, 0):  # row bound is device-side: no host count
@@ -284,7 +321,7 @@ class _SAGEStack(torch.autograd.Function):
                 _lib.check(rc, "ngnn_sage_dgrad_scatter")
             dy = dh
         dx = dy if (need_dx and L > 0) else None
-        return (dx, None, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, None, *grads)
 
 
 _IO_DTYPES = (torch.float32, torch.bfloat16)
@@ -330,11 +367,17 @@ def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor
     for conv in model.convs:
         params += [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
     out_dtype = x.dtype
+    # weight gradients straight into registered bucket views (ngnn.distributed.GradAllReduce)
+    # when autograd will adopt them: fp32 parameters whose .grad is unset
+    gouts = tuple(getattr(q, "_ngnn_grad_out", None)
+                  if (q.grad is None and q.dtype == torch.float32 and q.requires_grad) else None
+                  for q in params)
     if out_dtype != torch.float32 or any(q.dtype != torch.float32 for q in params):
         x = x.float()
         params = [q.float() for q in params]
+        gouts = (None,) * len(params)
     p = model.dropout if model.training else 0.0
     aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
-    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, *params)
+    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, *params)
     return out if out_dtype == torch.float32 else out.to(out_dtype)

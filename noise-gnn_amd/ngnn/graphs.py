@@ -71,26 +71,38 @@ class GraphedTrainStep:
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
         self.loss = None
+        self.out = None
         self._split_reduce = False
         self._one = None
         self.zero_copy = True
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
-             zero_copy: bool = False) -> None:
+             zero_copy: bool = False, batch_size: int | None = None) -> None:
         """zero_copy: store x's address for the captured kernels instead of
         copying its rows into the slot (replays); the copy serves eager use
-        of the slot (warm-up, tests)."""
+        of the slot (warm-up, tests).  batch_size: the block's seed count
+        (default: the captured B).  A short block (an epoch's last batch when
+        drop_last is off) gets ignore_index (-100) labels on rows
+        [batch_size, B), so the captured loss -- F.cross_entropy(out[:B],
+        y[:B]) with the default ignore_index -- is exactly the reference's
+        F.cross_entropy(out[:batch_size], y[:batch_size]) (pipeline.py:155-158):
+        mean over the real seeds, zero gradient on the other rows."""
         N, E = x.size(0), edge_index.size(1)
         if N + 1 > self.n_cap or E > self.e_cap:
             raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
+        bs = self.B if batch_size is None else int(batch_size)
+        if not 0 < bs <= min(self.B, N):
+            raise ValueError(f"batch_size {bs} outside (0, min(B={self.B}, N={N})]")
         if x.dtype != torch.float32:  # bf16 batches: the captured kernels read fp32 rows
             x = x.float()
         if x.stride(1) != 1 or x.stride(0) != self.x.stride(0) or x.data_ptr() % 16:
             x = x.clone(memory_format=torch.contiguous_format)
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
-        y = y[:self.B].contiguous()
+        y = y[:bs].contiguous()
+        if bs < self.B:  # rows [bs, B) carry no loss (F.cross_entropy's ignore_index)
+            y = torch.cat([y, y.new_full((self.B - bs,), -100)])
         # one launch: x rows, edges + padding self-loops, labels, device row count
         _lib.check(_lib.load().ngnn_slot_load(
             _lib.ptr(x), x.stride(0), N, x.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
@@ -114,6 +126,7 @@ class GraphedTrainStep:
 
     def _fwd_bwd(self):
         out = self.model(self.x, self.ei)
+        self.out = out  # the captured step's logits (static: rewritten by every replay)
         loss = self.loss_fn(out, self.y, self.B)
         # a persistent d(loss) = 1 instead of backward()'s ones_like fill launch
         if self._one is None or self._one.shape != loss.shape:
@@ -187,10 +200,11 @@ class GraphedTrainStep:
                         else:
                             t.zero_()  # state born in the warm-up: a fresh optimizer's zeros
 
-    def __call__(self, x, edge_index, y):
+    def __call__(self, x, edge_index, y, batch_size: int | None = None):
         """Load one batch into the slot and replay the captured step; returns
-        the (device) loss tensor of this step."""
-        self.load(x, edge_index, y, zero_copy=self.zero_copy)
+        the (device) loss tensor of this step.  batch_size: the block's seed
+        count when it is short of the captured B (see load)."""
+        self.load(x, edge_index, y, zero_copy=self.zero_copy, batch_size=batch_size)
         self.g_fb.replay()
         if self._split_reduce:
             self.reducer.allreduce()

@@ -26,6 +26,7 @@ Amazon-Computers / CitationFull-Cora and a power-law
 from __future__ import annotations
 
 import dataclasses
+import weakref
 
 import torch
 
@@ -49,6 +50,10 @@ class Graph:
     y: torch.Tensor        # int64 [N]
     train_idx: torch.Tensor
     num_classes: int
+    # further node-level tensors ([N, ...]) every batch carries gathered by
+    # n_id, as PyG's NeighborLoader does for each node attribute of `data`
+    # (the reference reads batch.yhn, pipeline.py:72,116,157)
+    node_attrs: dict = dataclasses.field(default_factory=dict)
 
     @property
     def num_nodes(self) -> int:
@@ -59,21 +64,69 @@ class Graph:
         return self.col.numel()
 
 
-@dataclasses.dataclass
 class Batch:
-    x: torch.Tensor
-    y: torch.Tensor
-    edge_index: torch.Tensor
-    n_id: torch.Tensor
-    batch_size: int
+    """One NeighborLoader mini-batch: ``x``, ``y``, ``edge_index``, ``n_id``,
+    ``batch_size`` and every further node attribute of the graph (``yhn``
+    ...) gathered by ``n_id`` -- the fields pipeline.py:110-118,152-160 read."""
+
+    def __init__(self, x, y, edge_index, n_id, batch_size, **node_attrs):
+        self.x, self.y, self.edge_index, self.n_id = x, y, edge_index, n_id
+        self.batch_size = int(batch_size)
+        self.node_attrs = dict(node_attrs)
+
+    def __getattr__(self, name):
+        attrs = self.__dict__.get("node_attrs")
+        if attrs is not None and name in attrs:
+            return attrs[name]
+        raise AttributeError(f"Batch has no attribute {name!r}")
 
     @property
     def num_nodes(self) -> int:
         return self.n_id.numel()
 
     def to(self, device):
-        return Batch(self.x.to(device), self.y.to(device), self.edge_index.to(device),
-                     self.n_id.to(device), self.batch_size)
+        mv = lambda t: None if t is None else t.to(device)  # noqa: E731
+        return Batch(mv(self.x), mv(self.y), mv(self.edge_index), mv(self.n_id), self.batch_size,
+                     **{k: mv(v) for k, v in self.node_attrs.items()})
+
+
+def graph_from_data(data, device=None, train_idx=None, num_classes: int | None = None) -> Graph:
+    """Adapter from a PyG-``Data``-like object (the ``data`` the reference
+    hands ``NeighborLoader``, pipeline.py:75-83): ``x`` [N, F], ``y`` [N] or
+    [N, 1] (OGB), ``edge_index`` [2, E] (row 0 = source, row 1 = target) and
+    any further node-level tensors (``yhn`` from flip_label, pipeline.py:72,
+    masks ...).  Builds the in-neighbour CSC the device sampler walks (each
+    node's sources in edge order, PyG's ``source_to_target`` flow) and moves
+    everything to ``device`` once; the feature table stays resident in HBM.
+    """
+    ei = data.edge_index
+    x = data.x
+    dev = torch.device(device) if device is not None else (x.device if x.is_cuda else torch.device("cuda"))
+    N = int(getattr(data, "num_nodes", None) or x.size(0))
+    src, dst = ei[0].to(dev, torch.int64), ei[1].to(dev, torch.int64)
+    order = torch.argsort(dst, stable=True)
+    counts = torch.bincount(dst, minlength=N)
+    rowptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    col = src[order].to(torch.int32)
+    y = data.y.to(dev).reshape(N, -1)[:, 0].to(torch.int64).contiguous() \
+        if getattr(data, "y", None) is not None else torch.zeros(N, dtype=torch.int64, device=dev)
+    if train_idx is None:
+        train_idx = getattr(data, "train_idx", None)
+        if train_idx is None and getattr(data, "train_mask", None) is not None:
+            train_idx = data.train_mask.nonzero().view(-1)
+        if train_idx is None:
+            train_idx = torch.arange(N)
+    skip = {"x", "y", "edge_index", "edge_attr", "train_idx"}
+    attrs = {}
+    items = data.items() if hasattr(data, "items") else vars(data).items()
+    for k, v in items:
+        if k in skip or not torch.is_tensor(v) or v.dim() == 0 or v.size(0) != N:
+            continue
+        attrs[k] = v.to(dev)
+    if num_classes is None:
+        num_classes = int(getattr(data, "num_classes", 0) or (int(y.max()) + 1 if N else 0))
+    return Graph(rowptr, col, x.to(dev).contiguous(), y, train_idx.to(dev), num_classes, attrs)
 
 
 def _gen(device, seed):
@@ -221,7 +274,28 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
         "ngnn_sample_block_finish")
     # built here: ids are in range and targets non-decreasing -> no probe needed
     hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active)
-    return Batch(x, y, edge_index, n_id, B)
+    # further node attributes (batch.yhn ...): one device gather each, on this stream
+    extra = {k: v.index_select(0, n_id) for k, v in graph.node_attrs.items()}
+    return Batch(x, y, edge_index, n_id, B, **extra)
+
+
+_graphs_of_data: "weakref.WeakKeyDictionary | dict" = {}
+
+
+def _graph_of(data) -> Graph:
+    """graph_from_data once per data object (the reference builds a train and
+    a subgraph loader over the same data, pipeline.py:75-92)."""
+    key = id(data)
+    hit = _graphs_of_data.get(key)
+    if hit is not None and hit[0]() is data:
+        return hit[1]
+    g = graph_from_data(data)
+    try:
+        ref = weakref.ref(data)
+    except TypeError:
+        ref = (lambda d: (lambda: d))(data)
+    _graphs_of_data[key] = (ref, g)
+    return g
 
 
 class NeighborLoader:
@@ -234,9 +308,11 @@ class NeighborLoader:
     parallelism: every rank draws the same permutation and takes its slice.
     """
 
-    def __init__(self, graph: Graph, input_nodes=None, num_neighbors=(15, 10), batch_size=1024,
+    def __init__(self, graph, input_nodes=None, num_neighbors=(15, 10), batch_size=1024,
                  shuffle=False, seed: int = 0, rank: int = 0, world_size: int = 1,
                  drop_last: bool = False, **_ignored):
+        if not isinstance(graph, Graph):  # the reference's `data` (pipeline.py:75-92)
+            graph = _graph_of(graph)
         self.graph = graph
         dev = graph.rowptr.device
         if input_nodes is None:
@@ -250,14 +326,16 @@ class NeighborLoader:
         self.epoch = 0
 
     def _seeds(self):
-        nodes = self.input_nodes
-        if self.shuffle:
-            g = _gen(nodes.device, self.seed + 1000 + self.epoch)
-            nodes = nodes[torch.randperm(nodes.numel(), device=nodes.device, generator=g)]
-        return nodes[self.rank::self.world_size]
+        # every rank gets the same number of seeds (the permutation is padded
+        # cyclically when world_size does not divide it), so every rank runs
+        # the same number of steps and gradient all-reduces per epoch
+        from .distributed import shard_seeds
+        return shard_seeds(self.input_nodes, self.rank, self.world_size, self.epoch, self.seed,
+                           shuffle=self.shuffle)
 
     def __len__(self):
-        n = (self.input_nodes.numel() - self.rank + self.world_size - 1) // self.world_size
+        from .distributed import shard_len
+        n = shard_len(self.input_nodes.numel(), self.world_size)
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
@@ -279,7 +357,7 @@ class NeighborLoader:
                                    seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size
                                    + self.rank)
             main.wait_stream(side)
-            for t in (blk.x, blk.y, blk.edge_index, blk.n_id):
+            for t in (blk.x, blk.y, blk.edge_index, blk.n_id, *blk.node_attrs.values()):
                 if t is not None:
                     t.record_stream(main)  # consumed on the main stream
             yield blk

@@ -81,11 +81,72 @@ def test_gloo_world2_sharding_and_grad_allreduce():
 
 
 def test_shard_seeds_single_process():
-    from ngnn.distributed import shard_seeds
+    from ngnn.distributed import shard_len, shard_seeds
     nodes = torch.arange(10)
     a = shard_seeds(nodes, 0, 3, epoch=0, seed=1)
     b = shard_seeds(nodes, 1, 3, epoch=0, seed=1)
     c = shard_seeds(nodes, 2, 3, epoch=0, seed=1)
-    assert torch.equal(torch.cat([a, b, c]).sort().values, nodes)
+    # equal shards (10 seeds over 3 ranks: padded cyclically to 12), covering every seed
+    assert a.numel() == b.numel() == c.numel() == shard_len(10, 3) == 4
+    assert torch.equal(torch.cat([a, b, c]).unique(), nodes)
+    assert torch.equal(shard_seeds(nodes, 0, 1, epoch=0, seed=1).sort().values, nodes)
     assert not torch.equal(shard_seeds(nodes, 0, 1, epoch=0, seed=1),
                            shard_seeds(nodes, 0, 1, epoch=1, seed=1))
+
+
+def _loader_worker(rank, world, port, q, n_seeds, bs):
+    """Every rank iterates its NeighborLoader shard's batch count and joins one
+    all-reduce per batch (the data-parallel step's collective), then a barrier:
+    unequal batch counts would leave some ranks in an all-reduce the others
+    never join (caught by the timeouts)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        import datetime
+        from ngnn.loader import Graph, NeighborLoader
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=60))
+        g = Graph(torch.zeros(n_seeds + 1, dtype=torch.int64), torch.zeros(0, dtype=torch.int32),
+                  torch.zeros(n_seeds, 4), torch.zeros(n_seeds, dtype=torch.int64),
+                  torch.arange(n_seeds), 2)
+        loader = NeighborLoader(g, g.train_idx, [2], bs, shuffle=True, seed=3, rank=rank,
+                                world_size=world)
+        seeds = loader._seeds()
+        n_batches = len(loader)
+        t = torch.zeros(1)
+        for _ in range(n_batches):
+            dist.all_reduce(t)
+        counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(counts, torch.tensor([n_batches, seeds.numel()]))
+        allseeds = [torch.empty_like(seeds) for _ in range(world)]
+        dist.all_gather(allseeds, seeds)
+        covered = bool(torch.equal(torch.cat(allseeds).unique(), torch.arange(n_seeds)))
+        dist.barrier()
+        q.put((rank, [tuple(c.tolist()) for c in counts], covered))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        q.put((rank, repr(e), False))
+
+
+@pytest.mark.timeout(180)
+def test_gloo_world8_equal_batch_counts():
+    """196,615 products seeds over 8 ranks would give rank 7 one
+    batch fewer at bs 1024 (24,577 vs 24,576 seeds).  Same arithmetic here:
+    n % world != 0 and the per-rank counts straddle a batch boundary."""
+    world, bs = 8, 4
+    n = 8 * 4 * 3 + 7  # ranks 0-6 would get 13 seeds (4 batches), rank 7 12 (3 batches)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loader_worker, args=(r, world, port, q, n, bs)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    for r in res:
+        assert isinstance(r[1], list), r
+        assert r[2], r
+    counts = res[0][1]
+    assert len(set(counts)) == 1, counts  # same (batches, seeds) on every rank
+    assert counts[0] == (4, 13)

@@ -1,0 +1,72 @@
+"""NeighborLoader contract on the host side (no GPU): the PyG-Data adapter
+(pipeline.py:75-83 hands NeighborLoader the dataset's ``data``), the Batch
+fields the pipelines read (``x, y, yhn, edge_index, n_id, batch_size``,
+pipeline.py:110-118,152-160) and per-rank shard sizes."""
+import torch
+
+from ngnn.loader import Batch, Graph, NeighborLoader, graph_from_data
+
+
+class _Data:
+    """Stand-in for torch_geometric.data.Data (attribute access + items())."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def items(self):
+        return self.__dict__.items()
+
+
+def _data(n=12, e=40, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return _Data(x=torch.randn(n, 5, generator=g), y=torch.randint(0, 4, (n, 1), generator=g),
+                 yhn=torch.randint(0, 4, (n,), generator=g),
+                 train_mask=torch.rand(n, generator=g) < 0.5,
+                 edge_index=torch.randint(0, n, (2, e), generator=g), num_nodes=n)
+
+
+def test_graph_from_data_csc_matches_edge_index():
+    d = _data()
+    g = graph_from_data(d, device="cpu")
+    n = d.num_nodes
+    assert g.num_nodes == n and g.num_edges == d.edge_index.size(1)
+    # each node's in-neighbours (sources of edges into it) in edge order
+    for v in range(n):
+        want = d.edge_index[0][d.edge_index[1] == v]
+        got = g.col[g.rowptr[v]:g.rowptr[v + 1]].to(torch.int64)
+        assert torch.equal(got, want), v
+    assert torch.equal(g.y, d.y[:, 0])  # OGB's [N, 1] labels flattened
+    assert torch.equal(g.node_attrs["yhn"], d.yhn)
+    assert torch.equal(g.train_idx, d.train_mask.nonzero().view(-1))
+    assert "x" not in g.node_attrs and "edge_index" not in g.node_attrs
+
+
+def test_batch_node_attrs_and_to():
+    b = Batch(torch.zeros(3, 2), torch.arange(3), torch.zeros(2, 0, dtype=torch.int64),
+              torch.tensor([5, 1, 2]), 2, yhn=torch.tensor([0, 1, 1]))
+    assert torch.equal(b.yhn, torch.tensor([0, 1, 1]))
+    assert b.num_nodes == 3 and b.batch_size == 2
+    c = b.to("cpu")
+    assert torch.equal(c.yhn, b.yhn) and c.batch_size == 2
+    try:
+        b.nope
+    except AttributeError:
+        pass
+    else:
+        raise AssertionError("unknown attributes must raise AttributeError")
+
+
+def test_loader_shards_equal_across_ranks():
+    n, world, bs = 196_615, 8, 1024  # ogbn-products train seeds over 8 ranks
+    g = Graph(torch.zeros(n + 1, dtype=torch.int64), torch.zeros(0, dtype=torch.int32),
+              torch.zeros(1, 1), torch.zeros(n, dtype=torch.int64), torch.arange(n), 47)
+    lens, sizes, allseeds = set(), set(), []
+    for r in range(world):
+        ld = NeighborLoader(g, g.train_idx, [15, 10], bs, shuffle=True, seed=7, rank=r,
+                            world_size=world)
+        s = ld._seeds()
+        lens.add(len(ld))
+        sizes.add(s.numel())
+        allseeds.append(s)
+    assert lens == {25} and sizes == {24_577}
+    assert torch.equal(torch.cat(allseeds).unique(), torch.arange(n))

@@ -16,7 +16,7 @@ stop_on_crash() {  # $1 = rc, $2 = step
 rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
 nproc > "$OUT/host.txt"; lscpu | grep -E "Model name|^CPU\(s\)" >> "$OUT/host.txt" || true
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:--x} > "$OUT/pytest_gpu.log" 2>&1
   stop_on_crash $? pytest
   tail -5 "$OUT/pytest_gpu.log"
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1

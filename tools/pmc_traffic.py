@@ -1,6 +1,7 @@
 """HBM traffic per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3
 passes (tools/gpu_pmc.sh), mapped to bench.py's timer spans, written to
-profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+profiles/pmc_traffic.json (read by bench.py for roofline.traffic), keyed
+"span|workload|dtype" so a line only ever carries its own workload's traffic.
 
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
 bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section), so it is
@@ -23,6 +24,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--map", action="append", default=[], help="span=kernel-name-substring")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--workload", default="products-[15,10]-bs1024",
+                    help="bench.py config.workload the profiled command ran")
+    ap.add_argument("--dtype", default="f32")
     a = ap.parse_args()
     spans = dict(m.split("=", 1) for m in a.map)
     # (span, counter) -> {dispatch: summed value}
@@ -46,10 +50,10 @@ def main():
             continue
         fetch = 2 * 1024 * statistics.mean(fv)
         write = 1024 * statistics.mean(wv)
-        out[span] = {"kernel": names[span], "fetch_bytes": int(fetch), "write_bytes": int(write),
+        out[f"{span}|{a.workload}|{a.dtype}"] = {"kernel": names[span], "fetch_bytes": int(fetch), "write_bytes": int(write),
                      "traffic_bytes": int(fetch + write), "dispatches": [len(fv), len(wv)],
                      "source": os.path.basename(os.path.normpath(a.dir))}
-        print(span, out[span])
+        print(span, out[f"{span}|{a.workload}|{a.dtype}"])
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
 
