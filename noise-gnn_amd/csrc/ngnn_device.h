@@ -56,10 +56,11 @@ __device__ __forceinline__ float nanmax(float acc, float v) {
 }
 
 // ---- dropout RNG: counter-based, keyed by (seed, row, col); the keep mask is
-// never stored.  One 32-bit hash per column PAIR (2c, 2c+1): its low half
-// decides column 2c, its high half 2c+1; keep <=> half >= thresh,
-// thresh = ceil(p * 2^16) (p resolved to 1/65536; p = 0.5 exactly).
-// Host replica: tests/test_gpu_fused.py::dropout_keep.
+// never stored.  One 32-bit hash per column QUAD (4c .. 4c+3): byte j of it
+// decides column 4c + j; keep <=> byte >= thresh, thresh = ceil(p * 256)
+// (p resolved to 1/256: exact for 0, 0.25, 0.5, 0.75, 1; the drop rate is
+// p_eff = thresh / 256 and survivors scale by 1 / (1 - p_eff), so E[out] =
+// in exactly).  Host replica: tests/test_gpu_fused.py::dropout_keep.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352dU;
@@ -70,26 +71,21 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 }
 
 struct Dropout {
-    uint32_t s0, s1, thresh;  // thresh == 0: no dropout; > 2^16: drop all
+    uint32_t s0, s1, thresh;  // thresh == 0: no dropout; 256: drop all
     float scale;
-    // one hash per row (seed-mixed), one per column pair: rkey + col/2 are
+    // one hash per row (seed-mixed), one per column quad: rkey + col/4 are
     // distinct within a row and lowbias32 is a bijection
     __device__ __forceinline__ uint32_t row_key(uint32_t row) const {
         return lowbias32(row ^ s0) ^ s1;
     }
-    __device__ __forceinline__ uint32_t pair_hash(uint32_t rkey, uint32_t col) const {
-        return lowbias32(rkey + (col >> 1));
+    __device__ __forceinline__ uint32_t quad_hash(uint32_t rkey, uint32_t col) const {
+        return lowbias32(rkey + (col >> 2));
     }
-    __device__ __forceinline__ bool keep_half(uint32_t h, uint32_t col) const {
-        return ((col & 1u) ? (h >> 16) : (h & 0xffffu)) >= thresh;
-    }
-    // the same with the column's parity known at compile time
-    template <int ODD>
-    __device__ __forceinline__ bool keep_par(uint32_t h) const {
-        return (ODD ? (h >> 16) : (h & 0xffffu)) >= thresh;
+    __device__ __forceinline__ bool keep_byte(uint32_t h, uint32_t col) const {
+        return ((h >> (8 * (col & 3u))) & 0xffu) >= thresh;
     }
     __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
-        return keep_half(pair_hash(rkey, col), col);
+        return keep_byte(quad_hash(rkey, col), col);
     }
     __device__ __forceinline__ void reseed(uint64_t d) {
         s0 ^= static_cast<uint32_t>(d);
@@ -113,16 +109,14 @@ inline Dropout make_dropout(float p, uint64_t seed) {
     if (!(p > 0.0f)) {
         d.thresh = 0;
         d.scale = 1.0f;
-    } else if (p >= 1.0f) {
-        d.thresh = (1u << 16) + 1;  // nothing kept
-        d.scale = 0.0f;
-    } else {
-        const double t = static_cast<double>(p) * 65536.0;
-        uint32_t ti = static_cast<uint32_t>(t);
-        if (static_cast<double>(ti) < t) ++ti;  // ceil
-        d.thresh = ti;
-        d.scale = 1.0f / (1.0f - p);
+        return d;
     }
+    const double t = static_cast<double>(p) * 256.0;
+    uint32_t ti = static_cast<uint32_t>(t < 256.0 ? t : 256.0);
+    if (static_cast<double>(ti) < t && ti < 256) ++ti;  // ceil
+    if (ti == 0) ti = 1;  // p > 0 drops something
+    d.thresh = ti;
+    d.scale = ti >= 256 ? 0.0f : 256.0f / static_cast<float>(256 - ti);
     return d;
 }
 

@@ -136,11 +136,14 @@ template <bool X3>
 __device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], const RtArgs &a, i32x4 xr, int r, int k0,
                                        int q) {
     if (X3) {
+        // all four chunks unconditionally: a chunk past the root term reads
+        // bytes of the same / next row (or 0 past the range) and is never
+        // used -- a uniform per-chunk select here becomes loop-invariant SGPR
+        // lane masks that the compiler hoists and spills
         const int voff = (r * static_cast<int>(a.ldx) + k0 + 8 * q) * 4;
-        const int ncc = a.C - k0 / 32;  // chunks of this group inside the root term
 #pragma unroll
         for (int g = 0; g < RT_KC; ++g)
-            xf[g] = buf_load4(xr, (g >> 1) < ncc ? voff + 4 * (32 * (g >> 1) + 4 * (g & 1)) : kOOB, 0, 0);
+            xf[g] = buf_load4(xr, voff + 4 * (32 * (g >> 1) + 4 * (g & 1)), 0, 0);
     } else {
         const int voff = (r * static_cast<int>(a.ldx) + k0 + 4 * q) * 4;
 #pragma unroll
@@ -154,7 +157,7 @@ __device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &
                                         int q) {
     const int voff = (r * static_cast<int>(a.ldx) + 32 * a.C + q) * 4;
 #pragma unroll
-    for (int s = 0; s < X3_TAIL_MAX; ++s) xt[s] = buf_load1(xr, s < a.T4 ? voff + 16 * s : kOOB, 0, 0);
+    for (int s = 0; s < X3_TAIL_MAX; ++s) xt[s] = buf_load1(xr, voff + 16 * s, 0, 0);  // masked at use
 }
 
 // root term of one 128-column group in the X3 layout: per 32-chunk, split x
@@ -169,10 +172,12 @@ __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[R
         if (c < ncc) {
             v4f lo = xf[2 * c], hi = xf[2 * c + 1];
             if (mask_last && c == ncc - 1) {  // padded last chunk: columns past K read the next row
+                int kq = kq8;
+                asm volatile("" : "+v"(kq));  // keep the masks here (not hoisted into SGPRs)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    lo[i] = i < kq8 ? lo[i] : 0.0f;
-                    hi[i] = 4 + i < kq8 ? hi[i] : 0.0f;
+                    lo[i] = __int_as_float(__float_as_int(lo[i]) & lt_mask(i, kq));
+                    hi[i] = __int_as_float(__float_as_int(hi[i]) & lt_mask(4 + i, kq));
                 }
             }
             bf16x8 x1, x2, x3;
@@ -235,7 +240,13 @@ template <int NTW, bool LDSW>
 __device__ __forceinline__ void mfma_chunk_rt(v4f (&acc)[NTW], const v4f (&xf)[RT_KC],
                                               const v4f *__restrict__ wsrc, int KG, int kg0,
                                               int nkg, int NT, int lane) {
-    constexpr int P = NTW >= 8 ? NTW / 4 : 1;
+    if (!LDSW) {  // streamed: address clamps per call, not hoisted as SGPR masks
+        asm volatile("" : "+s"(NT));
+        asm volatile("" : "+s"(KG));
+    }
+    // fragments per load group (double-buffered): 4 from LDS, 2 streamed
+    // from L2 (the streamed path's address registers are the tighter budget)
+    constexpr int P = NTW >= 8 ? NTW / (LDSW ? 4 : 2) : 1;
     constexpr int H = NTW / P;
     v4f wb[2][H];
     load_w<NTW, H, LDSW>(wb[0], wsrc, KG, kg0, 0, NT, lane);
@@ -375,35 +386,40 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 // epilogue: lane holds output features m*16 + 4q .. +3 of row r.  Stores go
 // through a buffer resource (rows past n_rows are dropped by the range);
 // `vec` (uniform): F_out a multiple of 16 with 16-B aligned rows -- one
-// 16-B store per m-tile, no per-lane predicates.
-template <int NTW, bool DROP>
+// 16-B store per m-tile, no per-lane predicates.  Branch-free: ReLU and the
+// dropout keep fold into one select per element (a keep test compiled as a
+// branch costs an exec save/restore per element), and the lane's four
+// columns f .. f+3 (f = col_base + 16 m + 4 q, col_base a multiple of 16) are
+// exactly one dropout quad: hash pb + 4 m, pb = row_key + (col_base + 4 q)/4.
+template <int NTW, bool DROP, bool RELU, bool VEC>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
-                                         const float *sbias, int r, bool vec, int q) {
-    // relu through a wave-uniform select; dropout (hash per element) only in
-    // the DROP instantiation
-    const uint32_t rk = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) : 0u;
+                                         const float *sbias, int r, int q) {
+    const uint32_t thresh = a.epi.drop.thresh;
+    const float scale = a.epi.drop.scale;
+    const uint32_t pb = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) +
+                                   static_cast<uint32_t>((a.epi.col_base + 4 * q) >> 2)
+                             : 0u;
     const int obase = r * static_cast<int>(a.ldo) * 4;
-    const bool relu = a.epi.relu;
+    // re-materialised per call: the per-tile-index tests below must not be
+    // hoisted out of the tile loop as SGPR lane masks (they spill)
+    int NT = a.NT;
+    asm volatile("" : "+s"(NT));
 #pragma unroll
     for (int m = 0; m < NTW; ++m) {
-        if (m >= a.NT) continue;  // padded tiles (uniform)
+        if (m >= NT) continue;  // padded tiles (uniform)
         const int f = m * 16 + 4 * q;
         const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
-        // two pair hashes cover the lane's 4 columns (col_base + f is even)
-        const uint32_t c0 = static_cast<uint32_t>(a.epi.col_base + f);
+        const uint32_t h = DROP ? lowbias32(pb + 4u * m) : 0u;
         v4f v;
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-            const uint32_t h = DROP ? a.epi.drop.pair_hash(rk, c0 + j) : 0u;
-#pragma unroll
-            for (int jj = j; jj < j + 2; ++jj) {
-                float y = acc[m][jj] + b[jj];
-                y = (relu && y < 0.0f) ? 0.0f : y;  // NaN passes, like torch.relu
-                if (DROP) y = a.epi.drop.keep_half(h, c0 + jj) ? y * a.epi.drop.scale : 0.0f;
-                v[jj] = y;
-            }
+        for (int j = 0; j < 4; ++j) {
+            const float y = acc[m][j] + b[j];
+            // y < 0 (ReLU; NaN passes, like torch.relu) or a dropped column -> 0
+            bool zero = RELU && y < 0.0f;
+            if (DROP) zero = zero || ((h >> (8 * j)) & 0xffu) < thresh;
+            v[j] = zero ? 0.0f : (DROP ? y * scale : y);
         }
-        if (vec) {
+        if (VEC) {
             buf_store4(v, orsrc, obase + 4 * f, 0, 0);
         } else {
 #pragma unroll
@@ -418,7 +434,7 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
 // 0.355 ms/step on products, the extra address VALU spills the L0 kernel.)
 // X3: root term on the 3 x bf16 split (LDS image of W_r split in the
 // prologue from the raw rows); otherwise exact fp32 MFMA.
-template <int NTW, int RED, int WLM, bool X3>
+template <int NTW, int RED, int WLM, bool X3, bool VEC>
 __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     constexpr bool WL_LDS = WLM == 1;
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
@@ -519,8 +535,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     }
     __syncthreads();
 
-    const int wave = wv, lane = ln;
-    const int q = lane >> 4, rl = lane & 15;
+    const int wave = wv;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
     const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
@@ -552,7 +567,21 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                                              ((n_rows - 1) * a.ldx + a.K) * 4 * (n_rows > 0)))
                              : make_rsrc(a.x, a.x_bytes);
     const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
+    // per-lane indices are re-derived per tile from threadIdx (behind an
+    // empty asm, so nothing derived from them is hoisted and kept live across
+    // the tile loop: such invariants were the VGPR spills, and their reloads
+    // drained the prefetch with a vmcnt(0))
+    auto lane_ids = [&](int &lane_, int &q_, int &rl_) {
+        int l = static_cast<int>(threadIdx.x) & 63;
+        asm volatile("" : "+v"(l));
+        lane_ = l;
+        q_ = l >> 4;
+        rl_ = l & 15;
+    };
     auto prefetch = [&](int tn) {
+        int lane, q, rl;
+        lane_ids(lane, q, rl);
+        (void)lane;
         const int rn = (tn < n_tiles ? tn : 0) * RT_ROWS + rl;
         load_x<X3>(xn, a, xr, rn, 0, q);
         if (X3) load_xt(xtn, a, xr, rn, q);
@@ -564,20 +593,33 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             nend = nbeg + ((nend - nbeg) & mr);  // rows past the end: degree 0
         }
     };
-    const bool vec = a.vec_out && (a.Fo == a.NT * 16);
-    // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
-    const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
     prefetch(t);
     for (; t < n_tiles; t = tile_of(++kt)) {
+        int lane, q, rl;
+        lane_ids(lane, q, rl);
+        // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
+        const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
         const int r = t * RT_ROWS + rl;
         const int beg = nbeg, deg = nend - nbeg;
         const int maxdeg = have_l ? rowgroup_max16(deg) : 0;
         v4f acc[NTW];
 #pragma unroll
         for (int m = 0; m < NTW; ++m) acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
-        float xt[X3_TAIL_MAX];
+        if (X3) {
+            // fp32 tail steps (the K % 32 columns past the bf16 chunks) first,
+            // while the prefetched tail values are still this tile's
 #pragma unroll
-        for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) xt[s2] = xtn[s2];
+            for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) {
+                if (s2 < a.T4) {
+                    const float xv = __int_as_float(__float_as_int(xtn[s2]) &
+                                                    lt_mask(32 * a.C + 4 * s2 + q, a.K));
+#pragma unroll
+                    for (int m = 0; m < NTW; ++m)
+                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(swt[(s2 * NTW + m) * 64 + lane], xv,
+                                                                      acc[m], 0, 0, 0);
+                }
+            }
+        }
 
         // ---- root term: x[r] . W_r^T, chunk by chunk; chunk c+1 (or, in the
         // last chunk, the next tile's chunk 0 and row bounds) loads behind
@@ -603,20 +645,6 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
             }
         }
-        if (X3) {
-            // fp32 tail steps (K % 32 columns past the bf16 chunks)
-#pragma unroll
-            for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) {
-                if (s2 < a.T4) {
-                    const float xv = __int_as_float(__float_as_int(xt[s2]) &
-                                                    lt_mask(32 * a.C + 4 * s2 + q, a.K));
-#pragma unroll
-                    for (int m = 0; m < NTW; ++m)
-                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(swt[(s2 * NTW + m) * 64 + lane], xv,
-                                                                      acc[m], 0, 0, 0);
-                }
-            }
-        }
 
         // ---- neighbour term (tiles with in-edges only)
         if (maxdeg > 0) {
@@ -630,11 +658,14 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 // are not live across the gather (register budget)
                 if (c == nchunk_l - 1) prefetch(tile_of(kt + 1));
                 if (a.agg_out) {
-                    const int kq = a.K - k0 - 4 * q;
+                    int kq = a.K - k0 - 4 * q;
+                    asm volatile("" : "+v"(kq));  // per-lane masks stay VGPR selects here
                     const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
 #pragma unroll
-                    for (int g = 0; g < RT_KC; ++g)
-                        if (g < nkg) buf_store4(ag[g], ar, 16 * g < kq ? aoff + 64 * g : kOOB, 0, 0);
+                    for (int g = 0; g < RT_KC; ++g) {
+                        const int mk = lt_mask(16 * g, kq);
+                        if (g < nkg) buf_store4(ag[g], ar, ((aoff + 64 * g) & mk) | (kOOB & ~mk), 0, 0);
+                    }
                 }
                 if constexpr (WL_LDS)
                     mfma_chunk_rt<NTW, true>(acc, ag, swl, a.KG, c * RT_KC, nkg, a.NT, lane);
@@ -644,10 +675,16 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         }
 
         // ---- epilogue (bias, relu, dropout and the stores)
-        if (a.epi.drop.thresh)
-            epilogue<NTW, true>(acc, a, orsrc, sbias, r, vec, q);
-        else
-            epilogue<NTW, false>(acc, a, orsrc, sbias, r, vec, q);
+        if (a.epi.drop.thresh) {
+            if (a.epi.relu)
+                epilogue<NTW, true, true, VEC>(acc, a, orsrc, sbias, r, q);
+            else
+                epilogue<NTW, true, false, VEC>(acc, a, orsrc, sbias, r, q);
+        } else if (a.epi.relu) {
+            epilogue<NTW, false, true, VEC>(acc, a, orsrc, sbias, r, q);
+        } else {
+            epilogue<NTW, false, false, VEC>(acc, a, orsrc, sbias, r, q);
+        }
     }
 }
 
@@ -666,9 +703,9 @@ int num_cus() {
     return g_num_cus[dev];
 }
 
-template <int NTW, int RED, int WLM, bool X3>
+template <int NTW, int RED, int WLM, bool X3, bool VEC>
 int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
-    auto fn = k_sage_rt<NTW, RED, WLM, X3>;
+    auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
@@ -684,13 +721,19 @@ int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
 template <int NTW>
 int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, size_t lds,
                 hipStream_t st) {
+    // vec: F_out a whole number of 16-column tiles with 16-B aligned rows
+    const bool vec = a.vec_out && (a.Fo == a.NT * 16);
     auto by_red = [&](auto red_c) {
         constexpr int RED = decltype(red_c)::value;
-        if (x3)
-            return wl_lds ? launch_rt<NTW, RED, 1, true>(a, n_tiles, lds, st)
-                          : launch_rt<NTW, RED, 0, true>(a, n_tiles, lds, st);
-        return wl_lds ? launch_rt<NTW, RED, 1, false>(a, n_tiles, lds, st)
-                      : launch_rt<NTW, RED, 0, false>(a, n_tiles, lds, st);
+        auto go = [&](auto x3_c, auto vec_c) {
+            constexpr bool X3 = decltype(x3_c)::value, VEC = decltype(vec_c)::value;
+            return wl_lds ? launch_rt<NTW, RED, 1, X3, VEC>(a, n_tiles, lds, st)
+                          : launch_rt<NTW, RED, 0, X3, VEC>(a, n_tiles, lds, st);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (x3) return vec ? go(T{}, T{}) : go(T{}, F{});
+        return vec ? go(F{}, T{}) : go(F{}, F{});
     };
     if (reduce == NGNN_REDUCE_MEAN) return by_red(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
     if (reduce == NGNN_REDUCE_SUM) return by_red(std::integral_constant<int, NGNN_REDUCE_SUM>{});

@@ -12,7 +12,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libngnn.so")
+# NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
+# read once, at import
+LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
 ABI_VERSION = 9
 
 OK = 0

@@ -43,6 +43,22 @@ _ws: dict = {}
 # section 3).  True: exact fp32 MFMA (a fmaf chain), like torch.backends'
 # allow_tf32 = False.
 _exact_f32 = False
+# debug hook (None in normal use): a list receives (layer, d output, saved
+# aggregate) from every fused-stack backward
+_debug_grads = None
+
+
+def dropout_scale(p: float) -> float:
+    """The fused kernels' survivor scale (ngnn_device.h Dropout): p is
+    resolved to p_eff = ceil(p * 256) / 256 and survivors scale by
+    1 / (1 - p_eff) (fp32), so the expectation is exact."""
+    import math
+    import numpy as np
+    pf = float(np.float32(p))
+    if pf <= 0.0:
+        return 1.0
+    t = max(1, min(256, math.ceil(pf * 256.0)))
+    return 0.0 if t >= 256 else float(np.float32(256.0) / np.float32(256 - t))
 
 
 def set_exact_f32(flag: bool) -> None:
@@ -233,11 +249,14 @@ class _SAGEStack(torch.autograd.Function):
         red = _lib.REDUCE[reduce]
         for i in reversed(range(L)):
             h_in, y_out, agg = acts[i], acts[i + 1], aggs[i]
+            if _debug_grads is not None:  # test/debug hook: d(acts[i+1]) per layer
+                _debug_grads.append((i, dy.detach().clone(), agg.detach().clone(),
+                                     h_in.detach().clone()))
             wl, bl, wr = params[3 * i:3 * i + 3]
             Fo, K = wl.shape
             hidden = i != L - 1
             ymask = y_out if hidden else None
-            yscale = (1.0 / (1.0 - p)) if (hidden and p > 0.0) else 1.0
+            yscale = dropout_scale(p) if (hidden and p > 0.0) else 1.0
             # gradient buffers: the data-parallel bucket's views when the caller
             # registered them (a fresh view each time, so autograd adopts it as
             # .grad instead of copying it), else new tensors

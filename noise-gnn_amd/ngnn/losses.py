@@ -33,8 +33,10 @@ def _workspace(dev, B: int) -> torch.Tensor:
 
 def _grad_buffer(dev, n: int, c: int, b: int) -> torch.Tensor:
     """[n, c] view of a cached zero-initialised buffer; only rows < b are
-    ever written, so rows >= b are zero.  Grown on demand (zeros)."""
-    key = (dev, c)
+    ever written, so rows >= b are zero.  Grown on demand (zeros).  One
+    buffer per (C, b): a buffer shared with a larger b would hold that
+    call's stale rows in [b, b_larger)."""
+    key = (dev, c, b)
     buf = _zero_rows.get(key)
     if buf is None or buf.size(0) < n:
         buf = torch.zeros(max(n, 1), c, dtype=torch.float32, device=dev)

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 import ngnn
 from oracle import pyg_ref
 
-from test_gpu_fused import GRAD, OUT, WGRAD, _MaskedSAGE, dropout_keep
+from test_gpu_fused import GRAD, OUT, WGRAD, _MaskedSAGE, dropout_keep, dropout_scale
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -129,14 +129,55 @@ def test_config_arxiv_15_10_bs1024():
 
 @pytest.mark.timeout(300)
 def test_config_computers_max_10_5():
-    """K = 767 (not a multiple of 4), max aggregator, the config's full batch."""
+    """K = 767 (not a multiple of 4), max aggregator, the config's full batch.
+
+    Forward end to end at 1e-5.  The max gradient goes to the argmax
+    neighbour, and fp32 rounding differences between the GPU's and the CPU's
+    layer-0 outputs (~1e-6) flip near-tied maxima (~1e6 (row, feature) pairs
+    here), so the backward is pinned LAYER BY LAYER on identical inputs: the
+    oracle's layer-1 backward runs on the GPU's layer-1 input, the oracle's
+    layer-0 backward on the GPU's layer-0 output gradient."""
+    from ngnn import fused
     from ngnn.loader import sample_block
     g = _graph("computers")
     b = sample_block(g, g.train_idx, [10, 5], seed=5)
     assert b.batch_size == 300
     torch.manual_seed(2)
-    mine = ngnn.SAGE(767, 512, 10, 2, dropout=0.5, aggr="max").to(DEV)
-    _eager_vs_oracle(b, mine, 512, train=True, aggr="max", check_dx=True)
+    mine = ngnn.SAGE(767, 512, 10, 2, dropout=0.5, aggr="max").to(DEV).train()
+    torch.manual_seed(99)
+    s = int(torch.randint(0, 2**62, (1,)).item())
+    torch.manual_seed(99)
+    fused._debug_grads = []
+    try:
+        out = mine(b.x, b.edge_index)
+        F.cross_entropy(out[:300], b.y[:300]).backward()
+        dbg = {i: (dy.cpu(), hin.cpu()) for i, dy, _, hin in fused._debug_grads}
+    finally:
+        fused._debug_grads = None
+    N = b.num_nodes
+    mask = dropout_keep(s, N, 512, 0.5).float()
+    ref = _MaskedSAGE(767, 512, 10, 2, dropout=0.5, aggr="max", masks=[mask])
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    x, ei, y = b.x.cpu(), b.edge_index.cpu(), b.y[:300].cpu()
+    with torch.no_grad():
+        torch.testing.assert_close(out.cpu(), ref(x, ei), **OUT)
+    grads = {k: p.grad.cpu() for k, p in mine.named_parameters()}
+    # layer 1 on the GPU's layer-1 input
+    h1 = dbg[1][1].clone().requires_grad_(True)
+    F.cross_entropy(ref.convs[1](h1, ei)[:300], y).backward()
+    # d(layer-1 input): the bounded backward writes rows < R' = max(R, 1 + max
+    # source of the edges into rows < R) only -- the oracle is zero past them
+    src, dst = ei
+    rn = max(300, int(src[dst < 300].max()) + 1)
+    assert not h1.grad[rn:].any()
+    torch.testing.assert_close(dbg[0][0][:rn], h1.grad[:rn], **GRAD)
+    for n, q in ref.convs[1].named_parameters():
+        torch.testing.assert_close(grads[f"convs.1.{n}"], q.grad, **WGRAD, msg=n)
+    # layer 0 (relu + dropout) under the GPU's output gradient
+    h0 = ref.convs[0](x, ei).relu() * mask * dropout_scale(0.5)
+    h0.backward(torch.cat([dbg[0][0][:rn], torch.zeros(N - rn, 512)]))
+    for n, q in ref.convs[0].named_parameters():
+        torch.testing.assert_close(grads[f"convs.0.{n}"], q.grad, **WGRAD, msg=n)
 
 
 @pytest.mark.timeout(300)

@@ -34,18 +34,30 @@ def _lowbias32(x):
 
 
 def dropout_keep(seed, n_rows, n_cols, p):
-    """Host replica of ngnn_device.h::Dropout: one hash per column pair,
-    keep <=> 16-bit half >= ceil(p * 2^16)."""
-    import math
+    """Host replica of ngnn_device.h::Dropout: one hash per column quad,
+    keep <=> byte (col % 4) >= ceil(p * 256)."""
     s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
-    pf = float(np.float32(p))
-    thresh = 0 if pf <= 0 else (65537 if pf >= 1 else math.ceil(pf * 65536.0))
+    thresh = dropout_thresh(p)
     r = np.arange(n_rows, dtype=np.uint64)[:, None]
     c = np.arange(n_cols, dtype=np.uint64)[None, :]
     rk = _lowbias32(r ^ s0) ^ s1
-    h = _lowbias32((rk + (c >> np.uint64(1))) & M32)
-    half = np.where((c & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
-    return torch.from_numpy(half >= np.uint64(thresh))
+    h = _lowbias32((rk + (c >> np.uint64(2))) & M32)
+    byte = (h >> (np.uint64(8) * (c & np.uint64(3)))) & np.uint64(0xFF)
+    return torch.from_numpy(byte >= np.uint64(thresh))
+
+
+def dropout_thresh(p):
+    import math
+    pf = float(np.float32(p))
+    if pf <= 0:
+        return 0
+    return max(1, min(256, math.ceil(pf * 256.0)))
+
+
+def dropout_scale(p):
+    """Survivor scale 1 / (1 - p_eff), p_eff = ceil(p * 256) / 256."""
+    t = dropout_thresh(p)
+    return 0.0 if t >= 256 else float(np.float32(256.0) / np.float32(256 - t))
 
 
 def rand_block(seed, N, E, order="dst"):
@@ -89,7 +101,7 @@ def test_fused_layer_dropout_mask_and_scale():
     got = sage_layer_fwd(x.to(DEV), blk, "mean", conv.lin_l.weight.to(DEV), conv.lin_l.bias.to(DEV),
                          conv.lin_r.weight.to(DEV), relu=True, p_drop=p, seed=seed).cpu()
     keep = dropout_keep(seed, N, Fo, p)
-    torch.testing.assert_close(got, pre * keep * (1.0 / (1.0 - p)), **OUT)
+    torch.testing.assert_close(got, pre * keep * dropout_scale(p), **OUT)
     frac = keep.float().mean().item()
     assert abs(frac - (1 - p)) < 0.01
     # deterministic in the seed, different for another seed
@@ -143,7 +155,7 @@ class _MaskedSAGE(pyg_ref.SAGE):
             x = conv(x, edge_index)
             if i != self.num_layers - 1:
                 x = x.relu()
-                x = x * self.masks[i] * (1.0 / (1.0 - self.dropout))
+                x = x * self.masks[i] * dropout_scale(self.dropout)
         return x
 
 

@@ -107,3 +107,54 @@ def test_slot_csr_and_seed(tight):
     assert torch.equal(step.rowptr, ref.rowptr)
     assert torch.equal(step.col, ref.col)
     assert seeds[0] != seeds[1]
+
+
+def test_graph_short_last_batch_matches_eager():
+    """an epoch's last batch (drop_last off) has fewer seeds than
+    the captured B.  Its replay must equal the reference loop on that batch,
+    F.cross_entropy(out[:bs], y[:bs]) (pipeline.py:155-158): rows [bs, B)
+    carry no loss."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import NeighborLoader, synthetic_graph
+    g = synthetic_graph("ogbn-arxiv", DEV, seed=0, scale=0.05)
+    seeds = g.train_idx[:256 * 2 + 37]
+    loader = NeighborLoader(g, seeds, [10, 5], 256, shuffle=False)
+    batches = list(loader)
+    assert [b.batch_size for b in batches] == [256, 256, 37]
+    torch.manual_seed(11)
+    m_e = ngnn.SAGE(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+    torch.manual_seed(11)
+    m_g = ngnn.SAGE(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+    le = _eager_train(m_e, batches)
+    opt = torch.optim.Adam(m_g.parameters(), lr=1e-2, fused=True, capturable=True)
+    n_cap, e_cap = slot_size(256, [10, 5])
+    step = GraphedTrainStep(m_g, opt, 256, n_cap, e_cap, g.x.size(1), DEV)
+    step.capture(batches[0].x, batches[0].edge_index, batches[0].y)
+    lg = [float(step(b.x, b.edge_index, b.y, b.batch_size)) for b in batches]
+    torch.cuda.synchronize()
+    for a, c in zip(le, lg):
+        assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
+    for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_bucket_view_gradients_adopted():
+    """GradAllReduce registers bucket views; the fused backward writes the
+    weight gradients into them and autograd adopts them as .grad (no pack /
+    unpack copies), in eager and in graph replay, with the same values as
+    without the bucket."""
+    import ngnn
+    from ngnn.distributed import GradAllReduce
+    m, batches = _setup(0.0)
+    ref = {k: None for k, _ in m.named_parameters()}
+    b = batches[0]
+    F.cross_entropy(m(b.x, b.edge_index)[:b.batch_size], b.y[:b.batch_size]).backward()
+    ref = {k: p.grad.clone() for k, p in m.named_parameters()}
+    red = GradAllReduce(m.parameters())
+    m.zero_grad(set_to_none=True)
+    F.cross_entropy(m(b.x, b.edge_index)[:b.batch_size], b.y[:b.batch_size]).backward()
+    for (k, p), v in zip(m.named_parameters(), red.views):
+        assert p.grad.data_ptr() == v.data_ptr(), k
+        # (the input-gradient scatter uses float atomics: order-dependent bits)
+        torch.testing.assert_close(p.grad, ref[k], rtol=1e-5, atol=1e-6, msg=k)
