@@ -51,6 +51,14 @@ extern "C" {
  * x . W_r^T on exact fp32 MFMA (v_mfma_f32_16x16x4_f32, a fmaf chain) instead
  * of the default fp32-accurate 3 x bf16 split. */
 #define NGNN_MATH_EXACT_F32 0x100
+/* flag OR-ed into ngnn_sage_fwd_raw's `reduce` (MEAN / SUM, no ReLU, no
+ * dropout, agg_out == NULL: an output layer): aggregate the neighbour term in
+ * the F_out-wide space -- z = x W_l^T for every row in the same launch as the
+ * root term (ws holds z: n_rows x ceil16(F_out) floats), then out[d] +=
+ * mean/sum_{j -> d} z[j] for the rows below n_edge_rows.  Equal to
+ * W_l . mean(x_j) up to fp32 rounding (the aggregation is linear); the
+ * K-wide gather becomes an F_out-wide one.  Other cases run the fused path. */
+#define NGNN_FWD_NARROW 0x200
 
 /* dtypes */
 #define NGNN_F32 0
@@ -244,8 +252,10 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * ngnn_sage_fwd.  x_dev (nullable): a device word holding x's address, read
  * at run time instead of x (a HIP-graph slot whose batch stays where the
  * loader put it; 16-B aligned, row stride ldx, rows < *n_rows_dev).
- * n_edge_rows / n_edge_rows_dev: accepted and unused (row hints of a retired
- * split path).
+ * n_edge_rows / n_edge_rows_dev (device int, nullable, min'd with the
+ * host value): rows at or past it have no in-edges (NGNN_FWD_NARROW's
+ * gather stops there; NeighborLoader numbers the rows that receive edges
+ * first).  Pass n_rows when unknown.
  * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes. */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,

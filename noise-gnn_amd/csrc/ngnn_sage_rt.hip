@@ -103,6 +103,15 @@ struct RtArgs {
     // when kpad), then T4 exact-fp32 steps of 4 columns
     int C, T4, kpad;
     const float *wr_raw;  // X3: raw W_r rows of this slice [Fo, K], stride ldw
+    // narrow mode (last layer, MEAN/SUM): output tiles [0, NT1) are W_r rows
+    // (out = b + x W_r^T, the root term), tiles [NT1, NT) W_l rows written to
+    // z = x W_l^T [n_rows, ldz] (the neighbour term is aggregated afterwards
+    // in the F_out-wide space); NT1 == NT otherwise
+    int NT1;
+    const float *wz_raw;
+    float *z;
+    int64_t ldz;
+    uint32_t z_bytes;
 };
 
 // -1 (all ones) when a < b, else 0: a lane mask held in a VGPR, built without
@@ -402,11 +411,17 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     const int obase = r * static_cast<int>(a.ldo) * 4;
     // re-materialised per call: the per-tile-index tests below must not be
     // hoisted out of the tile loop as SGPR lane masks (they spill)
-    int NT = a.NT;
+    int NT = a.NT, NT1 = a.NT1;
     asm volatile("" : "+s"(NT));
+    asm volatile("" : "+s"(NT1));
 #pragma unroll
     for (int m = 0; m < NTW; ++m) {
         if (m >= NT) continue;  // padded tiles (uniform)
+        if (m >= NT1) {         // narrow mode: z = x W_l^T rows, no epilogue
+            const i32x4 zr = make_rsrc(a.z, a.z_bytes);
+            buf_store4(acc[m], zr, (r * static_cast<int>(a.ldz) + (m - NT1) * 16 + 4 * q) * 4, 0, 0);
+            continue;
+        }
         const int f = m * 16 + 4 * q;
         const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
         const uint32_t h = DROP ? lowbias32(pb + 4u * m) : 0u;
@@ -455,13 +470,25 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             // W_r split into three bf16 parts, one lane fragment (8 consecutive
             // k of one output row) per slot; rows past F_out / columns past K
             // are zero
+            // image row n: W_r row n (tiles < NT1), W_l row n - 16 NT1 (narrow
+            // mode's tiles [NT1, NT)), nothing for padded tiles (>= NT) or
+            // rows past F_out of either half
+            auto wrow = [&](int n) -> const float * {
+                if (n >= 16 * a.NT) return nullptr;
+                const bool zt = n >= 16 * a.NT1;
+                const int nn = zt ? n - 16 * a.NT1 : n;
+                const float *base = zt ? a.wz_raw : a.wr_raw;
+                if (nn >= a.Fo || base == nullptr) return nullptr;
+                return base + static_cast<int64_t>(nn) * a.ldw;
+            };
             const int nslot = pst;
             for (int sl = threadIdx.x; sl < nslot; sl += RT_WAVES * 64) {
                 const int l = sl & 63, mt = (sl >> 6) % NTW, cc = (sl >> 6) / NTW;
                 const int n = mt * 16 + (l & 15), k = 32 * cc + 8 * (l >> 4);
                 v4f lo{0.f, 0.f, 0.f, 0.f}, hi{0.f, 0.f, 0.f, 0.f};
-                if (n < a.Fo) {
-                    const float *src = a.wr_raw + static_cast<int64_t>(n) * a.ldw + k;
+                const float *row = wrow(n);
+                if (row) {
+                    const float *src = row + k;
                     if (k + 8 <= a.K) {
                         lo = *reinterpret_cast<const v4f *>(src);
                         hi = *reinterpret_cast<const v4f *>(src + 4);
@@ -483,7 +510,8 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             for (int sl = threadIdx.x; sl < ntail; sl += RT_WAVES * 64) {
                 const int l = sl & 63, mt = (sl >> 6) % NTW, st = (sl >> 6) / NTW;
                 const int n = mt * 16 + (l & 15), k = 32 * a.C + 4 * st + (l >> 4);
-                swt[sl] = (n < a.Fo && k < a.K) ? a.wr_raw[static_cast<int64_t>(n) * a.ldw + k] : 0.0f;
+                const float *row = wrow(n);
+                swt[sl] = (row && k < a.K) ? row[k] : 0.0f;
             }
         }
         // fp32 images by LDS-DMA, 1 KiB (one n-tile x k-group fragment) per
@@ -740,6 +768,50 @@ int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, 
     return by_red(std::integral_constant<int, NGNN_REDUCE_MAX>{});
 }
 
+// ---- narrow-mode neighbour term: out[d, :Fo] += reduce_{e into d} z[col[e], :Fo]
+// for rows d with in-edges below min(n_rows, *n_rows_dev, *n_edge_rows_dev):
+// mean/sum of z = x W_l^T (linear, so equal to W_l . mean(x) up to fp32
+// rounding).  16 lanes per row (float4 columns), 4 rows per wave, 8
+// neighbour rows in flight per lane; per column edge order from 0, then
+// / deg for mean.
+constexpr int NA_UNR = 8;
+template <bool MEAN>
+__global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z, int64_t ldz, int Fo,
+                                                    const int32_t *__restrict__ rowptr,
+                                                    const int32_t *__restrict__ col, int n_rows,
+                                                    const int32_t *__restrict__ n_rows_dev,
+                                                    const int32_t *__restrict__ n_edge_dev,
+                                                    float *__restrict__ out, int64_t ldo) {
+    int nr = n_rows;
+    if (n_rows_dev) nr = min(nr, *n_rows_dev);
+    if (n_edge_dev) nr = min(nr, *n_edge_dev);
+    const int sub = threadIdx.x & 15;
+    const int F4 = (Fo + 3) >> 2;
+    for (int d = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; d < nr; d += (gridDim.x * blockDim.x) >> 4) {
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        if (beg == end) continue;
+        for (int c4 = sub; c4 < F4; c4 += 16) {
+            v4f acc{0.f, 0.f, 0.f, 0.f};
+            for (int e = beg; e < end; e += NA_UNR) {
+                v4f v[NA_UNR];
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u) {
+                    const int ee = min(e + u, end - 1);  // a short batch re-reads its last row
+                    v[u] = *reinterpret_cast<const v4f *>(z + static_cast<int64_t>(col[ee]) * ldz + 4 * c4);
+                }
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u)
+                    if (e + u < end) acc += v[u];
+            }
+            if (MEAN) acc = acc / static_cast<float>(end - beg);
+            float *o = out + static_cast<int64_t>(d) * ldo + 4 * c4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo) o[j] += acc[j];
+        }
+    }
+}
+
 }  // namespace
 
 // Returns 1 and stores the launch status in *rc when the row-tile kernel
@@ -756,7 +828,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
-                     const float *const *x_dev, bool exact) {
+                     const float *const *x_dev, bool exact, float *z, int64_t ldz) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -770,6 +842,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
     // columns become one zero-padded bf16 chunk)
     const bool x3 = !exact && ldw > 0;
+    // narrow mode: one launch computes [x W_r^T | x W_l^T] (2 NT1 tiles) --
+    // X3 only, no neighbour term, no saved aggregate, no column slicing
+    const bool narrow = z != nullptr;
+    if (narrow && (!x3 || !wl_packed || ldz < ceil_div(Fo, 16) * 16 || ldz % 4 != 0 || !aligned(z, 16) ||
+                   n_rows * ldz * 4 > lim))
+        return 0;
     int C = static_cast<int>(K / 32), T4 = static_cast<int>(ceil_div(K % 32, 4)), kpad = 0;
     if (T4 > X3_TAIL_MAX) {
         C += 1;
@@ -782,23 +860,26 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                               : frag_kb;
     const size_t lds_cap = 160 * 1024 - 1024;  // minus the bias slice
     int ntw_max = 0;
-    for (int c : {16, 8, 4, 3, 2})
+    for (int c : {16, 8, 6, 4, 3, 2})
         if (static_cast<size_t>(c) * root_kb <= lds_cap) {
             ntw_max = c;
             break;
         }
     if (ntw_max == 0) return 0;
-    const int64_t slice = 16 * static_cast<int64_t>(ntw_max);
+    if (narrow && 2 * ceil_div(Fo, 16) > ntw_max) return 0;  // both halves in one image
+    const int64_t slice = narrow ? Fo : 16 * static_cast<int64_t>(ntw_max);
     const Dropout drop = make_dropout(p_drop, seed);
     for (int64_t c0 = 0; c0 < Fo; c0 += slice) {
         const int64_t Fo_c = std::min<int64_t>(slice, Fo - c0);
-        const int NT = static_cast<int>(ceil_div(Fo_c, 16));
-        const int NTW = NT <= 2 ? 2 : NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 8 ? 8 : 16;
+        const int NT1 = static_cast<int>(ceil_div(Fo_c, 16));
+        const int NT = narrow ? 2 * NT1 : NT1;
+        const int NTW = NT <= 2 ? 2 : NT <= 3 ? 3 : NT <= 4 ? 4 : NT <= 6 ? 6 : NT <= 8 ? 8 : 16;
         const size_t rbytes = static_cast<size_t>(NTW) * root_kb;
         const size_t wbytes = static_cast<size_t>(NTW) * frag_kb;
         const size_t bbytes = static_cast<size_t>(NTW) * 16 * sizeof(float);
         // W_l (fp32) shares the LDS when both fit; otherwise its fragments stream from L2
-        const bool wl_lds = wl_packed == nullptr || rbytes + wbytes + bbytes <= lds_cap + 1024;
+        const bool has_l = wl_packed != nullptr && !narrow;
+        const bool wl_lds = has_l && rbytes + wbytes + bbytes <= lds_cap + 1024;
         const size_t lds = rbytes + (wl_lds ? wbytes : 0) + bbytes;
         const int64_t toff = (c0 / 16) * KG * 64;
         RtArgs a;
@@ -813,14 +894,14 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         // a slice's weights: packed fragments are n-tile major (contiguous
         // sub-array); raw weights are rows [c0, c0 + Fo_c)
         const int64_t woff = ldw ? c0 * ldw / 4 : toff;
-        a.wl = wl_packed ? static_cast<const v4f *>(wl_packed) + woff : nullptr;
+        a.wl = has_l ? static_cast<const v4f *>(wl_packed) + woff : nullptr;
         a.wr = static_cast<const v4f *>(wr_packed) + woff;
         a.wr_raw = ldw ? static_cast<const float *>(wr_packed) + c0 * ldw : nullptr;
         a.ldw = ldw;
         a.C = C;
         a.T4 = T4;
         a.kpad = kpad;
-        if (ldw && wl_packed && !wl_lds) {
+        if (ldw && has_l && !wl_lds) {
             // raw W_l that must stream from L2: pack it once (all slices) into
             // the caller's workspace -- fragment-ordered 1-KiB wave loads
             if (c0 == 0) {
@@ -838,11 +919,16 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             a.wl = static_cast<const v4f *>(wl_ws) + toff;
         }
         a.NT = NT;
+        a.NT1 = NT1;
+        a.wz_raw = narrow ? static_cast<const float *>(wl_packed) : nullptr;
+        a.z = z;
+        a.ldz = ldz;
+        a.z_bytes = narrow ? static_cast<uint32_t>(((n_rows - 1) * ldz + 16 * NT1) * 4) : 0u;
         a.Fo = static_cast<int>(Fo_c);
         a.out = out + c0;
         a.ldo = ldo;
         a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(out + c0, 16);
-        a.agg_out = c0 == 0 ? agg_out : nullptr;
+        a.agg_out = (c0 == 0 && !narrow) ? agg_out : nullptr;
         a.ld_agg = ld_agg;
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         a.seed_dev = seed_dev;
@@ -855,6 +941,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
             case 3: *rc = dispatch_rt<3>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
             case 4: *rc = dispatch_rt<4>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
+            case 6: *rc = dispatch_rt<6>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
             case 8: *rc = dispatch_rt<8>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
             default: *rc = dispatch_rt<16>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
         }
@@ -868,8 +955,10 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
 using namespace ngnn;
 
 extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows) {
-    (void)n_rows;  // a packed W_l (when it cannot sit in LDS)
-    return ngnn_pack_weight_bytes(Fo, K);
+    // a packed W_l (when it cannot sit in LDS), or narrow mode's z rows
+    const size_t z = static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * ceil_div(Fo, 16) * 16 *
+                     sizeof(float);
+    return std::max(ngnn_pack_weight_bytes(Fo, K), z);
 }
 
 extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx,
@@ -884,7 +973,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     (void)n_edge_rows;  // (row hints of the retired split path; kept for the ABI)
     (void)n_edge_rows_dev;
     const bool exact = (reduce & NGNN_MATH_EXACT_F32) != 0;
-    reduce &= ~NGNN_MATH_EXACT_F32;
+    const bool want_narrow = (reduce & NGNN_FWD_NARROW) != 0;
+    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW);
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
     NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || !wr, NGNN_E_ARG);
     NGNN_RETURN_IF(wl && !rowptr, NGNN_E_ARG);
@@ -896,9 +986,34 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     NGNN_RETURN_IF((!x && !x_dev) || !out, NGNN_E_ARG);
     hipStream_t st = as_stream(stream);
     int rc = NGNN_OK;
+    // narrow mode (MEAN / SUM): the neighbour term aggregated in the F_out-wide
+    // space (z = x W_l^T, then a gather of z), no saved aggregate
+    const int64_t ldz = ceil_div(Fo, 16) * 16;
+    if (want_narrow && wl && reduce != NGNN_REDUCE_MAX && !agg_out && !relu && !(p_drop > 0.0f) &&
+        ws && aligned(ws, 16) &&
+        ws_bytes >= static_cast<size_t>(n_rows) * ldz * sizeof(float)) {
+        float *z = static_cast<float *>(ws);
+        if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
+                             out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
+                             nullptr, 0, x_dev, exact, z, ldz)) {
+            if (rc) return rc;
+            const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
+            const unsigned grid = static_cast<unsigned>(
+                std::max<int64_t>(1, std::min<int64_t>(4 * num_cus(), ceil_div(rows, 16))));
+            if (reduce == NGNN_REDUCE_MEAN)
+                hipLaunchKernelGGL(k_narrow_agg<true>, dim3(grid), dim3(256), 0, st, z, ldz,
+                                   static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows),
+                                   n_rows_dev, n_edge_rows_dev, out, ldo);
+            else
+                hipLaunchKernelGGL(k_narrow_agg<false>, dim3(grid), dim3(256), 0, st, z, ldz,
+                                   static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows),
+                                   n_rows_dev, n_edge_rows_dev, out, ldo);
+            return launch_status();
+        }
+    }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
-                          ws_bytes, x_dev, exact))
+                          ws_bytes, x_dev, exact, nullptr, 0))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

@@ -21,6 +21,7 @@ OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
 MATH_EXACT_F32 = 0x100  # OR-ed into ngnn_sage_fwd_raw's reduce (include/ngnn.h)
+FWD_NARROW = 0x200      # same: output layer aggregated in the F_out-wide space
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one

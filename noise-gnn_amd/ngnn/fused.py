@@ -137,13 +137,25 @@ def _gemm_layer(x, K, n_rows, block, reduce, pl, pr, bias, Fo, out, relu, p_drop
     _lib.check(rc, "ngnn_sage_fwd")
 
 
+def narrow_ok(reduce: str, K: int, Fo: int, relu: bool, p_drop: float) -> bool:
+    """Can this layer aggregate its neighbour term in the F_out-wide space
+    (NGNN_FWD_NARROW)?  A linear aggregation into a narrower output layer
+    with no epilogue beyond the bias, on the split-MFMA path, with both
+    weight halves in one LDS image (2 ceil(F_out/16) <= 6 tiles)."""
+    return (reduce in ("mean", "sum") and not relu and p_drop == 0.0 and Fo < K
+            and -(-Fo // 16) <= 3 and not _exact_f32)
+
+
 def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu: bool,
                    p_drop: float, seed: int, agg_out: torch.Tensor | None = None,
                    seed_dev: torch.Tensor | None = None,
-                   x_dev: torch.Tensor | None = None, span: str = "sage_fwd") -> torch.Tensor:
+                   x_dev: torch.Tensor | None = None, span: str = "sage_fwd",
+                   narrow: bool = False) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
-    supplies the shape."""
+    supplies the shape.  narrow: aggregate the neighbour term as mean/sum of
+    z = x W_l^T (F_out wide) instead of x (K wide) -- the output layer's form
+    (no agg_out then)."""
     N, K = x.shape
     Fo = wl.shape[0]
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
@@ -164,7 +176,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         rc = lib.ngnn_sage_fwd_raw(
             _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, n_edge,
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
-            _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
+            _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
+            | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0),
             _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
@@ -190,11 +203,14 @@ class _SAGEStack(torch.autograd.Function):
         for i in range(L):
             wl, bl, wr = params[3 * i:3 * i + 3]
             last = i == L - 1
-            agg = torch.empty(h.shape, dtype=torch.float32, device=h.device)
+            # the output layer aggregates in the F_out-wide space when it can
+            # (its K-wide aggregate is rebuilt for the seed rows in backward)
+            narrow = last and i > 0 and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0)
+            agg = None if narrow else torch.empty(h.shape, dtype=torch.float32, device=h.device)
             h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=not last,
                                p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg,
                                seed_dev=seed_dev, x_dev=block.x_dev if i == 0 else None,
-                               span=f"sage_fwd_l{i}")
+                               span=f"sage_fwd_l{i}", narrow=narrow)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -250,7 +266,8 @@ class _SAGEStack(torch.autograd.Function):
         for i in reversed(range(L)):
             h_in, y_out, agg = acts[i], acts[i + 1], aggs[i]
             if _debug_grads is not None:  # test/debug hook: d(acts[i+1]) per layer
-                _debug_grads.append((i, dy.detach().clone(), agg.detach().clone(),
+                _debug_grads.append((i, dy.detach().clone(),
+                                     None if agg is None else agg.detach().clone(),
                                      h_in.detach().clone()))
             wl, bl, wr = params[3 * i:3 * i + 3]
             Fo, K = wl.shape
@@ -263,6 +280,17 @@ class _SAGEStack(torch.autograd.Function):
             dwl, dbl, dwr = (
                 (g.view(q.shape) if g is not None else torch.empty_like(q))
                 for g, q in zip(ctx.gouts[3 * i:3 * i + 3], (wl, bl, wr)))
+            if agg is None:
+                # narrow-mode layer: the K-wide aggregate the weight gradient
+                # reads (rows < R) gathered now -- R rows when the loss told us
+                # R (the seed rows), else every row
+                R = int(rows_hint) if (rows_hint is not None and i == L - 1) else N
+                agg = torch.empty(max(R, 1), K, dtype=torch.float32, device=dev)
+                with _timing.span("sage_agg_seed_rows", 0, 0):
+                    _lib.check(lib.ngnn_seg_agg_fwd(
+                        _lib.ptr(h_in), h_in.stride(0), K, _lib.ptr(block.rowptr),
+                        _lib.ptr(block.col), R, red, _lib.F32, _lib.ptr(agg), agg.stride(0),
+                        stream), "ngnn_seg_agg_fwd")
             wsb = lib.ngnn_sage_wgrad_workspace_bytes(Fo, K)
             ws = _workspace(dev, "wgrad", wsb)
             with _timing.span("sage_wgrad", 0, 0):  # row bound is device-side: no host count

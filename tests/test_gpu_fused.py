@@ -143,6 +143,31 @@ def test_math_modes_against_fp64(K, Fo):
     assert e_split <= 2.0 * max(e_exact, e_ref) + 1e-7, (e_split, e_exact, e_ref)
 
 
+@pytest.mark.parametrize("K,Fo", [(256, 47), (128, 40), (64, 10), (100, 16), (256, 48), (33, 20)])
+@pytest.mark.parametrize("reduce", ["mean", "sum"])
+def test_narrow_output_layer_matches_oracle(K, Fo, reduce):
+    """NGNN_FWD_NARROW (the output layer's form): z = x W_l^T for every row
+    in the root-term launch, then out[d] += mean/sum of z over d's in-edges
+    -- equal to the oracle's lin_l(agg(x)) + lin_r(x) at the fp32 bar, with
+    and without the edge-row bound (rows past it have no in-edges)."""
+    N = 900
+    g = torch.Generator().manual_seed(K + Fo)
+    ei = rand_block(K * 3 + Fo, N, 5000)
+    ei = ei[:, ei[1] < 600]  # rows >= 600 receive no edges
+    x = torch.randn(N, K, generator=g)
+    conv = pyg_ref.SAGEConv(K, Fo)
+    conv.aggr = reduce
+    with torch.no_grad():
+        want = conv(x, ei)
+    for n_act in (None, 600):
+        blk = Block(ei.to(DEV), N)
+        blk.n_active = n_act
+        got = sage_layer_fwd(x.to(DEV), blk, reduce, conv.lin_l.weight.to(DEV),
+                             conv.lin_l.bias.to(DEV), conv.lin_r.weight.to(DEV), relu=False,
+                             p_drop=0.0, seed=0, narrow=True).cpu()
+        torch.testing.assert_close(got, want, **OUT)
+
+
 class _MaskedSAGE(pyg_ref.SAGE):
     """Oracle SAGE whose dropout uses given keep masks (one per hidden layer)."""
 

@@ -46,7 +46,8 @@ def main():
     b = sample_block(g, g.train_idx[:1024], [15, 10], seed=1)
     N, E = b.num_nodes, b.edge_index.shape[1]
     blk = Block(b.edge_index, N)
-    res = {"N": N, "E": E}
+    blk.n_active = int(b.edge_index[1].max()) + 1  # the sampler's row hint
+    res = {"N": N, "E": E, "n_edge_rows": blk.n_active}
     torch.manual_seed(0)
     only = set(a.only.split(",")) if a.only else None
     h = torch.randn(N, 256, device=dev).relu()
@@ -63,7 +64,13 @@ def main():
                                    agg_out=agg_)
             return f
         empty = Block(torch.empty(2, 0, dtype=torch.long, device=dev), N)
+        def run_narrow():
+            def f():
+                sage_layer_fwd(x, blk, "mean", wl, bl, wr, relu=False, p_drop=0.0, seed=7,
+                               narrow=True)
+            return f
         cases = {f"{tag}_model_x3": run(), f"{tag}_model_exact": run(ex=True),
+                 f"{tag}_narrow_x3": run_narrow(),
                  f"{tag}_nodrop_x3": run(p_=0.0), f"{tag}_noedges_x3": run(blk_=empty, agg_=None),
                  f"{tag}_noedges_nodrop_x3": run(p_=0.0, blk_=empty, agg_=None),
                  f"{tag}_noedges_exact": run(ex=True, blk_=empty, agg_=None)}
