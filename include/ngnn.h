@@ -256,7 +256,8 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * host value): rows at or past it have no in-edges (NGNN_FWD_NARROW's
  * gather stops there; NeighborLoader numbers the rows that receive edges
  * first).  Pass n_rows when unknown.
- * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes. */
+ * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes (calls sharing
+ * a ws must be stream-ordered). */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,

@@ -453,6 +453,8 @@ template <int NTW, int RED, int WLM, bool X3, bool VEC>
 __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     constexpr bool WL_LDS = WLM == 1;
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
+    __shared__ int s_next_tile;       // the workgroup's tile-claim counter
+    if (threadIdx.x == 0) s_next_tile = RT_WAVES;  // each wave's first tile is fixed
     const int nfr = NTW * a.KG * 64;  // fragments per fp32 weight matrix (NTW tiles, zero padded)
     // X3 image: [3][C][NTW][64] bf16x8 (16 B each) + fp32 tail [T4][NTW][64]
     const int pst = a.C * NTW * 64;                        // bf16x8 per piece
@@ -579,8 +581,24 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // first (measured: -0.3..0.4 % step time)
     const int w0 = blockIdx.x + gridDim.x * wave;
     auto tile_of = [&](int k) { return k == 0 ? w0 : k * tstride + (tstride - 1 - w0); };
+    // dynamic scheduling inside the workgroup: the workgroup owns tiles
+    // blockIdx.x + j gridDim.x (round-robin over workgroups, as before) and
+    // its waves claim them one at a time from an LDS counter -- the rows with
+    // in-edges come first in a NeighborLoader block and their tiles take
+    // several times longer, so a fixed tile-per-wave map leaves the waves
+    // that drew them finishing last.  (A chip-wide counter in global memory
+    // serialises ~10k same-address atomics: measured 2x slower.)  A wave
+    // claims its next tile when it starts the current one.
+    auto claim = [&]() -> int {
+        int j = 0;
+        if ((threadIdx.x & 63) == 0) j = atomicAdd(&s_next_tile, 1);
+        return static_cast<int>(blockIdx.x) +
+               __builtin_amdgcn_readfirstlane(__shfl(j, 0)) * static_cast<int>(gridDim.x);
+    };
+    (void)tile_of;
     int kt = 0;
-    int t = w0;
+    int t = static_cast<int>(blockIdx.x) + wave * static_cast<int>(gridDim.x);  // first claims: waves 0..7
+    int tnext = 0;
     // next tile's chunk-0 x fragments and row bounds, loaded one tile ahead,
     // unconditionally (a tile past the end re-reads tile 0: valid, unused)
     v4f xn[RT_KC];
@@ -622,7 +640,8 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         }
     };
     prefetch(t);
-    for (; t < n_tiles; t = tile_of(++kt)) {
+    for (; t < n_tiles; t = tnext, ++kt) {
+        tnext = claim();
         int lane, q, rl;
         lane_ids(lane, q, rl);
         // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
@@ -664,7 +683,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             if (c + 1 < nchunk) {
                 load_x<X3>(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
             } else if (maxdeg == 0) {
-                prefetch(tile_of(kt + 1));  // next tile: a whole tile of MFMAs to land
+                prefetch(tnext);  // next tile: a whole tile of MFMAs to land
             }
             if (X3) {
                 const int ncc = min(4, a.C - 4 * c);
@@ -684,7 +703,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q);
                 // edge tiles prefetch the next tile only now: its x fragments
                 // are not live across the gather (register budget)
-                if (c == nchunk_l - 1) prefetch(tile_of(kt + 1));
+                if (c == nchunk_l - 1) prefetch(tnext);
                 if (a.agg_out) {
                     int kq = a.K - k0 - 4 * q;
                     asm volatile("" : "+v"(kq));  // per-lane masks stay VGPR selects here
@@ -736,8 +755,9 @@ int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
     auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
+        // 160 KiB per CU minus the kernel's static LDS (the tile counter)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
         attr_set = true;
     }
     const int grid = static_cast<int>(
@@ -858,7 +878,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // one m-tile of the root image: X3 3 parts x C chunks x 1 KiB + the tail
     const size_t root_kb = x3 ? (static_cast<size_t>(3 * C) * 64 * 16 + static_cast<size_t>(T4) * 64 * 4)
                               : frag_kb;
-    const size_t lds_cap = 160 * 1024 - 1024;  // minus the bias slice
+    const size_t lds_cap = 160 * 1024 - 1024 - 256;  // minus the bias slice and static LDS
     int ntw_max = 0;
     for (int c : {16, 8, 6, 4, 3, 2})
         if (static_cast<size_t>(c) * root_kb <= lds_cap) {

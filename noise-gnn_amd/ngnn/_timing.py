@@ -26,6 +26,7 @@ class Rec:
     start: torch.cuda.Event
     end: torch.cuda.Event
     flops: int = 0
+    mfma_s: float = 0.0  # ideal matrix-core time of the launch's instruction mix
 
 
 class KernelTimer:
@@ -60,16 +61,18 @@ class KernelTimer:
         _active = self._prev
 
     def summary(self):
-        """{name: (launches, total_ms, total_bytes, total_flops)} — call after a synchronize."""
+        """{name: (launches, total_ms, total_bytes, total_flops, total_mfma_s)} —
+        call after a synchronize."""
         out = {}
         for r in self.recs:
-            n, ms, b, f = out.get(r.name, (0, 0.0, 0, 0))
-            out[r.name] = (n + 1, ms + r.start.elapsed_time(r.end), b + r.bytes, f + r.flops)
+            n, ms, b, f, m = out.get(r.name, (0, 0.0, 0, 0, 0.0))
+            out[r.name] = (n + 1, ms + r.start.elapsed_time(r.end), b + r.bytes, f + r.flops,
+                           m + r.mfma_s)
         return out
 
 
 @contextlib.contextmanager
-def span(name: str, nbytes: int, flops: int = 0):
+def span(name: str, nbytes: int, flops: int = 0, mfma_s: float = 0.0):
     t = _active
     if t is None or (t.only is not None and name not in t.only):
         yield
@@ -78,4 +81,4 @@ def span(name: str, nbytes: int, flops: int = 0):
     s.record()
     yield
     e.record()
-    t.recs.append(Rec(name, int(nbytes), s, e, int(flops)))
+    t.recs.append(Rec(name, int(nbytes), s, e, int(flops), float(mfma_s)))

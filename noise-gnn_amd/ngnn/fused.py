@@ -43,6 +43,11 @@ _ws: dict = {}
 # section 3).  True: exact fp32 MFMA (a fmaf chain), like torch.backends'
 # allow_tf32 = False.
 _exact_f32 = False
+MFMA_F32_TFS = 157.3  # dense f32 MFMA peak, MI355X (MI355X_MICROARCH.md); bf16 is 16x
+
+
+def _pad16(n: int) -> int:
+    return -(-n // 16) * 16
 # debug hook (None in normal use): a list receives (layer, d output, saved
 # aggregate) from every fused-stack backward
 _debug_grads = None
@@ -162,14 +167,26 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     # algorithmic bytes: x + gathered rows + col + rowptr + out;  flops: root GEMM on
     # every row + neighbour GEMM on rows with in-edges (0 if not known: conservative)
     nbytes = (N * K + block.E * (K + 1) + N * Fo) * 4 + (N + 1) * 4
-    flops = 2 * N * K * Fo + 2 * (block.n_active or 0) * K * Fo
+    n_e = int(block.n_active or 0)
+    flops = 2 * N * K * Fo + 2 * n_e * K * Fo
+    # ideal matrix-core time of the instruction mix: the
+    # root term on 6 bf16 products per fp32 product (bf16 dense 16x the f32
+    # MFMA rate) unless exact, the neighbour term on f32 MFMA
+    root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
+    mfma_s = 2 * N * K * Fo / root_rate + 2 * n_e * K * Fo / (MFMA_F32_TFS * 1e12)
+    if narrow and agg_out is None:
+        # narrow mode: the root launch also computes z = x W_l^T (every row),
+        # then gathers z (F_out wide) instead of x
+        nbytes = (N * K + N * Fo + N * _pad16(Fo) + block.E * (_pad16(Fo) + 1)) * 4 + (N + 1) * 4
+        flops = 4 * N * K * Fo
+        mfma_s = 4 * N * K * Fo / root_rate
     wl_, wr_ = wl.detach(), wr.detach()
     if wl_.stride(1) != 1 or wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0):
         wl_, wr_ = wl_.contiguous(), wr_.contiguous()
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
-    with _timing.span(span, nbytes, flops):
+    with _timing.span(span, nbytes, flops, mfma_s):
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel
         n_edge = N if block.n_active is None else min(int(block.n_active), N)
