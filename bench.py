@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--dataset", default="ogbn-products",
                     help="synthetic graph shape (ngnn.loader.DATASETS); the headline is ogbn-products")
     ap.add_argument("--aggr", default="mean", choices=["mean", "max", "sum"])
+    ap.add_argument("--module", default="sage", choices=["sage", "gcn"],
+                    help="model.py's `module`: SAGE (sage.py) or SimpleGCN (convolution.py)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                     help="model / feature storage dtype (bf16: fp32 kernels inside)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,7 +62,7 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python instead of replaying the captured "
                          "HIP graph of the step")
-    ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1",
+    ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg",
                     help="comma list of kernel spans timed with HIP events in the timed region "
                          "('all', or 'none' for profiler runs)")
     return ap.parse_args()
@@ -134,7 +136,8 @@ def cpu_baseline(batches, args, layers):
     def run(threads, seconds, max_steps):
         torch.set_num_threads(threads)
         torch.manual_seed(0)
-        m = pyg_ref.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr)
+        m = (pyg_ref.SimpleGCN(F_in, args.hidden, C, layers, dropout=0.5) if args.module == "gcn"
+             else pyg_ref.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr))
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
         x, ei, y, bs = host[0]
         pyg_ref.train_step(m, opt, x, ei, y, bs)  # warm
@@ -193,7 +196,10 @@ def main():
     _, _, F_in, C, _ = DATASETS[args.dataset]
     graph = synthetic_graph(args.dataset, dev, seed=0, scale=args.scale)
     torch.manual_seed(1234)  # identical init on every rank
-    model = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
+    if args.module == "gcn":
+        model = ngnn.SimpleGCN(F_in, args.hidden, C, layers, dropout=0.5).to(dev)
+    else:
+        model = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
     if args.dtype == "bf16":
         model = model.to(torch.bfloat16)
         graph.x = graph.x.to(torch.bfloat16)
@@ -272,8 +278,10 @@ def main():
         dt, edges = float(t[0]), float(t[1])
 
     workload = f"{args.dataset.replace('ogbn-', '')}-[{args.fanout}]-bs{args.batch_size}"
-    if args.aggr != "mean":
+    if args.aggr != "mean" and args.module == "sage":
         workload += f"-{args.aggr}"
+    if args.module == "gcn":
+        workload += "-gcn"
     # dominant kernel roofline from the live events of the timed region
     summ = timer.summary()
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
@@ -342,7 +350,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic (seeded Chung-Lu graph with {args.dataset} sizes; random features)",
             "config": {"workload": workload,
-                       "model": f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)",
+                       "model": (f"SimpleGCN({F_in},{args.hidden},{C},L={layers}) sum-aggr + Adam(1e-3)"
+                                 if args.module == "gcn" else
+                                 f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)"),
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),
                        "parallelism": f"dp{world} (seed-sharded, {_allreduce_name(world)} grad all-reduce)"},

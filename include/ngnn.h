@@ -252,6 +252,8 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * ngnn_sage_fwd.  x_dev (nullable): a device word holding x's address, read
  * at run time instead of x (a HIP-graph slot whose batch stays where the
  * loader put it; 16-B aligned, row stride ldx, rows < *n_rows_dev).
+ * wr == NULL: no root term (GCNConv's form, see ngnn_gcn_agg_fwd; raw
+ * weights only, not with NGNN_FWD_NARROW).
  * n_edge_rows / n_edge_rows_dev (device int, nullable, min'd with the
  * host value): rows at or past it have no in-edges (NGNN_FWD_NARROW's
  * gather stops there; NeighborLoader numbers the rows that receive edges
@@ -267,6 +269,22 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, in
                       int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                       const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
                       size_t ws_bytes, void *stream);
+
+/* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
+ * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The
+ * fused path runs it as SAGE with W_r = 0 (linear aggregation: A x W^T ==
+ * (A x) W^T up to fp32 rounding): aggregate-first through
+ * ngnn_sage_fwd_raw(wr = NULL, wl = W, reduce = SUM) when F_in <= F_out,
+ * else transform-first: z = x W^T through ngnn_sage_fwd_raw(wl = NULL, wr =
+ * W, bias = NULL) into z [n_rows, ldz], then this launch:
+ *   out[d] = act(sum_{e into d, edge order} z[col[e]] + b)   for every row
+ *   d < min(n_rows, *n_rows_dev) (act = ReLU + quad-hash dropout as the
+ *   row-tile epilogue; rows without in-edges get act(b)).
+ * ldz >= ceil4(Fo), z 16-B aligned. */
+int ngnn_gcn_agg_fwd(const float *z, int64_t ldz, int64_t Fo, const int32_t *rowptr,
+                     const int32_t *col, int64_t n_rows, const int32_t *n_rows_dev,
+                     const float *bias, int relu, float p_drop, uint64_t seed,
+                     const uint64_t *seed_dev, float *out, int64_t ldo, void *stream);
 
 /* ------------------------------------------ backward receptive-field bounds
  * ngnn_row_extent: out[0] = max(out[0], 1 + last row of g[n_rows, F] holding a

@@ -832,6 +832,64 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
     }
 }
 
+// ---- GCNConv(normalize=False) aggregation of transformed rows, with the
+// layer epilogue: out[d] = act(sum_{e into d} z[col[e]] + b) for EVERY row
+// d < min(n_rows, *n_rows_dev) (rows without in-edges: act(b)) -- PyG's
+// propagate(lin(x)) (aggr='add', edge order from 0) then + bias
+// (convolution.py:29-35).  ReLU and the quad-hash dropout exactly as the
+// row-tile epilogue (global column keys, col_base 0).  16 lanes per row,
+// float4 columns, 8 neighbour rows in flight per lane.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gcn_agg(const float *__restrict__ z, int64_t ldz, int Fo,
+                                                 const int32_t *__restrict__ rowptr,
+                                                 const int32_t *__restrict__ col, int n_rows,
+                                                 const int32_t *__restrict__ n_rows_dev,
+                                                 const float *__restrict__ bias, Epi epi,
+                                                 const uint64_t *__restrict__ seed_dev,
+                                                 float *__restrict__ out, int64_t ldo) {
+    int nr = n_rows;
+    if (n_rows_dev) nr = min(nr, *n_rows_dev);
+    if (seed_dev) epi.drop.reseed(*seed_dev);
+    const int sub = threadIdx.x & 15;
+    const int F4 = (Fo + 3) >> 2;
+    for (int d = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; d < nr; d += (gridDim.x * blockDim.x) >> 4) {
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        const uint32_t rk = epi.drop.thresh ? epi.drop.row_key(static_cast<uint32_t>(d)) : 0u;
+        for (int c4 = sub; c4 < F4; c4 += 16) {
+            v4f acc{0.f, 0.f, 0.f, 0.f};
+            for (int e = beg; e < end; e += NA_UNR) {
+                v4f v[NA_UNR];
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u) {
+                    const int ee = min(e + u, end - 1);
+                    v[u] = *reinterpret_cast<const v4f *>(z + static_cast<int64_t>(col[ee]) * ldz + 4 * c4);
+                }
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u)
+                    if (e + u < end) acc += v[u];
+            }
+            const uint32_t h = epi.drop.thresh ? lowbias32(rk + static_cast<uint32_t>(c4)) : 0u;
+            v4f o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = 4 * c4 + j;
+                float y = acc[j] + ((bias && c < Fo) ? bias[c] : 0.0f);
+                bool zero = epi.relu && y < 0.0f;  // NaN passes, like torch.relu
+                if (epi.drop.thresh) zero = zero || ((h >> (8 * j)) & 0xffu) < epi.drop.thresh;
+                o[j] = zero ? 0.0f : (epi.drop.thresh ? y * epi.drop.scale : y);
+            }
+            float *op = out + static_cast<int64_t>(d) * ldo + 4 * c4;
+            if (VEC) {
+                *reinterpret_cast<v4f *>(op) = o;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * c4 + j < Fo) op[j] = o[j];
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // Returns 1 and stores the launch status in *rc when the row-tile kernel
@@ -853,6 +911,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
         return 0;
+    const bool no_root = wr_packed == nullptr;  // raw weights only (checked by the caller)
     if (agg_out && (ld_agg % 4 != 0 || !aligned(agg_out, 16))) return 0;
     // byte offsets are 32-bit (buffer resources): every buffer < 2 GiB
     const int64_t lim = (int64_t(1) << 31) - 4096;
@@ -861,7 +920,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     const int KG = static_cast<int>(ceil_div(K, 16));
     // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
     // columns become one zero-padded bf16 chunk)
-    const bool x3 = !exact && ldw > 0;
+    // (no root term: the X3 layout with an empty image -- no MFMAs, no LDS)
+    const bool x3 = (!exact && ldw > 0) || no_root;
     // narrow mode: one launch computes [x W_r^T | x W_l^T] (2 NT1 tiles) --
     // X3 only, no neighbour term, no saved aggregate, no column slicing
     const bool narrow = z != nullptr;
@@ -874,14 +934,17 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         T4 = 0;
         kpad = 1;
     }
+    if (no_root) C = T4 = kpad = 0;
     const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one fp32 m-tile, all of K
     // one m-tile of the root image: X3 3 parts x C chunks x 1 KiB + the tail
     const size_t root_kb = x3 ? (static_cast<size_t>(3 * C) * 64 * 16 + static_cast<size_t>(T4) * 64 * 4)
                               : frag_kb;
+    // (no root term: the slice width is set by the W_l image alone)
+    const size_t img_kb = no_root ? frag_kb : root_kb;
     const size_t lds_cap = 160 * 1024 - 1024 - 256;  // minus the bias slice and static LDS
     int ntw_max = 0;
     for (int c : {16, 8, 6, 4, 3, 2})
-        if (static_cast<size_t>(c) * root_kb <= lds_cap) {
+        if (static_cast<size_t>(c) * img_kb <= lds_cap) {
             ntw_max = c;
             break;
         }
@@ -915,8 +978,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         // sub-array); raw weights are rows [c0, c0 + Fo_c)
         const int64_t woff = ldw ? c0 * ldw / 4 : toff;
         a.wl = has_l ? static_cast<const v4f *>(wl_packed) + woff : nullptr;
-        a.wr = static_cast<const v4f *>(wr_packed) + woff;
-        a.wr_raw = ldw ? static_cast<const float *>(wr_packed) + c0 * ldw : nullptr;
+        a.wr = no_root ? nullptr : static_cast<const v4f *>(wr_packed) + woff;
+        a.wr_raw = (ldw && !no_root) ? static_cast<const float *>(wr_packed) + c0 * ldw : nullptr;
         a.ldw = ldw;
         a.C = C;
         a.T4 = T4;
@@ -996,7 +1059,10 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     const bool want_narrow = (reduce & NGNN_FWD_NARROW) != 0;
     reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW);
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
-    NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || !wr, NGNN_E_ARG);
+    // wr == NULL: no root term (GCNConv = SAGEConv with W_r = 0: the layer
+    // aggregates first, out = act(b + agg(x) W_l^T))
+    NGNN_RETURN_IF(K <= 0 || Fo <= 0 || n_rows < 0 || (!wr && !wl), NGNN_E_ARG);
+    NGNN_RETURN_IF(!wr && (want_narrow || ldw <= 0), NGNN_E_ARG);
     NGNN_RETURN_IF(wl && !rowptr, NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < K || ldo < Fo || ldw < K, NGNN_E_SHAPE);
     NGNN_RETURN_IF(agg_out && ld_agg < K, NGNN_E_SHAPE);
@@ -1036,4 +1102,29 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
                           ws_bytes, x_dev, exact, nullptr, 0))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
+}
+
+extern "C" int ngnn_gcn_agg_fwd(const float *z, int64_t ldz, int64_t Fo, const int32_t *rowptr,
+                                const int32_t *col, int64_t n_rows, const int32_t *n_rows_dev,
+                                const float *bias, int relu, float p_drop, uint64_t seed,
+                                const uint64_t *seed_dev, float *out, int64_t ldo, void *stream) {
+    NGNN_RETURN_IF(Fo <= 0 || n_rows < 0 || p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
+    NGNN_RETURN_IF(ldz < ceil_div(Fo, 4) * 4 || ldz % 4 != 0 || ldo < Fo, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(n_rows) || !fits_i32(Fo), NGNN_E_RANGE);
+    if (n_rows == 0) return NGNN_OK;
+    NGNN_RETURN_IF(!z || !rowptr || !col || !out, NGNN_E_ARG);
+    NGNN_RETURN_IF(!aligned(z, 16), NGNN_E_ALIGN);
+    const Epi epi{bias, relu, make_dropout(p_drop, seed), 0};
+    const unsigned grid = static_cast<unsigned>(
+        std::max<int64_t>(1, std::min<int64_t>(8 * num_cus(), ceil_div(n_rows, 16))));
+    const bool vec = Fo % 4 == 0 && ldo % 4 == 0 && aligned(out, 16);
+    if (vec)
+        hipLaunchKernelGGL(k_gcn_agg<true>, dim3(grid), dim3(256), 0, as_stream(stream), z, ldz,
+                           static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
+                           bias, epi, seed_dev, out, ldo);
+    else
+        hipLaunchKernelGGL(k_gcn_agg<false>, dim3(grid), dim3(256), 0, as_stream(stream), z, ldz,
+                           static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
+                           bias, epi, seed_dev, out, ldo);
+    return launch_status();
 }

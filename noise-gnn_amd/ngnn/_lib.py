@@ -63,6 +63,8 @@ SIGNATURES = {
     "ngnn_sage_fwd_raw": (_int, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _int, _p, _p, _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
+    "ngnn_gcn_agg_fwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _int, ctypes.c_float,
+                                ctypes.c_uint64, _p, _p, _i64, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),

@@ -164,25 +164,27 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     N, K = x.shape
     Fo = wl.shape[0]
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
+    root = wr is not None  # (None: GCNConv's aggregate-first form, no root term)
     # algorithmic bytes: x + gathered rows + col + rowptr + out;  flops: root GEMM on
     # every row + neighbour GEMM on rows with in-edges (0 if not known: conservative)
     nbytes = (N * K + block.E * (K + 1) + N * Fo) * 4 + (N + 1) * 4
     n_e = int(block.n_active or 0)
-    flops = 2 * N * K * Fo + 2 * n_e * K * Fo
+    flops = 2 * N * K * Fo * root + 2 * n_e * K * Fo
     # ideal matrix-core time of the instruction mix: the
     # root term on 6 bf16 products per fp32 product (bf16 dense 16x the f32
     # MFMA rate) unless exact, the neighbour term on f32 MFMA
     root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
-    mfma_s = 2 * N * K * Fo / root_rate + 2 * n_e * K * Fo / (MFMA_F32_TFS * 1e12)
+    mfma_s = 2 * N * K * Fo * root / root_rate + 2 * n_e * K * Fo / (MFMA_F32_TFS * 1e12)
     if narrow and agg_out is None:
         # narrow mode: the root launch also computes z = x W_l^T (every row),
         # then gathers z (F_out wide) instead of x
         nbytes = (N * K + N * Fo + N * _pad16(Fo) + block.E * (_pad16(Fo) + 1)) * 4 + (N + 1) * 4
         flops = 4 * N * K * Fo
         mfma_s = 4 * N * K * Fo / root_rate
-    wl_, wr_ = wl.detach(), wr.detach()
-    if wl_.stride(1) != 1 or wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0):
-        wl_, wr_ = wl_.contiguous(), wr_.contiguous()
+    wl_ = wl.detach()
+    wr_ = wr.detach() if root else None
+    if wl_.stride(1) != 1 or (root and (wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0))):
+        wl_, wr_ = wl_.contiguous(), (wr_.contiguous() if root else None)
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
@@ -195,18 +197,66 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0),
-            _lib.ptr(wl_), _lib.ptr(wr_), wr_.stride(0), _lib.ptr(bl), Fo,
+            _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
         if rc == _lib.E_SHAPE:
             if x_dev is not None:
                 raise _lib.NGNNError("zero-copy input outside the row-tile kernel's envelope")
-            pl, pr = pack_weight(wl), pack_weight(wr)
+            pl = pack_weight(wl)
+            pr = pack_weight(wr if root else _zeros_like_cached(wl))
             _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
                         agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
         else:
             _lib.check(rc, "ngnn_sage_fwd_raw")
+    return out
+
+
+def _zeros_like_cached(w: torch.Tensor) -> torch.Tensor:
+    """A persistent zero matrix shaped like w (GCN layers' W_r = 0)."""
+    key = (w.device, "zeros", tuple(w.shape))
+    z = _ws.get(key)
+    if z is None:
+        z = torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+        _ws[key] = z
+    return z
+
+
+def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: int,
+                        seed_dev=None, x_dev=None, span: str = "gcn_fwd"):
+    """GCNConv(normalize=False) layer in PyG's own order (convolution.py:19-35,
+    GCNConv [ext]): z = x W^T on the row-tile kernel (no bias, no epilogue),
+    then ngnn_gcn_agg_fwd: out = act(sum_{j->i} z_j + b) -- the form for
+    F_in > F_out (the gather runs at the narrower width)."""
+    N, K = x.shape
+    Fo = w.shape[0]
+    ldz = _pad16(Fo)
+    lib = _lib.load()
+    z = _workspace(x.device, "gcn_z", N * ldz * 4).view(torch.float32)[:N * ldz].view(N, ldz)
+    wd = w.detach() if w.stride(1) == 1 else w.detach().contiguous()
+    ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
+    nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
+    out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
+    root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
+    with _timing.span(span + "_z", (N * K + N * ldz) * 4, 2 * N * K * Fo, 2 * N * K * Fo / root_rate):
+        rc = lib.ngnn_sage_fwd_raw(
+            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, N, None, _lib.ptr(block.rowptr),
+            _lib.ptr(block.col), _lib.REDUCE["sum"] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
+            None, _lib.ptr(wd), wd.stride(0), None, Fo, _lib.ptr(z), ldz, 0, 0.0, 0, None, None, K,
+            _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
+        if rc == _lib.E_SHAPE:
+            if x_dev is not None:
+                raise _lib.NGNNError("zero-copy input outside the row-tile kernel's envelope")
+            _gemm_layer(x, K, N, None, "sum", None, pack_weight(w), None, Fo, z, False, 0.0, 0,
+                        n_rows_dev=block.n_rows_dev)
+        else:
+            _lib.check(rc, "ngnn_sage_fwd_raw")
+    with _timing.span(span + "_agg", (block.E * (ldz + 1) + N * Fo) * 4 + (N + 1) * 4):
+        _lib.check(lib.ngnn_gcn_agg_fwd(
+            _lib.ptr(z), ldz, Fo, _lib.ptr(block.rowptr), _lib.ptr(block.col), N, nrd, _lib.ptr(b),
+            int(relu), float(p_drop), seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(out),
+            out.stride(0), _lib.stream_handle(x.device)), "ngnn_gcn_agg_fwd")
     return out
 
 
@@ -220,14 +270,23 @@ class _SAGEStack(torch.autograd.Function):
         for i in range(L):
             wl, bl, wr = params[3 * i:3 * i + 3]
             last = i == L - 1
-            # the output layer aggregates in the F_out-wide space when it can
-            # (its K-wide aggregate is rebuilt for the seed rows in backward)
-            narrow = last and i > 0 and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0)
-            agg = None if narrow else torch.empty(h.shape, dtype=torch.float32, device=h.device)
-            h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=not last,
-                               p_drop=0.0 if last else p_drop, seed=seed + 7919 * i, agg_out=agg,
-                               seed_dev=seed_dev, x_dev=block.x_dev if i == 0 else None,
-                               span=f"sage_fwd_l{i}", narrow=narrow)
+            relu, p_i, seed_i = not last, (0.0 if last else p_drop), seed + 7919 * i
+            x_dev = block.x_dev if i == 0 else None
+            if wr is None and h.size(1) > wl.shape[0]:
+                # GCN layer narrowing its input: transform first (PyG's order),
+                # no saved aggregate (rebuilt for the rows backward needs)
+                agg = None
+                h = gcn_transform_first(h, block, wl, bl, relu, p_i, seed_i, seed_dev, x_dev,
+                                        span=f"gcn_fwd_l{i}")
+            else:
+                # the output layer aggregates in the F_out-wide space when it can
+                # (its K-wide aggregate is rebuilt for the seed rows in backward)
+                narrow = (wr is not None and last and i > 0
+                          and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0))
+                agg = None if narrow else torch.empty(h.shape, dtype=torch.float32, device=h.device)
+                h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
+                                   seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
+                                   span=f"sage_fwd_l{i}", narrow=narrow)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -287,6 +346,9 @@ class _SAGEStack(torch.autograd.Function):
                                      None if agg is None else agg.detach().clone(),
                                      h_in.detach().clone()))
             wl, bl, wr = params[3 * i:3 * i + 3]
+            gcn = wr is None  # GCN layer: SAGE with W_r = 0 (no root-term gradient)
+            if gcn:
+                wr = _zeros_like_cached(wl)
             Fo, K = wl.shape
             hidden = i != L - 1
             ymask = y_out if hidden else None
@@ -297,6 +359,9 @@ class _SAGEStack(torch.autograd.Function):
             dwl, dbl, dwr = (
                 (g.view(q.shape) if g is not None else torch.empty_like(q))
                 for g, q in zip(ctx.gouts[3 * i:3 * i + 3], (wl, bl, wr)))
+            if gcn:
+                dwr = _workspace(dev, "gcn_dwr", wr.numel() * 4).view(torch.float32)[
+                    :wr.numel()].view(wr.shape)
             if agg is None:
                 # narrow-mode layer: the K-wide aggregate the weight gradient
                 # reads (rows < R) gathered now -- R rows when the loss told us
@@ -319,7 +384,7 @@ class _SAGEStack(torch.autograd.Function):
                     bptr(i + 1), Fo, K, _lib.ptr(dwl), _lib.ptr(dbl), _lib.ptr(dwr),
                     _lib.ptr(ws), ws.numel(), stream)
             _lib.check(rc, "ngnn_sage_wgrad")
-            grads[3 * i:3 * i + 3] = [dwl, dbl, dwr]
+            grads[3 * i:3 * i + 3] = [dwl, dbl, None if gcn else dwr]
             if i == 0 and not need_dx:
                 break
             if not (pre_top and i == L - 1):
@@ -412,14 +477,37 @@ def zero_copy_ok(model, n_rows: int, in_dim: int) -> bool:
     buffer offsets over the slot's rows (x, the output, the saved aggregate)."""
     if not isinstance(getattr(model, "convs", None), torch.nn.ModuleList):
         return False
-    if getattr(model, "use_bn", False) or not hasattr(model.convs[0], "lin_r"):
+    if getattr(model, "use_bn", False):
         return False
-    if len({c.aggr for c in model.convs}) != 1:
+    c0 = model.convs[0]
+    if hasattr(c0, "lin_r"):
+        if len({c.aggr for c in model.convs}) != 1:
+            return False
+        fo = c0.lin_r.weight.shape[0]
+    elif hasattr(c0, "lin"):  # SimpleGCN: layer 0 reads x in either form
+        fo = c0.lin.weight.shape[0]
+    else:
         return False
-    fo = model.convs[0].lin_r.weight.shape[0]
     lim = (1 << 31) - 4096
     return (in_dim % 4 == 0 and n_rows * in_dim * 4 <= lim and n_rows * fo * 4 <= lim
             and -(-in_dim // 16) <= 79)
+
+
+def gcn_stack_supported(model, x) -> bool:
+    return (x.is_cuda and x.dtype in _IO_DTYPES and x.dim() == 2
+            and all(p.dtype in _IO_DTYPES for p in model.parameters()))
+
+
+def gcn_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor:
+    """SimpleGCN's forward (convolution.py:29-35) as ONE autograd node on the
+    fused kernels: each GCNConv(normalize=False) is the SAGE layer with W_r
+    = 0 and a sum aggregation (aggregate-first when F_in <= F_out, PyG's
+    transform-first otherwise), the backward the bounded SAGE backward.
+    bf16 models: bf16 storage, fp32 arithmetic (as sage_stack)."""
+    params = []
+    for conv in model.convs:
+        params += [conv.lin.weight, conv.bias, None]
+    return _run_stack(model, x, block, seed, seed_dev, params, "sum")
 
 
 def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor:
@@ -430,18 +518,23 @@ def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor
     params = []
     for conv in model.convs:
         params += [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
+    aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
+    return _run_stack(model, x, block, seed, seed_dev, params, aggr)
+
+
+def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str) -> torch.Tensor:
     out_dtype = x.dtype
     # weight gradients straight into registered bucket views (ngnn.distributed.GradAllReduce)
     # when autograd will adopt them: fp32 parameters whose .grad is unset
     gouts = tuple(getattr(q, "_ngnn_grad_out", None)
-                  if (q.grad is None and q.dtype == torch.float32 and q.requires_grad) else None
+                  if (q is not None and q.grad is None and q.dtype == torch.float32
+                      and q.requires_grad) else None
                   for q in params)
-    if out_dtype != torch.float32 or any(q.dtype != torch.float32 for q in params):
+    if out_dtype != torch.float32 or any(q is not None and q.dtype != torch.float32 for q in params):
         x = x.float()
-        params = [q.float() for q in params]
+        params = [None if q is None else q.float() for q in params]
         gouts = (None,) * len(params)
     p = model.dropout if model.training else 0.0
-    aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
     out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, *params)
     return out if out_dtype == torch.float32 else out.to(out_dtype)

@@ -22,6 +22,22 @@ from .block import get_block
 from .nn import GCNConv, SAGEConv
 
 
+def _dropout_seed(model, x, block):
+    """(host seed, device seed word) of a fused stack's hash dropout."""
+    seed, seed_dev = 0, None
+    if model.training and model.dropout > 0:
+        if torch.cuda.is_current_stream_capturing():
+            # HIP-graph capture: a device seed, fresh at every replay -- the
+            # slot's (advanced by each slot load), else drawn by torch's
+            # graph-safe generator inside the graph
+            seed_dev = block.seed_dev
+            if seed_dev is None:
+                seed_dev = torch.randint(0, 2**62, (1,), device=x.device)
+        else:
+            seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
+    return seed, seed_dev
+
+
 class SAGE(nn.Module):
     def __init__(self, in_size, hidden_size, out_size, num_layers, dropout=0.5, use_bn=False,
                  aggr: str = "mean"):
@@ -47,18 +63,7 @@ class SAGE(nn.Module):
         if fused.sage_stack_supported(self, x):
             # one autograd node for the stack: fused layer kernels forward,
             # receptive-field-bounded backward (ngnn/fused.py)
-            seed, seed_dev = 0, None
-            if self.training and self.dropout > 0:
-                if torch.cuda.is_current_stream_capturing():
-                    # HIP-graph capture: a device seed, fresh at every replay --
-                    # the slot's (advanced by each slot load), else drawn by
-                    # torch's graph-safe generator inside the graph
-                    seed_dev = block.seed_dev
-                    if seed_dev is None:
-                        seed_dev = torch.randint(0, 2**62, (1,), device=x.device)
-                else:
-                    seed = int(torch.randint(0, 2**62, (1,)).item())  # torch's (CPU) RNG stream
-            return fused.sage_stack(self, x, block, seed, seed_dev)
+            return fused.sage_stack(self, x, block, *_dropout_seed(self, x, block))
         if self.use_bn:
             x = self.bn1(x)
         for i, conv in enumerate(self.convs):
@@ -101,6 +106,10 @@ class SimpleGCN(nn.Module):
 
     def forward(self, x, edge_index):
         block = get_block(edge_index, x.size(0))
+        if fused.gcn_stack_supported(self, x):
+            # one autograd node for the stack (ngnn/fused.py: SAGE layers with
+            # W_r = 0, sum aggregation); dropout seed as SAGE.forward
+            return fused.gcn_stack(self, x, block, *_dropout_seed(self, x, block))
         for i, conv in enumerate(self.convs):
             x = conv(x, block)
             if i != self.num_layers - 1:

@@ -375,3 +375,90 @@ def test_dgrad_lowdim_shape_envelope():
         _lib.ptr(blk.col), N, bnd.data_ptr(), bnd.data_ptr() + 4, _lib.REDUCE["mean"],
         _lib.ptr(dh), K, 0, _lib.ptr(ws), ws.numel(), _lib.stream_handle(DEV))
     assert rc == _lib.E_SHAPE
+
+
+class _MaskedGCN(pyg_ref.SimpleGCN):
+    """Oracle SimpleGCN whose dropout uses given keep masks."""
+
+    def __init__(self, *a, masks=None, **k):
+        super().__init__(*a, **k)
+        self.masks = masks
+
+    def forward(self, x, edge_index):
+        for i, conv in enumerate(self.convs):
+            x = conv(x, edge_index)
+            if i != self.num_layers - 1:
+                x = x.relu()
+                x = x * self.masks[i] * dropout_scale(self.dropout)
+        return x
+
+
+@pytest.mark.parametrize("dims", [(100, 256, 47), (20, 32, 6), (64, 32, 40), (256, 128, 47)])
+@pytest.mark.parametrize("layers", [2, 3])
+@pytest.mark.parametrize("train", [False, True])
+def test_gcn_stack_fwd_bwd_matches_oracle(dims, layers, train):
+    """SimpleGCN (convolution.py:7-35) on the fused stack -- aggregate-first
+    layers (F_in <= F_out) and PyG's transform-first form (F_in > F_out) --
+    against the oracle: outputs, dx and every parameter gradient, with the
+    hash dropout replicated on the host."""
+    from ngnn.loader import sample_block, synthetic_graph
+    K, H, C = dims
+    graph = synthetic_graph("ogbn-products", DEV, seed=7, scale=0.005, num_features=K)
+    fan = [8, 5, 3][:layers]
+    b = sample_block(graph, graph.train_idx[:128], fan, seed=4)
+    N = b.num_nodes
+    torch.manual_seed(layers + K)
+    mine = ngnn.SimpleGCN(K, H, C, layers, dropout=0.5).to(DEV).train(train)
+    if train:
+        torch.manual_seed(99)
+        s = int(torch.randint(0, 2**62, (1,)).item())
+        torch.manual_seed(99)
+    x = b.x.clone().requires_grad_(True)
+    out = mine(x, b.edge_index)
+    F.cross_entropy(out[:b.batch_size], b.y[:b.batch_size]).backward()
+    if train:
+        masks = [dropout_keep(s + 7919 * i, N, H, 0.5).float() for i in range(layers - 1)]
+        ref = _MaskedGCN(K, H, C, layers, dropout=0.5, masks=masks)
+    else:
+        ref = pyg_ref.SimpleGCN(K, H, C, layers, dropout=0.5).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    xr = b.x.cpu().clone().requires_grad_(True)
+    out_r = ref(xr, b.edge_index.cpu())
+    F.cross_entropy(out_r[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
+    torch.testing.assert_close(out.detach().cpu(), out_r.detach(), **OUT)
+    torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
+    for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+
+
+def test_gcn_graph_step_matches_eager():
+    """SimpleGCN through GraphedTrainStep (zero-copy slot, captured step)
+    equals eager training on the same batches (dropout off)."""
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import NeighborLoader, synthetic_graph
+    g = synthetic_graph("ogbn-arxiv", DEV, seed=0, scale=0.05)
+    loader = NeighborLoader(g, g.train_idx, [10, 5], 256, shuffle=True, seed=3)
+    batches = [b for _, b in zip(range(4), loader)]
+    torch.manual_seed(11)
+    m_e = ngnn.SimpleGCN(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+    m_g = ngnn.SimpleGCN(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+    m_g.load_state_dict(m_e.state_dict())
+    o_e = torch.optim.Adam(m_e.parameters(), lr=1e-2, fused=True, capturable=True)
+    le = []
+    for b in batches:
+        loss = F.cross_entropy(m_e(b.x, b.edge_index)[:b.batch_size], b.y[:b.batch_size])
+        o_e.zero_grad(set_to_none=False)
+        loss.backward()
+        o_e.step()
+        le.append(float(loss))
+    o_g = torch.optim.Adam(m_g.parameters(), lr=1e-2, fused=True, capturable=True)
+    n_cap, e_cap = slot_size(256, [10, 5])
+    step = GraphedTrainStep(m_g, o_g, 256, n_cap, e_cap, g.x.size(1), DEV)
+    step.capture(batches[0].x, batches[0].edge_index, batches[0].y)
+    assert step.zero_copy
+    lg = [float(step(b.x, b.edge_index, b.y)) for b in batches]
+    torch.cuda.synchronize()
+    for a, c in zip(le, lg):
+        assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
+    for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
