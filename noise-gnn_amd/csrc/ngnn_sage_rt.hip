@@ -96,7 +96,6 @@ struct RtArgs {
     float *agg_out;
     int64_t ld_agg;
     Epi epi;
-    uint32_t x_bytes, out_bytes, agg_bytes;  // buffer-resource ranges (all < 4 GiB)
     const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
     const float *const *x_dev;                // non-null: x's address read at run time (graph slot)
     // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
@@ -111,7 +110,6 @@ struct RtArgs {
     const float *wz_raw;
     float *z;
     int64_t ldz;
-    uint32_t z_bytes;
 };
 
 // -1 (all ones) when a < b, else 0: a lane mask held in a VGPR, built without
@@ -131,7 +129,23 @@ __device__ __forceinline__ v4f and_mask(v4f v, int m) {
 // beyond n_rows and padded neighbour slots need no lane predicates; the byte
 // offset is one VGPR and the per-k-group step an immediate.
 
-constexpr int kOOB = 0x7ffffff0;  // byte offset past every range: load 0 / drop
+// byte offset past every range (load 0 / store dropped): the whole-buffer
+// resource of the gather source is capped below it (host check), every other
+// resource covers one 16-row tile; offsets are unsigned 32-bit
+constexpr int kOOB = static_cast<int>(0xF0000000u);
+constexpr int64_t kRangeMax = 0xF0000000ll - 4096;  // largest whole-buffer range
+
+// resource over tile t's rows of a row-major [n_rows, ld] matrix (64-bit
+// base per tile: no whole-buffer size limit).  It covers the 16 rows plus
+// 128 columns of the next row (the X3 / fp32 row loads read whole 128-column
+// groups past K), or up to column `cols` of the last row for the last tile.
+__device__ __forceinline__ i32x4 tile_rsrc(const float *base, int64_t ld, int cols, int t,
+                                           int n_rows) {
+    const int left = n_rows - t * 16;
+    const uint32_t bytes = left > 16 ? static_cast<uint32_t>((16 * ld + 128) * 4)
+                                     : static_cast<uint32_t>(((left - 1) * ld + cols) * 4) * (left > 0);
+    return make_rsrc(base + static_cast<int64_t>(t) * 16 * ld, bytes);
+}
 
 // x fragments of one 128-column chunk: lane (rl, q) holds
 // x[r][k0 + 16 g + 4 q .. +3]; rows past n_rows read 0 (buffer range).
@@ -143,7 +157,7 @@ constexpr int kOOB = 0x7ffffff0;  // byte offset past every range: load 0 / drop
 // 32-chunks past the root term's C read nothing (offset past the range).
 template <bool X3>
 __device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], const RtArgs &a, i32x4 xr, int r, int k0,
-                                       int q) {
+                                       int q) {  // xr: the tile's resource, r: row in the tile
     if (X3) {
         // all four chunks unconditionally: a chunk past the root term reads
         // bytes of the same / next row (or 0 past the range) and is never
@@ -324,8 +338,8 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
     const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) ag[g] = v4f{ident, ident, ident, ident};
-    const int kofs = (k0 + 4 * q) * 4;
-    const int ld4 = static_cast<int>(a.ldx) * 4;
+    const uint32_t kofs = static_cast<uint32_t>((k0 + 4 * q) * 4);
+    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;  // (whole-buffer offsets < 3.75 GiB)
 #pragma unroll 1
     for (int e0 = 0; e0 < maxdeg; e0 += 16) {
         int cb[4];
@@ -342,8 +356,10 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
             for (int j = 0; j < 4; j += 2) {
                 const int e = e0 + 4 * e4 + j;
                 const int m0 = lt_mask(e, deg), m1 = lt_mask(e + 1, deg);
-                const int o0 = m0 ? __shfl(cb[j], srcl) * ld4 + kofs : kOOB;
-                const int o1 = m1 ? __shfl(cb[j + 1], srcl) * ld4 + kofs : kOOB;
+                const int o0 = m0 ? static_cast<int>(static_cast<uint32_t>(__shfl(cb[j], srcl)) * ld4 + kofs)
+                                  : kOOB;
+                const int o1 = m1 ? static_cast<int>(static_cast<uint32_t>(__shfl(cb[j + 1], srcl)) * ld4 + kofs)
+                                  : kOOB;
                 // all 8 k-groups unconditionally (conditional writes into the
                 // fragment arrays make the compiler copy them whole); groups
                 // past K read the next row or 0 and are zeroed at the end
@@ -402,13 +418,15 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 // exactly one dropout quad: hash pb + 4 m, pb = row_key + (col_base + 4 q)/4.
 template <int NTW, bool DROP, bool RELU, bool VEC>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
-                                         const float *sbias, int r, int q) {
+                                         i32x4 zr, const float *sbias, int r, int rl, int q) {
+    // orsrc / zr: the tile's output / z rows (rl = row in the tile); r, the
+    // global row, keys the dropout hash
     const uint32_t thresh = a.epi.drop.thresh;
     const float scale = a.epi.drop.scale;
     const uint32_t pb = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) +
                                    static_cast<uint32_t>((a.epi.col_base + 4 * q) >> 2)
                              : 0u;
-    const int obase = r * static_cast<int>(a.ldo) * 4;
+    const int obase = rl * static_cast<int>(a.ldo) * 4;
     // re-materialised per call: the per-tile-index tests below must not be
     // hoisted out of the tile loop as SGPR lane masks (they spill)
     int NT = a.NT, NT1 = a.NT1;
@@ -418,8 +436,7 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     for (int m = 0; m < NTW; ++m) {
         if (m >= NT) continue;  // padded tiles (uniform)
         if (m >= NT1) {         // narrow mode: z = x W_l^T rows, no epilogue
-            const i32x4 zr = make_rsrc(a.z, a.z_bytes);
-            buf_store4(acc[m], zr, (r * static_cast<int>(a.ldz) + (m - NT1) * 16 + 4 * q) * 4, 0, 0);
+            buf_store4(acc[m], zr, (rl * static_cast<int>(a.ldz) + (m - NT1) * 16 + 4 * q) * 4, 0, 0);
             continue;
         }
         const int f = m * 16 + 4 * q;
@@ -609,10 +626,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
     // x: the address given at launch, or (graph replay of a changing batch)
     // the one the slot load stored, ranged by the device row count
-    const i32x4 xr = a.x_dev ? make_rsrc(*a.x_dev, static_cast<uint32_t>(
-                                             ((n_rows - 1) * a.ldx + a.K) * 4 * (n_rows > 0)))
-                             : make_rsrc(a.x, a.x_bytes);
-    const i32x4 orsrc = make_rsrc(a.out, a.out_bytes);
+    const float *xbase = a.x_dev ? *a.x_dev : a.x;
+    // the gather's whole-buffer resource (neighbour rows anywhere in x)
+    const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(
+                                          ((static_cast<int64_t>(n_rows) - 1) * a.ldx + a.K) * 4 * (n_rows > 0)));
     // per-lane indices are re-derived per tile from threadIdx (behind an
     // empty asm, so nothing derived from them is hoisted and kept live across
     // the tile loop: such invariants were the VGPR spills, and their reloads
@@ -628,9 +645,11 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         int lane, q, rl;
         lane_ids(lane, q, rl);
         (void)lane;
-        const int rn = (tn < n_tiles ? tn : 0) * RT_ROWS + rl;
-        load_x<X3>(xn, a, xr, rn, 0, q);
-        if (X3) load_xt(xtn, a, xr, rn, q);
+        const int tl = tn < n_tiles ? tn : 0;
+        const int rn = tl * RT_ROWS + rl;
+        const i32x4 xt_r = tile_rsrc(xbase, a.ldx, a.K, tl, n_rows);
+        load_x<X3>(xn, a, xt_r, rl, 0, q);
+        if (X3) load_xt(xtn, a, xt_r, rl, q);
         if (have_l) {
             const int mr = lt_mask(rn, n_rows);
             const int rr = rn & mr;
@@ -681,7 +700,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             }
             const int nkg = min(RT_KC, a.KG - c * RT_KC);
             if (c + 1 < nchunk) {
-                load_x<X3>(xn, a, xr, r, (c + 1) * RT_KC * 16, q);
+                load_x<X3>(xn, a, tile_rsrc(xbase, a.ldx, a.K, t, n_rows), rl, (c + 1) * RT_KC * 16, q);
             } else if (maxdeg == 0) {
                 prefetch(tnext);  // next tile: a whole tile of MFMAs to land
             }
@@ -695,7 +714,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
 
         // ---- neighbour term (tiles with in-edges only)
         if (maxdeg > 0) {
-            const i32x4 ar = make_rsrc(a.agg_out, a.agg_bytes);
+            const i32x4 ar = tile_rsrc(a.agg_out, a.ld_agg, a.K, t, n_rows);
             for (int c = 0; c < nchunk_l; ++c) {
                 const int k0 = c * RT_KC * 16;
                 const int nkg = min(RT_KC, a.KG - c * RT_KC);
@@ -707,7 +726,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 if (a.agg_out) {
                     int kq = a.K - k0 - 4 * q;
                     asm volatile("" : "+v"(kq));  // per-lane masks stay VGPR selects here
-                    const int aoff = (r * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
+                    const int aoff = (rl * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
 #pragma unroll
                     for (int g = 0; g < RT_KC; ++g) {
                         const int mk = lt_mask(16 * g, kq);
@@ -722,15 +741,17 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         }
 
         // ---- epilogue (bias, relu, dropout and the stores)
+        const i32x4 orsrc = tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
+        const i32x4 zr = a.z ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
         if (a.epi.drop.thresh) {
             if (a.epi.relu)
-                epilogue<NTW, true, true, VEC>(acc, a, orsrc, sbias, r, q);
+                epilogue<NTW, true, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
             else
-                epilogue<NTW, true, false, VEC>(acc, a, orsrc, sbias, r, q);
+                epilogue<NTW, true, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         } else if (a.epi.relu) {
-            epilogue<NTW, false, true, VEC>(acc, a, orsrc, sbias, r, q);
+            epilogue<NTW, false, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         } else {
-            epilogue<NTW, false, false, VEC>(acc, a, orsrc, sbias, r, q);
+            epilogue<NTW, false, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         }
     }
 }
@@ -913,10 +934,10 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         return 0;
     const bool no_root = wr_packed == nullptr;  // raw weights only (checked by the caller)
     if (agg_out && (ld_agg % 4 != 0 || !aligned(agg_out, 16))) return 0;
-    // byte offsets are 32-bit (buffer resources): every buffer < 2 GiB
-    const int64_t lim = (int64_t(1) << 31) - 4096;
-    if (n_rows * ldx * 4 > lim || n_rows * ldo * 4 > lim || (agg_out && n_rows * ld_agg * 4 > lim))
-        return 0;
+    // the gather reads neighbour rows through one resource over all of x
+    // (unsigned 32-bit offsets below kOOB); every other operand is addressed
+    // per 16-row tile (no size limit)
+    if (n_rows * ldx * 4 > kRangeMax) return 0;
     const int KG = static_cast<int>(ceil_div(K, 16));
     // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
     // columns become one zero-padded bf16 chunk)
@@ -925,8 +946,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // narrow mode: one launch computes [x W_r^T | x W_l^T] (2 NT1 tiles) --
     // X3 only, no neighbour term, no saved aggregate, no column slicing
     const bool narrow = z != nullptr;
-    if (narrow && (!x3 || !wl_packed || ldz < ceil_div(Fo, 16) * 16 || ldz % 4 != 0 || !aligned(z, 16) ||
-                   n_rows * ldz * 4 > lim))
+    if (narrow && (!x3 || !wl_packed || ldz < ceil_div(Fo, 16) * 16 || ldz % 4 != 0 || !aligned(z, 16)))
         return 0;
     int C = static_cast<int>(K / 32), T4 = static_cast<int>(ceil_div(K % 32, 4)), kpad = 0;
     if (T4 > X3_TAIL_MAX) {
@@ -1006,7 +1026,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.wz_raw = narrow ? static_cast<const float *>(wl_packed) : nullptr;
         a.z = z;
         a.ldz = ldz;
-        a.z_bytes = narrow ? static_cast<uint32_t>(((n_rows - 1) * ldz + 16 * NT1) * 4) : 0u;
         a.Fo = static_cast<int>(Fo_c);
         a.out = out + c0;
         a.ldo = ldo;
@@ -1016,9 +1035,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         a.seed_dev = seed_dev;
         a.x_dev = x_dev;
-        a.x_bytes = static_cast<uint32_t>(((n_rows - 1) * ldx + K) * 4);
-        a.out_bytes = static_cast<uint32_t>(((n_rows - 1) * ldo + Fo_c) * 4);
-        a.agg_bytes = a.agg_out ? static_cast<uint32_t>(((n_rows - 1) * ld_agg + K) * 4) : 0u;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;

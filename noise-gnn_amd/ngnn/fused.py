@@ -488,9 +488,10 @@ def zero_copy_ok(model, n_rows: int, in_dim: int) -> bool:
         fo = c0.lin.weight.shape[0]
     else:
         return False
-    lim = (1 << 31) - 4096
-    return (in_dim % 4 == 0 and n_rows * in_dim * 4 <= lim and n_rows * fo * 4 <= lim
-            and -(-in_dim // 16) <= 79)
+    # the layer-0 gather reads x through one 32-bit-offset resource (< 3.75
+    # GiB, ngnn_sage_rt.hip kRangeMax); outputs are addressed per tile
+    lim = 0xF0000000 - 4096
+    return (in_dim % 4 == 0 and n_rows * in_dim * 4 <= lim and -(-in_dim // 16) <= 79)
 
 
 def gcn_stack_supported(model, x) -> bool:
