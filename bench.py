@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python instead of replaying the captured "
                          "HIP graph of the step")
+    ap.add_argument("--gather", default="fused", choices=["fused", "loader"],
+                    help="fused: batches carry x = graph.x[n_id] unmaterialized and the "
+                         "layer-0 kernels gather the rows (graph replay); loader: the sampler "
+                         "copies the rows into each batch")
     ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg",
                     help="comma list of kernel spans timed with HIP events in the timed region "
                          "('all', or 'none' for profiler runs)")
@@ -83,6 +87,11 @@ def pmc_traffic(span, workload, dtype):
     if not rec:
         return None, None
     return int(rec["traffic_bytes"]), f"profiles/pmc_traffic.json ({rec.get('source', '?')})"
+
+
+def _rows(x):
+    """A batch's feature rows as a tensor (IndexedRows: gathered here)."""
+    return x.materialize() if hasattr(x, "materialize") else x
 
 
 def train_step(model, opt, reducer, b):
@@ -131,7 +140,7 @@ def cpu_baseline(batches, args, layers):
     from oracle import pyg_ref
     from ngnn.loader import DATASETS
     _, _, F_in, C, _ = DATASETS[args.dataset]
-    host = [(b.x.cpu(), b.edge_index.cpu(), b.y.cpu(), b.batch_size) for b in batches]
+    host = [(_rows(b.x).cpu(), b.edge_index.cpu(), b.y.cpu(), b.batch_size) for b in batches]
 
     def run(threads, seconds, max_steps):
         torch.set_num_threads(threads)
@@ -212,7 +221,7 @@ def main():
 
     # pre-sample this rank's batches (inputs resident in HBM before timing)
     loader = NeighborLoader(graph, graph.train_idx, fanout, args.batch_size, shuffle=True, seed=7,
-                            rank=rank, world_size=world)
+                            rank=rank, world_size=world, gather_features=args.gather == "loader")
     it = iter(loader)
     nb = min(len(loader), args.steps + args.warmup)
     batches = [next(it) for _ in range(nb)]
@@ -358,6 +367,8 @@ def main():
                        "parallelism": f"dp{world} (seed-sharded, {_allreduce_name(world)} grad all-reduce)"},
             "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 4),
             "launch": "eager" if not graph else "hip-graph replay (step captured once)",
+            "feature_gather": ("fused x[n_id] in the layer-0 kernels" if args.gather == "fused"
+                               and graph and gstep.x_rows else "loader copies x[n_id]"),
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
             "epoch_batches_per_rank": len(loader),
             "roofline": roof,

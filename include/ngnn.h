@@ -252,6 +252,12 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * ngnn_sage_fwd.  x_dev (nullable): a device word holding x's address, read
  * at run time instead of x (a HIP-graph slot whose batch stays where the
  * loader put it; 16-B aligned, row stride ldx, rows < *n_rows_dev).
+ * xrow / xrow_dev (nullable; the device word overrides): the fused
+ * NeighborLoader feature gather -- logical row r of the layer input is row
+ * xrow[r] (int64, the block's n_id) of x, the HBM-resident feature table of
+ * x_rows rows (< 3.75 GiB), so x[n_id] is never materialised (pipeline.py:153
+ * copies it per batch).  Root rows and gathered neighbour rows both go
+ * through it; outputs and agg_out stay in block order.
  * wr == NULL: no root term (GCNConv's form, see ngnn_gcn_agg_fwd; raw
  * weights only, not with NGNN_FWD_NARROW).
  * n_edge_rows / n_edge_rows_dev (device int, nullable, min'd with the
@@ -261,7 +267,8 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes (calls sharing
  * a ws must be stream-ordered). */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
-int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx, int64_t K,
+int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *xrow,
+                      const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                       const int32_t *n_edge_rows_dev, const int32_t *rowptr,
                       const int32_t *col,
@@ -310,8 +317,12 @@ int ngnn_block_prefix_stats(const int32_t *rowptr, const int32_t *col, const int
 size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K);
 /* h_dev (nullable): device word holding h's address, read at run time (as
  * ngnn_sage_fwd_raw's x_dev). */
+/* h_idx / h_idx_dev (nullable; the device word overrides): row r of h is
+ * row h_idx[r] of h, a table of h_rows rows (< 2 GiB) -- layer 0 under the
+ * fused x[n_id] gather (see ngnn_sage_fwd_raw's xrow). */
 int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy, float yscale,
-                    const float *h, const float *const *h_dev, int64_t ldh, const float *agg,
+                    const float *h, const float *const *h_dev, const int64_t *h_idx,
+                    const int64_t *const *h_idx_dev, int64_t h_rows, int64_t ldh, const float *agg,
                     int64_t ld_agg, const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
                     int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
                     size_t ws_bytes, void *stream);
@@ -442,7 +453,8 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
-                   int32_t *n_edge_rows, void *stream);
+                   int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
+                   void *stream);
 
 #ifdef __cplusplus
 }

@@ -62,12 +62,16 @@ struct Chunk {
     T m[MASK ? N : 1];
     int d0[DEG ? N : 1], d1[DEG ? N : 1];
 
+    // ridx (nullable): row r of the operand is row ridx[r] of src, a table of
+    // src_rows rows (the fused x[n_id] gather of layer 0; < 2 GiB)
     __device__ __forceinline__ void load(const float *__restrict__ src, int64_t ld,
                                          const float *__restrict__ mask, int64_t ldm,
                                          const int32_t *__restrict__ rowptr, int64_t c0, int re,
-                                         int k0, int K) {
+                                         int k0, int K, const int64_t *__restrict__ ridx = nullptr,
+                                         int64_t src_rows = 0) {
         const uint32_t nr = static_cast<uint32_t>(re - c0);
-        const i32x4 rs = make_rsrc(src + c0 * ld, nr * static_cast<uint32_t>(ld) * 4u);
+        const i32x4 rs = ridx ? make_rsrc(src, static_cast<uint32_t>(src_rows * ld * 4))
+                             : make_rsrc(src + c0 * ld, nr * static_cast<uint32_t>(ld) * 4u);
         i32x4 rm = rs, rp = rs;
         if (MASK) rm = make_rsrc(mask + c0 * ldm, nr * static_cast<uint32_t>(ldm) * 4u);
         if (DEG) rp = make_rsrc(rowptr + c0, (nr + 1u) * 4u);
@@ -77,7 +81,13 @@ struct Chunk {
             const int r = idx / CPR, c = (idx % CPR) * W;
             const int k = k0 + c;
             const bool kok = k < K;
-            const int vo = kok ? (r * static_cast<int>(ld) + k) * 4 : kBufOOB;
+            int vo;
+            if (ridx) {
+                const int pr = r < static_cast<int>(nr) ? static_cast<int>(ridx[c0 + r]) : -1;
+                vo = (kok && pr >= 0) ? (pr * static_cast<int>(ld) + k) * 4 : kBufOOB;
+            } else {
+                vo = kok ? (r * static_cast<int>(ld) + k) * 4 : kBufOOB;
+            }
             if constexpr (VEC) v[u] = buf_load4(rs, vo, 0, 0);
             else v[u] = buf_load1(rs, vo, 0, 0);
             if (MASK) {
@@ -158,10 +168,12 @@ template <int NTW, int KTW, bool SPLIT_N, bool VZ, bool VH, bool MASK>
 __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
     float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
+    const int64_t *h_idx_arg, const int64_t *const *h_idx_dev, int64_t h_rows,
     const float *__restrict__ agg, int64_t ld_agg, const int32_t *__restrict__ rowptr,
     const int32_t *__restrict__ r_ptr, int Fo, int K, float *__restrict__ ws) {
     __shared__ __attribute__((aligned(16))) float smem[WG_BM * LDZ + 2 * WG_BM * LDH];  // 94 KB
     const float *__restrict__ h = h_dev ? *h_dev : h_arg;  // run-time address (graph slot)
+    const int64_t *h_idx = h_idx_dev ? *h_idx_dev : h_idx_arg;  // fused x[n_id] (layer 0)
     float *sz = smem;                       // [64][LDZ]
     float *sh = sz + WG_BM * LDZ;           // [64][LDH]
     float *sa = sh + WG_BM * LDH;           // [64][LDH]
@@ -199,7 +211,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     Chunk<WG_KC, VH, false, true> ca;
     if (rb < re) {
         cz.load(dy, ldy, y, ldyy, nullptr, rb, re, n0, Fo);
-        ch.load(h, ldh, nullptr, 0, nullptr, rb, re, k0, K);
+        ch.load(h, ldh, nullptr, 0, nullptr, rb, re, k0, K, h_idx, h_rows);
         ca.load(agg, ld_agg, nullptr, 0, rowptr, rb, re, k0, K);
     }
     for (int c0 = rb; c0 < re; c0 += WG_BM) {
@@ -211,7 +223,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
         const int c1 = c0 + WG_BM;
         if (c1 < re) {  // next chunk's loads overlap this chunk's MFMAs
             cz.load(dy, ldy, y, ldyy, nullptr, c1, re, n0, Fo);
-            ch.load(h, ldh, nullptr, 0, nullptr, c1, re, k0, K);
+            ch.load(h, ldh, nullptr, 0, nullptr, c1, re, k0, K, h_idx, h_rows);
             ca.load(agg, ld_agg, nullptr, 0, rowptr, c1, re, k0, K);
         }
         const int nks = min(WG_BM / 4, (re - c0 + 3) >> 2);
@@ -801,13 +813,15 @@ extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
 template <int NTW, int KTW, bool SPLIT_N>
 static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const float *dy, int64_t ldy,
                          const float *y, int64_t ldyy, float yscale, const float *h,
-                         const float *const *h_dev, int64_t ldh, const float *agg, int64_t ld_agg,
-                         const int32_t *rowptr, const int32_t *r_ptr, int Fo, int K, float *ws) {
+                         const float *const *h_dev, int64_t ldh, const int64_t *h_idx,
+                         const int64_t *const *h_idx_dev, int64_t h_rows, const float *agg,
+                         int64_t ld_agg, const int32_t *rowptr, const int32_t *r_ptr, int Fo, int K,
+                         float *ws) {
     auto go = [&](auto vz_c, auto vh_c, auto m_c) {
         hipLaunchKernelGGL((k_wgrad_partial<NTW, KTW, SPLIT_N, decltype(vz_c)::value,
                                             decltype(vh_c)::value, decltype(m_c)::value>),
-                           grid, dim3(512), 0, st, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, agg,
-                           ld_agg, rowptr, r_ptr, Fo, K, ws);
+                           grid, dim3(512), 0, st, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, h_idx,
+                           h_idx_dev, h_rows, agg, ld_agg, rowptr, r_ptr, Fo, K, ws);
     };
     using T = std::true_type;
     using F = std::false_type;
@@ -826,6 +840,7 @@ static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const floa
 
 extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
                                float yscale, const float *h, const float *const *h_dev,
+                               const int64_t *h_idx, const int64_t *const *h_idx_dev, int64_t h_rows,
                                int64_t ldh, const float *agg, int64_t ld_agg,
                                const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
                                int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
@@ -840,6 +855,10 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     NGNN_RETURN_IF(ldy > (1 << 22) || ldh > (1 << 22) || ld_agg > (1 << 22) ||
                    (y && ldyy > (1 << 22)) || Fo * K > (int64_t{1} << 28), NGNN_E_RANGE);
     NGNN_RETURN_IF(!ws || ws_bytes < ngnn_sage_wgrad_workspace_bytes(Fo, K), NGNN_E_WORKSPACE);
+    // indexed h (the feature table under the fused x[n_id] gather): 32-bit
+    // offsets over the whole table
+    NGNN_RETURN_IF((h_idx || h_idx_dev) && (h_rows <= 0 || h_rows * ldh * 4 >= (int64_t{1} << 31)),
+                   NGNN_E_RANGE);
     // 16-B staging per operand pair: dz (+ its mask y) and h / agg
     const bool vz = (Fo % 4 == 0) && (ldy % 4 == 0) && aligned(dy, 16) &&
                     (!y || ((ldyy % 4 == 0) && aligned(y, 16)));
@@ -854,8 +873,8 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
         1, std::min<int64_t>(ceil_div(n_rows, WG_BM), std::max<int64_t>(1, S_MAX / (gy * gz)))));
     const dim3 grid(S, static_cast<unsigned>(gy), static_cast<unsigned>(gz));
     const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
-#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, agg, ld_agg, rowptr, \
-                     r_ptr, (int)Fo, (int)K, wsf
+#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, h_idx, h_idx_dev, \
+                     h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf
     if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
     else if (NT == 1) launch_wgrad<1, 2, false>(NGNN_WG_ARGS);
     else if (NT == 2) launch_wgrad<2, 2, false>(NGNN_WG_ARGS);

@@ -98,6 +98,12 @@ struct RtArgs {
     Epi epi;
     const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
     const float *const *x_dev;                // non-null: x's address read at run time (graph slot)
+    // fused x[n_id] gather: logical row r is row xrow[r] of x (the resident
+    // feature table, x_rows rows); the device word xrow_dev (graph slot)
+    // overrides xrow; both null: identity
+    const int64_t *xrow;
+    const int64_t *const *xrow_dev;
+    int64_t x_rows;
     // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
     // when kpad), then T4 exact-fp32 steps of 4 columns
     int C, T4, kpad;
@@ -155,32 +161,34 @@ __device__ __forceinline__ i32x4 tile_rsrc(const float *base, int64_t ld, int co
 // X3 layout instead: lane (rl, q) holds x[r][k0 + 32 c + 8 q + 4 h .. +3] in
 // xf[2 c + h] (the B fragment of 16x16x32 bf16: 8 consecutive k per lane);
 // 32-chunks past the root term's C read nothing (offset past the range).
+// rowoff: byte offset of the lane's (physical) row in x, kOOB for rows past
+// the block (those read 0).
 template <bool X3>
-__device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], const RtArgs &a, i32x4 xr, int r, int k0,
-                                       int q) {  // xr: the tile's resource, r: row in the tile
+__device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], i32x4 xr, uint32_t rowoff, int k0, int q) {
     if (X3) {
         // all four chunks unconditionally: a chunk past the root term reads
         // bytes of the same / next row (or 0 past the range) and is never
         // used -- a uniform per-chunk select here becomes loop-invariant SGPR
         // lane masks that the compiler hoists and spills
-        const int voff = (r * static_cast<int>(a.ldx) + k0 + 8 * q) * 4;
+        const uint32_t voff = rowoff + static_cast<uint32_t>((k0 + 8 * q) * 4);
 #pragma unroll
         for (int g = 0; g < RT_KC; ++g)
-            xf[g] = buf_load4(xr, voff + 4 * (32 * (g >> 1) + 4 * (g & 1)), 0, 0);
+            xf[g] = buf_load4(xr, static_cast<int>(voff + 4 * (32 * (g >> 1) + 4 * (g & 1))), 0, 0);
     } else {
-        const int voff = (r * static_cast<int>(a.ldx) + k0 + 4 * q) * 4;
+        const uint32_t voff = rowoff + static_cast<uint32_t>((k0 + 4 * q) * 4);
 #pragma unroll
-        for (int g = 0; g < RT_KC; ++g) xf[g] = buf_load4(xr, voff + 64 * g, 0, 0);
+        for (int g = 0; g < RT_KC; ++g) xf[g] = buf_load4(xr, static_cast<int>(voff + 64 * g), 0, 0);
     }
 }
 
 // X3 fp32 tail: lane (rl, q) holds x[r][32 C + 4 s + q] (the B operand of
 // 16x16x4 f32 step s)
-__device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &a, i32x4 xr, int r,
-                                        int q) {
-    const int voff = (r * static_cast<int>(a.ldx) + 32 * a.C + q) * 4;
+__device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &a, i32x4 xr,
+                                        uint32_t rowoff, int q) {
+    const uint32_t voff = rowoff + static_cast<uint32_t>((32 * a.C + q) * 4);
 #pragma unroll
-    for (int s = 0; s < X3_TAIL_MAX; ++s) xt[s] = buf_load1(xr, voff + 16 * s, 0, 0);  // masked at use
+    for (int s = 0; s < X3_TAIL_MAX; ++s)
+        xt[s] = buf_load1(xr, static_cast<int>(voff + 16 * s), 0, 0);  // masked at use
 }
 
 // root term of one 128-column group in the X3 layout: per 32-chunk, split x
@@ -334,7 +342,8 @@ __device__ __forceinline__ v4f red_mask(v4f v, int m) {
 // end.
 template <int RED>
 __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, i32x4 xr, int beg,
-                                             int deg, int maxdeg, int k0, int nkg, int rl, int q) {
+                                             int deg, int maxdeg, int k0, int nkg, int rl, int q,
+                                             const int64_t *xrow) {
     const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) ag[g] = v4f{ident, ident, ident, ident};
@@ -347,6 +356,10 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
         for (int j = 0; j < 4; ++j) {
             const int e = e0 + 4 * q + j;
             cb[j] = a.col[(beg + e) & lt_mask(e, deg)];  // invalid slots read col[0]
+        }
+        if (xrow) {  // fused x[n_id]: the neighbours' rows in the feature table
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cb[j] = static_cast<int>(xrow[cb[j]]);
         }
         const int ne = min(16, maxdeg - e0);
 #pragma unroll 1  // one neighbour pair in flight: keep the register budget
@@ -627,9 +640,21 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // x: the address given at launch, or (graph replay of a changing batch)
     // the one the slot load stored, ranged by the device row count
     const float *xbase = a.x_dev ? *a.x_dev : a.x;
-    // the gather's whole-buffer resource (neighbour rows anywhere in x)
-    const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(
-                                          ((static_cast<int64_t>(n_rows) - 1) * a.ldx + a.K) * 4 * (n_rows > 0)));
+    const int64_t *xrow = a.xrow_dev ? *a.xrow_dev : a.xrow;
+    // one resource over all of x (root rows and gathered neighbour rows;
+    // x_rows: the feature table's rows under the fused x[n_id] gather)
+    const int64_t xrows = xrow ? a.x_rows : static_cast<int64_t>(n_rows);
+    const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(((xrows - 1) * a.ldx + a.K) * 4 * (xrows > 0)));
+    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
+    // byte offset of logical row rr in x (kOOB past the block's rows)
+    auto row_off = [&](int rr) -> uint32_t {
+        if (rr >= n_rows) return static_cast<uint32_t>(kOOB);
+        const int pr = xrow ? static_cast<int>(xrow[rr]) : rr;
+        return static_cast<uint32_t>(pr) * ld4;
+    };
+    uint32_t roff_n = 0;   // the next tile's row offset (its rows are in flight)
+    uint32_t roff_nn = 0;  // the claimed tile's row offset, computed when claimed: under the
+                           // fused gather its xrow[] load then lands behind the current tile
     // per-lane indices are re-derived per tile from threadIdx (behind an
     // empty asm, so nothing derived from them is hoisted and kept live across
     // the tile loop: such invariants were the VGPR spills, and their reloads
@@ -641,15 +666,15 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         q_ = l >> 4;
         rl_ = l & 15;
     };
-    auto prefetch = [&](int tn) {
+    auto prefetch = [&](int tn, uint32_t roff_tn) {
         int lane, q, rl;
         lane_ids(lane, q, rl);
         (void)lane;
         const int tl = tn < n_tiles ? tn : 0;
         const int rn = tl * RT_ROWS + rl;
-        const i32x4 xt_r = tile_rsrc(xbase, a.ldx, a.K, tl, n_rows);
-        load_x<X3>(xn, a, xt_r, rl, 0, q);
-        if (X3) load_xt(xtn, a, xt_r, rl, q);
+        roff_n = roff_tn;
+        load_x<X3>(xn, xr, roff_n, 0, q);
+        if (X3) load_xt(xtn, a, xr, roff_n, q);
         if (have_l) {
             const int mr = lt_mask(rn, n_rows);
             const int rr = rn & mr;
@@ -658,11 +683,17 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             nend = nbeg + ((nend - nbeg) & mr);  // rows past the end: degree 0
         }
     };
-    prefetch(t);
+    {
+        int lane0, q0, rl0;
+        lane_ids(lane0, q0, rl0);
+        prefetch(t, row_off(t * RT_ROWS + rl0));
+    }
     for (; t < n_tiles; t = tnext, ++kt) {
         tnext = claim();
+        const uint32_t roff = roff_n;  // this tile's row offset (prefetch overwrites roff_n)
         int lane, q, rl;
         lane_ids(lane, q, rl);
+        roff_nn = row_off(tnext * RT_ROWS + rl);
         // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
         const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
         const int r = t * RT_ROWS + rl;
@@ -700,9 +731,9 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             }
             const int nkg = min(RT_KC, a.KG - c * RT_KC);
             if (c + 1 < nchunk) {
-                load_x<X3>(xn, a, tile_rsrc(xbase, a.ldx, a.K, t, n_rows), rl, (c + 1) * RT_KC * 16, q);
+                load_x<X3>(xn, xr, roff, (c + 1) * RT_KC * 16, q);
             } else if (maxdeg == 0) {
-                prefetch(tnext);  // next tile: a whole tile of MFMAs to land
+                prefetch(tnext, roff_nn);  // next tile: a whole tile of MFMAs to land
             }
             if (X3) {
                 const int ncc = min(4, a.C - 4 * c);
@@ -719,10 +750,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 const int k0 = c * RT_KC * 16;
                 const int nkg = min(RT_KC, a.KG - c * RT_KC);
                 v4f ag[RT_KC];
-                gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q);
+                gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q, xrow);
                 // edge tiles prefetch the next tile only now: its x fragments
                 // are not live across the gather (register budget)
-                if (c == nchunk_l - 1) prefetch(tnext);
+                if (c == nchunk_l - 1) prefetch(tnext, roff_nn);
                 if (a.agg_out) {
                     int kq = a.K - k0 - 4 * q;
                     asm volatile("" : "+v"(kq));  // per-lane masks stay VGPR selects here
@@ -927,7 +958,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
-                     const float *const *x_dev, bool exact, float *z, int64_t ldz) {
+                     const float *const *x_dev, bool exact, float *z, int64_t ldz,
+                     const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -937,7 +969,10 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // the gather reads neighbour rows through one resource over all of x
     // (unsigned 32-bit offsets below kOOB); every other operand is addressed
     // per 16-row tile (no size limit)
-    if (n_rows * ldx * 4 > kRangeMax) return 0;
+    const bool indexed = xrow != nullptr || xrow_dev != nullptr;
+    // (a graph slot may load materialized batches too: the word then holds 0)
+    if ((indexed ? std::max(x_rows, n_rows) : n_rows) * ldx * 4 > kRangeMax || (indexed && x_rows <= 0))
+        return 0;
     const int KG = static_cast<int>(ceil_div(K, 16));
     // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
     // columns become one zero-padded bf16 chunk)
@@ -1035,6 +1070,9 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         a.seed_dev = seed_dev;
         a.x_dev = x_dev;
+        a.xrow = xrow;
+        a.xrow_dev = xrow_dev;
+        a.x_rows = x_rows;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
@@ -1060,7 +1098,8 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64
     return std::max(ngnn_pack_weight_bytes(Fo, K), z);
 }
 
-extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int64_t ldx,
+extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *xrow,
+                                 const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx,
                                  int64_t K, int64_t n_rows, const int32_t *n_rows_dev,
                                  int64_t n_edge_rows, const int32_t *n_edge_rows_dev,
                                  const int32_t *rowptr,
@@ -1097,7 +1136,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
         float *z = static_cast<float *>(ws);
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
-                             nullptr, 0, x_dev, exact, z, ldz)) {
+                             nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -1115,7 +1154,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, int6
     }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
-                          ws_bytes, x_dev, exact, nullptr, 0))
+                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

@@ -26,11 +26,16 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int64_t lds, int64_t n_cap, int64_t *__restrict__ sei, int64_t e_cap, int64_t *__restrict__ sy,
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
-    uint32_t gen, int32_t *__restrict__ n_edge_rows, int vec) {
+    uint32_t gen, int32_t *__restrict__ n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
+    int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
-        if (tid == 0) *x_dev = x;
+        if (tid == 0) {
+            *x_dev = x;
+            // fused x[n_id]: x is the feature table, row r of the block is xrow[r]
+            if (xrow_dev) *xrow_dev = xrow;
+        }
     } else if (vec) {
         const int64_t f4 = F >> 2, total = N * f4;
         for (int64_t i = tid; i < total; i += nthr) {
@@ -136,10 +141,12 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int64_t *slot_ei, int64_t e_cap, int64_t *slot_y, int32_t *n_valid,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
-                              int32_t *n_edge_rows, void *stream) {
+                              int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
+                              void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
+    NGNN_RETURN_IF(xrow && (!x_dev || !xrow_dev), NGNN_E_ARG);  // indexed rows are zero-copy only
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
                    NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E, NGNN_E_SHAPE);
@@ -154,6 +161,6 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
                        n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
-                       vec);
+                       xrow, xrow_dev, vec);
     return launch_status();
 }

@@ -55,12 +55,14 @@ SIGNATURES = {
     "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
-                              _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p]),
+                              _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p, _p,
+                              _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
     "ngnn_sage_fwd_raw_workspace_bytes": (_sz, [_i64, _i64, _i64]),
-    "ngnn_sage_fwd_raw": (_int, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _int, _p, _p, _i64, _p, _i64,
+    "ngnn_sage_fwd_raw": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _int, _p, _p,
+                                 _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
     "ngnn_gcn_agg_fwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _int, ctypes.c_float,
@@ -68,7 +70,8 @@ SIGNATURES = {
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
-    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _i64, _p, _i64, _p, _i64,
+    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64, _p,
+                               _i64, _p, _i64,
                                _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
     "ngnn_sage_dgrad_workspace_bytes": (_sz, [_i64, _i64, _int]),
     "ngnn_sage_dgrad_gather": (_int, [_p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p, _p, _i64,

@@ -108,6 +108,11 @@ class Block:
         self.r_next = None
         # device int32: rows at or past it have no in-edges (graph slot), or None
         self.n_edge_rows_dev = None
+        # fused x[n_id] gather (graph slot): device word holding the address of
+        # the batch's n_id (0: x_dev's rows are the block's rows), and the row
+        # count of the feature table x_dev then points at
+        self.xrow_dev = None
+        self.x_rows = 0
 
     @property
     def rowptr(self):
@@ -153,6 +158,8 @@ class _BlockCache:
             blk.x_dev = hint[6]
             blk.r_next = hint[7]
             blk.n_edge_rows_dev = hint[8]
+            if hint[9] is not None:
+                blk.xrow_dev, blk.x_rows = hint[9]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -179,7 +186,7 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
                     n_active: int | None = None, n_rows_dev: torch.Tensor | None = None,
                     csr: CSR | None = None, seed_dev: torch.Tensor | None = None,
                     x_dev: torch.Tensor | None = None, r_next=None,
-                    n_edge_rows_dev: torch.Tensor | None = None) -> None:
+                    n_edge_rows_dev: torch.Tensor | None = None, xrow=None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
     later rows have none) -- only used for roofline accounting.  n_rows_dev:
     device int32 scalar bounding the real rows of a padded slot.  csr: a
@@ -188,11 +195,14 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     x_dev: device word the producer fills with the address of the feature
     rows the layer-0 kernels must read (zero-copy slot).  r_next: (device int32,
     R): the producer keeps ngnn_block_prefix_stats' bound for R there.
-    n_edge_rows_dev: device int32 holding n_active for a changing batch."""
+    n_edge_rows_dev: device int32 holding n_active for a changing batch.
+    xrow: (device word, table rows): the producer stores the address of the
+    batch's n_id in the word when x_dev points at the whole feature table
+    (fused x[n_id] gather), 0 otherwise."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
-                                  n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev)
+                                  n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev, xrow)
 
 
 def _drop_hint(key):
@@ -205,7 +215,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]
+    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

@@ -155,12 +155,15 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
                    p_drop: float, seed: int, agg_out: torch.Tensor | None = None,
                    seed_dev: torch.Tensor | None = None,
                    x_dev: torch.Tensor | None = None, span: str = "sage_fwd",
-                   narrow: bool = False) -> torch.Tensor:
+                   narrow: bool = False, xrow_dev: torch.Tensor | None = None,
+                   x_rows: int = 0) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
-    supplies the shape.  narrow: aggregate the neighbour term as mean/sum of
-    z = x W_l^T (F_out wide) instead of x (K wide) -- the output layer's form
-    (no agg_out then)."""
+    supplies the shape.  xrow_dev (with x_dev): device word holding the
+    address of the block's n_id when x_dev points at the whole x_rows-row
+    feature table (fused x[n_id] gather; 0 at run time: plain rows).
+    narrow: aggregate the neighbour term as mean/sum of z = x W_l^T (F_out
+    wide) instead of x (K wide) -- the output layer's form (no agg_out then)."""
     N, K = x.shape
     Fo = wl.shape[0]
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
@@ -175,6 +178,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     # MFMA rate) unless exact, the neighbour term on f32 MFMA
     root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
     mfma_s = 2 * N * K * Fo * root / root_rate + 2 * n_e * K * Fo / (MFMA_F32_TFS * 1e12)
+    if xrow_dev is not None:  # the n_id loads of the fused gather (rows, neighbours)
+        nbytes += (N + block.E) * 8
     if narrow and agg_out is None:
         # narrow mode: the root launch also computes z = x W_l^T (every row),
         # then gathers z (F_out wide) instead of x
@@ -193,7 +198,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel
         n_edge = N if block.n_active is None else min(int(block.n_active), N)
         rc = lib.ngnn_sage_fwd_raw(
-            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, n_edge,
+            _lib.ptr(x), _lib.ptr(x_dev), None, _lib.ptr(xrow_dev), int(x_rows), x.stride(0), K, N,
+            nrd, n_edge,
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0),
@@ -224,7 +230,8 @@ def _zeros_like_cached(w: torch.Tensor) -> torch.Tensor:
 
 
 def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: int,
-                        seed_dev=None, x_dev=None, span: str = "gcn_fwd"):
+                        seed_dev=None, x_dev=None, span: str = "gcn_fwd", xrow_dev=None,
+                        x_rows: int = 0):
     """GCNConv(normalize=False) layer in PyG's own order (convolution.py:19-35,
     GCNConv [ext]): z = x W^T on the row-tile kernel (no bias, no epilogue),
     then ngnn_gcn_agg_fwd: out = act(sum_{j->i} z_j + b) -- the form for
@@ -241,7 +248,8 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
     root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
     with _timing.span(span + "_z", (N * K + N * ldz) * 4, 2 * N * K * Fo, 2 * N * K * Fo / root_rate):
         rc = lib.ngnn_sage_fwd_raw(
-            _lib.ptr(x), _lib.ptr(x_dev), x.stride(0), K, N, nrd, N, None, _lib.ptr(block.rowptr),
+            _lib.ptr(x), _lib.ptr(x_dev), None, _lib.ptr(xrow_dev), int(x_rows), x.stride(0), K, N,
+            nrd, N, None, _lib.ptr(block.rowptr),
             _lib.ptr(block.col), _lib.REDUCE["sum"] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
             None, _lib.ptr(wd), wd.stride(0), None, Fo, _lib.ptr(z), ldz, 0, 0.0, 0, None, None, K,
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
@@ -272,12 +280,13 @@ class _SAGEStack(torch.autograd.Function):
             last = i == L - 1
             relu, p_i, seed_i = not last, (0.0 if last else p_drop), seed + 7919 * i
             x_dev = block.x_dev if i == 0 else None
+            xrow = dict(xrow_dev=block.xrow_dev, x_rows=block.x_rows) if i == 0 else {}
             if wr is None and h.size(1) > wl.shape[0]:
                 # GCN layer narrowing its input: transform first (PyG's order),
                 # no saved aggregate (rebuilt for the rows backward needs)
                 agg = None
                 h = gcn_transform_first(h, block, wl, bl, relu, p_i, seed_i, seed_dev, x_dev,
-                                        span=f"gcn_fwd_l{i}")
+                                        span=f"gcn_fwd_l{i}", **xrow)
             else:
                 # the output layer aggregates in the F_out-wide space when it can
                 # (its K-wide aggregate is rebuilt for the seed rows in backward)
@@ -286,7 +295,7 @@ class _SAGEStack(torch.autograd.Function):
                 agg = None if narrow else torch.empty(h.shape, dtype=torch.float32, device=h.device)
                 h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
                                    seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
-                                   span=f"sage_fwd_l{i}", narrow=narrow)
+                                   span=f"sage_fwd_l{i}", narrow=narrow, **xrow)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -363,6 +372,8 @@ class _SAGEStack(torch.autograd.Function):
                 dwr = _workspace(dev, "gcn_dwr", wr.numel() * 4).view(torch.float32)[
                     :wr.numel()].view(wr.shape)
             if agg is None:
+                if i == 0 and block.x_dev is not None:  # (zero_copy_ok excludes it)
+                    raise _lib.NGNNError("layer-0 aggregate rebuild from a zero-copy input")
                 # narrow-mode layer: the K-wide aggregate the weight gradient
                 # reads (rows < R) gathered now -- R rows when the loss told us
                 # R (the seed rows), else every row
@@ -380,7 +391,8 @@ class _SAGEStack(torch.autograd.Function):
                     _lib.ptr(dy), dy.stride(0), _lib.ptr(ymask),
                     ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(h_in),
                     _lib.ptr(block.x_dev) if i == 0 else None,
-                    h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
+                    None, _lib.ptr(block.xrow_dev) if i == 0 else None,
+                    block.x_rows if i == 0 else 0, h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
                     bptr(i + 1), Fo, K, _lib.ptr(dwl), _lib.ptr(dbl), _lib.ptr(dwr),
                     _lib.ptr(ws), ws.numel(), stream)
             _lib.check(rc, "ngnn_sage_wgrad")
@@ -470,11 +482,13 @@ def sage_stack_supported(model, x) -> bool:
     return True
 
 
-def zero_copy_ok(model, n_rows: int, in_dim: int) -> bool:
+def zero_copy_ok(model, n_rows: int, in_dim: int, table_rows: int = 0) -> bool:
     """Can a HIP-graph slot hand this model's layer 0 the batch's feature rows
     in place (ngnn_sage_fwd_raw's x_dev)?  Only the fused SAGE stack reads
     x_dev, and only the row-tile kernel accepts it: K % 4 == 0 and 32-bit
-    buffer offsets over the slot's rows (x, the output, the saved aggregate)."""
+    buffer offsets over the slot's rows (x, the output, the saved aggregate).
+    table_rows > 0: the rows are gathered from a feature table of that many
+    rows (fused x[n_id]; the weight gradient then needs it under 2 GiB)."""
     if not isinstance(getattr(model, "convs", None), torch.nn.ModuleList):
         return False
     if getattr(model, "use_bn", False):
@@ -484,14 +498,19 @@ def zero_copy_ok(model, n_rows: int, in_dim: int) -> bool:
         if len({c.aggr for c in model.convs}) != 1:
             return False
         fo = c0.lin_r.weight.shape[0]
-    elif hasattr(c0, "lin"):  # SimpleGCN: layer 0 reads x in either form
+    elif hasattr(c0, "lin"):  # SimpleGCN
         fo = c0.lin.weight.shape[0]
+        if in_dim > fo:  # transform-first layer 0: backward rebuilds its aggregate from x
+            return False
     else:
         return False
     # the layer-0 gather reads x through one 32-bit-offset resource (< 3.75
     # GiB, ngnn_sage_rt.hip kRangeMax); outputs are addressed per tile
     lim = 0xF0000000 - 4096
-    return (in_dim % 4 == 0 and n_rows * in_dim * 4 <= lim and -(-in_dim // 16) <= 79)
+    if table_rows and table_rows * in_dim * 4 >= 2**31:
+        return False
+    return (in_dim % 4 == 0 and max(n_rows, table_rows) * in_dim * 4 <= lim
+            and -(-in_dim // 16) <= 79)
 
 
 def gcn_stack_supported(model, x) -> bool:

@@ -35,6 +35,7 @@ import torch
 
 from . import _lib
 from .block import CSR, block_cache, hint_edge_index
+from .loader import IndexedRows
 from .losses import seed_cross_entropy
 
 
@@ -67,6 +68,11 @@ class GraphedTrainStep:
         self.r_next = torch.zeros(1, dtype=torch.int64, device=dev)
         # rows past the batch's last target have no in-edges (dense forward kernel)
         self.n_edge_rows = torch.zeros(1, dtype=torch.int32, device=dev)
+        # fused x[n_id]: when captured on an IndexedRows batch, x_dev holds the
+        # feature table's address and this word the batch's n_id (0: plain
+        # rows); x_rows = the table's rows the captured kernels range over
+        self.xrow_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.x_rows = 0
         self._gen = 0
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
@@ -82,13 +88,27 @@ class GraphedTrainStep:
         """zero_copy: store x's address for the captured kernels instead of
         copying its rows into the slot (replays); the copy serves eager use
         of the slot (warm-up, tests).  batch_size: the block's seed count
-        (default: the captured B).  A short block (an epoch's last batch when
+        (default: the captured B).  x may be an IndexedRows (a batch of
+        NeighborLoader(gather_features=False)): zero-copy replays of a step
+        captured on one pass the feature table and n_id (the layer-0 kernels
+        gather the rows); otherwise its rows are gathered here.  A short block (an epoch's last batch when
         drop_last is off) gets ignore_index (-100) labels on rows
         [batch_size, B), so the captured loss -- F.cross_entropy(out[:B],
         y[:B]) with the default ignore_index -- is exactly the reference's
         F.cross_entropy(out[:batch_size], y[:batch_size]) (pipeline.py:155-158):
         mean over the real seeds, zero gradient on the other rows."""
-        N, E = x.size(0), edge_index.size(1)
+        xrow = None
+        if isinstance(x, IndexedRows):
+            t, idx = x.table, x.index
+            if (zero_copy and self.x_rows and t.dtype == torch.float32 and t.stride(1) == 1
+                    and t.stride(0) == self.x.stride(0) and t.data_ptr() % 16 == 0
+                    and t.size(0) <= self.x_rows and idx.dtype == torch.int64
+                    and idx.is_contiguous()):
+                xrow = idx
+                x = t
+            else:
+                x = x.materialize()
+        N, E = (x.size(0) if xrow is None else xrow.numel()), edge_index.size(1)
         if N + 1 > self.n_cap or E > self.e_cap:
             raise ValueError(f"batch (N={N}, E={E}) exceeds the slot ({self.n_cap}, {self.e_cap})")
         bs = self.B if batch_size is None else int(batch_size)
@@ -98,6 +118,8 @@ class GraphedTrainStep:
             x = x.float()
         if x.stride(1) != 1 or x.stride(0) != self.x.stride(0) or x.data_ptr() % 16:
             x = x.clone(memory_format=torch.contiguous_format)
+        # a step captured for indexed rows: the word gets n_id's address or 0
+        xrow_word = self.xrow_dev if (zero_copy and self.x_rows) else None
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
         y = y[:bs].contiguous()
@@ -113,9 +135,9 @@ class GraphedTrainStep:
             else _lib.ptr(self.ei), self.e_cap, _lib.ptr(self.y), _lib.ptr(self.n_valid),
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
             _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
-            _lib.ptr(self.n_edge_rows), _lib.stream_handle(self.x.device)),
-            "ngnn_slot_load")
-        self._x_live = x if zero_copy else None
+            _lib.ptr(self.n_edge_rows), _lib.ptr(xrow), _lib.ptr(xrow_word),
+            _lib.stream_handle(self.x.device)), "ngnn_slot_load")
+        self._x_live = (x, xrow) if zero_copy else None
 
     def _next_gen(self) -> int:
         self._gen += 1
@@ -162,11 +184,19 @@ class GraphedTrainStep:
         # zero-copy features only where the layer-0 kernel can take them
         # (otherwise every replay copies the rows into the slot)
         from .fused import zero_copy_ok
-        self.zero_copy = zero_copy_ok(self.model, self.n_cap, self.x.size(1))
+        table_rows = 0
+        if isinstance(x, IndexedRows) and x.table.dtype == torch.float32:
+            table_rows = x.table.size(0)
+        self.zero_copy = zero_copy_ok(self.model, self.n_cap, self.x.size(1), table_rows)
+        if not self.zero_copy and table_rows:  # materialized rows, plain zero-copy if possible
+            table_rows = 0
+            self.zero_copy = zero_copy_ok(self.model, self.n_cap, self.x.size(1))
+        self.x_rows = table_rows if self.zero_copy else 0
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
                         x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B),
-                        n_edge_rows_dev=self.n_edge_rows)
+                        n_edge_rows_dev=self.n_edge_rows,
+                        xrow=(self.xrow_dev, self.x_rows) if self.x_rows else None)
         self.opt.zero_grad(set_to_none=True)
         # data parallel: the bucket pack is the tail of the first graph and the
         # unpack (/ world) the head of the second, so between the replays the

@@ -64,6 +64,42 @@ class Graph:
         return self.col.numel()
 
 
+class IndexedRows:
+    """x[index] without the copy: the rows of ``table`` (a resident feature
+    matrix) that a block's ``n_id`` names.  A batch of
+    ``NeighborLoader(..., gather_features=False)`` carries one as ``x``; the
+    HIP-graph step (ngnn.graphs) hands table and index to the layer-0 kernels,
+    which gather the rows themselves (fused x[n_id]); anything else calls
+    :meth:`materialize`."""
+
+    def __init__(self, table: torch.Tensor, index: torch.Tensor):
+        self.table, self.index = table, index
+
+    @property
+    def shape(self):
+        return torch.Size((self.index.numel(), self.table.size(1)))
+
+    def size(self, dim=None):
+        return self.shape if dim is None else self.shape[dim]
+
+    @property
+    def dtype(self):
+        return self.table.dtype
+
+    @property
+    def device(self):
+        return self.table.device
+
+    def to(self, device):
+        return IndexedRows(self.table.to(device), self.index.to(device))
+
+    def materialize(self) -> torch.Tensor:
+        return self.table.index_select(0, self.index)
+
+    def record_stream(self, stream):
+        self.index.record_stream(stream)
+
+
 class Batch:
     """One NeighborLoader mini-batch: ``x``, ``y``, ``edge_index``, ``n_id``,
     ``batch_size`` and every further node attribute of the graph (``yhn``
@@ -310,7 +346,7 @@ class NeighborLoader:
 
     def __init__(self, graph, input_nodes=None, num_neighbors=(15, 10), batch_size=1024,
                  shuffle=False, seed: int = 0, rank: int = 0, world_size: int = 1,
-                 drop_last: bool = False, **_ignored):
+                 drop_last: bool = False, gather_features: bool = True, **_ignored):
         if not isinstance(graph, Graph):  # the reference's `data` (pipeline.py:75-92)
             graph = _graph_of(graph)
         self.graph = graph
@@ -323,6 +359,8 @@ class NeighborLoader:
         self.shuffle, self.seed = shuffle, seed
         self.rank, self.world_size = rank, world_size
         self.drop_last = drop_last
+        # False: batches carry x = IndexedRows(graph.x, n_id) (no row copy)
+        self.gather_features = gather_features
         self.epoch = 0
 
     def _seeds(self):
@@ -355,7 +393,9 @@ class NeighborLoader:
             with torch.cuda.stream(side):
                 blk = sample_block(self.graph, s, self.num_neighbors,
                                    seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size
-                                   + self.rank)
+                                   + self.rank, gather_features=self.gather_features)
+                if not self.gather_features:
+                    blk.x = IndexedRows(self.graph.x, blk.n_id)
             main.wait_stream(side)
             for t in (blk.x, blk.y, blk.edge_index, blk.n_id, *blk.node_attrs.values()):
                 if t is not None:

@@ -19,6 +19,7 @@ import torch.nn.functional as F
 
 from . import fused
 from .block import get_block
+from .loader import IndexedRows
 from .nn import GCNConv, SAGEConv
 
 
@@ -59,6 +60,8 @@ class SAGE(nn.Module):
             conv.reset_parameters()
 
     def forward(self, x, edge_index):
+        if isinstance(x, IndexedRows):  # eager: gather the rows (graph replays fuse it)
+            x = x.materialize()
         block = get_block(edge_index, x.size(0))
         if fused.sage_stack_supported(self, x):
             # one autograd node for the stack: fused layer kernels forward,
@@ -105,6 +108,8 @@ class SimpleGCN(nn.Module):
             conv.reset_parameters()
 
     def forward(self, x, edge_index):
+        if isinstance(x, IndexedRows):  # eager: gather the rows (graph replays fuse it)
+            x = x.materialize()
         block = get_block(edge_index, x.size(0))
         if fused.gcn_stack_supported(self, x):
             # one autograd node for the stack (ngnn/fused.py: SAGE layers with

@@ -158,3 +158,42 @@ def test_bucket_view_gradients_adopted():
         assert p.grad.data_ptr() == v.data_ptr(), k
         # (the input-gradient scatter uses float atomics: order-dependent bits)
         torch.testing.assert_close(p.grad, ref[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("arch", ["sage", "gcn"])
+def test_graph_fused_row_gather_matches_eager(arch):
+    """NeighborLoader(gather_features=False) batches carry x = graph.x[n_id]
+    unmaterialized; the captured step hands table + n_id to the layer-0
+    kernels (forward gather and weight gradient read table rows n_id[r]).
+    Same losses and parameters as eager training on the materialized rows,
+    and a plain batch loaded into the same graph (index word 0) still works."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import IndexedRows, NeighborLoader, synthetic_graph
+    g = synthetic_graph("ogbn-arxiv", DEV, seed=0, scale=0.05)
+    lo = NeighborLoader(g, g.train_idx, [10, 5], 256, shuffle=True, seed=3, gather_features=False)
+    batches = [b for _, b in zip(range(4), lo)]
+    assert isinstance(batches[0].x, IndexedRows)
+    torch.testing.assert_close(batches[0].x.materialize(), g.x[batches[0].n_id], rtol=0, atol=0)
+
+    def make():
+        torch.manual_seed(11)
+        if arch == "sage":
+            return ngnn.SAGE(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+        return ngnn.SimpleGCN(g.x.size(1), 160, g.num_classes, 2, dropout=0.0).to(DEV)
+
+    m_e, m_g = make(), make()
+    plain = [type(b)(b.x.materialize(), b.y, b.edge_index, b.n_id, b.batch_size) for b in batches]
+    le = _eager_train(m_e, plain)
+    opt = torch.optim.Adam(m_g.parameters(), lr=1e-2, fused=True, capturable=True)
+    n_cap, e_cap = slot_size(256, [10, 5])
+    step = GraphedTrainStep(m_g, opt, 256, n_cap, e_cap, g.x.size(1), DEV)
+    step.capture(batches[0].x, batches[0].edge_index, batches[0].y)
+    assert step.zero_copy and step.x_rows == g.num_nodes
+    lg = [float(step(b.x, b.edge_index, b.y)) for b in batches[:3]]
+    lg.append(float(step(plain[3].x, plain[3].edge_index, plain[3].y)))  # word 0: plain rows
+    torch.cuda.synchronize()
+    for a, c in zip(le, lg):
+        assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
+    for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)

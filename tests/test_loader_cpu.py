@@ -70,3 +70,25 @@ def test_loader_shards_equal_across_ranks():
         allseeds.append(s)
     assert lens == {25} and sizes == {24_577}
     assert torch.equal(torch.cat(allseeds).unique(), torch.arange(n))
+
+
+def test_indexed_rows_and_zero_copy_envelope():
+    """IndexedRows (NeighborLoader(gather_features=False)'s x) behaves as
+    table[index] for shape/materialize; the graph slot's zero-copy envelope
+    admits a fused x[n_id] gather only within the kernels' offset ranges."""
+    import ngnn
+    from ngnn.fused import zero_copy_ok
+    from ngnn.loader import IndexedRows
+    t = torch.randn(50, 8)
+    idx = torch.tensor([3, 0, 49, 3])
+    r = IndexedRows(t, idx)
+    assert r.shape == (4, 8) and r.size(0) == 4 and r.size(1) == 8 and r.dtype == t.dtype
+    assert torch.equal(r.materialize(), t[idx])
+    assert torch.equal(r.to("cpu").materialize(), t[idx])
+    m = ngnn.SAGE(100, 64, 10, 2)
+    assert zero_copy_ok(m, 200_000, 100, table_rows=2_449_029)      # ogbn-products table
+    assert not zero_copy_ok(m, 200_000, 100, table_rows=6_000_000)  # > 2 GiB (weight gradient)
+    assert not zero_copy_ok(m, 200_000, 102)                        # K % 4
+    g = ngnn.SimpleGCN(100, 16, 10, 2)  # transform-first layer 0: no zero-copy
+    assert not zero_copy_ok(g, 1000, 100)
+    assert zero_copy_ok(ngnn.SimpleGCN(100, 256, 10, 2), 1000, 100)

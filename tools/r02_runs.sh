@@ -8,6 +8,7 @@ tail -1 $O/pytest.log
 timeout -k 10 300 python3 tools/kbench_fwd.py > $O/kbench.json 2>&1 || exit $?
 timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench.log 2>&1 || exit $?
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --module gcn > $O/bench_gcn.log 2>&1 || exit $?
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --gather loader > $O/bench_loadergather.log 2>&1 || exit $?
 if [ "${CONFIGS:-0}" = 1 ]; then
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --dataset ogbn-arxiv > $O/bench_arxiv.log 2>&1 || exit $?
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --dataset computers --fanout 10,5 --batch-size 300 --hidden 512 --aggr max > $O/bench_computers.log 2>&1 || exit $?
