@@ -426,7 +426,11 @@ def test_gcn_stack_fwd_bwd_matches_oracle(dims, layers, train):
     xr = b.x.cpu().clone().requires_grad_(True)
     out_r = ref(xr, b.edge_index.cpu())
     F.cross_entropy(out_r[:b.batch_size], y.cpu()).backward()
-    torch.testing.assert_close(out.detach().cpu(), out_r.detach(), **OUT)
+    # sum aggregation, no normalisation: outputs grow with degree x width, so the
+    # absolute tolerance is OUT's relative to the output scale (fp32 reordering)
+    scale = max(1.0, float(out_r.detach().abs().max()))
+    torch.testing.assert_close(out.detach().cpu(), out_r.detach(), rtol=OUT["rtol"],
+                               atol=OUT["atol"] * scale)
     torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
         torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
