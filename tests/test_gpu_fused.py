@@ -436,17 +436,20 @@ def test_gcn_stack_fwd_bwd_matches_oracle(dims, layers, train):
         torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
 
 
-def test_gcn_graph_step_matches_eager():
-    """SimpleGCN through GraphedTrainStep (zero-copy slot, captured step)
-    equals eager training on the same batches (dropout off)."""
+@pytest.mark.parametrize("hidden", [64, 160])
+def test_gcn_graph_step_matches_eager(hidden):
+    """SimpleGCN through GraphedTrainStep (captured step) equals eager
+    training on the same batches (dropout off).  hidden 160 > F_in 128:
+    aggregate-first layer 0, zero-copy slot; hidden 64: transform-first layer
+    0, whose backward rebuilds its aggregate from the slot's rows (copied)."""
     from ngnn.graphs import GraphedTrainStep, slot_size
     from ngnn.loader import NeighborLoader, synthetic_graph
     g = synthetic_graph("ogbn-arxiv", DEV, seed=0, scale=0.05)
     loader = NeighborLoader(g, g.train_idx, [10, 5], 256, shuffle=True, seed=3)
     batches = [b for _, b in zip(range(4), loader)]
     torch.manual_seed(11)
-    m_e = ngnn.SimpleGCN(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
-    m_g = ngnn.SimpleGCN(g.x.size(1), 64, g.num_classes, 2, dropout=0.0).to(DEV)
+    m_e = ngnn.SimpleGCN(g.x.size(1), hidden, g.num_classes, 2, dropout=0.0).to(DEV)
+    m_g = ngnn.SimpleGCN(g.x.size(1), hidden, g.num_classes, 2, dropout=0.0).to(DEV)
     m_g.load_state_dict(m_e.state_dict())
     o_e = torch.optim.Adam(m_e.parameters(), lr=1e-2, fused=True, capturable=True)
     le = []
@@ -460,7 +463,7 @@ def test_gcn_graph_step_matches_eager():
     n_cap, e_cap = slot_size(256, [10, 5])
     step = GraphedTrainStep(m_g, o_g, 256, n_cap, e_cap, g.x.size(1), DEV)
     step.capture(batches[0].x, batches[0].edge_index, batches[0].y)
-    assert step.zero_copy
+    assert step.zero_copy == (hidden >= g.x.size(1))
     lg = [float(step(b.x, b.edge_index, b.y)) for b in batches]
     torch.cuda.synchronize()
     for a, c in zip(le, lg):
