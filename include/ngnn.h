@@ -257,7 +257,9 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * xrow[r] (int64, the block's n_id) of x, the HBM-resident feature table of
  * x_rows rows (< 3.75 GiB), so x[n_id] is never materialised (pipeline.py:153
  * copies it per batch).  Root rows and gathered neighbour rows both go
- * through it; outputs and agg_out stay in block order.
+ * through it; outputs and agg_out stay in block order.  col_x (nullable,
+ * with xrow): col with every entry already mapped through xrow (the slot
+ * load writes it), so the neighbour gather makes no dependent index load.
  * wr == NULL: no root term (GCNConv's form, see ngnn_gcn_agg_fwd; raw
  * weights only, not with NGNN_FWD_NARROW).
  * n_edge_rows / n_edge_rows_dev (device int, nullable, min'd with the
@@ -271,7 +273,7 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
                       const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                       const int32_t *n_edge_rows_dev, const int32_t *rowptr,
-                      const int32_t *col,
+                      const int32_t *col, const int32_t *col_x,
                       int reduce, const float *wl, const float *wr, int64_t ldw, const float *bias,
                       int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                       const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
@@ -454,7 +456,7 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
                    int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-                   void *stream);
+                   int32_t *slot_colx, void *stream);
 
 #ifdef __cplusplus
 }

@@ -131,6 +131,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int *rc, int64_t ldw = 0, void *wl_ws = nullptr, size_t wl_ws_bytes = 0,
                      const float *const *x_dev = nullptr, bool exact = true,
                      float *z = nullptr, int64_t ldz = 0, const int64_t *xrow = nullptr,
-                     const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0);
+                     const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
+                     const int32_t *col_x = nullptr);
 
 }  // namespace ngnn

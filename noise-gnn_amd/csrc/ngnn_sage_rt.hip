@@ -95,6 +95,10 @@ struct RtArgs {
     int vec_out;
     float *agg_out;
     int64_t ld_agg;
+    // non-null: the neighbour aggregate of every row is already in agg_in
+    // (ld_agg), written by the first column slice of this layer -- later
+    // slices read it densely instead of gathering again
+    const float *agg_in;
     Epi epi;
     const uint64_t *seed_dev;                 // XORed into the dropout seed (HIP-graph replays)
     const float *const *x_dev;                // non-null: x's address read at run time (graph slot)
@@ -104,6 +108,9 @@ struct RtArgs {
     const int64_t *xrow;
     const int64_t *const *xrow_dev;
     int64_t x_rows;
+    // (with xrow) col already mapped through xrow: the gather's sources are
+    // table rows, no dependent index load per neighbour
+    const int32_t *col_x;
     // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
     // when kpad), then T4 exact-fp32 steps of 4 columns
     int C, T4, kpad;
@@ -352,12 +359,13 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 #pragma unroll 1
     for (int e0 = 0; e0 < maxdeg; e0 += 16) {
         int cb[4];
+        const int32_t *cl = a.col_x ? a.col_x : a.col;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int e = e0 + 4 * q + j;
-            cb[j] = a.col[(beg + e) & lt_mask(e, deg)];  // invalid slots read col[0]
+            cb[j] = cl[(beg + e) & lt_mask(e, deg)];  // invalid slots read col[0]
         }
-        if (xrow) {  // fused x[n_id]: the neighbours' rows in the feature table
+        if (xrow && !a.col_x) {  // fused x[n_id]: the neighbours' rows in the feature table
 #pragma unroll
             for (int j = 0; j < 4; ++j) cb[j] = static_cast<int>(xrow[cb[j]]);
         }
@@ -750,11 +758,18 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 const int k0 = c * RT_KC * 16;
                 const int nkg = min(RT_KC, a.KG - c * RT_KC);
                 v4f ag[RT_KC];
-                gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q, xrow);
+                if (a.agg_in) {
+                    const i32x4 air = tile_rsrc(a.agg_in, a.ld_agg, a.K, t, n_rows);
+                    v4f av[RT_KC];
+                    load_x<false>(av, air, static_cast<uint32_t>(rl * a.ld_agg * 4), k0, q);
+                    mask_x(ag, av, a, k0, q);
+                } else {
+                    gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q, xrow);
+                }
                 // edge tiles prefetch the next tile only now: its x fragments
                 // are not live across the gather (register budget)
                 if (c == nchunk_l - 1) prefetch(tnext, roff_nn);
-                if (a.agg_out) {
+                if (a.agg_out && !a.agg_in) {
                     int kq = a.K - k0 - 4 * q;
                     asm volatile("" : "+v"(kq));  // per-lane masks stay VGPR selects here
                     const int aoff = (rl * static_cast<int>(a.ld_agg) + k0 + 4 * q) * 4;
@@ -959,7 +974,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, hipStream_t st,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
                      const float *const *x_dev, bool exact, float *z, int64_t ldz,
-                     const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows) {
+                     const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
+                     const int32_t *col_x) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -1067,12 +1083,16 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(out + c0, 16);
         a.agg_out = (c0 == 0 && !narrow) ? agg_out : nullptr;
         a.ld_agg = ld_agg;
+        // later column slices read the aggregate the first one saved (the
+        // launches are stream-ordered) instead of gathering it again
+        a.agg_in = (c0 > 0 && !narrow && has_l) ? agg_out : nullptr;
         a.epi = Epi{bias ? bias + c0 : nullptr, relu, drop, static_cast<int>(c0)};
         a.seed_dev = seed_dev;
         a.x_dev = x_dev;
         a.xrow = xrow;
         a.xrow_dev = xrow_dev;
         a.x_rows = x_rows;
+        a.col_x = (xrow || xrow_dev) ? col_x : nullptr;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
@@ -1102,8 +1122,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
                                  const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx,
                                  int64_t K, int64_t n_rows, const int32_t *n_rows_dev,
                                  int64_t n_edge_rows, const int32_t *n_edge_rows_dev,
-                                 const int32_t *rowptr,
-                                 const int32_t *col, int reduce, const float *wl, const float *wr,
+                                 const int32_t *rowptr, const int32_t *col, const int32_t *col_x,
+                                 int reduce, const float *wl, const float *wr,
                                  int64_t ldw, const float *bias, int64_t Fo, float *out,
                                  int64_t ldo, int relu, float p_drop, uint64_t seed,
                                  const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
@@ -1136,7 +1156,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         float *z = static_cast<float *>(ws);
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
-                             nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows)) {
+                             nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -1154,7 +1174,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
-                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows))
+                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

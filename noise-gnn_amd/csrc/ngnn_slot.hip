@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
     uint32_t gen, int32_t *__restrict__ n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-    int vec) {
+    int32_t *__restrict__ colx, int vec) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
@@ -95,6 +95,12 @@ __global__ __launch_bounds__(256) void k_slot_load(
         for (int64_t e = tid; e < e_cap; e += nthr)
             col[e] = static_cast<int32_t>(e < E ? ei[e] : N + ((e - E) * span) / n_pad);
     }
+    if (colx) {
+        // layer 0's gather columns: the sources' rows in the feature table
+        // (padding edges feed skipped rows only: 0)
+        for (int64_t e = tid; e < e_cap; e += nthr)
+            colx[e] = static_cast<int32_t>(e < E ? (xrow ? xrow[ei[e]] : ei[e]) : 0);
+    }
     if (r_next) {
         // max(B, 1 + max source over the edges into rows < B), as a 64-bit
         // atomicMax of (gen << 32 | value): this load's generation outranks
@@ -142,7 +148,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
                               int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-                              void *stream) {
+                              int32_t *slot_colx, void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
@@ -161,6 +167,6 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
                        n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
-                       xrow, xrow_dev, vec);
+                       xrow, xrow_dev, slot_colx, vec);
     return launch_status();
 }

@@ -56,12 +56,12 @@ SIGNATURES = {
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                               _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p, _p,
-                              _p]),
+                              _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
     "ngnn_sage_fwd_raw_workspace_bytes": (_sz, [_i64, _i64, _i64]),
-    "ngnn_sage_fwd_raw": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _int, _p, _p,
+    "ngnn_sage_fwd_raw": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int, _p, _p,
                                  _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),

@@ -113,6 +113,7 @@ class Block:
         # count of the feature table x_dev then points at
         self.xrow_dev = None
         self.x_rows = 0
+        self.col_x = None  # int32 col mapped through n_id (the slot load writes it)
 
     @property
     def rowptr(self):
@@ -159,7 +160,7 @@ class _BlockCache:
             blk.r_next = hint[7]
             blk.n_edge_rows_dev = hint[8]
             if hint[9] is not None:
-                blk.xrow_dev, blk.x_rows = hint[9]
+                blk.xrow_dev, blk.x_rows, blk.col_x = hint[9]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -196,9 +197,9 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     rows the layer-0 kernels must read (zero-copy slot).  r_next: (device int32,
     R): the producer keeps ngnn_block_prefix_stats' bound for R there.
     n_edge_rows_dev: device int32 holding n_active for a changing batch.
-    xrow: (device word, table rows): the producer stores the address of the
-    batch's n_id in the word when x_dev points at the whole feature table
-    (fused x[n_id] gather), 0 otherwise."""
+    xrow: (device word, table rows, col_x): the producer stores the address of
+    the batch's n_id in the word when x_dev points at the whole feature table
+    (fused x[n_id] gather), 0 otherwise, and keeps col_x = n_id[col] (int32)."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,

@@ -190,6 +190,17 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     wr_ = wr.detach() if root else None
     if wl_.stride(1) != 1 or (root and (wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0))):
         wl_, wr_ = wl_.contiguous(), (wr_.contiguous() if root else None)
+    xk = x
+    if K % 4 and pad_k_ok(K) and x_dev is None and not narrow and (
+            agg_out is None or agg_out.stride(0) % 4 == 0):
+        # the row-tile kernel reads 16-B column quads: one zero column (or
+        # three) appended to x and to the weights -- 0 * 0 terms, the same
+        # sums -- instead of the 64-row fallback (Amazon-Computers' K = 767)
+        K4 = K + (-K) % 4
+        xk = torch.zeros(N, K4, dtype=torch.float32, device=x.device)
+        xk[:, :K].copy_(x)
+        wl_ = _pad_cols(wl_, K4)
+        wr_ = _pad_cols(wr_, K4) if root else None
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
@@ -198,14 +209,16 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel
         n_edge = N if block.n_active is None else min(int(block.n_active), N)
         rc = lib.ngnn_sage_fwd_raw(
-            _lib.ptr(x), _lib.ptr(x_dev), None, _lib.ptr(xrow_dev), int(x_rows), x.stride(0), K, N,
-            nrd, n_edge,
+            _lib.ptr(xk), _lib.ptr(x_dev), None, _lib.ptr(xrow_dev), int(x_rows), xk.stride(0),
+            xk.size(1), N, nrd, n_edge,
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.ptr(block.col_x) if xrow_dev is not None else None,
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0),
             _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
-            _lib.ptr(seed_dev), _lib.ptr(agg_out), agg_out.stride(0) if agg_out is not None else K,
+            _lib.ptr(seed_dev), _lib.ptr(agg_out),
+            agg_out.stride(0) if agg_out is not None else xk.size(1),
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
         if rc == _lib.E_SHAPE:
             if x_dev is not None:
@@ -216,6 +229,27 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
                         agg_out=agg_out, seed_dev=seed_dev, n_rows_dev=block.n_rows_dev)
         else:
             _lib.check(rc, "ngnn_sage_fwd_raw")
+    return out
+
+
+def pad_k_ok(K: int) -> bool:
+    """Does a K % 4 != 0 layer run on the row-tile kernel after padding K to
+    a multiple of 4?  (Its split-bf16 W image must fit the LDS.)"""
+    return K <= 1536
+
+
+def agg_buffer(N: int, K: int, device) -> torch.Tensor:
+    """[N, K] saved-aggregate buffer; rows padded to a multiple of 4 floats
+    when the forward pads K (pad_k_ok), so the kernel can write it whole."""
+    if K % 4 and pad_k_ok(K):
+        K4 = K + (-K) % 4
+        return torch.empty(N, K4, dtype=torch.float32, device=device)[:, :K]
+    return torch.empty(N, K, dtype=torch.float32, device=device)
+
+
+def _pad_cols(w: torch.Tensor, K4: int) -> torch.Tensor:
+    out = torch.zeros(w.shape[0], K4, dtype=torch.float32, device=w.device)
+    out[:, :w.shape[1]].copy_(w)
     return out
 
 
@@ -250,7 +284,7 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
         rc = lib.ngnn_sage_fwd_raw(
             _lib.ptr(x), _lib.ptr(x_dev), None, _lib.ptr(xrow_dev), int(x_rows), x.stride(0), K, N,
             nrd, N, None, _lib.ptr(block.rowptr),
-            _lib.ptr(block.col), _lib.REDUCE["sum"] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
+            _lib.ptr(block.col), None, _lib.REDUCE["sum"] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0),
             None, _lib.ptr(wd), wd.stride(0), None, Fo, _lib.ptr(z), ldz, 0, 0.0, 0, None, None, K,
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
         if rc == _lib.E_SHAPE:
@@ -292,7 +326,7 @@ class _SAGEStack(torch.autograd.Function):
                 # (its K-wide aggregate is rebuilt for the seed rows in backward)
                 narrow = (wr is not None and last and i > 0
                           and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0))
-                agg = None if narrow else torch.empty(h.shape, dtype=torch.float32, device=h.device)
+                agg = None if narrow else agg_buffer(h.size(0), h.size(1), h.device)
                 h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
                                    seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
                                    span=f"sage_fwd_l{i}", narrow=narrow, **xrow)

@@ -73,6 +73,7 @@ class GraphedTrainStep:
         # rows); x_rows = the table's rows the captured kernels range over
         self.xrow_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         self.x_rows = 0
+        self.col_x = None  # layer 0's gather columns (table rows), allocated at capture
         self._gen = 0
         self._x_live = None  # the loaded batch's features, kept alive until the next load
         self.g_fb = self.g_opt = None
@@ -136,6 +137,7 @@ class GraphedTrainStep:
             _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.seed_state),
             _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
             _lib.ptr(self.n_edge_rows), _lib.ptr(xrow), _lib.ptr(xrow_word),
+            _lib.ptr(self.col_x) if xrow_word is not None else None,
             _lib.stream_handle(self.x.device)), "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
 
@@ -192,11 +194,13 @@ class GraphedTrainStep:
             table_rows = 0
             self.zero_copy = zero_copy_ok(self.model, self.n_cap, self.x.size(1))
         self.x_rows = table_rows if self.zero_copy else 0
+        if self.x_rows:
+            self.col_x = torch.zeros(self.e_cap, dtype=torch.int32, device=self.x.device)
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
                         x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B),
                         n_edge_rows_dev=self.n_edge_rows,
-                        xrow=(self.xrow_dev, self.x_rows) if self.x_rows else None)
+                        xrow=(self.xrow_dev, self.x_rows, self.col_x) if self.x_rows else None)
         self.opt.zero_grad(set_to_none=True)
         # data parallel: the bucket pack is the tail of the first graph and the
         # unpack (/ world) the head of the second, so between the replays the
