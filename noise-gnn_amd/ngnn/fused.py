@@ -191,7 +191,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     if wl_.stride(1) != 1 or (root and (wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0))):
         wl_, wr_ = wl_.contiguous(), (wr_.contiguous() if root else None)
     xk = x
-    if K % 4 and pad_k_ok(K) and x_dev is None and not narrow and (
+    if K % 4 and pad_k_ok(K, Fo) and x_dev is None and not narrow and (
             agg_out is None or agg_out.stride(0) % 4 == 0):
         # the row-tile kernel reads 16-B column quads: one zero column (or
         # three) appended to x and to the weights -- 0 * 0 terms, the same
@@ -232,16 +232,23 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     return out
 
 
-def pad_k_ok(K: int) -> bool:
-    """Does a K % 4 != 0 layer run on the row-tile kernel after padding K to
-    a multiple of 4?  (Its split-bf16 W image must fit the LDS.)"""
-    return K <= 1536
+def pad_k_ok(K: int, Fo: int = 0) -> bool:
+    """Does a K % 4 != 0 layer run well on the row-tile kernel after padding
+    K to a multiple of 4?  Its split-bf16 W_r image (3 x ceil(K/32) KiB per
+    16 outputs) must fit the LDS for enough output tiles that F_out takes at
+    most two column slices (each slice re-reads x: measured on
+    Amazon-Computers' 767 -> 512 layer, 16 slices ran 1.4x slower than the
+    64-row kernel)."""
+    K4 = K + (-K) % 4
+    img = 3 * (-(-K4 // 32)) * 1024
+    ntw = next((c for c in (16, 8, 6, 4, 3, 2) if c * img <= 160 * 1024 - 1280), 0)
+    return ntw > 0 and -(-Fo // (16 * ntw)) <= 2
 
 
-def agg_buffer(N: int, K: int, device) -> torch.Tensor:
+def agg_buffer(N: int, K: int, device, Fo: int = 0) -> torch.Tensor:
     """[N, K] saved-aggregate buffer; rows padded to a multiple of 4 floats
     when the forward pads K (pad_k_ok), so the kernel can write it whole."""
-    if K % 4 and pad_k_ok(K):
+    if K % 4 and pad_k_ok(K, Fo):
         K4 = K + (-K) % 4
         return torch.empty(N, K4, dtype=torch.float32, device=device)[:, :K]
     return torch.empty(N, K, dtype=torch.float32, device=device)
@@ -326,7 +333,7 @@ class _SAGEStack(torch.autograd.Function):
                 # (its K-wide aggregate is rebuilt for the seed rows in backward)
                 narrow = (wr is not None and last and i > 0
                           and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0))
-                agg = None if narrow else agg_buffer(h.size(0), h.size(1), h.device)
+                agg = None if narrow else agg_buffer(h.size(0), h.size(1), h.device, wl.shape[0])
                 h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
                                    seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
                                    span=f"sage_fwd_l{i}", narrow=narrow, **xrow)
