@@ -5,6 +5,14 @@
 
 namespace ngnn {
 
+// a load through a global (address-space 1) pointer: a pointer read from
+// memory (e.g. a graph slot's device word) is otherwise generic and becomes a
+// flat load, which also counts against lgkmcnt and serialises LDS waits
+template <typename T>
+__device__ __forceinline__ T gload(const T *p, int64_t i) {
+    return ((const __attribute__((address_space(1))) T *)(p))[i];
+}
+
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 

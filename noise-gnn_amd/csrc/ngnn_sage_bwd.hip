@@ -83,7 +83,7 @@ struct Chunk {
             const bool kok = k < K;
             int vo;
             if (ridx) {
-                const int pr = r < static_cast<int>(nr) ? static_cast<int>(ridx[c0 + r]) : -1;
+                const int pr = r < static_cast<int>(nr) ? static_cast<int>(gload(ridx, c0 + r)) : -1;
                 vo = (kok && pr >= 0) ? (pr * static_cast<int>(ld) + k) * 4 : kBufOOB;
             } else {
                 vo = kok ? (r * static_cast<int>(ld) + k) * 4 : kBufOOB;

@@ -367,7 +367,7 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
         }
         if (xrow && !a.col_x) {  // fused x[n_id]: the neighbours' rows in the feature table
 #pragma unroll
-            for (int j = 0; j < 4; ++j) cb[j] = static_cast<int>(xrow[cb[j]]);
+            for (int j = 0; j < 4; ++j) cb[j] = static_cast<int>(gload(xrow, cb[j]));
         }
         const int ne = min(16, maxdeg - e0);
 #pragma unroll 1  // one neighbour pair in flight: keep the register budget
@@ -503,7 +503,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     v4f *swl = lds + (X3 ? x3_v4f : nfr);
     float *sbias = reinterpret_cast<float *>(swl + (WL_LDS ? nfr : 0));
     const int have_l = a.wl != nullptr;
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    // (wave index uniform: readfirstlane, so tile indices and the per-tile
+    // buffer resources derived from them stay scalar -- no waterfall loops)
+    const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int ln = threadIdx.x & 63;
     {
         const int nch = a.NT * a.KG;  // valid 1-KiB fp32 fragments per matrix
         if (X3) {
@@ -657,7 +660,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // byte offset of logical row rr in x (kOOB past the block's rows)
     auto row_off = [&](int rr) -> uint32_t {
         if (rr >= n_rows) return static_cast<uint32_t>(kOOB);
-        const int pr = xrow ? static_cast<int>(xrow[rr]) : rr;
+        const int pr = xrow ? static_cast<int>(gload(xrow, rr)) : rr;
         return static_cast<uint32_t>(pr) * ld4;
     };
     uint32_t roff_n = 0;   // the next tile's row offset (its rows are in flight)
