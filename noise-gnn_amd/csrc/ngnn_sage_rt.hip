@@ -46,6 +46,10 @@
 
 #include "ngnn_device.h"
 
+#ifndef NGNN_RT_STATIC
+#define NGNN_RT_STATIC 0  // (A/B build flag) 1: fixed tile-per-wave schedule
+#endif
+
 namespace ngnn {
 
 namespace {
@@ -221,9 +225,24 @@ __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[R
             bf16x8 x1, x2, x3;
             split3(lo, hi, x1, x2, x3);
             const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
+            // W parts of tile m + 1 are read from LDS while tile m's six
+            // MFMAs run (double-buffered): the reads' latency stays off the
+            // matrix pipe (read just in time, each tile waited on lgkmcnt(0))
+            bf16x8 wb[2][3];
+            wb[0][0] = w[0];
+            wb[0][1] = w[pst];
+            wb[0][2] = w[2 * pst];
 #pragma unroll
             for (int m = 0; m < NTW; ++m) {
-                const bf16x8 w1 = w[m * 64], w2 = w[pst + m * 64], w3 = w[2 * pst + m * 64];
+                if (m + 1 < NTW) {
+                    const int o = (m + 1) * 64;
+                    wb[(m + 1) & 1][0] = w[o];
+                    wb[(m + 1) & 1][1] = w[pst + o];
+                    wb[(m + 1) & 1][2] = w[2 * pst + o];
+                }
+                // (keeps the scheduler from sinking those reads down to their use)
+                __builtin_amdgcn_sched_barrier(0);
+                const bf16x8 w1 = wb[m & 1][0], w2 = wb[m & 1][1], w3 = wb[m & 1][2];
                 v4f t = acc[m];
                 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3, x1, t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x3, t, 0, 0, 0);
@@ -638,7 +657,11 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     };
     (void)tile_of;
     int kt = 0;
+#if NGNN_RT_STATIC
+    int t = tile_of(0);
+#else
     int t = static_cast<int>(blockIdx.x) + wave * static_cast<int>(gridDim.x);  // first claims: waves 0..7
+#endif
     int tnext = 0;
     // next tile's chunk-0 x fragments and row bounds, loaded one tile ahead,
     // unconditionally (a tile past the end re-reads tile 0: valid, unused)
@@ -700,7 +723,12 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         prefetch(t, row_off(t * RT_ROWS + rl0));
     }
     for (; t < n_tiles; t = tnext, ++kt) {
+#if NGNN_RT_STATIC
+        tnext = tile_of(kt + 1);
+        (void)claim;
+#else
         tnext = claim();
+#endif
         const uint32_t roff = roff_n;  // this tile's row offset (prefetch overwrites roff_n)
         int lane, q, rl;
         lane_ids(lane, q, rl);
