@@ -46,6 +46,12 @@
 
 #include "ngnn_device.h"
 
+#ifndef NGNN_RT_WSTREAM_DEPTH
+#define NGNN_RT_WSTREAM_DEPTH 2  // (A/B build flag) W_l fragment groups in flight from L2
+#endif
+#ifndef NGNN_RT_MAXNTW
+#define NGNN_RT_MAXNTW 16  // (A/B build flag) widest output-tile slice
+#endif
 #ifndef NGNN_RT_STATIC
 #define NGNN_RT_STATIC 0  // (A/B build flag) 1: fixed tile-per-wave schedule
 #endif
@@ -305,19 +311,26 @@ __device__ __forceinline__ void mfma_chunk_rt(v4f (&acc)[NTW], const v4f (&xf)[R
     // from L2 (the streamed path's address registers are the tighter budget)
     constexpr int P = NTW >= 8 ? NTW / (LDSW ? 4 : 2) : 1;
     constexpr int H = NTW / P;
-    v4f wb[2][H];
-    load_w<NTW, H, LDSW>(wb[0], wsrc, KG, kg0, 0, NT, lane);
+    // NB-deep ring: groups s + 1 .. s + NB - 1 in flight while group s's
+    // MFMAs run (L2 latency is ~10x a group's MFMA time when streamed)
+    constexpr int NB = LDSW ? 2 : NGNN_RT_WSTREAM_DEPTH;
+    constexpr int NS = RT_KC * P;
+    v4f wb[NB][H];
 #pragma unroll
-    for (int s = 0; s < RT_KC * P; ++s) {
+    for (int s = 0; s < NB - 1; ++s)
+        if (s < NS) load_w<NTW, H, LDSW>(wb[s], wsrc, KG, kg0 + s / P, s % P, NT, lane);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
         const int g = s / P, p = s % P;
-        const int sn = s + 1, gn = sn / P, pn = sn % P;
-        if (sn < RT_KC * P) load_w<NTW, H, LDSW>(wb[sn & 1], wsrc, KG, kg0 + gn, pn, NT, lane);
+        const int sn = s + NB - 1, gn = sn / P, pn = sn % P;
+        if (sn < NS) load_w<NTW, H, LDSW>(wb[sn % NB], wsrc, KG, kg0 + gn, pn, NT, lane);
+        if (LDSW) __builtin_amdgcn_sched_barrier(0);  // keep the next group's reads ahead
         if (g < nkg) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int h = 0; h < H; ++h)
-                    acc[p * H + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[s & 1][h][i], xf[g][i],
+                    acc[p * H + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[s % NB][h][i], xf[g][i],
                                                                           acc[p * H + h], 0, 0, 0);
         }
     }
@@ -1046,7 +1059,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     const size_t lds_cap = 160 * 1024 - 1024 - 256;  // minus the bias slice and static LDS
     int ntw_max = 0;
     for (int c : {16, 8, 6, 4, 3, 2})
-        if (static_cast<size_t>(c) * img_kb <= lds_cap) {
+        if (c <= NGNN_RT_MAXNTW && static_cast<size_t>(c) * img_kb <= lds_cap) {
             ntw_max = c;
             break;
         }
