@@ -59,6 +59,13 @@ extern "C" {
  * W_l . mean(x_j) up to fp32 rounding (the aggregation is linear); the
  * K-wide gather becomes an F_out-wide one.  Other cases run the fused path. */
 #define NGNN_FWD_NARROW 0x200
+/* flag OR-ed into ngnn_sage_fwd_raw's `reduce`: x (and x_dev's rows) are
+ * bf16 [*, ldx] (ldx in elements, a multiple of 4; 16-B aligned base).  The
+ * rows are read as bf16 -- half the bytes of the fp32 layout -- and widened
+ * exactly: the split-bf16 root term needs one part (3 products), the gather
+ * sums in fp32.  Outputs and agg_out stay fp32.  Not with NGNN_MATH_EXACT_F32
+ * or NGNN_FWD_NARROW (NGNN_E_SHAPE: convert x and call again). */
+#define NGNN_X_BF16 0x400
 
 /* dtypes */
 #define NGNN_F32 0
@@ -321,11 +328,14 @@ size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K);
  * ngnn_sage_fwd_raw's x_dev). */
 /* h_idx / h_idx_dev (nullable; the device word overrides): row r of h is
  * row h_idx[r] of h, a table of h_rows rows (< 2 GiB) -- layer 0 under the
- * fused x[n_id] gather (see ngnn_sage_fwd_raw's xrow). */
+ * fused x[n_id] gather (see ngnn_sage_fwd_raw's xrow).  h_bf16: h holds bf16
+ * (a bf16 model's layer input, as ngnn_sage_fwd_raw's NGNN_X_BF16; K and ldh
+ * multiples of 4), widened exactly when staged. */
 int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy, float yscale,
                     const float *h, const float *const *h_dev, const int64_t *h_idx,
-                    const int64_t *const *h_idx_dev, int64_t h_rows, int64_t ldh, const float *agg,
-                    int64_t ld_agg, const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
+                    const int64_t *const *h_idx_dev, int64_t h_rows, int h_bf16, int64_t ldh,
+                    const float *agg, int64_t ld_agg, const int32_t *rowptr, int64_t n_rows,
+                    const int32_t *r_ptr,
                     int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
                     size_t ws_bytes, void *stream);
 /* Input gradient of one layer, rows j < Rn = *rnext_ptr (R = *r_ptr):

@@ -23,6 +23,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ v4f buf_load4(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 __device__ float buf_load1(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
 __device__ int buf_load1i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ i32x2 buf_load2i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ i32x4 buf_load4i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void buf_store4(v4f v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
 __device__ void buf_store1(float v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
 
@@ -48,6 +51,17 @@ __device__ __forceinline__ i32x4 make_rsrc_u(const void *p, uint32_t bytes) {
     r.w = 0x00020000;
     return r;
 }
+// 4 bf16 (two little-endian words: element 2j in the low half of word j) ->
+// 4 floats, exactly
+__device__ __forceinline__ v4f bf16x4_to_f32(i32x2 w) {
+    v4f o;
+    o[0] = __int_as_float(w.x << 16);
+    o[1] = __int_as_float(w.x & static_cast<int>(0xffff0000u));
+    o[2] = __int_as_float(w.y << 16);
+    o[3] = __int_as_float(w.y & static_cast<int>(0xffff0000u));
+    return o;
+}
+
 // byte offset that is always outside a resource of < 2 GiB
 constexpr int kBufOOB = 0x7fffffff;
 
@@ -140,6 +154,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const float *const *x_dev = nullptr, bool exact = true,
                      float *z = nullptr, int64_t ldz = 0, const int64_t *xrow = nullptr,
                      const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
-                     const int32_t *col_x = nullptr);
+                     const int32_t *col_x = nullptr, bool x_bf16 = false);
 
 }  // namespace ngnn

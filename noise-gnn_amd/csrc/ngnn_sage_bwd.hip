@@ -51,8 +51,8 @@ __device__ __forceinline__ int wgrad_slices(int R, int S) {
 // "has in-edges" test (rowptr: the saved aggregate of an edgeless row is never
 // written) are applied when the registers are written to LDS, so no load
 // waits on another.  Needs ld * 64 * 4 < 2^31 (host-checked).
-template <int COLS, bool VEC, bool MASK, bool DEG>
-struct Chunk {
+template <int COLS, bool VEC, bool MASK, bool DEG, bool BF = false>
+struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
     static constexpr int W = VEC ? 4 : 1;
     static constexpr int CPR = COLS / W;               // loads per row
     static constexpr int N = WG_BM * CPR / 512;        // loads per thread
@@ -69,9 +69,11 @@ struct Chunk {
                                          const int32_t *__restrict__ rowptr, int64_t c0, int re,
                                          int k0, int K, const int64_t *__restrict__ ridx = nullptr,
                                          int64_t src_rows = 0) {
+        constexpr uint32_t EB = BF ? 2u : 4u;
         const uint32_t nr = static_cast<uint32_t>(re - c0);
-        const i32x4 rs = ridx ? make_rsrc(src, static_cast<uint32_t>(src_rows * ld * 4))
-                             : make_rsrc(src + c0 * ld, nr * static_cast<uint32_t>(ld) * 4u);
+        const char *sb = reinterpret_cast<const char *>(src);
+        const i32x4 rs = ridx ? make_rsrc(sb, static_cast<uint32_t>(src_rows * ld * EB))
+                             : make_rsrc(sb + c0 * ld * EB, nr * static_cast<uint32_t>(ld) * EB);
         i32x4 rm = rs, rp = rs;
         if (MASK) rm = make_rsrc(mask + c0 * ldm, nr * static_cast<uint32_t>(ldm) * 4u);
         if (DEG) rp = make_rsrc(rowptr + c0, (nr + 1u) * 4u);
@@ -84,12 +86,20 @@ struct Chunk {
             int vo;
             if (ridx) {
                 const int pr = r < static_cast<int>(nr) ? static_cast<int>(gload(ridx, c0 + r)) : -1;
-                vo = (kok && pr >= 0) ? (pr * static_cast<int>(ld) + k) * 4 : kBufOOB;
+                vo = (kok && pr >= 0) ? (pr * static_cast<int>(ld) + k) * static_cast<int>(EB) : kBufOOB;
             } else {
-                vo = kok ? (r * static_cast<int>(ld) + k) * 4 : kBufOOB;
+                vo = kok ? (r * static_cast<int>(ld) + k) * static_cast<int>(EB) : kBufOOB;
             }
-            if constexpr (VEC) v[u] = buf_load4(rs, vo, 0, 0);
-            else v[u] = buf_load1(rs, vo, 0, 0);
+            if constexpr (BF && VEC) {
+                v[u] = bf16x4_to_f32(buf_load2i(rs, vo, 0, 0));
+            } else if constexpr (BF) {  // the dword holding the element, then its half
+                const int w = buf_load1i(rs, vo & ~3, 0, 0);
+                v[u] = __int_as_float((vo & 2) ? (w & static_cast<int>(0xffff0000u)) : (w << 16));
+            } else if constexpr (VEC) {
+                v[u] = buf_load4(rs, vo, 0, 0);
+            } else {
+                v[u] = buf_load1(rs, vo, 0, 0);
+            }
             if (MASK) {
                 const int mo = kok ? (r * static_cast<int>(ldm) + k) * 4 : kBufOOB;
                 if constexpr (VEC) m[u] = buf_load4(rm, mo, 0, 0);
@@ -164,7 +174,7 @@ __device__ __forceinline__ void wgrad_mfma_dispatch(int ktn, v4f (&acc)[NTW][KTW
 // matrix split the (4) Fo tiles of the workgroup; else they split the K tiles.
 // Slice s owns rows [rb, re) (R split into S ranges on 4-row boundaries, so
 // every used slice gets the same work +-4 rows), walked in 64-row chunks.
-template <int NTW, int KTW, bool SPLIT_N, bool VZ, bool VH, bool MASK>
+template <int NTW, int KTW, bool SPLIT_N, bool VZ, int VH, bool MASK>
 __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
     float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
@@ -206,9 +216,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     // column sums of dz: thread (row group wave, column lane) over 8 rows/chunk
     float dbias = 0.0f;
 
+    // VH: 0 scalar fp32, 1 16-B fp32, 2 bf16 h (8-B loads; agg stays fp32)
     Chunk<WG_NC, VZ, MASK, false> cz;
-    Chunk<WG_KC, VH, false, false> ch;
-    Chunk<WG_KC, VH, false, true> ca;
+    Chunk<WG_KC, VH != 0, false, false, VH == 2> ch;
+    Chunk<WG_KC, VH != 0, false, true> ca;
     if (rb < re) {
         cz.load(dy, ldy, y, ldyy, nullptr, rb, re, n0, Fo);
         ch.load(h, ldh, nullptr, 0, nullptr, rb, re, k0, K, h_idx, h_rows);
@@ -811,7 +822,7 @@ extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
 }
 
 template <int NTW, int KTW, bool SPLIT_N>
-static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const float *dy, int64_t ldy,
+static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, int vh, const float *dy, int64_t ldy,
                          const float *y, int64_t ldyy, float yscale, const float *h,
                          const float *const *h_dev, int64_t ldh, const int64_t *h_idx,
                          const int64_t *const *h_idx_dev, int64_t h_rows, const float *agg,
@@ -829,19 +840,24 @@ static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, bool vh, const floa
         if (y) go(vz_c, vh_c, T{});
         else go(vz_c, vh_c, F{});
     };
+    using V0 = std::integral_constant<int, 0>;
+    using V1 = std::integral_constant<int, 1>;
+    using V2 = std::integral_constant<int, 2>;
     if (vz) {
-        if (vh) with_mask(T{}, T{});
-        else with_mask(T{}, F{});
+        if (vh == 2) with_mask(T{}, V2{});
+        else if (vh) with_mask(T{}, V1{});
+        else with_mask(T{}, V0{});
     } else {
-        if (vh) with_mask(F{}, T{});
-        else with_mask(F{}, F{});
+        if (vh == 2) with_mask(F{}, V2{});
+        else if (vh) with_mask(F{}, V1{});
+        else with_mask(F{}, V0{});
     }
 }
 
 extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
                                float yscale, const float *h, const float *const *h_dev,
                                const int64_t *h_idx, const int64_t *const *h_idx_dev, int64_t h_rows,
-                               int64_t ldh, const float *agg, int64_t ld_agg,
+                               int h_bf16, int64_t ldh, const float *agg, int64_t ld_agg,
                                const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
                                int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
                                size_t ws_bytes, void *stream) {
@@ -859,11 +875,16 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     // offsets over the whole table
     NGNN_RETURN_IF((h_idx || h_idx_dev) && (h_rows <= 0 || h_rows * ldh * 4 >= (int64_t{1} << 31)),
                    NGNN_E_RANGE);
+    // bf16 h (a bf16 model's layer input): 8-B loads, rows 8-B aligned
+    NGNN_RETURN_IF(h_bf16 && (K % 4 != 0 || ldh % 4 != 0 || ld_agg % 4 != 0 ||
+                              (!h_dev && !aligned(h, 8)) || !aligned(agg, 16)),
+                   NGNN_E_SHAPE);
     // 16-B staging per operand pair: dz (+ its mask y) and h / agg
     const bool vz = (Fo % 4 == 0) && (ldy % 4 == 0) && aligned(dy, 16) &&
                     (!y || ((ldyy % 4 == 0) && aligned(y, 16)));
-    const bool vh = (K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) &&
-                    (h_dev || aligned(h, 16)) && aligned(agg, 16);  // h_dev: 16-B aligned by contract
+    const int vh = h_bf16 ? 2
+                          : ((K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) &&
+                             (h_dev || aligned(h, 16)) && aligned(agg, 16));  // h_dev: 16-B aligned by contract
     hipStream_t st = as_stream(stream);
     float *wsf = static_cast<float *>(ws);
     // slices x K-chunks x Fo-chunks ~ one workgroup per CU; the kernel uses

@@ -121,6 +121,7 @@ struct RtArgs {
     // (with xrow) col already mapped through xrow: the gather's sources are
     // table rows, no dependent index load per neighbour
     const int32_t *col_x;
+    int x_bf16;  // x (and the gathered rows) are bf16: 2-B elements, ldx in elements
     // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
     // when kpad), then T4 exact-fp32 steps of 4 columns
     int C, T4, kpad;
@@ -180,9 +181,19 @@ __device__ __forceinline__ i32x4 tile_rsrc(const float *base, int64_t ld, int co
 // 32-chunks past the root term's C read nothing (offset past the range).
 // rowoff: byte offset of the lane's (physical) row in x, kOOB for rows past
 // the block (those read 0).
-template <bool X3>
+// XB (X3 only): x is bf16 -- a 32-chunk's 8 values per lane are ONE 16-B
+// load, already the bf16 B operand (x = x1 exactly, x2 = x3 = 0); it lands
+// in xf[2 c] (xf[2 c + 1] unused).
+template <bool X3, bool XB = false>
 __device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], i32x4 xr, uint32_t rowoff, int k0, int q) {
-    if (X3) {
+    if (XB) {
+        const uint32_t voff = rowoff + static_cast<uint32_t>((k0 + 8 * q) * 2);
+#pragma unroll
+        for (int c = 0; c < RT_KC / 2; ++c) {
+            xf[2 * c] = buf_load4(xr, static_cast<int>(voff + 64 * c), 0, 0);
+            xf[2 * c + 1] = v4f{0.f, 0.f, 0.f, 0.f};
+        }
+    } else if (X3) {
         // all four chunks unconditionally: a chunk past the root term reads
         // bytes of the same / next row (or 0 past the range) and is never
         // used -- a uniform per-chunk select here becomes loop-invariant SGPR
@@ -200,8 +211,18 @@ __device__ __forceinline__ void load_x(v4f (&xf)[RT_KC], i32x4 xr, uint32_t rowo
 
 // X3 fp32 tail: lane (rl, q) holds x[r][32 C + 4 s + q] (the B operand of
 // 16x16x4 f32 step s)
+template <bool XB = false>
 __device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &a, i32x4 xr,
                                         uint32_t rowoff, int q) {
+    if (XB) {  // bf16 element e: the dword holding it (rows start on 8 B), then its half
+#pragma unroll
+        for (int s = 0; s < X3_TAIL_MAX; ++s) {
+            const int e = 32 * a.C + 4 * s + q;
+            const int w = buf_load1i(xr, static_cast<int>(rowoff + static_cast<uint32_t>((e & ~1) * 2)), 0, 0);
+            xt[s] = __int_as_float((e & 1) ? (w & static_cast<int>(0xffff0000u)) : (w << 16));
+        }
+        return;
+    }
     const uint32_t voff = rowoff + static_cast<uint32_t>((32 * a.C + q) * 4);
 #pragma unroll
     for (int s = 0; s < X3_TAIL_MAX; ++s)
@@ -211,13 +232,43 @@ __device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &
 // root term of one 128-column group in the X3 layout: per 32-chunk, split x
 // into three bf16 parts and issue the six products per output tile (W parts
 // from the LDS image [3][C][NTW][64] bf16x8, piece stride pst)
-template <int NTW>
+template <int NTW, bool XB = false>
 __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[RT_KC],
                                               const bf16x8 *__restrict__ sw3, int pst, int cc0,
                                               int ncc, int mask_last, int kq8, int lane) {
 #pragma unroll
     for (int c = 0; c < RT_KC / 2; ++c) {
-        if (c < ncc) {
+        if (XB && c < ncc) {
+            // bf16 x: exact in one part, so only the three products with x1
+            i32x4 xw = __builtin_bit_cast(i32x4, xf[2 * c]);
+            if (mask_last && c == ncc - 1) {  // padded last chunk: elements past K
+                int kq = kq8;
+                asm volatile("" : "+v"(kq));
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    xw[j] &= (lt_mask(2 * j, kq) & 0xffff) | (lt_mask(2 * j + 1, kq) & static_cast<int>(0xffff0000u));
+            }
+            const bf16x8 x1 = __builtin_bit_cast(bf16x8, xw);
+            const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
+            bf16x8 wb[2][3];
+            wb[0][0] = w[0];
+            wb[0][1] = w[pst];
+            wb[0][2] = w[2 * pst];
+#pragma unroll
+            for (int m = 0; m < NTW; ++m) {
+                if (m + 1 < NTW) {
+                    const int o = (m + 1) * 64;
+                    wb[(m + 1) & 1][0] = w[o];
+                    wb[(m + 1) & 1][1] = w[pst + o];
+                    wb[(m + 1) & 1][2] = w[2 * pst + o];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                v4f t = acc[m];
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1][2], x1, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1][1], x1, t, 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1][0], x1, t, 0, 0, 0);
+            }
+        } else if (!XB && c < ncc) {
             v4f lo = xf[2 * c], hi = xf[2 * c + 1];
             if (mask_last && c == ncc - 1) {  // padded last chunk: columns past K read the next row
                 int kq = kq8;
@@ -379,15 +430,16 @@ __device__ __forceinline__ v4f red_mask(v4f v, int m) {
 // buffer range (read 0 = the sum identity; max masks them to -inf).
 // Columns past K accumulate garbage from the next row and are zeroed at the
 // end.
-template <int RED>
+template <int RED, bool XB = false>
 __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, i32x4 xr, int beg,
                                              int deg, int maxdeg, int k0, int nkg, int rl, int q,
                                              const int64_t *xrow) {
+    constexpr uint32_t EB = XB ? 2u : 4u;  // bytes per x element
     const float ident = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) ag[g] = v4f{ident, ident, ident, ident};
-    const uint32_t kofs = static_cast<uint32_t>((k0 + 4 * q) * 4);
-    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;  // (whole-buffer offsets < 3.75 GiB)
+    const uint32_t kofs = static_cast<uint32_t>(k0 + 4 * q) * EB;
+    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * EB;  // (whole-buffer offsets < 3.75 GiB)
 #pragma unroll 1
     for (int e0 = 0; e0 < maxdeg; e0 += 16) {
         int cb[4];
@@ -419,8 +471,13 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
                 v4f v0[RT_KC], v1[RT_KC];
 #pragma unroll
                 for (int g = 0; g < RT_KC; ++g) {
-                    v0[g] = buf_load4(xr, o0 + 64 * g, 0, 0);
-                    v1[g] = buf_load4(xr, o1 + 64 * g, 0, 0);
+                    if (XB) {  // 4 bf16 per lane and k-group: one 8-B load, widened exactly
+                        v0[g] = bf16x4_to_f32(buf_load2i(xr, o0 + 32 * g, 0, 0));
+                        v1[g] = bf16x4_to_f32(buf_load2i(xr, o1 + 32 * g, 0, 0));
+                    } else {
+                        v0[g] = buf_load4(xr, o0 + 64 * g, 0, 0);
+                        v1[g] = buf_load4(xr, o1 + 64 * g, 0, 0);
+                    }
                 }
 #pragma unroll
                 for (int g = 0; g < RT_KC; ++g) {
@@ -519,8 +576,10 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
 // 0.355 ms/step on products, the extra address VALU spills the L0 kernel.)
 // X3: root term on the 3 x bf16 split (LDS image of W_r split in the
 // prologue from the raw rows); otherwise exact fp32 MFMA.
-template <int NTW, int RED, int WLM, bool X3, bool VEC>
+template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB>
 __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
+    static_assert(!XB || X3, "bf16 rows feed the split-bf16 root term");
+    constexpr uint32_t EB = XB ? 2u : 4u;  // bytes per x element
     constexpr bool WL_LDS = WLM == 1;
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
     __shared__ int s_next_tile;       // the workgroup's tile-claim counter
@@ -686,13 +745,13 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
     // x: the address given at launch, or (graph replay of a changing batch)
     // the one the slot load stored, ranged by the device row count
-    const float *xbase = a.x_dev ? *a.x_dev : a.x;
+    const void *xbase = a.x_dev ? *a.x_dev : a.x;
     const int64_t *xrow = a.xrow_dev ? *a.xrow_dev : a.xrow;
     // one resource over all of x (root rows and gathered neighbour rows;
     // x_rows: the feature table's rows under the fused x[n_id] gather)
     const int64_t xrows = xrow ? a.x_rows : static_cast<int64_t>(n_rows);
-    const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(((xrows - 1) * a.ldx + a.K) * 4 * (xrows > 0)));
-    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
+    const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(((xrows - 1) * a.ldx + a.K) * EB * (xrows > 0)));
+    const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * EB;
     // byte offset of logical row rr in x (kOOB past the block's rows)
     auto row_off = [&](int rr) -> uint32_t {
         if (rr >= n_rows) return static_cast<uint32_t>(kOOB);
@@ -720,8 +779,8 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         const int tl = tn < n_tiles ? tn : 0;
         const int rn = tl * RT_ROWS + rl;
         roff_n = roff_tn;
-        load_x<X3>(xn, xr, roff_n, 0, q);
-        if (X3) load_xt(xtn, a, xr, roff_n, q);
+        load_x<X3, XB>(xn, xr, roff_n, 0, q);
+        if (X3) load_xt<XB>(xtn, a, xr, roff_n, q);
         if (have_l) {
             const int mr = lt_mask(rn, n_rows);
             const int rr = rn & mr;
@@ -783,13 +842,13 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             }
             const int nkg = min(RT_KC, a.KG - c * RT_KC);
             if (c + 1 < nchunk) {
-                load_x<X3>(xn, xr, roff, (c + 1) * RT_KC * 16, q);
+                load_x<X3, XB>(xn, xr, roff, (c + 1) * RT_KC * 16, q);
             } else if (maxdeg == 0) {
                 prefetch(tnext, roff_nn);  // next tile: a whole tile of MFMAs to land
             }
             if (X3) {
                 const int ncc = min(4, a.C - 4 * c);
-                mfma_group_x3<NTW>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
+                mfma_group_x3<NTW, XB>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
             } else {
                 mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
             }
@@ -808,7 +867,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                     load_x<false>(av, air, static_cast<uint32_t>(rl * a.ld_agg * 4), k0, q);
                     mask_x(ag, av, a, k0, q);
                 } else {
-                    gather_chunk<RED>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q, xrow);
+                    gather_chunk<RED, XB>(ag, a, xr, beg, deg, maxdeg, k0, nkg, rl, q, xrow);
                 }
                 // edge tiles prefetch the next tile only now: its x fragments
                 // are not live across the gather (register budget)
@@ -861,9 +920,9 @@ int num_cus() {
     return g_num_cus[dev];
 }
 
-template <int NTW, int RED, int WLM, bool X3, bool VEC>
+template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB>
 int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
-    auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC>;
+    auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC, XB>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         // 160 KiB per CU minus the kernel's static LDS (the tile counter)
@@ -884,15 +943,17 @@ int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, 
     const bool vec = a.vec_out && (a.Fo == a.NT * 16);
     auto by_red = [&](auto red_c) {
         constexpr int RED = decltype(red_c)::value;
-        auto go = [&](auto x3_c, auto vec_c) {
+        auto go = [&](auto x3_c, auto vec_c, auto xb_c) {
             constexpr bool X3 = decltype(x3_c)::value, VEC = decltype(vec_c)::value;
-            return wl_lds ? launch_rt<NTW, RED, 1, X3, VEC>(a, n_tiles, lds, st)
-                          : launch_rt<NTW, RED, 0, X3, VEC>(a, n_tiles, lds, st);
+            constexpr bool XB = decltype(xb_c)::value;
+            return wl_lds ? launch_rt<NTW, RED, 1, X3, VEC, XB>(a, n_tiles, lds, st)
+                          : launch_rt<NTW, RED, 0, X3, VEC, XB>(a, n_tiles, lds, st);
         };
         using T = std::true_type;
         using F = std::false_type;
-        if (x3) return vec ? go(T{}, T{}) : go(T{}, F{});
-        return vec ? go(F{}, T{}) : go(F{}, F{});
+        if (a.x_bf16) return vec ? go(T{}, T{}, T{}) : go(T{}, F{}, T{});  // (x3 checked by the caller)
+        if (x3) return vec ? go(T{}, T{}, F{}) : go(T{}, F{}, F{});
+        return vec ? go(F{}, T{}, F{}) : go(F{}, F{}, F{});
     };
     if (reduce == NGNN_REDUCE_MEAN) return by_red(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
     if (reduce == NGNN_REDUCE_SUM) return by_red(std::integral_constant<int, NGNN_REDUCE_SUM>{});
@@ -1019,7 +1080,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
                      const float *const *x_dev, bool exact, float *z, int64_t ldz,
                      const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
-                     const int32_t *col_x) {
+                     const int32_t *col_x, bool x_bf16) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -1031,13 +1092,16 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // per 16-row tile (no size limit)
     const bool indexed = xrow != nullptr || xrow_dev != nullptr;
     // (a graph slot may load materialized batches too: the word then holds 0)
-    if ((indexed ? std::max(x_rows, n_rows) : n_rows) * ldx * 4 > kRangeMax || (indexed && x_rows <= 0))
+    const int64_t ebytes = x_bf16 ? 2 : 4;
+    if ((indexed ? std::max(x_rows, n_rows) : n_rows) * ldx * ebytes > kRangeMax || (indexed && x_rows <= 0))
         return 0;
     const int KG = static_cast<int>(ceil_div(K, 16));
     // X3 root term: C bf16 chunks of 32 + T4 fp32 steps of 4 (tails over 12
     // columns become one zero-padded bf16 chunk)
     // (no root term: the X3 layout with an empty image -- no MFMAs, no LDS)
     const bool x3 = (!exact && ldw > 0) || no_root;
+    // bf16 rows: X3 layout only, 8-B aligned rows (ldx a multiple of 4 elements)
+    if (x_bf16 && (!x3 || z != nullptr || ldx % 4 != 0)) return 0;
     // narrow mode: one launch computes [x W_r^T | x W_l^T] (2 NT1 tiles) --
     // X3 only, no neighbour term, no saved aggregate, no column slicing
     const bool narrow = z != nullptr;
@@ -1137,6 +1201,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.xrow_dev = xrow_dev;
         a.x_rows = x_rows;
         a.col_x = (xrow || xrow_dev) ? col_x : nullptr;
+        a.x_bf16 = x_bf16;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
@@ -1176,7 +1241,10 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     (void)n_edge_rows_dev;
     const bool exact = (reduce & NGNN_MATH_EXACT_F32) != 0;
     const bool want_narrow = (reduce & NGNN_FWD_NARROW) != 0;
-    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW);
+    const bool x_bf16 = (reduce & NGNN_X_BF16) != 0;
+    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW | NGNN_X_BF16);
+    // bf16 rows: the split-bf16 root term and the fused path only
+    if (x_bf16 && (exact || want_narrow)) return NGNN_E_SHAPE;
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
     // wr == NULL: no root term (GCNConv = SAGEConv with W_r = 0: the layer
     // aggregates first, out = act(b + agg(x) W_l^T))
@@ -1218,7 +1286,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
-                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x))
+                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

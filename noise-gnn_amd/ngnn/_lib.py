@@ -22,6 +22,7 @@ E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
 REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
 MATH_EXACT_F32 = 0x100  # OR-ed into ngnn_sage_fwd_raw's reduce (include/ngnn.h)
 FWD_NARROW = 0x200      # same: output layer aggregated in the F_out-wide space
+X_BF16 = 0x400          # same: x rows are bf16 (read as bf16, widened exactly)
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one
@@ -70,7 +71,7 @@ SIGNATURES = {
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
-    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64, _p,
+    "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _int, _i64, _p,
                                _i64, _p, _i64,
                                _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
     "ngnn_sage_dgrad_workspace_bytes": (_sz, [_i64, _i64, _int]),

@@ -166,11 +166,14 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     wide) instead of x (K wide) -- the output layer's form (no agg_out then)."""
     N, K = x.shape
     Fo = wl.shape[0]
+    if x.dtype == torch.bfloat16 and not bf16_rows_ok(x, narrow):
+        x = x.float()
+    xb = x.dtype == torch.bfloat16  # bf16 rows read as such (NGNN_X_BF16)
     out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
     root = wr is not None  # (None: GCNConv's aggregate-first form, no root term)
     # algorithmic bytes: x + gathered rows + col + rowptr + out;  flops: root GEMM on
     # every row + neighbour GEMM on rows with in-edges (0 if not known: conservative)
-    nbytes = (N * K + block.E * (K + 1) + N * Fo) * 4 + (N + 1) * 4
+    nbytes = (N * K + block.E * K) * (2 if xb else 4) + (block.E + N * Fo) * 4 + (N + 1) * 4
     n_e = int(block.n_active or 0)
     flops = 2 * N * K * Fo * root + 2 * n_e * K * Fo
     # ideal matrix-core time of the instruction mix (DESIGN.md section 5): the
@@ -191,7 +194,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     if wl_.stride(1) != 1 or (root and (wr_.stride(1) != 1 or wl_.stride(0) != wr_.stride(0))):
         wl_, wr_ = wl_.contiguous(), (wr_.contiguous() if root else None)
     xk = x
-    if K % 4 and pad_k_ok(K, Fo) and x_dev is None and not narrow and (
+    if K % 4 and not xb and pad_k_ok(K, Fo) and x_dev is None and not narrow and (
             agg_out is None or agg_out.stride(0) % 4 == 0):
         # the row-tile kernel reads 16-B column quads: one zero column (or
         # three) appended to x and to the weights -- 0 * 0 terms, the same
@@ -214,12 +217,17 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
             _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
             _lib.ptr(block.col_x) if xrow_dev is not None else None,
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
-            | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0),
+            | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0)
+            | (_lib.X_BF16 if xb else 0),
             _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out),
             agg_out.stride(0) if agg_out is not None else xk.size(1),
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
+        if rc == _lib.E_SHAPE and xb and x_dev is None:
+            # bf16 rows outside the bf16 envelope: the fp32 path on widened rows
+            return sage_layer_fwd(x.float(), block, reduce, wl, bl, wr, relu, p_drop, seed,
+                                  agg_out, seed_dev, None, span, narrow)
         if rc == _lib.E_SHAPE:
             if x_dev is not None:
                 raise _lib.NGNNError("zero-copy input outside the row-tile kernel's envelope")
@@ -230,6 +238,15 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         else:
             _lib.check(rc, "ngnn_sage_fwd_raw")
     return out
+
+
+def bf16_rows_ok(x: torch.Tensor, narrow: bool = False) -> bool:
+    """Can the row-tile kernel read these bf16 rows directly (NGNN_X_BF16)?
+    Split-bf16 root term (not the exact-fp32 mode), not a narrow layer, rows
+    of a multiple of 4 elements on 8-B boundaries, a 16-B aligned base."""
+    return (x.dtype == torch.bfloat16 and not _exact_f32 and not narrow and x.dim() == 2
+            and x.stride(1) == 1 and x.size(1) % 4 == 0 and x.stride(0) % 4 == 0
+            and x.data_ptr() % 16 == 0)
 
 
 def pad_k_ok(K: int, Fo: int = 0) -> bool:
@@ -433,7 +450,7 @@ class _SAGEStack(torch.autograd.Function):
                     ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(h_in),
                     _lib.ptr(block.x_dev) if i == 0 else None,
                     None, _lib.ptr(block.xrow_dev) if i == 0 else None,
-                    block.x_rows if i == 0 else 0, h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
+                    block.x_rows if i == 0 else 0, int(h_in.dtype == torch.bfloat16), h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
                     bptr(i + 1), Fo, K, _lib.ptr(dwl), _lib.ptr(dbl), _lib.ptr(dwr),
                     _lib.ptr(ws), ws.numel(), stream)
             _lib.check(rc, "ngnn_sage_wgrad")
@@ -580,10 +597,11 @@ def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor
     for conv in model.convs:
         params += [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
     aggr = "sum" if model.convs[0].aggr == "add" else model.convs[0].aggr
-    return _run_stack(model, x, block, seed, seed_dev, params, aggr)
+    return _run_stack(model, x, block, seed, seed_dev, params, aggr, keep_bf16_x=True)
 
 
-def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str) -> torch.Tensor:
+def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
+               keep_bf16_x: bool = False) -> torch.Tensor:
     out_dtype = x.dtype
     # weight gradients straight into registered bucket views (ngnn.distributed.GradAllReduce)
     # when autograd will adopt them: fp32 parameters whose .grad is unset
@@ -592,7 +610,12 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str) -
                       and q.requires_grad) else None
                   for q in params)
     if out_dtype != torch.float32 or any(q is not None and q.dtype != torch.float32 for q in params):
-        x = x.float()
+        # bf16 features stay bf16 for a SAGE stack's layer 0 (the kernels read
+        # bf16 rows, NGNN_X_BF16: half the bytes, no widened copy) unless an
+        # input gradient is wanted; everything else is widened
+        if not (keep_bf16_x and x.dtype == torch.bfloat16 and not x.requires_grad
+                and bf16_rows_ok(x)):
+            x = x.float()
         params = [None if q is None else q.float() for q in params]
         gouts = (None,) * len(params)
     p = model.dropout if model.training else 0.0

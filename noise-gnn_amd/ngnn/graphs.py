@@ -115,8 +115,8 @@ class GraphedTrainStep:
         bs = self.B if batch_size is None else int(batch_size)
         if not 0 < bs <= min(self.B, N):
             raise ValueError(f"batch_size {bs} outside (0, min(B={self.B}, N={N})]")
-        if x.dtype != torch.float32:  # bf16 batches: the captured kernels read fp32 rows
-            x = x.float()
+        if x.dtype != self.x.dtype:  # the slot's dtype (bf16 slots: bf16-reading kernels)
+            x = x.to(self.x.dtype)
         if x.stride(1) != 1 or x.stride(0) != self.x.stride(0) or x.data_ptr() % 16:
             x = x.clone(memory_format=torch.contiguous_format)
         # a step captured for indexed rows: the word gets n_id's address or 0
@@ -127,9 +127,12 @@ class GraphedTrainStep:
         if bs < self.B:  # rows [bs, B) carry no loss (F.cross_entropy's ignore_index)
             y = torch.cat([y, y.new_full((self.B - bs,), -100)])
         # one launch: x rows, edges + padding self-loops, labels, device row count
+        # (bf16 rows move as float32 pairs: the slot kernel copies 32-bit words)
+        xw = x.view(torch.float32) if x.dtype == torch.bfloat16 else x
+        sx = self.x.view(torch.float32) if self.x.dtype == torch.bfloat16 else self.x
         _lib.check(_lib.load().ngnn_slot_load(
-            _lib.ptr(x), x.stride(0), N, x.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
-            _lib.ptr(y), y.numel(), _lib.ptr(self.x), self.x.stride(0), self.n_cap,
+            _lib.ptr(xw), xw.stride(0), N, xw.size(1), _lib.ptr(edge_index), edge_index.stride(0), E,
+            _lib.ptr(y), y.numel(), _lib.ptr(sx), sx.stride(0), self.n_cap,
             # replays read only the slot's CSR (the int64 edge copy serves eager
             # use and the deterministic mode's transposed CSR)
             None if (zero_copy and not torch.are_deterministic_algorithms_enabled())
@@ -168,6 +171,13 @@ class GraphedTrainStep:
             snap = ([p.detach().clone() for p in self.model.parameters()],
                     {k: {n: (t.clone() if torch.is_tensor(t) else t) for n, t in v.items()}
                      for k, v in self.opt.state.items()})
+        # bf16 features for a SAGE model: a bf16 slot, read as bf16 by layer 0
+        xd = x.table.dtype if isinstance(x, IndexedRows) else x.dtype
+        c0 = getattr(getattr(self.model, "convs", [None])[0], "lin_r", None)
+        if (xd == torch.bfloat16 and self.x.dtype != torch.bfloat16 and c0 is not None
+                and self.x.size(1) % 4 == 0):
+            self.x = torch.zeros(self.n_cap, self.x.size(1), dtype=torch.bfloat16,
+                                 device=self.x.device)
         self.load(x, edge_index, y)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -470,3 +470,58 @@ def test_gcn_graph_step_matches_eager(hidden):
         assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
+
+
+@pytest.mark.parametrize("K,Fo", [(100, 256), (128, 40), (256, 256), (36, 7), (300, 512),
+                                  (24, 47)])
+@pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
+def test_bf16_rows_equal_widened_rows(K, Fo, reduce):
+    """NGNN_X_BF16: bf16 rows read as bf16 (root term on the single bf16
+    part, gather widened exactly) give BITWISE the layer of the same rows
+    widened to fp32 (the split of an exact bf16 value is (x, 0, 0): the three
+    dropped products are exact zeros), outputs and saved aggregate; and both
+    match the fp32 oracle on the widened rows."""
+    N, E = 900, 6000
+    g = torch.Generator().manual_seed(K + 7 * Fo)
+    ei = rand_block(K * Fo, N, E)
+    ei = ei[:, ei[1] < N - 150]
+    xb = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    conv = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
+    blk = Block(ei.to(DEV), N)
+    args = (blk, reduce, conv.lin_l.weight.to(DEV), conv.lin_l.bias.to(DEV),
+            conv.lin_r.weight.to(DEV))
+    outs = []
+    for x in (xb.to(DEV), xb.float().to(DEV)):
+        agg = torch.full((N, K), 7.0, device=DEV)
+        o = sage_layer_fwd(x, *args, relu=True, p_drop=0.25, seed=99, agg_out=agg)
+        outs.append((o.cpu(), agg.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    with torch.no_grad():
+        pre = conv(xb.float(), ei).relu()
+    keep = dropout_keep(99, N, Fo, 0.25)
+    torch.testing.assert_close(outs[0][0], pre * keep * dropout_scale(0.25), **OUT)
+
+
+@pytest.mark.parametrize("layers", [2, 3])
+def test_bf16_features_stack_matches_widened(layers):
+    """A SAGE stack on bf16 features (no input gradient) keeps them bf16 for
+    layer 0 (forward and weight gradient read bf16 rows): logits and every
+    parameter gradient equal the run on the widened features up to the
+    input-gradient scatter's atomic ordering."""
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.005)
+    b = sample_block(graph, graph.train_idx[:256], [8, 5, 3][:layers], seed=2)
+    torch.manual_seed(5)
+    m = ngnn.SAGE(100, 64, 47, layers, dropout=0.5).to(DEV).train()
+    res = []
+    for x in (b.x.to(torch.bfloat16), b.x.to(torch.bfloat16).float()):
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(42)
+        out = m(x, b.edge_index).float()
+        F.cross_entropy(out[:256], b.y[:256]).backward()
+        res.append((out.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    # (bf16 input: logits returned in bf16)
+    torch.testing.assert_close(res[0][0], res[1][0].to(torch.bfloat16).float(), rtol=0, atol=0)
+    for k in res[0][1]:
+        torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=1e-5, atol=1e-6, msg=k)

@@ -197,3 +197,26 @@ def test_graph_fused_row_gather_matches_eager(arch):
         assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_graph_bf16_features_slot_matches_eager():
+    """bf16 features: the slot is bf16 and the captured layer 0 reads the
+    batch's bf16 rows in place (NGNN_X_BF16 + zero-copy); same losses and
+    parameters as eager training on the same bf16 batches."""
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    m_e, batches = _setup(0.0)
+    m_g, _ = _setup(0.0)
+    m_g.load_state_dict(m_e.state_dict())
+    bb = [type(b)(b.x.to(torch.bfloat16), b.y, b.edge_index, b.n_id, b.batch_size) for b in batches]
+    le = _eager_train(m_e, bb)
+    opt = torch.optim.Adam(m_g.parameters(), lr=1e-2, fused=True, capturable=True)
+    n_cap, e_cap = slot_size(256, [10, 5])
+    step = GraphedTrainStep(m_g, opt, 256, n_cap, e_cap, bb[0].x.size(1), DEV)
+    step.capture(bb[0].x, bb[0].edge_index, bb[0].y)
+    assert step.x.dtype == torch.bfloat16 and step.zero_copy
+    lg = [float(step(b.x, b.edge_index, b.y)) for b in bb]
+    torch.cuda.synchronize()
+    for a, c in zip(le, lg):
+        assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
+    for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
