@@ -518,10 +518,11 @@ def test_bf16_features_stack_matches_widened(layers):
     for x in (b.x.to(torch.bfloat16), b.x.to(torch.bfloat16).float()):
         m.zero_grad(set_to_none=True)
         torch.manual_seed(42)
-        out = m(x, b.edge_index).float()
+        # both runs end in the same bf16 cast (the bf16-input stack returns
+        # bf16 logits), so the loss backward feeds both the same dlogits
+        out = m(x, b.edge_index).to(torch.bfloat16).float()
         F.cross_entropy(out[:256], b.y[:256]).backward()
         res.append((out.detach(), {k: p.grad.clone() for k, p in m.named_parameters()}))
-    # (bf16 input: logits returned in bf16)
-    torch.testing.assert_close(res[0][0], res[1][0].to(torch.bfloat16).float(), rtol=0, atol=0)
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
     for k in res[0][1]:
         torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=1e-5, atol=1e-6, msg=k)
