@@ -621,22 +621,7 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
     out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, *params)
-    return out if out_dtype == torch.float32 else _CastKeepRows.apply(out, out_dtype)
-
-
-class _CastKeepRows(torch.autograd.Function):
-    """out.to(dtype) whose backward keeps the loss's nonzero-row hint on the
-    widened gradient (a plain cast's backward returns a fresh tensor without
-    it, and the stack's backward would then bound nothing: every row)."""
-
-    @staticmethod
-    def forward(ctx, x, dtype):
-        return x.to(dtype)
-
-    @staticmethod
-    def backward(ctx, g):
-        g32 = g.float()
-        rows = getattr(g, "_ngnn_nonzero_rows", None)
-        if rows is not None:
-            g32._ngnn_nonzero_rows = rows
-        return g32, None
+    if out_dtype == torch.float32:
+        return out
+    from .losses import cast_keep_rows
+    return cast_keep_rows(out, out_dtype)

@@ -75,13 +75,36 @@ class _SeedXent(torch.autograd.Function):
         return dx, None, None, None
 
 
+class _CastKeepRows(torch.autograd.Function):
+    """x.to(dtype) whose backward keeps the nonzero-row hint on the gradient
+    (a plain cast's backward returns a fresh tensor without it, and the SAGE
+    stack's backward would then bound nothing: every row)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return x.to(dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        gi = g.to(ctx.src)
+        rows = getattr(g, "_ngnn_nonzero_rows", None)
+        if rows is not None:
+            gi._ngnn_nonzero_rows = rows
+        return gi, None
+
+
+def cast_keep_rows(x: torch.Tensor, dtype) -> torch.Tensor:
+    return x if x.dtype == dtype else _CastKeepRows.apply(x, dtype)
+
+
 def seed_cross_entropy(logits: torch.Tensor, y: torch.Tensor, batch_size: int,
                        ignore_index: int = -100) -> torch.Tensor:
     """Mean cross entropy of ``logits[:batch_size]`` against ``y[:batch_size]``."""
     if not logits.is_cuda:
         raise RuntimeError("ngnn.losses.seed_cross_entropy: GPU only (no CPU fallback)")
     if logits.dtype == torch.bfloat16:  # bf16 models: the loss is taken in fp32
-        logits = logits.float()
+        logits = cast_keep_rows(logits, torch.float32)
     if logits.dim() != 2 or logits.dtype != torch.float32:
         raise ValueError("logits must be a 2-D float32 (or bf16) tensor")
     if batch_size <= 0 or batch_size > logits.size(0) or y.numel() < batch_size:
