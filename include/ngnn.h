@@ -432,6 +432,10 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * = all NGNN_F32): per tensor NGNN_F32 or NGNN_BF16 (params and grads in that
  * dtype; exp_avgs / exp_avg_sqs always fp32).  Replaces the reference's
  * torch.optim.Adam(...).step() (model.py:66-69). */
+/* dst[i] = bf16(src[i]) (round to nearest even, NaN kept) for i < n: a bf16
+ * model's fp32 logits handed back in bf16 (Tensor.to(torch.bfloat16), the
+ * `SAGE.forward` return dtype of a bf16 model).  src 16-B, dst 8-B aligned. */
+int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream);
 int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
                    const int32_t *dtypes, float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,

@@ -120,3 +120,41 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
     hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, st, step);
     return launch_status();
 }
+
+// ---- fp32 -> bf16 rows (a bf16 model's logits): round to nearest even, NaN
+// kept quiet (torch's rule); 4 values per thread, grid-stride.  Replaces
+// Tensor.to(torch.bfloat16) on the [N, C] logits.
+namespace ngnn {
+namespace {
+__global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src,
+                                                    uint16_t *__restrict__ dst, int64_t n) {
+    auto rne = [](float f) -> uint16_t {
+        const uint32_t u = __float_as_uint(f);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+        return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    };
+    const int64_t n4 = n >> 2;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n4; i += stride) {
+        const float4 v = reinterpret_cast<const float4 *>(src)[i];
+        const uint2 o{static_cast<uint32_t>(rne(v.x)) | (static_cast<uint32_t>(rne(v.y)) << 16),
+                      static_cast<uint32_t>(rne(v.z)) | (static_cast<uint32_t>(rne(v.w)) << 16)};
+        reinterpret_cast<uint2 *>(dst)[i] = o;
+    }
+    for (int64_t i = 4 * n4 + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += stride)
+        dst[i] = rne(src[i]);
+}
+}  // namespace
+}  // namespace ngnn
+
+extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream) {
+    using namespace ngnn;
+    NGNN_RETURN_IF(n < 0 || (n > 0 && (!src || !dst)), NGNN_E_ARG);
+    NGNN_RETURN_IF(!aligned(src, 16) || !aligned(dst, 8), NGNN_E_SHAPE);
+    if (n == 0) return NGNN_OK;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 4), 256), 4096));
+    hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, as_stream(stream), src,
+                       static_cast<uint16_t *>(dst), n);
+    return launch_status();
+}

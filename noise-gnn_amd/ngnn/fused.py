@@ -623,5 +623,41 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
     out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, *params)
     if out_dtype == torch.float32:
         return out
+    if out_dtype == torch.bfloat16 and out.is_contiguous():
+        return _StackOutBF16.apply(out)
     from .losses import cast_keep_rows
     return cast_keep_rows(out, out_dtype)
+
+
+_out_grads: dict = {}
+
+
+class _StackOutBF16(torch.autograd.Function):
+    """The stack's fp32 logits handed back in bf16 (a bf16 model's output
+    dtype) by one ngnn_cast_f32_bf16 launch.  Backward: the only consumer of
+    its gradient is _SAGEStack.backward, which reads rows < R of dout when the
+    loss says R (ngnn.losses' row hint) -- so only those rows are widened,
+    into a cached buffer, and the hint travels on."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        _lib.check(_lib.load().ngnn_cast_f32_bf16(_lib.ptr(x), _lib.ptr(y), x.numel(),
+                                                  _lib.stream_handle(x.device)),
+                   "ngnn_cast_f32_bf16")
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        rows = getattr(g, "_ngnn_nonzero_rows", None)
+        if rows is None:
+            return g.float()
+        key = (g.device, tuple(g.shape))
+        buf = _out_grads.get(key)
+        if buf is None:
+            buf = torch.empty(g.shape, dtype=torch.float32, device=g.device)
+            _out_grads[key] = buf
+        R = min(int(rows), g.size(0))
+        buf[:R].copy_(g[:R])
+        buf._ngnn_nonzero_rows = R  # rows >= R are stale: the stack never reads them
+        return buf

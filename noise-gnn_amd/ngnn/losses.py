@@ -75,6 +75,38 @@ class _SeedXent(torch.autograd.Function):
         return dx, None, None, None
 
 
+_bf16_rows: dict = {}
+
+
+class _SeedXentBF16(torch.autograd.Function):
+    """seed_cross_entropy of bf16 logits: only rows < B are widened (B x C, not
+    the N x C logits), the fp32 kernels run on them, and the gradient comes
+    back as bf16 [N, C] with rows >= B zero (a cached buffer, like the fp32
+    path's) carrying the row hint."""
+
+    @staticmethod
+    def forward(ctx, logits, y, batch_size: int, ignore_index: int):
+        B = int(batch_size)
+        ctx.n_full = logits.size(0)
+        # the fp32 node's forward on the widened seed rows (it fills ctx for
+        # its backward: saved rows, ws, B, n = B)
+        return _SeedXent.forward(ctx, logits[:B].float(), y, B, ignore_index)
+
+    @staticmethod
+    def backward(ctx, g):
+        dx, _, _, _ = _SeedXent.backward(ctx, g)  # fp32 [B, C] (ctx.n == B there)
+        n, B, C = ctx.n_full, ctx.B, dx.size(1)
+        key = (dx.device, C, B, "bf16")
+        buf = _bf16_rows.get(key)
+        if buf is None or buf.size(0) < n:
+            buf = torch.zeros(max(n, 1), C, dtype=torch.bfloat16, device=dx.device)
+            _bf16_rows[key] = buf
+        out = buf[:n]
+        out[:B].copy_(dx[:B])
+        out._ngnn_nonzero_rows = B
+        return out, None, None, None
+
+
 class _CastKeepRows(torch.autograd.Function):
     """x.to(dtype) whose backward keeps the nonzero-row hint on the gradient
     (a plain cast's backward returns a fresh tensor without it, and the SAGE
@@ -104,6 +136,8 @@ def seed_cross_entropy(logits: torch.Tensor, y: torch.Tensor, batch_size: int,
     if not logits.is_cuda:
         raise RuntimeError("ngnn.losses.seed_cross_entropy: GPU only (no CPU fallback)")
     if logits.dtype == torch.bfloat16:  # bf16 models: the loss is taken in fp32
+        if logits.dim() == 2 and 0 < batch_size <= logits.size(0) and y.numel() >= batch_size:
+            return _SeedXentBF16.apply(logits, y, batch_size, ignore_index)
         logits = cast_keep_rows(logits, torch.float32)
     if logits.dim() != 2 or logits.dtype != torch.float32:
         raise ValueError("logits must be a 2-D float32 (or bf16) tensor")

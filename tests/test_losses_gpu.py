@@ -164,3 +164,31 @@ def test_ct_loss_backwards_are_independent():
     assert w1.grad is not None and w2.grad is None
     out[1].backward()
     assert w2.grad is not None
+
+
+def test_bf16_logits_seed_rows_only():
+    """bf16 logits: only the seed rows are widened; value equals
+    F.cross_entropy on the widened rows, the gradient is bf16 with rows >= B
+    exactly zero and carries the row hint; the bf16 stack output (one cast
+    launch) equals Tensor.to(bfloat16) bitwise."""
+    from ngnn.fused import _StackOutBF16
+    from ngnn.losses import seed_cross_entropy
+    g = torch.Generator().manual_seed(3)
+    N, C, B = 3000, 47, 512
+    xf = (torch.randn(N, C, generator=g) * 4).to(DEV)
+    xf[7, 3] = float("nan")
+    xf[8, 1] = float("inf")
+    xb = _StackOutBF16.apply(xf)
+    assert torch.equal(xb.view(torch.int16), xf.to(torch.bfloat16).view(torch.int16))
+    x = (torch.randn(N, C, generator=g) * 3).to(DEV).to(torch.bfloat16).requires_grad_(True)
+    y = torch.randint(0, C, (N,), generator=g).to(DEV)
+    got = seed_cross_entropy(x, y, B)
+    x2 = x.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(x2[:B], y[:B])
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    got.backward()
+    ref.backward()
+    assert x.grad.dtype == torch.bfloat16
+    assert torch.equal(x.grad[B:], torch.zeros_like(x.grad[B:]))
+    # (fp32 gradients equal to ~1 ulp, then each rounded to bf16: <= 1 bf16 ulp apart)
+    torch.testing.assert_close(x.grad.float(), x2.grad.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-7)
