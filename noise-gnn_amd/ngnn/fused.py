@@ -600,45 +600,6 @@ def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor
     return _run_stack(model, x, block, seed, seed_dev, params, aggr, keep_bf16_x=True)
 
 
-class _WidenParams(torch.autograd.Function):
-    """bf16 parameters widened to fp32 for the kernels in two launches (one
-    cat, one cast) instead of one per tensor, their fp32 gradients narrowed
-    back the same way: a bf16 model's per-step conversions are otherwise ~20
-    small launches."""
-
-    @staticmethod
-    def forward(ctx, *ps):
-        ctx.meta = [(p.shape, p.dtype) for p in ps]
-        flat = torch.cat([p.reshape(-1) for p in ps]).float()
-        outs, o = [], 0
-        for p in ps:
-            outs.append(flat[o:o + p.numel()].view(p.shape))
-            o += p.numel()
-        return tuple(outs)
-
-    @staticmethod
-    def backward(ctx, *gs):
-        dev = gs[0].device if gs[0] is not None else None
-        parts = [g.reshape(-1) if g is not None else
-                 torch.zeros(int(torch.Size(sh).numel()), dtype=torch.float32, device=dev)
-                 for g, (sh, _) in zip(gs, ctx.meta)]
-        flat = torch.cat(parts).to(ctx.meta[0][1])
-        outs, o = [], 0
-        for sh, _ in ctx.meta:
-            n = int(torch.Size(sh).numel())
-            outs.append(flat[o:o + n].view(sh))
-            o += n
-        return tuple(outs)
-
-
-def _widen_params(params):
-    live = [q for q in params if q is not None]
-    if not live or any(q.dtype == torch.float32 for q in live) or len({q.dtype for q in live}) != 1:
-        return [None if q is None else q.float() for q in params]
-    wide = iter(_WidenParams.apply(*live))
-    return [None if q is None else next(wide) for q in params]
-
-
 def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                keep_bf16_x: bool = False) -> torch.Tensor:
     out_dtype = x.dtype
@@ -655,7 +616,7 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
         if not (keep_bf16_x and x.dtype == torch.bfloat16 and not x.requires_grad
                 and bf16_rows_ok(x)):
             x = x.float()
-        params = _widen_params(params)
+        params = [None if q is None else q.float() for q in params]
         gouts = (None,) * len(params)
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
