@@ -353,7 +353,8 @@ def test_dgrad_lowdim_abi(Fo, K, reduce, masked):
         outs.append(dh.cpu())
     torch.testing.assert_close(outs[0][:Rn], ref[:Rn], **GRAD)
     assert torch.all(outs[0][Rn:] == 7.0)  # rows >= R' untouched
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-6, atol=1e-6)
+    # (the narrow-space scatter uses float atomics: run-to-run order noise)
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-5)
 
 
 def test_dgrad_lowdim_shape_envelope():
