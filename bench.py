@@ -179,6 +179,42 @@ def cpu_baseline(batches, args, layers):
                       f"oracle/pyg_ref.py"}
 
 
+def l0_replay_us(gstep, model, aggr: str, reps: int = 20) -> float:
+    """Average duration of the captured step's layer-0 launch under replay
+    conditions: HIP events around ONE graph replay of `reps` back-to-back
+    launches of that kernel on the slot's current batch (the last timed
+    one).  Events cannot be recorded inside the step's own graph on ROCm;
+    the eager pass instead leaves the GPU idle between host-issued launches,
+    so its per-launch time reads ~15 % long against rocprof's replay time."""
+    from ngnn import fused
+    from ngnn.block import get_block
+    blk = get_block(gstep.ei, gstep.n_cap)
+    c = model.convs[0]
+    wl, bl, wr = (q.detach().float() for q in (c.lin_l.weight, c.lin_l.bias, c.lin_r.weight))
+    x = gstep.x
+    agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])
+    p = model.dropout if model.training else 0.0
+
+    def run():
+        fused.sage_layer_fwd(x, blk, aggr, wl, bl, wr, relu=True, p_drop=p, seed=0, agg_out=agg,
+                             seed_dev=blk.seed_dev, x_dev=blk.x_dev, xrow_dev=blk.xrow_dev,
+                             x_rows=blk.x_rows)
+    run()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            run()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
 def _allreduce_name(world: int) -> str:
     """Which collective carries the gradient all-reduce (gloo only in rehearsals)."""
     import torch.distributed as dist
@@ -297,8 +333,15 @@ def main():
     summ = timer.summary()
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
     roof = None
+    replay_us = eager_us = None
     if dom:
         name, (n, ms, nbytes, flops, mfma_s) = dom
+        eager_us = 1e3 * ms / n
+        if graph and name == "sage_fwd_l0" and args.module == "sage":
+            # the same kernel timed under replay conditions (see l0_replay_us);
+            # algorithmic bytes / flops per launch from the eager records
+            replay_us = l0_replay_us(gstep, model, args.aggr)
+            ms = replay_us * 1e-3 * n
         t = ms * 1e-3
         gbs = nbytes / t / 1e9
         tfs = flops / t / 1e12
@@ -319,8 +362,12 @@ def main():
         roof.update({
             "traffic": traffic, "traffic_src": traffic_src, "launches": n,
             "avg_us": round(1e3 * ms / n, 2),
-            "timed_in": "timed region (eager)" if not graph else
-                        "eager pass over the timed batches, right after the graph replays",
+            "timed_in": "timed region (eager)" if not graph else (
+                "HIP events around a graph replay of 20 back-to-back launches of this kernel "
+                "on the last timed batch, right after the timed region (alg. bytes/flops per "
+                "launch from an eager pass over the timed batches)" if replay_us is not None else
+                "eager pass over the timed batches, right after the graph replays"),
+            "avg_us_eager_pass": None if eager_us is None else round(eager_us, 2),
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),
             "mfma_peak_note": "f32-equivalent peak of the instruction mix: root term 6 bf16 "
