@@ -410,10 +410,9 @@ int ngnn_sage_dgrad_lowdim(const float *dy, int64_t ldy, const float *y, int64_t
  * Replaces F.cross_entropy(out[:batch_size], y[:batch_size]) in the
  * reference's training loop (pipeline.py:158) and its autograd. */
 size_t ngnn_seed_xent_workspace_bytes(int64_t B);
-/* ws: ngnn_seed_xent_workspace_bytes(B), 16-B aligned (reserved: the
- * forward is one single-workgroup launch; calls sharing a ws must be
- * stream-ordered).  The backward takes the same ws and recomputes the row
- * log-sum-exps. */
+/* ws: ngnn_seed_xent_workspace_bytes(B), 16-B aligned (row losses; calls
+ * sharing a ws must be stream-ordered).  The backward takes the same ws
+ * (reserved) and recomputes the row log-sum-exps. */
 int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
                        int64_t ignore_index, float *loss, float *count, void *ws,
                        size_t ws_bytes, void *stream);

@@ -39,33 +39,42 @@ __device__ __forceinline__ float row_lse(const float *__restrict__ xr, int C, in
 }
 
 // one wave per row: ws[r] = row loss (0 if ignored), ws[B + r] = 1/0 valid
-// the whole seed-row loss in ONE workgroup and one launch: a thread per row
-// (the row's C logits loaded back to back, max, sum of exp, log), then a
-// fixed-order tree over the per-thread partial sums -> deterministic.  For a
-// products batch (B = 1024, C = 47) one pass of 1024 threads; the previous
-// wave-per-row launch + a separate sum launch cost two dispatches.
-__global__ __launch_bounds__(1024) void k_xent_fwd(const float *__restrict__ x, int64_t ld, int B,
+__global__ __launch_bounds__(256) void k_xent_rows(const float *__restrict__ x, int64_t ld, int B,
                                                    int C, const int64_t *__restrict__ y,
-                                                   int64_t ignore, float *__restrict__ loss,
-                                                   float *__restrict__ count) {
-    float s = 0.0f, n = 0.0f;
-    for (int r = threadIdx.x; r < B; r += 1024) {
-        const int64_t t = y[r];
-        if (t == ignore) continue;
+                                                   int64_t ignore, float *__restrict__ ws) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= B) return;
+    const int64_t t = y[r];
+    float l = 0.0f, v = 0.0f;
+    if (t != ignore) {
         const float *xr = x + static_cast<int64_t>(r) * ld;
-        float m = -INFINITY;
-        for (int c = 0; c < C; ++c) m = fmaxf(m, xr[c]);
-        float e = 0.0f;
-        for (int c = 0; c < C; ++c) e += expf(xr[c] - m);
-        const float lse = m + logf(e);
-        s += (t >= 0 && t < C) ? lse - xr[t] : NAN;  // out-of-range label: NaN, no OOB read
-        n += 1.0f;
+        const float lse = row_lse(xr, C, lane);
+        l = (t >= 0 && t < C) ? lse - xr[t] : NAN;  // out-of-range label: NaN, no OOB read
+        v = 1.0f;
     }
-    __shared__ float ss[1024], sn[1024];
+    if (lane == 0) {
+        ws[r] = l;
+        ws[B + r] = v;
+    }
+}
+
+// one workgroup adds the row losses in a fixed order (strided per thread,
+// then a fixed tree) -> deterministic; a separate launch, so no cross-XCD
+// fences or tickets are needed
+__global__ __launch_bounds__(256) void k_xent_sum(const float *__restrict__ ws, int B,
+                                                  float *__restrict__ loss,
+                                                  float *__restrict__ count) {
+    float s = 0.0f, n = 0.0f;
+    for (int i = threadIdx.x; i < B; i += 256) {
+        s += ws[i];
+        n += ws[B + i];
+    }
+    __shared__ float ss[256], sn[256];
     ss[threadIdx.x] = s;
     sn[threadIdx.x] = n;
     __syncthreads();
-    for (int h = 512; h > 0; h >>= 1) {
+    for (int h = 128; h > 0; h >>= 1) {
         if (threadIdx.x < h) {
             ss[threadIdx.x] += ss[threadIdx.x + h];
             sn[threadIdx.x] += sn[threadIdx.x + h];
@@ -263,8 +272,12 @@ extern "C" int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, in
     NGNN_RETURN_IF(ld < C, NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(B) || !fits_i32(C), NGNN_E_RANGE);
     NGNN_RETURN_IF(ws_bytes < ngnn_seed_xent_workspace_bytes(B) || !aligned(ws, 16), NGNN_E_WORKSPACE);
-    hipLaunchKernelGGL(k_xent_fwd, dim3(1), dim3(1024), 0, as_stream(stream), logits, ld, (int)B,
-                       (int)C, y, ignore_index, loss, count);
+    float *w = static_cast<float *>(ws);
+    hipLaunchKernelGGL(k_xent_rows, dim3(static_cast<unsigned>(ceil_div(B, 4))), dim3(256), 0,
+                       as_stream(stream), logits, ld, (int)B, (int)C, y, ignore_index, w);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_xent_sum, dim3(1), dim3(256), 0, as_stream(stream), w, (int)B, loss, count);
     return launch_status();
 }
 
