@@ -372,7 +372,8 @@ def main():
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),
             "mfma_peak_note": "f32-equivalent peak of the instruction mix: root term 6 bf16 "
                               "products per f32 product (16x the 157.3 TF f32 MFMA rate), "
-                              "neighbour term f32 MFMA",
+                              "neighbour term f32 MFMA; a layer on the 64-row fallback kernel "
+                              "(exact f32 MFMA throughout) is priced at the 157.3 TF f32 peak",
             "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
                                 "GBps": round(v[2] / (v[1] * 1e-3) / 1e9, 1),
                                 "TFps": round(v[3] / (v[1] * 1e-3) / 1e12, 2),

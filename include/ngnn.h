@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 9
+#define NGNN_ABI_VERSION 10
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -66,6 +66,16 @@ extern "C" {
  * sums in fp32.  Outputs and agg_out stay fp32.  Not with NGNN_MATH_EXACT_F32
  * or NGNN_FWD_NARROW (NGNN_E_SHAPE: convert x and call again). */
 #define NGNN_X_BF16 0x400
+/* flag OR-ed into ngnn_sage_fwd_raw's `reduce`: the weights (W_r, and W_l of
+ * NGNN_FWD_NARROW) hold bf16-exact values -- a bf16 model's parameters
+ * (sage.py:40 under model.to(torch.bfloat16)) widened to fp32.  The split-bf16
+ * root term then needs ONE weight part (its other two parts are zero): the
+ * LDS image is a third of the size (wider column slices, fewer re-reads of x)
+ * and each 32-deep chunk issues 3 MFMAs (1 with NGNN_X_BF16) instead of 6.
+ * The result is bitwise the one without the flag on such weights (the
+ * skipped products are exact zeros); weights that are not bf16-exact are
+ * rounded to bf16.  MEAN / SUM only (NGNN_E_SHAPE otherwise: call without). */
+#define NGNN_W_BF16 0x800
 
 /* dtypes */
 #define NGNN_F32 0

@@ -154,6 +154,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const float *const *x_dev = nullptr, bool exact = true,
                      float *z = nullptr, int64_t ldz = 0, const int64_t *xrow = nullptr,
                      const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
-                     const int32_t *col_x = nullptr, bool x_bf16 = false);
+                     const int32_t *col_x = nullptr, bool x_bf16 = false,
+                     bool w_bf16 = false);
 
 }  // namespace ngnn

@@ -122,6 +122,7 @@ struct RtArgs {
     // table rows, no dependent index load per neighbour
     const int32_t *col_x;
     int x_bf16;  // x (and the gathered rows) are bf16: 2-B elements, ldx in elements
+    int w1;      // NGNN_W_BF16: the root image holds one weight part
     // X3 root term: C 32-deep bf16 chunks (the last one zero-padded past K
     // when kpad), then T4 exact-fp32 steps of 4 columns
     int C, T4, kpad;
@@ -232,13 +233,56 @@ __device__ __forceinline__ void load_xt(float (&xt)[X3_TAIL_MAX], const RtArgs &
 // root term of one 128-column group in the X3 layout: per 32-chunk, split x
 // into three bf16 parts and issue the six products per output tile (W parts
 // from the LDS image [3][C][NTW][64] bf16x8, piece stride pst)
-template <int NTW, bool XB = false>
+// W1 (NGNN_W_BF16): the image holds only W's first part (bf16-exact
+// weights, parts 2 and 3 are zero): the products with w2 / w3 are exact zeros
+// and are skipped -- the remaining ones in the same order, so the sums are
+// bitwise those of the three-part image
+template <int NTW, bool XB = false, bool W1 = false>
 __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[RT_KC],
                                               const bf16x8 *__restrict__ sw3, int pst, int cc0,
                                               int ncc, int mask_last, int kq8, int lane) {
 #pragma unroll
     for (int c = 0; c < RT_KC / 2; ++c) {
-        if (XB && c < ncc) {
+        if (W1 && c < ncc) {
+            bf16x8 x1, x2, x3;
+            if (XB) {
+                i32x4 xw = __builtin_bit_cast(i32x4, xf[2 * c]);
+                if (mask_last && c == ncc - 1) {
+                    int kq = kq8;
+                    asm volatile("" : "+v"(kq));
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        xw[j] &= (lt_mask(2 * j, kq) & 0xffff) | (lt_mask(2 * j + 1, kq) & static_cast<int>(0xffff0000u));
+                }
+                x1 = __builtin_bit_cast(bf16x8, xw);
+            } else {
+                v4f lo = xf[2 * c], hi = xf[2 * c + 1];
+                if (mask_last && c == ncc - 1) {
+                    int kq = kq8;
+                    asm volatile("" : "+v"(kq));
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        lo[i] = __int_as_float(__float_as_int(lo[i]) & lt_mask(i, kq));
+                        hi[i] = __int_as_float(__float_as_int(hi[i]) & lt_mask(4 + i, kq));
+                    }
+                }
+                split3(lo, hi, x1, x2, x3);
+            }
+            const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
+            bf16x8 wb[2];
+            wb[0] = w[0];
+#pragma unroll
+            for (int m = 0; m < NTW; ++m) {
+                if (m + 1 < NTW) wb[(m + 1) & 1] = w[(m + 1) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+                v4f t = acc[m];
+                if (!XB) {
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1], x3, t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1], x2, t, 0, 0, 0);
+                }
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m & 1], x1, t, 0, 0, 0);
+            }
+        } else if (XB && c < ncc) {
             // bf16 x: exact in one part, so only the three products with x1
             i32x4 xw = __builtin_bit_cast(i32x4, xf[2 * c]);
             if (mask_last && c == ncc - 1) {  // padded last chunk: elements past K
@@ -576,20 +620,22 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
 // 0.355 ms/step on products, the extra address VALU spills the L0 kernel.)
 // X3: root term on the 3 x bf16 split (LDS image of W_r split in the
 // prologue from the raw rows); otherwise exact fp32 MFMA.
-template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB>
+template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB, bool W1>
 __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     static_assert(!XB || X3, "bf16 rows feed the split-bf16 root term");
+    static_assert(!W1 || X3, "one weight part: the split-bf16 image");
+    constexpr int NP = W1 ? 1 : 3;  // weight parts in the image
     constexpr uint32_t EB = XB ? 2u : 4u;  // bytes per x element
     constexpr bool WL_LDS = WLM == 1;
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
     __shared__ int s_next_tile;       // the workgroup's tile-claim counter
     if (threadIdx.x == 0) s_next_tile = RT_WAVES;  // each wave's first tile is fixed
     const int nfr = NTW * a.KG * 64;  // fragments per fp32 weight matrix (NTW tiles, zero padded)
-    // X3 image: [3][C][NTW][64] bf16x8 (16 B each) + fp32 tail [T4][NTW][64]
+    // X3 image: [NP][C][NTW][64] bf16x8 (16 B each) + fp32 tail [T4][NTW][64]
     const int pst = a.C * NTW * 64;                        // bf16x8 per piece
-    const int x3_v4f = X3 ? 3 * pst + (a.T4 * NTW * 64) / 4 : 0;
+    const int x3_v4f = X3 ? NP * pst + (a.T4 * NTW * 64) / 4 : 0;
     bf16x8 *sw3 = reinterpret_cast<bf16x8 *>(lds);
-    float *swt = reinterpret_cast<float *>(lds + 3 * pst);
+    float *swt = reinterpret_cast<float *>(lds + NP * pst);
     v4f *swr = lds;                                        // fp32 W_r image (X3 == false)
     v4f *swl = lds + (X3 ? x3_v4f : nfr);
     float *sbias = reinterpret_cast<float *>(swl + (WL_LDS ? nfr : 0));
@@ -637,8 +683,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 bf16x8 p1, p2, p3;
                 split3(lo, hi, p1, p2, p3);
                 sw3[sl] = p1;
-                sw3[pst + sl] = p2;
-                sw3[2 * pst + sl] = p3;
+                if (!W1) {
+                    sw3[pst + sl] = p2;
+                    sw3[2 * pst + sl] = p3;
+                }
             }
             const int ntail = a.T4 * NTW * 64;
             for (int sl = threadIdx.x; sl < ntail; sl += RT_WAVES * 64) {
@@ -848,7 +896,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             }
             if (X3) {
                 const int ncc = min(4, a.C - 4 * c);
-                mfma_group_x3<NTW, XB>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
+                mfma_group_x3<NTW, XB, W1>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
             } else {
                 mfma_chunk_rt<NTW, true>(acc, xc, swr, a.KG, c * RT_KC, nkg, a.NT, lane);
             }
@@ -920,9 +968,9 @@ int num_cus() {
     return g_num_cus[dev];
 }
 
-template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB>
+template <int NTW, int RED, int WLM, bool X3, bool VEC, bool XB, bool W1>
 int launch_rt(const RtArgs &a, int n_tiles, size_t lds_bytes, hipStream_t st) {
-    auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC, XB>;
+    auto fn = k_sage_rt<NTW, RED, WLM, X3, VEC, XB, W1>;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         // 160 KiB per CU minus the kernel's static LDS (the tile counter)
@@ -943,17 +991,24 @@ int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, 
     const bool vec = a.vec_out && (a.Fo == a.NT * 16);
     auto by_red = [&](auto red_c) {
         constexpr int RED = decltype(red_c)::value;
-        auto go = [&](auto x3_c, auto vec_c, auto xb_c) {
+        auto go = [&](auto x3_c, auto vec_c, auto xb_c, auto w1_c) {
             constexpr bool X3 = decltype(x3_c)::value, VEC = decltype(vec_c)::value;
-            constexpr bool XB = decltype(xb_c)::value;
-            return wl_lds ? launch_rt<NTW, RED, 1, X3, VEC, XB>(a, n_tiles, lds, st)
-                          : launch_rt<NTW, RED, 0, X3, VEC, XB>(a, n_tiles, lds, st);
+            constexpr bool XB = decltype(xb_c)::value, W1 = decltype(w1_c)::value;
+            return wl_lds ? launch_rt<NTW, RED, 1, X3, VEC, XB, W1>(a, n_tiles, lds, st)
+                          : launch_rt<NTW, RED, 0, X3, VEC, XB, W1>(a, n_tiles, lds, st);
         };
         using T = std::true_type;
         using F = std::false_type;
-        if (a.x_bf16) return vec ? go(T{}, T{}, T{}) : go(T{}, F{}, T{});  // (x3 checked by the caller)
-        if (x3) return vec ? go(T{}, T{}, F{}) : go(T{}, F{}, F{});
-        return vec ? go(F{}, T{}, F{}) : go(F{}, F{}, F{});
+        // one-part images (bf16-exact weights): MEAN / SUM only (the caller checks)
+        if constexpr (RED != NGNN_REDUCE_MAX) {
+            if (a.w1) {
+                if (a.x_bf16) return vec ? go(T{}, T{}, T{}, T{}) : go(T{}, F{}, T{}, T{});
+                return vec ? go(T{}, T{}, F{}, T{}) : go(T{}, F{}, F{}, T{});
+            }
+        }
+        if (a.x_bf16) return vec ? go(T{}, T{}, T{}, F{}) : go(T{}, F{}, T{}, F{});  // (x3 checked by the caller)
+        if (x3) return vec ? go(T{}, T{}, F{}, F{}) : go(T{}, F{}, F{}, F{});
+        return vec ? go(F{}, T{}, F{}, F{}) : go(F{}, F{}, F{}, F{});
     };
     if (reduce == NGNN_REDUCE_MEAN) return by_red(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
     if (reduce == NGNN_REDUCE_SUM) return by_red(std::integral_constant<int, NGNN_REDUCE_SUM>{});
@@ -1080,7 +1135,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
                      const float *const *x_dev, bool exact, float *z, int64_t ldz,
                      const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
-                     const int32_t *col_x, bool x_bf16) {
+                     const int32_t *col_x, bool x_bf16, bool w_bf16) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -1114,9 +1169,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         kpad = 1;
     }
     if (no_root) C = T4 = kpad = 0;
+    // bf16-exact weights (NGNN_W_BF16): a one-part image (MEAN / SUM kernels)
+    const bool w1 = w_bf16 && x3 && !no_root && reduce != NGNN_REDUCE_MAX;
     const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one fp32 m-tile, all of K
-    // one m-tile of the root image: X3 3 parts x C chunks x 1 KiB + the tail
-    const size_t root_kb = x3 ? (static_cast<size_t>(3 * C) * 64 * 16 + static_cast<size_t>(T4) * 64 * 4)
+    // one m-tile of the root image: X3 3 parts (1 with w1) x C chunks x 1 KiB + the tail
+    const size_t root_kb = x3 ? (static_cast<size_t>((w1 ? 1 : 3) * C) * 64 * 16 +
+                                 static_cast<size_t>(T4) * 64 * 4)
                               : frag_kb;
     // (no root term: the slice width is set by the W_l image alone)
     const size_t img_kb = no_root ? frag_kb : root_kb;
@@ -1202,6 +1260,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.x_rows = x_rows;
         a.col_x = (xrow || xrow_dev) ? col_x : nullptr;
         a.x_bf16 = x_bf16;
+        a.w1 = w1;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         switch (NTW) {
             case 2: *rc = dispatch_rt<2>(a, reduce, wl_lds, x3, n_tiles, lds, st); break;
@@ -1242,7 +1301,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     const bool exact = (reduce & NGNN_MATH_EXACT_F32) != 0;
     const bool want_narrow = (reduce & NGNN_FWD_NARROW) != 0;
     const bool x_bf16 = (reduce & NGNN_X_BF16) != 0;
-    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW | NGNN_X_BF16);
+    const bool w_bf16 = (reduce & NGNN_W_BF16) != 0;
+    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW | NGNN_X_BF16 | NGNN_W_BF16);
     // bf16 rows: the split-bf16 root term and the fused path only
     if (x_bf16 && (exact || want_narrow)) return NGNN_E_SHAPE;
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
@@ -1268,7 +1328,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         float *z = static_cast<float *>(ws);
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
-                             nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x)) {
+                             nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x, false,
+                             w_bf16)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -1286,7 +1347,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
-                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16))
+                          ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16,
+                          w_bf16))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -23,6 +23,7 @@ REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
 MATH_EXACT_F32 = 0x100  # OR-ed into ngnn_sage_fwd_raw's reduce (include/ngnn.h)
 FWD_NARROW = 0x200      # same: output layer aggregated in the F_out-wide space
 X_BF16 = 0x400          # same: x rows are bf16 (read as bf16, widened exactly)
+W_BF16 = 0x800          # same: weights are bf16-exact (one split part)
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one

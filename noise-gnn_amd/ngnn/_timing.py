@@ -74,11 +74,15 @@ class KernelTimer:
 @contextlib.contextmanager
 def span(name: str, nbytes: int, flops: int = 0, mfma_s: float = 0.0):
     t = _active
+    """Times the launches inside; yields the record (None when no timer is
+    active) so the caller can correct its counts once it knows which kernel
+    ran (e.g. the fp32 64-row fallback's matrix time)."""
     if t is None or (t.only is not None and name not in t.only):
-        yield
+        yield None
         return
     s, e = t._event(), t._event()
+    rec = Rec(name, int(nbytes), s, e, int(flops), float(mfma_s))
     s.record()
-    yield
+    yield rec
     e.record()
-    t.recs.append(Rec(name, int(nbytes), s, e, int(flops), float(mfma_s)))
+    t.recs.append(rec)

@@ -156,14 +156,17 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
                    seed_dev: torch.Tensor | None = None,
                    x_dev: torch.Tensor | None = None, span: str = "sage_fwd",
                    narrow: bool = False, xrow_dev: torch.Tensor | None = None,
-                   x_rows: int = 0) -> torch.Tensor:
+                   x_rows: int = 0, w_bf16: bool = False) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
     supplies the shape.  xrow_dev (with x_dev): device word holding the
     address of the block's n_id when x_dev points at the whole x_rows-row
     feature table (fused x[n_id] gather; 0 at run time: plain rows).
     narrow: aggregate the neighbour term as mean/sum of z = x W_l^T (F_out
-    wide) instead of x (K wide) -- the output layer's form (no agg_out then)."""
+    wide) instead of x (K wide) -- the output layer's form (no agg_out then).
+    w_bf16: the weights hold bf16-exact values (a bf16 model's parameters,
+    widened): NGNN_W_BF16, a one-part split image (same sums, fewer MFMAs and
+    wider column slices)."""
     N, K = x.shape
     Fo = wl.shape[0]
     if x.dtype == torch.bfloat16 and not bf16_rows_ok(x, narrow):
@@ -179,7 +182,11 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     # ideal matrix-core time of the instruction mix: the
     # root term on 6 bf16 products per fp32 product (bf16 dense 16x the f32
     # MFMA rate) unless exact, the neighbour term on f32 MFMA
-    root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / 6.0)
+    w1 = w_bf16 and not _exact_f32 and reduce != "max"
+    # bf16 products per fp32 product of the root term: 6 (3 with bf16 rows);
+    # one-part weights: 3 (1 with bf16 rows)
+    nprod = (1 if xb else 3) if w1 else (3 if xb else 6)
+    root_rate = MFMA_F32_TFS * 1e12 * (1.0 if _exact_f32 else 16.0 / nprod)
     mfma_s = 2 * N * K * Fo * root / root_rate + 2 * n_e * K * Fo / (MFMA_F32_TFS * 1e12)
     if xrow_dev is not None:  # the n_id loads of the fused gather (rows, neighbours)
         nbytes += (N + block.E) * 8
@@ -207,7 +214,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
-    with _timing.span(span, nbytes, flops, mfma_s):
+    with _timing.span(span, nbytes, flops, mfma_s) as rec:
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel
         n_edge = N if block.n_active is None else min(int(block.n_active), N)
@@ -218,7 +225,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
             _lib.ptr(block.col_x) if xrow_dev is not None else None,
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0)
-            | (_lib.X_BF16 if xb else 0),
+            | (_lib.X_BF16 if xb else 0) | (_lib.W_BF16 if w1 else 0),
             _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out),
@@ -227,10 +234,12 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         if rc == _lib.E_SHAPE and xb and x_dev is None:
             # bf16 rows outside the bf16 envelope: the fp32 path on widened rows
             return sage_layer_fwd(x.float(), block, reduce, wl, bl, wr, relu, p_drop, seed,
-                                  agg_out, seed_dev, None, span, narrow)
+                                  agg_out, seed_dev, None, span, narrow, w_bf16=w_bf16)
         if rc == _lib.E_SHAPE:
             if x_dev is not None:
                 raise _lib.NGNNError("zero-copy input outside the row-tile kernel's envelope")
+            if rec is not None:  # the 64-row kernel is exact fp32 MFMA throughout
+                rec.mfma_s = flops / (MFMA_F32_TFS * 1e12)
             pl = pack_weight(wl)
             pr = pack_weight(wr if root else _zeros_like_cached(wl))
             _gemm_layer(x, K, N, block, reduce, pl, pr, bl, Fo, out, relu, p_drop, seed,
@@ -329,7 +338,7 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
-                *params):
+                w_bf16: bool, *params):
         L = len(params) // 3
         acts, aggs = [x], []
         h = x
@@ -353,7 +362,8 @@ class _SAGEStack(torch.autograd.Function):
                 agg = None if narrow else agg_buffer(h.size(0), h.size(1), h.device, wl.shape[0])
                 h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
                                    seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
-                                   span=f"sage_fwd_l{i}", narrow=narrow, **xrow)
+                                   span=f"sage_fwd_l{i}", narrow=narrow, w_bf16=w_bf16,
+                                   **xrow)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -520,7 +530,7 @@ class _SAGEStack(torch.autograd.Function):
                 _lib.check(rc, "ngnn_sage_dgrad_scatter")
             dy = dh
         dx = dy if (need_dx and L > 0) else None
-        return (dx, None, None, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, None, None, *grads)
 
 
 _IO_DTYPES = (torch.float32, torch.bfloat16)
@@ -609,6 +619,8 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                   if (q is not None and q.grad is None and q.dtype == torch.float32
                       and q.requires_grad) else None
                   for q in params)
+    # a bf16 model's weights are bf16-exact once widened: one-part split images
+    w_bf16 = all(q is None or q.dtype == torch.bfloat16 for q in params)
     if out_dtype != torch.float32 or any(q is not None and q.dtype != torch.float32 for q in params):
         # bf16 features stay bf16 for a SAGE stack's layer 0 (the kernels read
         # bf16 rows, NGNN_X_BF16: half the bytes, no widened copy) unless an
@@ -620,7 +632,8 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
         gouts = (None,) * len(params)
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
-    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, *params)
+    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16,
+                           *params)
     if out_dtype == torch.float32:
         return out
     if out_dtype == torch.bfloat16 and out.is_contiguous():

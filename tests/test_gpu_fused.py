@@ -527,3 +527,43 @@ def test_bf16_features_stack_matches_widened(layers):
     torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
     for k in res[0][1]:
         torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("K,Fo,narrow", [(100, 256, False), (256, 256, False), (36, 7, False),
+                                         (300, 512, False), (256, 47, True), (24, 47, True)])
+@pytest.mark.parametrize("reduce", ["mean", "sum"])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_bf16_weights_one_part_image_bitwise(K, Fo, narrow, reduce, xdt):
+    """NGNN_W_BF16 (a bf16 model's weights, widened): the one-part split
+    image skips the products with the weights' second and third parts, which
+    are exact zeros, so the layer is BITWISE the three-part layer -- with
+    fp32 and bf16 rows, across column slices (256 -> 256 takes 3 slices with
+    the three-part image and 1 with one part), and in narrow mode."""
+    if narrow and xdt == torch.bfloat16:
+        pytest.skip("narrow mode reads fp32 rows")
+    N, E = 900, 6000
+    g = torch.Generator().manual_seed(K + 3 * Fo)
+    ei = rand_block(K * Fo + 1, N, E)
+    ei = ei[:, ei[1] < N - 150]
+    x = torch.randn(N, K, generator=g).to(xdt).to(DEV)
+    conv = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
+    wl, bl, wr = (t.detach().to(torch.bfloat16).float().to(DEV)
+                  for t in (conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight))
+    blk = Block(ei.to(DEV), N)
+    epi = dict(relu=False, p_drop=0.0) if narrow else dict(relu=True, p_drop=0.25)
+    outs = []
+    for w1 in (False, True):
+        agg = None if narrow else torch.full((N, K), 7.0, device=DEV)
+        o = sage_layer_fwd(x, blk, reduce, wl, bl, wr, seed=5, agg_out=agg, narrow=narrow,
+                           w_bf16=w1, **epi)
+        outs.append((o.cpu(), None if agg is None else agg.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if not narrow:
+        assert torch.equal(outs[0][1], outs[1][1])
+    with torch.no_grad():
+        c2 = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
+        c2.lin_l.weight.copy_(wl.cpu()), c2.lin_l.bias.copy_(bl.cpu()), c2.lin_r.weight.copy_(wr.cpu())
+        ref = c2(x.float().cpu(), ei)
+    if not narrow:
+        ref = ref.relu() * dropout_keep(5, N, Fo, 0.25) * dropout_scale(0.25)
+    torch.testing.assert_close(outs[1][0], ref, **OUT)
