@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--module", default="sage", choices=["sage", "gcn"],
                     help="model.py's `module`: SAGE (sage.py) or SimpleGCN (convolution.py)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
-                    help="model / feature storage dtype (bf16: fp32 kernels inside)")
+                    help="model / feature storage dtype (bf16: bf16 feature rows and one-part bf16 weight images, fp32 accumulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -329,6 +329,9 @@ def main():
         workload += f"-{args.aggr}"
     if args.module == "gcn":
         workload += "-gcn"
+    # the layer-0 kernel reads rows through n_id under the fused gather: its
+    # own traffic key (a loader-copy PMC record is not its evidence)
+    pmc_workload = workload + ("-fusedgather" if args.gather == "fused" else "")
     # dominant kernel roofline from the live events of the timed region
     summ = timer.summary()
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
@@ -358,7 +361,7 @@ def main():
         else:
             roof = {"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(f_hbm, 4)}
-        traffic, traffic_src = pmc_traffic(name, workload, args.dtype)
+        traffic, traffic_src = pmc_traffic(name, pmc_workload, args.dtype)
         roof.update({
             "traffic": traffic, "traffic_src": traffic_src, "launches": n,
             "avg_us": round(1e3 * ms / n, 2),
