@@ -335,6 +335,15 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
     return out
 
 
+def _dgrad_fused_ok(Fo: int, K: int) -> bool:
+    """ngnn_sage_dgrad_fused (per target row, VALU products, W_r and W_l in
+    LDS) only while both weights fit its LDS: a wave re-reads the whole of W
+    for every row, so with W streamed from L2 (the 3-layer products hidden
+    layer, 256 x 256: 512 KiB per row) it ran 845 us/step.  Wider layers take
+    the dgrad GEMM (MFMA, rows < R) + scatter."""
+    return Fo <= 512 and 2 * Fo * K * 4 + 4 * 512 * 4 <= 150 * 1024
+
+
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
@@ -489,7 +498,7 @@ class _SAGEStack(torch.autograd.Function):
                     continue
                 if rc != _lib.E_SHAPE:
                     _lib.check(rc, "ngnn_sage_dgrad_lowdim")
-            if not deterministic and Fo <= 512:
+            if not deterministic and _dgrad_fused_ok(Fo, K):
                 # atomic path: per-row VALU products + scatter, no dgrad GEMM launch
                 dh = torch.empty(N, K, dtype=torch.float32, device=dev)
                 wlc, wrc = wl.detach().contiguous(), wr.detach().contiguous()

@@ -260,3 +260,18 @@ def test_config_products_3layer_bf16_graph_slot():
         want = _oracle_rows(ref, b.x.float().cpu(), b.edge_index.cpu(), rows)
     torch.testing.assert_close(out[rows], want, rtol=2e-2, atol=2e-2)
     assert torch.isfinite(out).all()
+
+
+def test_3layer_h256_backward_gemm_scatter_path():
+    """SAGE(100,256,256,47), train mode, input gradient wanted: the 256 x 256
+    and 100 -> 256 layers' input gradients run the dgrad GEMM + scatter
+    (weights too large for the fused kernel's LDS); every gradient against
+    the oracle."""
+    from ngnn.fused import _dgrad_fused_ok
+    from ngnn.loader import sample_block
+    assert not _dgrad_fused_ok(256, 256) and not _dgrad_fused_ok(256, 100)
+    g = _graph("ogbn-products", scale=0.01)
+    b = sample_block(g, g.train_idx[:256], [8, 5, 3], seed=5)
+    torch.manual_seed(7)
+    mine = ngnn.SAGE(100, 256, 47, 3, dropout=0.5).to(DEV)
+    _eager_vs_oracle(b, mine, 256, train=True, aggr="mean", check_dx=True)
