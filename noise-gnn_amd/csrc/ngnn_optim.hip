@@ -135,12 +135,22 @@ __global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src
     };
     const int64_t n4 = n >> 2;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n4; i += stride) {
-        const float4 v = reinterpret_cast<const float4 *>(src)[i];
+    auto put = [&](int64_t i, float4 v) {
         const uint2 o{static_cast<uint32_t>(rne(v.x)) | (static_cast<uint32_t>(rne(v.y)) << 16),
                       static_cast<uint32_t>(rne(v.z)) | (static_cast<uint32_t>(rne(v.w)) << 16)};
         reinterpret_cast<uint2 *>(dst)[i] = o;
+    };
+    int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+    // four 16-B loads in flight per thread before the first store
+    constexpr int U = 4;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = reinterpret_cast<const float4 *>(src)[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) put(i + u * stride, v[u]);
     }
+    for (; i < n4; i += stride) put(i, reinterpret_cast<const float4 *>(src)[i]);
     for (int64_t i = 4 * n4 + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += stride)
         dst[i] = rne(src[i]);
@@ -153,7 +163,7 @@ extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *
     NGNN_RETURN_IF(n < 0 || (n > 0 && (!src || !dst)), NGNN_E_ARG);
     NGNN_RETURN_IF(!aligned(src, 16) || !aligned(dst, 8), NGNN_E_SHAPE);
     if (n == 0) return NGNN_OK;
-    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 4), 256), 4096));
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 4), 256), 2048));
     hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, as_stream(stream), src,
                        static_cast<uint16_t *>(dst), n);
     return launch_status();

@@ -58,7 +58,11 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
     static constexpr int N = WG_BM * CPR / 512;        // loads per thread
     static_assert(N >= 1 && (WG_BM * CPR) % 512 == 0, "chunk must tile the workgroup");
     using T = std::conditional_t<VEC, v4f, float>;
-    T v[N];
+    T v[BF && VEC ? 1 : N];
+    // bf16 quads stay packed until store(): widening them in load() would
+    // make every load wait at once (the next chunk's loads must stay in
+    // flight under this chunk's MFMAs)
+    i32x2 raw[BF && VEC ? N : 1];
     T m[MASK ? N : 1];
     int d0[DEG ? N : 1], d1[DEG ? N : 1];
 
@@ -91,7 +95,7 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
                 vo = kok ? (r * static_cast<int>(ld) + k) * static_cast<int>(EB) : kBufOOB;
             }
             if constexpr (BF && VEC) {
-                v[u] = bf16x4_to_f32(buf_load2i(rs, vo, 0, 0));
+                raw[u] = buf_load2i(rs, vo, 0, 0);
             } else if constexpr (BF) {  // the dword holding the element, then its half
                 const int w = buf_load1i(rs, vo & ~3, 0, 0);
                 v[u] = __int_as_float((vo & 2) ? (w & static_cast<int>(0xffff0000u)) : (w << 16));
@@ -117,7 +121,9 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
         for (int u = 0; u < N; ++u) {
             const int idx = static_cast<int>(threadIdx.x) + u * 512;
             const int r = idx / CPR, c = (idx % CPR) * W;
-            T w = v[u];
+            T w;
+            if constexpr (BF && VEC) w = bf16x4_to_f32(raw[u]);
+            else w = v[u];
             float *wf = reinterpret_cast<float *>(&w);
             const float *mf = reinterpret_cast<const float *>(&m[MASK ? u : 0]);
 #pragma unroll
