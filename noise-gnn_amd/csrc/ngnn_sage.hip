@@ -55,7 +55,6 @@ struct Extra {
     int64_t ldm;
     float xscale;
     const uint64_t *seed_dev;  // XORed into the dropout seed (HIP-graph replays)
-    int dbg;  // ablation switch for profiling (NGNN_SAGE_ABLATE): 0 in normal runs
 };
 
 // ---- X rows [row0, row0+64) x [k0, k0+128) -> LDS, zero padded
@@ -257,9 +256,9 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
         const int nkg = (min(KC, K - k0) + 15) >> 4;
         if (!first) __syncthreads();
         first = false;
-        if (!(ex.dbg & 4)) stage_x<VEC>(s, x, ldx, row0, rows, k0, K, ex.xmask, ex.ldm, ex.xscale);
+        stage_x<VEC>(s, x, ldx, row0, rows, k0, K, ex.xmask, ex.ldm, ex.xscale);
         __syncthreads();
-        if (!(ex.dbg & 1)) mfma_chunk<MTW, NTW>(acc, s, wr, KG, k0 >> 4, nkg, mbase, nbase, NT);
+        mfma_chunk<MTW, NTW>(acc, s, wr, KG, k0 >> 4, nkg, mbase, nbase, NT);
     }
     if (has_edges) {
         for (int k0 = 0; k0 < K; k0 += KC) {
@@ -282,7 +281,6 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
     // barrier): in a 16x16 C tile lane l holds rows 4*(l>>4)+j of column l&15,
     // so one store instruction writes four 64-B row segments; the neighbouring
     // n-tile completes each 128-B line in L2.
-    if (ex.dbg & 8) return;
     const int q = lane >> 4, cl = lane & 15;
     (void)vec_out;
     if (ex.seed_dev) epi.drop.reseed(*ex.seed_dev);
@@ -308,7 +306,7 @@ __global__ __launch_bounds__(256, (MTW * NTW >= 32) ? 2 : ((MTW * NTW >= 16) ? 3
                 if (epi.relu) v = (v < 0.0f) ? 0.0f : v;  // NaN passes, like torch.relu
                 if (epi.drop.thresh)
                     v = epi.drop.keep(rk[mt][j], epi.col_base + c) ? v * epi.drop.scale : 0.0f;
-                if (!(ex.dbg & 2)) out[(row0 + r) * ldo + c] = v;
+                out[(row0 + r) * ldo + c] = v;
             }
     }
 }
@@ -498,7 +496,7 @@ extern "C" int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_r
     for (int64_t c0 = 0; c0 < Fo; c0 += 512) {
         const int64_t Fo_c = std::min<int64_t>(512, Fo - c0);
         const int64_t toff = (c0 / 16) * KG * 64;  // float4 offset of the slice's first n-tile
-        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, seed_dev, 0};
+        Extra ex{n_rows_dev, c0 == 0 ? agg_out : nullptr, ld_agg, xmask, ldm, xscale, seed_dev};
         float *of = out + c0;
         const int vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(of, 16);
         const int NT = static_cast<int>(ceil_div(Fo_c, 16));

@@ -25,8 +25,6 @@ fi
 if [ "${KBENCH:-0}" = 1 ]; then
   timeout -k 10 300 python3 tools/bench_kernels.py --reps 20 > "$OUT/kbench.json" 2> "$OUT/kbench.err"
   stop_on_crash $? kbench
-  NGNN_NO_ROWTILE=1 timeout -k 10 300 python3 tools/bench_kernels.py --reps 20 > "$OUT/kbench_64row.json" 2> "$OUT/kbench_64row.err"
-  stop_on_crash $? kbench_64row
 fi
 if [ "${SKIP_BENCH:-0}" != 1 ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
