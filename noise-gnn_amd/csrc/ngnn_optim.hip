@@ -23,6 +23,7 @@ struct AdamTensors {
     float *m[kMaxT];
     float *v[kMaxT];
     int64_t off[kMaxT + 1];  // prefix sums of numel
+    int64_t boff[kMaxT + 1];  // prefix sums of workgroups (ceil(numel / 256) per tensor)
     int n;
 };
 
@@ -33,12 +34,12 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
     const float bc1 = 1.0f - powf(b1, t);
     const float bc2s = sqrtf(1.0f - powf(b2, t));
     const float step_size = lr / bc1;
-    const int64_t total = T.off[T.n];
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int k = 0;
-        while (k + 1 < T.n && i >= T.off[k + 1]) ++k;
-        const int64_t j = i - T.off[k];
+    // workgroup -> tensor: uniform (scalar loads of the tensor's pointers,
+    // no per-lane search and dependent pointer loads)
+    int k = 0;
+    while (k + 1 < T.n && static_cast<int64_t>(blockIdx.x) >= T.boff[k + 1]) ++k;
+    const int64_t j = (static_cast<int64_t>(blockIdx.x) - T.boff[k]) * blockDim.x + threadIdx.x;
+    if (j < T.off[k + 1] - T.off[k]) {
         float g, p;
         if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
             g = __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(T.g[k])[j]);
@@ -109,7 +110,10 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
             T.off[k + 1] = T.off[k] + numels[base + k];
         }
         if (T.off[T.n] == 0) continue;
-        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(T.off[T.n], 256), 2048));
+        T.boff[0] = 0;
+        for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], 256);
+        NGNN_RETURN_IF(T.boff[T.n] > (int64_t{1} << 31) - 1, NGNN_E_RANGE);
+        const unsigned grid = static_cast<unsigned>(T.boff[T.n]);
         hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
                            eps, weight_decay);
         const int rc = launch_status();
