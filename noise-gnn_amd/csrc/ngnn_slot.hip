@@ -67,24 +67,24 @@ __global__ __launch_bounds__(256) void k_slot_load(
     }
     for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
     if (rowptr) {
-        // rowptr[r] = first padded edge with target >= r.  Real edges
-        // (targets < N, sorted): binary search; padding: closed form
-        // (target of padding edge j is N + floor(j span / n_pad)).
-        // rows past the last real target (NeighborLoader: every row that
-        // received no edges, ~90% of a products block) need no search
+        // rowptr[r] = first padded edge with target >= r.  Padding: closed
+        // form (target of padding edge j is N + floor(j span / n_pad)); rows
+        // past the last real target (NeighborLoader: every row that received
+        // no edges, ~90% of a products block): E.
         const int64_t last_dst = E > 0 ? ei[ld_ei + E - 1] : -1;
-        for (int64_t r = tid; r <= n_cap; r += nthr) {
+        // rows up to the last target: edge e writes rowptr[r] = e for every
+        // r in (dst[e-1], dst[e]] -- the lower bound of r over the sorted
+        // targets, each row written once, two independent loads per edge
+        // (a per-row binary search was a chain of ~17 dependent loads)
+        for (int64_t e = tid; e < E; e += nthr) {
+            const int64_t d = ei[ld_ei + e];
+            const int64_t p = e > 0 ? ei[ld_ei + e - 1] : -1;
+            for (int64_t r = p + 1; r <= d; ++r) rowptr[r] = static_cast<int32_t>(e);
+        }
+        for (int64_t r = last_dst + 1 + tid; r <= n_cap; r += nthr) {
             int64_t e;
-            if (r > last_dst && r <= N) {
+            if (r <= N) {
                 e = E;
-            } else if (r <= N) {
-                int64_t lo = 0, hi = E;
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi) >> 1;
-                    if (ei[ld_ei + mid] < r) lo = mid + 1;
-                    else hi = mid;
-                }
-                e = lo;
             } else if (n_pad > 0) {
                 e = E + min(n_pad, ((r - N) * n_pad + span - 1) / span);
             } else {

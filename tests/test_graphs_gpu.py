@@ -241,3 +241,51 @@ def _graph_bf16_features_slot_matches_eager():
         assert abs(a - c) < 1e-4 * max(1.0, abs(a)), (le, lg)
     for (n, pe), pg in zip(m_e.named_parameters(), m_g.parameters()):
         torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=lambda m, n=n: f"{n}: {m}")
+
+
+@pytest.mark.parametrize("case", ["block", "gaps", "empty", "full"])
+def test_slot_load_csr_equals_lower_bound(case):
+    """ngnn_slot_load's target-grouped CSR of the padded edges: rowptr[r] =
+    the lower bound of r over the padded targets (real edges, then padding
+    self-loops spread over rows N .. n_cap), rowptr[n_cap] = e_cap, col the
+    sources -- for a NeighborLoader-like block, targets with gaps (rows with
+    no in-edges among the targets, first target > 0), no edges, and a full
+    slot (E = e_cap)."""
+    from ngnn import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(3)
+    N, n_cap, e_cap, F = 500, 700, 3000, 4
+    if case == "empty":
+        dst = torch.zeros(0, dtype=torch.int64)
+    elif case == "gaps":
+        dst = torch.sort(5 + 2 * torch.randint(0, 120, (2000,), generator=g)).values
+    elif case == "full":
+        N = n_cap = 500
+        dst = torch.sort(torch.randint(0, N, (e_cap,), generator=g)).values
+    else:
+        dst = torch.sort(torch.randint(0, 300, (2500,), generator=g)).values
+    E = dst.numel()
+    src = torch.randint(0, N, (E,), generator=g)
+    ei = torch.stack([src, dst]).to(DEV).contiguous()
+    x = torch.randn(N, F, generator=g).to(DEV)
+    y = torch.zeros(8, dtype=torch.int64, device=DEV)
+    sx = torch.zeros(n_cap, F, device=DEV)
+    sei = torch.full((2 * e_cap,), -1, dtype=torch.int64, device=DEV)
+    sy = torch.zeros(8, dtype=torch.int64, device=DEV)
+    nv = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rowptr = torch.full((n_cap + 1,), -7, dtype=torch.int32, device=DEV)
+    col = torch.full((e_cap,), -7, dtype=torch.int32, device=DEV)
+    _lib.check(lib.ngnn_slot_load(
+        _lib.ptr(x), x.stride(0), N, F, _lib.ptr(ei) if E else None, max(E, 0), E, _lib.ptr(y), 8,
+        _lib.ptr(sx), sx.stride(0), n_cap, _lib.ptr(sei), e_cap, _lib.ptr(sy), _lib.ptr(nv),
+        _lib.ptr(rowptr), _lib.ptr(col), None, None, None, 0, None, None, None, None,
+        _lib.stream_handle(DEV)), "ngnn_slot_load")
+    torch.cuda.synchronize()
+    n_pad, span = e_cap - E, n_cap - N
+    pad = N + (torch.arange(n_pad) * span) // max(n_pad, 1) if n_pad else torch.zeros(0, dtype=torch.int64)
+    dst_p = torch.cat([dst, pad])
+    want = torch.searchsorted(dst_p, torch.arange(n_cap + 1), right=False).to(torch.int32)
+    want[n_cap] = e_cap
+    assert torch.equal(rowptr.cpu(), want)
+    assert torch.equal(col.cpu(), torch.cat([src, pad]).to(torch.int32))
+    assert torch.equal(sei.cpu()[e_cap:], dst_p)
