@@ -702,19 +702,21 @@ __global__ __launch_bounds__(512, 1) void k_lowdim_gemm(
     const int rb = 16 * static_cast<int>(static_cast<int64_t>(blockIdx.x) * T16 / G);
     const int re = min(Rn, 16 * static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * T16 / G));
     if (rb >= re) return;
-    {  // W image -> LDS, LD_SU 16-B loads in flight per thread
+    {  // W image -> LDS, 2 LD_SU 16-B loads in flight per thread (the
+       // products output layer's 96 KiB image: one batch)
         const int n4 = KS * NTP * 16;
         const v4f *src = reinterpret_cast<const v4f *>(img);
         v4f *dst = reinterpret_cast<v4f *>(wimg);
-        for (int base = 0; base < n4; base += 512 * LD_SU) {
-            v4f t[LD_SU];
+        constexpr int IU = 2 * LD_SU;
+        for (int base = 0; base < n4; base += 512 * IU) {
+            v4f t[IU];
 #pragma unroll
-            for (int u = 0; u < LD_SU; ++u) {
+            for (int u = 0; u < IU; ++u) {
                 const int i = base + u * 512 + threadIdx.x;
                 if (i < n4) t[u] = src[i];
             }
 #pragma unroll
-            for (int u = 0; u < LD_SU; ++u) {
+            for (int u = 0; u < IU; ++u) {
                 const int i = base + u * 512 + threadIdx.x;
                 if (i < n4) dst[i] = t[u];
             }
@@ -727,9 +729,11 @@ __global__ __launch_bounds__(512, 1) void k_lowdim_gemm(
     for (int c0 = rb; c0 < re; c0 += LD_ROWS) {
         __syncthreads();  // W image written / previous stage's reads done
         const int nr = min(LD_ROWS, re - c0);
-        // dz half: scalar (Fo need not be a multiple of 4), rows < R only
-        for (int base = 0; base < LD_ROWS * C4; base += 512 * LD_SU) {
-            float t[LD_SU];
+        // dz half (scalar: Fo need not be a multiple of 4; rows < R only)
+        // and g half (16-B loads, each read row cleared behind it), one
+        // batch of each: every load of the stage is in flight before the
+        // first LDS store (C4 <= 64: 64 C4 <= 512 LD_SU)
+        auto ld_dz = [&](int base, float (&t)[LD_SU]) {
 #pragma unroll
             for (int u = 0; u < LD_SU; ++u) {
                 const int idx = base + u * 512 + threadIdx.x;
@@ -742,16 +746,16 @@ __global__ __launch_bounds__(512, 1) void k_lowdim_gemm(
                     t[u] = v;
                 }
             }
+        };
+        auto st_dz = [&](int base, const float (&t)[LD_SU]) {
 #pragma unroll
             for (int u = 0; u < LD_SU; ++u) {
                 const int idx = base + u * 512 + threadIdx.x;
                 const int r = idx / C4, c = idx - r * C4;
                 if (r < LD_ROWS) xs[r * LDX + c] = t[u];
             }
-        }
-        // g half: 16-B loads, each read row cleared behind it
-        for (int base = 0; base < LD_ROWS * C44; base += 512 * LD_SU) {
-            v4f t[LD_SU];
+        };
+        auto ld_g = [&](int base, v4f (&t)[LD_SU]) {
 #pragma unroll
             for (int u = 0; u < LD_SU; ++u) {
                 const int idx = base + u * 512 + threadIdx.x;
@@ -763,11 +767,32 @@ __global__ __launch_bounds__(512, 1) void k_lowdim_gemm(
                     *gp = v4f{0.f, 0.f, 0.f, 0.f};  // leave g zero for the next call
                 }
             }
+        };
+        auto st_g = [&](int base, const v4f (&t)[LD_SU]) {
 #pragma unroll
             for (int u = 0; u < LD_SU; ++u) {
                 const int idx = base + u * 512 + threadIdx.x;
                 const int r = idx / C44, c = (idx - r * C44) * 4;
                 if (r < LD_ROWS) *reinterpret_cast<v4f *>(xs + r * LDX + C4 + c) = t[u];
+            }
+        };
+        if (LD_ROWS * C4 <= 512 * LD_SU) {
+            float tz[LD_SU];
+            v4f tg[LD_SU];
+            ld_dz(0, tz);
+            ld_g(0, tg);
+            st_dz(0, tz);
+            st_g(0, tg);
+        } else {
+            for (int base = 0; base < LD_ROWS * C4; base += 512 * LD_SU) {
+                float t[LD_SU];
+                ld_dz(base, t);
+                st_dz(base, t);
+            }
+            for (int base = 0; base < LD_ROWS * C44; base += 512 * LD_SU) {
+                v4f t[LD_SU];
+                ld_g(base, t);
+                st_g(base, t);
             }
         }
         __syncthreads();
