@@ -125,8 +125,9 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
     return launch_status();
 }
 
-// ---- fp32 -> bf16 rows (a bf16 model's logits): round to nearest even, NaN
-// kept quiet (torch's rule); 4 values per thread, grid-stride.  Replaces
+// ---- fp32 -> bf16 rows (a bf16 model's logits): round to nearest even, every
+// NaN to the canonical quiet NaN 0x7FC0 (c10::BFloat16's round_to_nearest_even,
+// which torch's device cast uses); 4 values per thread, grid-stride.  Replaces
 // Tensor.to(torch.bfloat16) on the [N, C] logits.
 namespace ngnn {
 namespace {
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src
                                                     uint16_t *__restrict__ dst, int64_t n) {
     auto rne = [](float f) -> uint16_t {
         const uint32_t u = __float_as_uint(f);
-        if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>(0x7fc0u);
         return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
     };
     const int64_t n4 = n >> 2;

@@ -30,6 +30,8 @@ graph's up to fp32 summation order; nothing is read back to the host.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import _lib, _timing
@@ -376,7 +378,7 @@ class _SAGEStack(torch.autograd.Function):
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
-        ctx.gouts = gouts  # per parameter: a buffer the weight gradient is written into, or None
+        ctx.gouts = gouts  # _GradViews (buffers the weight gradients go into) or None
         ctx.save_for_backward(*acts, *aggs, *params)
         return h
 
@@ -393,6 +395,12 @@ class _SAGEStack(torch.autograd.Function):
             raise _lib.NGNNError("input gradient of a zero-copy slot input is not supported")
         N = block.n_dst
         grads = [None] * (3 * L)
+        # the claimed bucket views serve the FIRST backward only (a second one,
+        # retain_graph, would write into a view autograd already adopted)
+        gv = ctx.gouts
+        views = gv.views if (gv is not None and gv.live) else [None] * (3 * L)
+        if gv is not None:
+            gv.live = False
         dy = dout if dout.stride(1) == 1 else dout.contiguous()
         # bnd[L] = rows of dout that can be nonzero; bnd[i] = same for d(acts[i])
         # (prefix_stats takes max(bnd[i], R, ...), so R is a valid initial bnd[i])
@@ -444,7 +452,7 @@ class _SAGEStack(torch.autograd.Function):
             # .grad instead of copying it), else new tensors
             dwl, dbl, dwr = (
                 (g.view(q.shape) if g is not None else torch.empty_like(q))
-                for g, q in zip(ctx.gouts[3 * i:3 * i + 3], (wl, bl, wr)))
+                for g, q in zip(views[3 * i:3 * i + 3], (wl, bl, wr)))
             if gcn:
                 dwr = _workspace(dev, "gcn_dwr", wr.numel() * 4).view(torch.float32)[
                     :wr.numel()].view(wr.shape)
@@ -619,15 +627,52 @@ def sage_stack(model, x, block: Block, seed: int, seed_dev=None) -> torch.Tensor
     return _run_stack(model, x, block, seed, seed_dev, params, aggr, keep_bf16_x=True)
 
 
+class _GradViews:
+    """The bucket views (ngnn.distributed.GradAllReduce) one pending stack
+    node may write its weight gradients into.  A parameter's view goes to ONE
+    node at a time: the node claims it at forward time and gives it up in its
+    first backward (or when its graph is freed without one -- the parameter
+    holds only a weak reference).  Without the claim, two forwards before one
+    backward (the reference's pipeline_contrast.py:146-154 runs the model on
+    several batches per step) would both write into the same view, autograd
+    would adopt the first write and then add the view to itself: 2 g2 instead
+    of g1 + g2."""
+
+    __slots__ = ("views", "live", "__weakref__")
+
+    def __init__(self, n: int):
+        self.views = [None] * n
+        self.live = True
+
+
+def _claim_grad_views(params) -> "_GradViews | None":
+    """Views for the fp32 parameters whose .grad is unset (autograd will adopt
+    them) and whose view no other pending node holds; None when there are none."""
+    if not torch.is_grad_enabled():
+        return None
+    gv = _GradViews(len(params))
+    for i, q in enumerate(params):
+        if (q is None or q.grad is not None or q.dtype != torch.float32
+                or not q.requires_grad):
+            continue
+        v = getattr(q, "_ngnn_grad_out", None)
+        if v is None:
+            continue
+        held = getattr(q, "_ngnn_grad_claim", None)
+        holder = held() if held is not None else None
+        if holder is not None and holder.live:
+            continue  # another forward's backward is still to write it
+        q._ngnn_grad_claim = weakref.ref(gv)
+        gv.views[i] = v
+    return gv if any(v is not None for v in gv.views) else None
+
+
 def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                keep_bf16_x: bool = False) -> torch.Tensor:
     out_dtype = x.dtype
     # weight gradients straight into registered bucket views (ngnn.distributed.GradAllReduce)
-    # when autograd will adopt them: fp32 parameters whose .grad is unset
-    gouts = tuple(getattr(q, "_ngnn_grad_out", None)
-                  if (q is not None and q.grad is None and q.dtype == torch.float32
-                      and q.requires_grad) else None
-                  for q in params)
+    # when autograd will adopt them (see _GradViews)
+    gouts = None
     # a bf16 model's weights are bf16-exact once widened: one-part split images
     w_bf16 = all(q is None or q.dtype == torch.bfloat16 for q in params)
     if out_dtype != torch.float32 or any(q is not None and q.dtype != torch.float32 for q in params):
@@ -638,7 +683,8 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                 and bf16_rows_ok(x)):
             x = x.float()
         params = [None if q is None else q.float() for q in params]
-        gouts = (None,) * len(params)
+    else:
+        gouts = _claim_grad_views(params)
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
     out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16,

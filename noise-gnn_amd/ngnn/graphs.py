@@ -34,7 +34,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .block import CSR, block_cache, hint_edge_index
+from .block import CSR, _hint_for, block_cache, hint_edge_index
 from .loader import IndexedRows
 from .losses import seed_cross_entropy
 
@@ -121,6 +121,14 @@ class GraphedTrainStep:
             x = x.clone(memory_format=torch.contiguous_format)
         # a step captured for indexed rows: the word gets n_id's address or 0
         xrow_word = self.xrow_dev if (zero_copy and self.x_rows) else None
+        # the slot kernel's CSR assumes non-decreasing targets; a producer hint
+        # (ngnn.loader's sampler) vouches for that, anything else is checked
+        # here (one host read-back) instead of yielding a corrupt rowptr
+        hint = _hint_for(edge_index)
+        if (hint is None or not hint[0]) and E > 1 and not bool(
+                (edge_index[1, 1:] >= edge_index[1, :-1]).all()):
+            raise ValueError("GraphedTrainStep needs target-sorted edges (NeighborLoader's "
+                             "order); sort edge_index by edge_index[1] (stable) first")
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
         y = y[:bs].contiguous()

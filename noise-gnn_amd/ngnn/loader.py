@@ -315,21 +315,32 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
     return Batch(x, y, edge_index, n_id, B, **extra)
 
 
-_graphs_of_data: "weakref.WeakKeyDictionary | dict" = {}
+# id(data) -> (weakref to data, Graph); an entry leaves with its data object
+# (the weakref's callback), so the device copies of a freed data object's
+# features and CSR are released with it
+_graphs_of_data: dict = {}
+
+
+def _forget_graph(key, ref) -> None:
+    hit = _graphs_of_data.get(key)
+    if hit is not None and hit[0] is ref:  # (not an entry of a later object with the same id)
+        del _graphs_of_data[key]
 
 
 def _graph_of(data) -> Graph:
     """graph_from_data once per data object (the reference builds a train and
-    a subgraph loader over the same data, pipeline.py:75-92)."""
+    a subgraph loader over the same data, pipeline.py:75-92).  Objects that
+    cannot be weakly referenced are not cached (a strong reference would keep
+    them, and their device graph, alive for the life of the process)."""
     key = id(data)
     hit = _graphs_of_data.get(key)
     if hit is not None and hit[0]() is data:
         return hit[1]
     g = graph_from_data(data)
     try:
-        ref = weakref.ref(data)
+        ref = weakref.ref(data, lambda r, k=key: _forget_graph(k, r))
     except TypeError:
-        ref = (lambda d: (lambda: d))(data)
+        return g
     _graphs_of_data[key] = (ref, g)
     return g
 

@@ -572,13 +572,18 @@ def test_bf16_weights_one_part_image_bitwise(K, Fo, narrow, reduce, xdt):
 @pytest.mark.parametrize("n", [0, 1, 7, 4096 + 3, 3_000_001])
 def test_cast_f32_bf16_equals_torch(n):
     """ngnn_cast_f32_bf16 (a bf16 model's logits) is torch's .to(bfloat16)
-    bit for bit: round to nearest even, inf kept, NaN stays NaN; ragged
-    lengths and a size that takes the 4-deep unrolled loop."""
+    bit for bit: round to nearest even, inf kept, every NaN (either sign, any
+    payload) the canonical 0x7FC0; ragged lengths and a size that takes the
+    4-deep unrolled loop."""
     from ngnn import _lib
     g = torch.Generator().manual_seed(n)
     x = (torch.randn(n, generator=g) * 3).to(DEV)
     if n > 8:
         x[:4] = torch.tensor([float("inf"), -float("inf"), 1.0 + 2**-8, -(1.0 + 3 * 2**-8)])
+        # NaNs: quiet +/-, a signalling payload, one with low payload bits only
+        nan_bits = torch.tensor([0x7FC00000, -0x00400000, 0x7F800001, 0x7FBFFFFF],
+                                dtype=torch.int64).to(torch.int32)
+        x[4:8] = nan_bits.view(torch.float32).to(DEV)
     y = torch.empty(n, dtype=torch.bfloat16, device=DEV)
     _lib.check(_lib.load().ngnn_cast_f32_bf16(_lib.ptr(x), _lib.ptr(y), n,
                                               _lib.stream_handle(DEV)), "cast")

@@ -160,6 +160,47 @@ def test_bucket_view_gradients_adopted():
         torch.testing.assert_close(p.grad, ref[k], rtol=1e-5, atol=1e-6, msg=k)
 
 
+@pytest.mark.parametrize("mode", ["two_forwards", "retain_graph", "accumulate"])
+def test_bucket_views_not_aliased(mode):
+    """Bucket views registered, the gradients must equal the ones computed
+    without the bucket when the views could alias: two forwards (sharing the
+    parameters) before one backward (pipeline_contrast.py:146-154 runs the
+    model on several batches per step), one graph back-propagated twice
+    (retain_graph), and accumulation over two steps without zero_grad."""
+    from ngnn.distributed import GradAllReduce
+    m, batches = _setup(0.0)
+    b0, b1 = batches[0], batches[1]
+
+    def loss_of(b):
+        return F.cross_entropy(m(b.x, b.edge_index)[:b.batch_size], b.y[:b.batch_size])
+
+    def run():
+        m.zero_grad(set_to_none=True)
+        if mode == "two_forwards":
+            (loss_of(b0) + loss_of(b1)).backward()
+        elif mode == "retain_graph":
+            l0 = loss_of(b0)
+            l0.backward(retain_graph=True)
+            l0.backward()
+        else:
+            loss_of(b0).backward()
+            loss_of(b1).backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in m.named_parameters()}
+
+    ref = run()
+    red = GradAllReduce(m.parameters())
+    got = run()
+    for k in ref:
+        # (the input-gradient scatter uses float atomics: order-dependent bits)
+        torch.testing.assert_close(got[k], ref[k], rtol=1e-5, atol=1e-6, msg=k)
+    # the bucket still works for the next plain step
+    got2 = run()
+    for k in ref:
+        torch.testing.assert_close(got2[k], ref[k], rtol=1e-5, atol=1e-6, msg=k)
+    del red
+
+
 @pytest.mark.parametrize("arch", ["sage", "gcn"])
 def test_graph_fused_row_gather_matches_eager(arch):
     """NeighborLoader(gather_features=False) batches carry x = graph.x[n_id]
@@ -289,3 +330,20 @@ def test_slot_load_csr_equals_lower_bound(case):
     assert torch.equal(rowptr.cpu(), want)
     assert torch.equal(col.cpu(), torch.cat([src, pad]).to(torch.int32))
     assert torch.equal(sei.cpu()[e_cap:], dst_p)
+
+
+def test_slot_rejects_unsorted_targets():
+    """The slot load writes the CSR for non-decreasing targets only: edges the
+    sampler did not vouch for are checked, and unsorted ones are refused
+    (instead of a rowptr with rows never written)."""
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    m, batches = _setup(0.0)
+    b = batches[0]
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, fused=True, capturable=True)
+    n_cap, e_cap = slot_size(256, [10, 5])
+    step = GraphedTrainStep(m, opt, 256, n_cap, e_cap, b.x.size(1), DEV)
+    step.load(b.x, b.edge_index, b.y)            # sampler output (hinted): accepted
+    step.load(b.x, b.edge_index.clone(), b.y)    # unhinted but sorted: accepted
+    perm = torch.randperm(b.edge_index.size(1), device=DEV)
+    with pytest.raises(ValueError, match="target-sorted"):
+        step.load(b.x, b.edge_index[:, perm], b.y)

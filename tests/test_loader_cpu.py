@@ -92,3 +92,27 @@ def test_indexed_rows_and_zero_copy_envelope():
     g = ngnn.SimpleGCN(100, 16, 10, 2)  # transform-first layer 0: no zero-copy
     assert not zero_copy_ok(g, 1000, 100)
     assert zero_copy_ok(ngnn.SimpleGCN(100, 256, 10, 2), 1000, 100)
+
+
+def test_graph_cache_releases_freed_data(monkeypatch):
+    """The data -> Graph cache behind NeighborLoader(data, ...) holds its
+    data object weakly: the entry (and the device graph it holds) leaves with
+    the data object; objects that cannot be weakly referenced are not cached."""
+    import gc
+
+    from ngnn import loader
+    built = []
+    monkeypatch.setattr(loader, "graph_from_data", lambda d: built.append(d) or object())
+    d = _data()
+    g1 = loader._graph_of(d)
+    assert loader._graph_of(d) is g1 and len(built) == 1  # one build per data object
+    assert id(d) in loader._graphs_of_data
+    key = id(d)
+    built.clear()
+    del d
+    gc.collect()
+    assert key not in loader._graphs_of_data
+    slots = type("Slots", (), {"__slots__": ("x",)})()  # no __weakref__
+    loader._graph_of(slots)
+    loader._graph_of(slots)
+    assert len(built) == 2 and id(slots) not in loader._graphs_of_data
