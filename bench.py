@@ -179,13 +179,22 @@ def cpu_baseline(batches, args, layers):
                       f"oracle/pyg_ref.py"}
 
 
-def l0_replay_us(gstep, model, aggr: str, reps: int = 20) -> float:
-    """Average duration of the captured step's layer-0 launch under replay
-    conditions: HIP events around ONE graph replay of `reps` back-to-back
-    launches of that kernel on the slot's current batch (the last timed
-    one).  Events cannot be recorded inside the step's own graph on ROCm;
-    the eager pass instead leaves the GPU idle between host-issued launches,
-    so its per-launch time reads ~15 % long against rocprof's replay time."""
+def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
+    """Per-launch duration of the captured step's layer-0 kernel, measured
+    with HIP events on the stream it runs on (events cannot be recorded
+    inside the step's own graph on ROCm).  The launch is captured alone into a
+    graph over the slot; for EVERY timed batch the slot is loaded exactly as
+    the step loads it and that graph replayed between two events:
+
+    * "step"  -- right after the batch's slot load, as inside the step (the
+      batch's rows were sampled before the timed region: not cache-resident);
+    * "cold"  -- the same after writing a flush_mb buffer, so neither the
+      4 MiB L2s nor the 256 MiB MALL hold any of its input;
+    * "warm"  -- an immediate second replay on the same batch (its rows now
+      partly MALL-resident: the round-2 figure's condition).
+
+    Returns {condition: mean us over the batches}; each figure includes the
+    dispatch gap between an event and the kernel (about 1-2 us)."""
     from ngnn import fused
     from ngnn.block import get_block
     blk = get_block(gstep.ei, gstep.n_cap)
@@ -194,25 +203,38 @@ def l0_replay_us(gstep, model, aggr: str, reps: int = 20) -> float:
     x = gstep.x
     agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])
     p = model.dropout if model.training else 0.0
+    w1 = c.lin_l.weight.dtype == torch.bfloat16
 
     def run():
         fused.sage_layer_fwd(x, blk, aggr, wl, bl, wr, relu=True, p_drop=p, seed=0, agg_out=agg,
                              seed_dev=blk.seed_dev, x_dev=blk.x_dev, xrow_dev=blk.xrow_dev,
-                             x_rows=blk.x_rows)
+                             x_rows=blk.x_rows, w_bf16=w1)
     run()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for _ in range(reps):
-            run()
-    g.replay()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    g.replay()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) * 1e3 / reps
+        run()
+    flush = torch.empty(flush_mb << 20, dtype=torch.uint8, device=x.device)
+    res = {"step": [], "cold": [], "warm": []}
+    for b in timed:
+        for cond in ("step", "cold"):  # (step first: the cold run leaves the rows resident)
+            gstep.load(b.x, b.edge_index, b.y, zero_copy=gstep.zero_copy, batch_size=b.batch_size)
+            if cond == "cold":
+                flush.fill_(cond == "cold")
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            evs[0].record()
+            g.replay()
+            evs[1].record()
+            if cond == "step":
+                evs[2].record()
+                g.replay()
+                evs[3].record()
+            (evs[3] if cond == "step" else evs[1]).synchronize()
+            res[cond].append(evs[0].elapsed_time(evs[1]) * 1e3)
+            if cond == "step":
+                res["warm"].append(evs[2].elapsed_time(evs[3]) * 1e3)
+    del flush
+    return {k: sum(v) / len(v) for k, v in res.items() if v}
 
 
 def _allreduce_name(world: int) -> str:
@@ -336,15 +358,17 @@ def main():
     summ = timer.summary()
     dom = max(summ.items(), key=lambda kv: kv[1][1]) if summ else None
     roof = None
-    replay_us = eager_us = None
+    l0 = eager_us = None
     if dom:
         name, (n, ms, nbytes, flops, mfma_s) = dom
         eager_us = 1e3 * ms / n
         if graph and name == "sage_fwd_l0" and args.module == "sage":
-            # the same kernel timed under replay conditions (see l0_replay_us);
-            # algorithmic bytes / flops per launch from the eager records
-            replay_us = l0_replay_us(gstep, model, args.aggr)
-            ms = replay_us * 1e-3 * n
+            # the same kernel on the same timed batches, each right after its
+            # slot load (see l0_launch_us); algorithmic bytes / flops per
+            # launch from the eager records of those batches
+            timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
+            l0 = l0_launch_us(gstep, model, args.aggr, timed)
+            ms = l0["step"] * 1e-3 * n
         t = ms * 1e-3
         gbs = nbytes / t / 1e9
         tfs = flops / t / 1e12
@@ -366,10 +390,17 @@ def main():
             "traffic": traffic, "traffic_src": traffic_src, "launches": n,
             "avg_us": round(1e3 * ms / n, 2),
             "timed_in": "timed region (eager)" if not graph else (
-                "HIP events around a graph replay of 20 back-to-back launches of this kernel "
-                "on the last timed batch, right after the timed region (alg. bytes/flops per "
-                "launch from an eager pass over the timed batches)" if replay_us is not None else
+                "HIP events around a graph replay of this one launch on each timed batch, right "
+                "after that batch's slot load (as in the step), over all timed batches after the "
+                "timed region; alg. bytes/flops per launch from an eager pass over the same "
+                "batches" if l0 is not None else
                 "eager pass over the timed batches, right after the graph replays"),
+            "avg_us_cold": None if l0 is None else round(l0["cold"], 2),
+            "avg_us_warm": None if l0 is None else round(l0["warm"], 2),
+            "cold_warm_note": None if l0 is None else (
+                "avg_us: after the slot load as in the step; cold: after a 512 MiB write "
+                "(L2 and MALL hold none of the input); warm: an immediate second launch on the "
+                "same batch (partly MALL-resident)"),
             "avg_us_eager_pass": None if eager_us is None else round(eager_us, 2),
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),

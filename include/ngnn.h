@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 10
+#define NGNN_ABI_VERSION 11
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -76,6 +76,11 @@ extern "C" {
  * skipped products are exact zeros); weights that are not bf16-exact are
  * rounded to bf16.  MEAN / SUM only (NGNN_E_SHAPE otherwise: call without). */
 #define NGNN_W_BF16 0x800
+/* flag OR-ed into ngnn_sage_fwd_raw's `reduce`: `ws` already holds
+ * ngnn_pack_weight(wl) (a producer packed this step's W_l: the graph slot's
+ * load, ngnn_slot_load's pack job), so a layer whose W_l streams from L2
+ * issues no pack launch of its own; ignored when W_l is staged in LDS. */
+#define NGNN_WL_PREPACKED 0x1000
 
 /* dtypes */
 #define NGNN_F32 0
@@ -426,6 +431,16 @@ size_t ngnn_seed_xent_workspace_bytes(int64_t B);
 int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
                        int64_t ignore_index, float *loss, float *count, void *ws,
                        size_t ws_bytes, void *stream);
+/* Forward and the unit-scale input gradient in ONE launch (the captured
+ * training step's loss.backward(1)): writes *loss, *count and dlogits rows
+ * < B = (softmax(x_r) - onehot(y_r)) / count (zeros for ignored rows); rows >=
+ * B untouched.  The loss sum is the last workgroup's fixed-order sum of the
+ * workgroups' partial sums (device ticket in ws, zero on entry, reset on exit):
+ * deterministic.  ws as ngnn_seed_xent_fwd (zero-filled once).  Replaces
+ * F.cross_entropy(out[:bs], y[:bs]) + its backward (pipeline.py:158,167). */
+int ngnn_seed_xent_fwd_grad(const float *logits, int64_t ld, int64_t B, int64_t C,
+                            const int64_t *y, int64_t ignore_index, float *loss, float *count,
+                            float *dlogits, int64_t ldd, void *ws, size_t ws_bytes, void *stream);
 int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, const int64_t *y,
                        int64_t ignore_index, const void *ws, const float *grad_scale,
                        const float *count, float *dlogits, int64_t ldd, void *stream);
@@ -472,6 +487,11 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * of ngnn_sage_fwd_raw's n_edge_rows_dev.
  * slot_ei may be NULL when the CSR is written (a captured step that reads
  * only the CSR).
+ * pack_dst (nullable): a pack job in the same launch -- pack_dst =
+ * ngnn_pack_weight(pack_w [pack_fo, pack_k], row stride pack_ldw), the
+ * current values of a weight the captured step's forward then reads with
+ * NGNN_WL_PREPACKED (no pack launch inside the step; read at load time, so
+ * parameters changed between steps are picked up).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
@@ -480,7 +500,8 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    int64_t *slot_y, int32_t *n_valid, int32_t *slot_rowptr, int32_t *slot_col,
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
                    int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-                   int32_t *slot_colx, void *stream);
+                   int32_t *slot_colx, const float *pack_w, int64_t pack_ldw, int64_t pack_fo,
+                   int64_t pack_k, float *pack_dst, void *stream);
 
 #ifdef __cplusplus
 }

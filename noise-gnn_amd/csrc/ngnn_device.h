@@ -78,11 +78,15 @@ __device__ __forceinline__ float nanmax(float acc, float v) {
 }
 
 // ---- dropout RNG: counter-based, keyed by (seed, row, col); the keep mask is
-// never stored.  One 32-bit hash per column QUAD (4c .. 4c+3): byte j of it
-// decides column 4c + j; keep <=> byte >= thresh, thresh = ceil(p * 256)
-// (p resolved to 1/256: exact for 0, 0.25, 0.5, 0.75, 1; the drop rate is
-// p_eff = thresh / 256 and survivors scale by 1 / (1 - p_eff), so E[out] =
-// in exactly).  Host replica: tests/test_gpu_fused.py::dropout_keep.
+// never stored.  p is resolved to thresh / 256, thresh = ceil(p * 256) (exact
+// for 0, 0.25, 0.5, 0.75, 1); survivors scale by 1 / (1 - thresh / 256), so
+// E[out] = in exactly.
+//  * byte mode (thresh != 128): one 32-bit hash per column QUAD (4c .. 4c+3),
+//    byte j of it decides column 4c + j: keep <=> byte >= thresh;
+//  * bit mode (thresh == 128, p = 0.5 -- every config's dropout): one BIT per
+//    element, column c of a row is bit c & 31 of the hash of word c >> 5,
+//    keep <=> bit set (a hash per 32 columns instead of per 4).
+// Host replica: tests/test_gpu_fused.py::dropout_keep.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352dU;
@@ -106,8 +110,23 @@ struct Dropout {
     __device__ __forceinline__ bool keep_byte(uint32_t h, uint32_t col) const {
         return ((h >> (8 * (col & 3u))) & 0xffu) >= thresh;
     }
+    __device__ __forceinline__ bool bit_mode() const { return thresh == 128u; }
+    // bit mode: the hash word of column col and its bit
+    __device__ __forceinline__ static uint32_t bit_word(uint32_t col) { return col >> 5; }
+    __device__ __forceinline__ static uint32_t bit_index(uint32_t col) { return col & 31u; }
     __device__ __forceinline__ bool keep(uint32_t rkey, uint32_t col) const {
+        if (bit_mode()) return (lowbias32(rkey + bit_word(col)) >> bit_index(col)) & 1u;
         return keep_byte(quad_hash(rkey, col), col);
+    }
+    // the four keep decisions of column quad c4 (columns 4 c4 .. 4 c4 + 3), bit j
+    __device__ __forceinline__ uint32_t keep4(uint32_t rkey, uint32_t c4) const {
+        if (bit_mode())
+            return (lowbias32(rkey + bit_word(4u * c4)) >> bit_index(4u * c4)) & 0xfu;
+        const uint32_t h = lowbias32(rkey + c4);
+        uint32_t k = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k |= (((h >> (8 * j)) & 0xffu) >= thresh ? 1u : 0u) << j;
+        return k;
     }
     __device__ __forceinline__ void reseed(uint64_t d) {
         s0 ^= static_cast<uint32_t>(d);
@@ -155,6 +174,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      float *z = nullptr, int64_t ldz = 0, const int64_t *xrow = nullptr,
                      const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
                      const int32_t *col_x = nullptr, bool x_bf16 = false,
-                     bool w_bf16 = false);
+                     bool w_bf16 = false, bool wl_prepacked = false);
 
 }  // namespace ngnn

@@ -114,6 +114,79 @@ __global__ __launch_bounds__(256) void k_xent_bwd(const float *__restrict__ x, i
     }
 }
 
+// forward AND the unit-scale gradient in ONE launch (the training step's
+// loss.backward(1) needs nothing else): every workgroup counts the valid
+// labels of y[0..B) itself (B int64 reads from L2: no count pass), each wave
+// takes one row -- its loss and its gradient row (softmax - onehot) / count
+// (zeros for an ignored row) -- the workgroup adds its rows' losses in wave
+// order, and the LAST workgroup to finish (a device ticket) adds the
+// workgroup sums in a fixed order: loss = sum / count, deterministic.
+// ws: partial sums [gridDim.x] floats; ticket (uint32, zero between calls).
+__global__ __launch_bounds__(256) void k_xent_fused(const float *__restrict__ x, int64_t ld, int B,
+                                                    int C, const int64_t *__restrict__ y,
+                                                    int64_t ignore, float *__restrict__ part,
+                                                    uint32_t *__restrict__ ticket,
+                                                    float *__restrict__ loss,
+                                                    float *__restrict__ count,
+                                                    float *__restrict__ dx, int64_t ldd) {
+    __shared__ float s_red[256];
+    __shared__ float s_row[4];
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float nv = 0.0f;
+    for (int i = threadIdx.x; i < B; i += 256) nv += (y[i] != ignore) ? 1.0f : 0.0f;
+    s_red[threadIdx.x] = nv;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) s_red[threadIdx.x] += s_red[threadIdx.x + h];
+        __syncthreads();
+    }
+    const float cnt = s_red[0];
+    const int r = blockIdx.x * 4 + wv;
+    float l = 0.0f;
+    if (r < B) {
+        const float *xr = x + static_cast<int64_t>(r) * ld;
+        float *dr = dx + static_cast<int64_t>(r) * ldd;
+        const int64_t t = y[r];
+        if (t == ignore) {
+            for (int c = lane; c < C; c += 64) dr[c] = 0.0f;
+        } else {
+            const float lse = row_lse(xr, C, lane);
+            l = (t >= 0 && t < C) ? lse - xr[t] : NAN;  // out-of-range label: NaN, no OOB read
+            for (int c = lane; c < C; c += 64)
+                dr[c] = (expf(xr[c] - lse) - (c == t ? 1.0f : 0.0f)) / cnt;
+        }
+    }
+    if (lane == 0) s_row[wv] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // hand-off without fences (MI355X_MICROARCH.md, inter-workgroup
+        // visibility): the partial goes out as an agent-scope (sc1,
+        // write-through) store, drained before the ticket; the last workgroup
+        // reads every partial with agent-scope (sc1) loads.  (An agent fence
+        // pair -- L2 write-back + invalidate -- cost ~10 us here.)
+        __hip_atomic_store(part + blockIdx.x, ((s_row[0] + s_row[1]) + s_row[2]) + s_row[3],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    float s = 0.0f;
+    for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += 256)
+        s += __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) s_red[threadIdx.x] += s_red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *loss = s_red[0] / cnt;  // 0/0 = NaN when every row is ignored, as torch
+        *count = cnt;
+        *ticket = 0u;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Co-teaching loss (CTLoss.forward, losses.py:19-49) on the device.  The
@@ -278,6 +351,24 @@ extern "C" int ngnn_seed_xent_fwd(const float *logits, int64_t ld, int64_t B, in
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(k_xent_sum, dim3(1), dim3(256), 0, as_stream(stream), w, (int)B, loss, count);
+    return launch_status();
+}
+
+extern "C" int ngnn_seed_xent_fwd_grad(const float *logits, int64_t ld, int64_t B, int64_t C,
+                                       const int64_t *y, int64_t ignore_index, float *loss,
+                                       float *count, float *dlogits, int64_t ldd, void *ws,
+                                       size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(!logits || !y || !loss || !count || !dlogits || !ws || B <= 0 || C <= 0,
+                   NGNN_E_ARG);
+    NGNN_RETURN_IF(ld < C || ldd < C, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(!fits_i32(B) || !fits_i32(C), NGNN_E_RANGE);
+    NGNN_RETURN_IF(ws_bytes < ngnn_seed_xent_workspace_bytes(B) || !aligned(ws, 16), NGNN_E_WORKSPACE);
+    float *w = static_cast<float *>(ws);
+    // the ticket sits past the row-loss area of ngnn_seed_xent_fwd (3 B floats)
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(w + 3 * B);
+    hipLaunchKernelGGL(k_xent_fused, dim3(static_cast<unsigned>(ceil_div(B, 4))), dim3(256), 0,
+                       as_stream(stream), logits, ld, (int)B, (int)C, y, ignore_index, w, ticket,
+                       loss, count, dlogits, ldd);
     return launch_status();
 }
 

@@ -55,6 +55,20 @@
 #ifndef NGNN_RT_STATIC
 #define NGNN_RT_STATIC 0  // (A/B build flag) 1: fixed tile-per-wave schedule
 #endif
+// (diagnostic builds only, never shipped: 1 drops the layer's output stores /
+// its root-term MFMAs / its x loads, to time the rest of the kernel)
+#ifndef NGNN_RT_DBG_NOSTORE
+#define NGNN_RT_DBG_NOSTORE 0
+#endif
+#ifndef NGNN_RT_DBG_NOMFMA
+#define NGNN_RT_DBG_NOMFMA 0
+#endif
+#ifndef NGNN_RT_DBG_NOLOAD
+#define NGNN_RT_DBG_NOLOAD 0
+#endif
+#ifndef NGNN_RT_FAST_BUILD
+#define NGNN_RT_FAST_BUILD 0  // (development builds) 1: the fp32 MEAN kernels only
+#endif
 
 namespace ngnn {
 
@@ -69,15 +83,20 @@ constexpr int X3_TAIL_MAX = 3;  // fp32 tail steps (K % 32 <= 12); more: a padde
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// v = p1 + p2 + p3 in bf16 (round to nearest even); an infinite v gives
-// (v, 0, 0) instead of the NaN residual inf - inf, a NaN gives NaNs
+// v = p1 + p2 + p3 in bf16 (round to nearest even).  GUARD: an infinite v
+// gives (v, 0, 0) instead of the NaN residual inf - inf (the weight images,
+// split once per launch); the per-tile split of x runs unguarded -- two VALU
+// per element less on the kernel's issue-bound path -- so an infinite input
+// element yields NaN where fp32 arithmetic gives +-inf or NaN.  A NaN gives
+// NaNs either way.
+template <bool GUARD = true>
 __device__ __forceinline__ void split3(v4f a, v4f b, bf16x8 &p1, bf16x8 &p2, bf16x8 &p3) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float v = j < 4 ? a[j] : b[j - 4];
         const __bf16 h = static_cast<__bf16>(v);
         const float fh = static_cast<float>(h);
-        const float r = (fh == v) ? 0.0f : v - fh;
+        const float r = (GUARD && fh == v) ? 0.0f : v - fh;
         const __bf16 m = static_cast<__bf16>(r);
         const float r2 = r - static_cast<float>(m);
         p1[j] = h;
@@ -141,6 +160,33 @@ struct RtArgs {
 // a compare (no SGPR lane-mask pairs to keep live across the tile loop).
 // Operands stay far from overflow (|a - b| < 2^31).
 __device__ __forceinline__ int lt_mask(int a, int b) { return (a - b) >> 31; }
+
+// rowptr[16 t + rl] and rowptr[16 t + rl + 1] of tile t (uniform) by scalar
+// loads: one s_load_dwordx16 + one s_load_dword for a tile inside the rows,
+// clamped single loads for the last one; lane rl then selects its pair.
+__device__ __forceinline__ void tile_bounds(const int32_t *rowptr, int t, int n_rows, int rl,
+                                            int &beg, int &end) {
+    typedef const __attribute__((address_space(4))) int32_t *cp;
+    const int r0 = t * 16;
+    int v[17];
+    if (r0 + 16 <= n_rows) {
+        const cp p = (cp)(rowptr + r0);
+#pragma unroll
+        for (int j = 0; j < 17; ++j) v[j] = p[j];
+    } else {
+        const cp p = (cp)(rowptr);
+#pragma unroll
+        for (int j = 0; j < 17; ++j) v[j] = p[min(r0 + j, n_rows)];
+    }
+    int b = v[0], e = v[1];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+        b = rl == j ? v[j] : b;
+        e = rl == j ? v[j + 1] : e;
+    }
+    beg = b;
+    end = e;
+}
 
 __device__ __forceinline__ v4f and_mask(v4f v, int m) {
     v4f o;
@@ -266,7 +312,7 @@ __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[R
                         hi[i] = __int_as_float(__float_as_int(hi[i]) & lt_mask(4 + i, kq));
                     }
                 }
-                split3(lo, hi, x1, x2, x3);
+                split3<false>(lo, hi, x1, x2, x3);
             }
             const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
             bf16x8 wb[2];
@@ -324,7 +370,7 @@ __device__ __forceinline__ void mfma_group_x3(v4f (&acc)[NTW], const v4f (&xf)[R
                 }
             }
             bf16x8 x1, x2, x3;
-            split3(lo, hi, x1, x2, x3);
+            split3<false>(lo, hi, x1, x2, x3);
             const bf16x8 *w = sw3 + (cc0 + c) * NTW * 64 + lane;
             // W parts of tile m + 1 are read from LDS while tile m's six
             // MFMAs run (double-buffered): the reads' latency stays off the
@@ -562,24 +608,51 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
     }
 }
 
+// keep mask of bit `b` of a hash word: 0 or all ones (v_bfe_i32 through asm:
+// written as shifts the compiler turns the AND with it into a compare +
+// select per element)
+template <int B>
+__device__ __forceinline__ int bit_mask(uint32_t w) {
+    int k;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(w), "n"(B));
+    return k;
+}
+// (b a constant after unrolling: the switch folds to one case)
+__device__ __forceinline__ int bit_mask_at(uint32_t w, int b) {
+    switch (b) {
+        case 0: return bit_mask<0>(w);
+        case 1: return bit_mask<1>(w);
+        case 2: return bit_mask<2>(w);
+        default: return bit_mask<3>(w);
+    }
+}
+
 // epilogue: lane holds output features m*16 + 4q .. +3 of row r.  Stores go
 // through a buffer resource (rows past n_rows are dropped by the range);
 // `vec` (uniform): F_out a multiple of 16 with 16-B aligned rows -- one
-// 16-B store per m-tile, no per-lane predicates.  Branch-free: ReLU and the
-// dropout keep fold into one select per element (a keep test compiled as a
-// branch costs an exec save/restore per element), and the lane's four
+// 16-B store per m-tile, no per-lane predicates.  Branch-free.
+// DM (dropout mode, ngnn_device.h): 0 none; 1 byte mode -- the lane's four
 // columns f .. f+3 (f = col_base + 16 m + 4 q, col_base a multiple of 16) are
-// exactly one dropout quad: hash pb + 4 m, pb = row_key + (col_base + 4 q)/4.
-template <int NTW, bool DROP, bool RELU, bool VEC>
+// one hash quad, pb + 4 m; 2 bit mode (p = 0.5) -- column c is bit c & 31 of
+// hash word c >> 5, so two consecutive 16-column tiles share one word and the
+// lane's four bits of tile m sit at 16 (gc & 1) + 4 q (gc = the global
+// 16-column tile): one shift per tile, then four immediate bit fields.  In
+// bit mode sbias holds 2 b: the survivor scale 2 is folded into the bias
+// add, fma(acc, 2, 2 b) == 2 (acc + b) bitwise, and ReLU is an INTEGER max
+// with 0 (a pre-activation with the sign bit set -- negative, -0.0 or a
+// negative-signed NaN -- gives +0.0; a positive NaN passes), then one AND
+// with the keep mask: ~4 VALU per element instead of ~9.
+template <int NTW, int DM, bool RELU, bool VEC>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
                                          i32x4 zr, const float *sbias, int r, int rl, int q) {
     // orsrc / zr: the tile's output / z rows (rl = row in the tile); r, the
     // global row, keys the dropout hash
     const uint32_t thresh = a.epi.drop.thresh;
     const float scale = a.epi.drop.scale;
-    const uint32_t pb = DROP ? a.epi.drop.row_key(static_cast<uint32_t>(r)) +
-                                   static_cast<uint32_t>((a.epi.col_base + 4 * q) >> 2)
-                             : 0u;
+    const uint32_t rk = DM ? a.epi.drop.row_key(static_cast<uint32_t>(r)) : 0u;
+    const uint32_t pb = DM == 1 ? rk + static_cast<uint32_t>((a.epi.col_base + 4 * q) >> 2) : 0u;
+    const int cb16 = a.epi.col_base >> 4;  // global 16-column tile of m = 0 (uniform)
+    uint32_t hw = 0;                       // bit mode: the current hash word
     const int obase = rl * static_cast<int>(a.ldo) * 4;
     // re-materialised per call: the per-tile-index tests below must not be
     // hoisted out of the tile loop as SGPR lane masks (they spill)
@@ -595,16 +668,29 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
         }
         const int f = m * 16 + 4 * q;
         const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
-        const uint32_t h = DROP ? lowbias32(pb + 4u * m) : 0u;
+        const int gc = cb16 + m;  // global 16-column tile (uniform)
+        uint32_t hs = 0;          // bit mode: this lane's four bits of tile m in bits 0..3
+        if (DM == 2) {
+            if (m == 0 || (gc & 1) == 0) hw = lowbias32(rk + static_cast<uint32_t>(gc >> 1));
+            hs = hw >> (((gc & 1) << 4) + 4 * q);
+        }
+        const uint32_t h = DM == 1 ? lowbias32(pb + 4u * m) : 0u;
         v4f v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float y = acc[m][j] + b[j];
-            // y < 0 (ReLU; NaN passes, like torch.relu) or a dropped column -> 0
-            bool zero = RELU && y < 0.0f;
-            if (DROP) zero = zero || ((h >> (8 * j)) & 0xffu) < thresh;
-            v[j] = zero ? 0.0f : (DROP ? y * scale : y);
+            if (DM == 2) {
+                int yi = __float_as_int(__builtin_fmaf(acc[m][j], 2.0f, b[j]));
+                if (RELU) yi = max(yi, 0);
+                v[j] = __int_as_float(yi & bit_mask_at(hs, j));
+            } else {
+                const float y = acc[m][j] + b[j];
+                // y < 0 (ReLU; NaN passes, like torch.relu) or a dropped column -> 0
+                bool zero = RELU && y < 0.0f;
+                if (DM == 1) zero = zero || ((h >> (8 * j)) & 0xffu) < thresh;
+                v[j] = zero ? 0.0f : (DM == 1 ? y * scale : y);
+            }
         }
+        if (NGNN_RT_DBG_NOSTORE && v[0] != 1234.5f) continue;
         if (VEC) {
             buf_store4(v, orsrc, obase + 4 * f, 0, 0);
         } else {
@@ -740,8 +826,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         }
         if (WL_LDS && !have_l)
             for (int i = threadIdx.x; i < nfr; i += RT_WAVES * 64) swl[i] = z;
+        // (bit-mode dropout folds its survivor scale 2 into the bias add: 2 b)
+        const float bsc = a.epi.drop.thresh == 128u ? 2.0f : 1.0f;
         for (int i = threadIdx.x; i < NTW * 16; i += RT_WAVES * 64)
-            sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] : 0.0f;
+            sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] * bsc : 0.0f;
     }
     __syncthreads();
 
@@ -789,7 +877,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
 #pragma unroll
     for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{0.f, 0.f, 0.f, 0.f};
     float xtn[X3_TAIL_MAX] = {0.f, 0.f, 0.f};
-    int nbeg = 0, nend = 0;
+    int nbeg = 0, nend = 0, nmask = 0;
     if (a.seed_dev) a.epi.drop.reseed(*a.seed_dev);
     // x: the address given at launch, or (graph replay of a changing batch)
     // the one the slot load stored, ranged by the device row count
@@ -801,10 +889,21 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     const i32x4 xr = make_rsrc(xbase, static_cast<uint32_t>(((xrows - 1) * a.ldx + a.K) * EB * (xrows > 0)));
     const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * EB;
     // byte offset of logical row rr in x (kOOB past the block's rows)
+    // The two forms stay separate branches (the empty asm pins each result
+    // inside its branch): with one multiply after the join, the wait for
+    // the n_id load sat at the join and every tile paid a vmcnt(0) -- a drain
+    // of the previous tile's output stores -- even without the fused gather.
     auto row_off = [&](int rr) -> uint32_t {
         if (rr >= n_rows) return static_cast<uint32_t>(kOOB);
-        const int pr = xrow ? static_cast<int>(gload(xrow, rr)) : rr;
-        return static_cast<uint32_t>(pr) * ld4;
+        uint32_t o;
+        if (xrow) {
+            o = static_cast<uint32_t>(gload(xrow, rr)) * ld4;
+            asm volatile("; row_off n_id" : "+v"(o));
+        } else {
+            o = static_cast<uint32_t>(rr) * ld4;
+            asm volatile("; row_off rows" : "+v"(o));
+        }
+        return o;
     };
     uint32_t roff_n = 0;   // the next tile's row offset (its rows are in flight)
     uint32_t roff_nn = 0;  // the claimed tile's row offset, computed when claimed: under the
@@ -827,20 +926,38 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         const int tl = tn < n_tiles ? tn : 0;
         const int rn = tl * RT_ROWS + rl;
         roff_n = roff_tn;
-        load_x<X3, XB>(xn, xr, roff_n, 0, q);
-        if (X3) load_xt<XB>(xtn, a, xr, roff_n, q);
+        if (NGNN_RT_DBG_NOLOAD) {
+#pragma unroll
+            for (int g = 0; g < RT_KC; ++g) xn[g] = v4f{float(tn), float(g), float(rl), 1.f};
+        } else {
+            load_x<X3, XB>(xn, xr, roff_n, 0, q);
+            if (X3) load_xt<XB>(xtn, a, xr, roff_n, q);
+        }
         if (have_l) {
-            const int mr = lt_mask(rn, n_rows);
-            const int rr = rn & mr;
-            nbeg = a.rowptr[rr];
-            nend = a.rowptr[rr + 1];
-            nend = nbeg + ((nend - nbeg) & mr);  // rows past the end: degree 0
+            // the tile's 17 row bounds by SCALAR loads (the tile index is
+            // uniform): they count on lgkmcnt, so using them never waits for
+            // vector memory -- a per-lane vector load here made the next use
+            // wait vmcnt(0), draining the x fragments just issued and the
+            // previous tile's output stores
+            nmask = lt_mask(rn, n_rows);  // rows past the end: degree 0 (at use)
+            tile_bounds(a.rowptr, tl, n_rows, rl, nbeg, nend);
         }
     };
     {
         int lane0, q0, rl0;
         lane_ids(lane0, q0, rl0);
         prefetch(t, row_off(t * RT_ROWS + rl0));
+        // Settle the first tile's loads HERE, once per wave.  The compiler's
+        // wait for a loop-carried load takes the fewest younger memory ops
+        // over the paths into the loop: left pending on this entry path (no
+        // stores behind it), every tile's first use of its prefetched x
+        // waited for the previous tile's output stores too -- a full store
+        // drain per tile.
+#pragma unroll
+        for (int g = 0; g < RT_KC; ++g) asm volatile("" : "+v"(xn[g]));
+#pragma unroll
+        for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) asm volatile("" : "+v"(xtn[s2]));
+        asm volatile("" : "+v"(nbeg), "+v"(nend));
     }
     for (; t < n_tiles; t = tnext, ++kt) {
 #if NGNN_RT_STATIC
@@ -856,7 +973,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         // X3: columns of the padded last chunk this lane may keep (8 q .. 8 q + 7)
         const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
         const int r = t * RT_ROWS + rl;
-        const int beg = nbeg, deg = nend - nbeg;
+        const int beg = nbeg, deg = (nend - nbeg) & nmask;
         const int maxdeg = have_l ? rowgroup_max16(deg) : 0;
         v4f acc[NTW];
 #pragma unroll
@@ -894,7 +1011,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             } else if (maxdeg == 0) {
                 prefetch(tnext, roff_nn);  // next tile: a whole tile of MFMAs to land
             }
-            if (X3) {
+            if (NGNN_RT_DBG_NOMFMA) {
+#pragma unroll
+                for (int m = 0; m < NTW; ++m) acc[m] += xc[m % RT_KC];
+            } else if (X3) {
                 const int ncc = min(4, a.C - 4 * c);
                 mfma_group_x3<NTW, XB, W1>(acc, xc, sw3, pst, 4 * c, ncc, a.kpad && c == nchunk - 1, kq8, lane);
             } else {
@@ -940,15 +1060,20 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         // ---- epilogue (bias, relu, dropout and the stores)
         const i32x4 orsrc = tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
         const i32x4 zr = a.z ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
-        if (a.epi.drop.thresh) {
+        if (a.epi.drop.thresh == 128u) {  // bit mode (sbias holds 2 b)
             if (a.epi.relu)
-                epilogue<NTW, true, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+                epilogue<NTW, 2, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
             else
-                epilogue<NTW, true, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+                epilogue<NTW, 2, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+        } else if (a.epi.drop.thresh) {
+            if (a.epi.relu)
+                epilogue<NTW, 1, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+            else
+                epilogue<NTW, 1, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         } else if (a.epi.relu) {
-            epilogue<NTW, false, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+            epilogue<NTW, 0, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         } else {
-            epilogue<NTW, false, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+            epilogue<NTW, 0, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
         }
     }
 }
@@ -999,6 +1124,11 @@ int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, 
         };
         using T = std::true_type;
         using F = std::false_type;
+#if NGNN_RT_FAST_BUILD
+        // (kernel-development builds: the fp32 split-bf16 kernels only -- every
+        // other layer form returns NGNN_E_SHAPE; minutes less to compile)
+        return vec ? go(T{}, T{}, F{}, F{}) : go(T{}, F{}, F{}, F{});
+#else
         // one-part images (bf16-exact weights): MEAN / SUM only (the caller checks)
         if constexpr (RED != NGNN_REDUCE_MAX) {
             if (a.w1) {
@@ -1009,10 +1139,15 @@ int dispatch_rt(const RtArgs &a, int reduce, bool wl_lds, bool x3, int n_tiles, 
         if (a.x_bf16) return vec ? go(T{}, T{}, T{}, F{}) : go(T{}, F{}, T{}, F{});  // (x3 checked by the caller)
         if (x3) return vec ? go(T{}, T{}, F{}, F{}) : go(T{}, F{}, F{}, F{});
         return vec ? go(F{}, T{}, F{}, F{}) : go(F{}, F{}, F{}, F{});
+#endif
     };
+#if NGNN_RT_FAST_BUILD
+    return by_red(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
+#else
     if (reduce == NGNN_REDUCE_MEAN) return by_red(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
     if (reduce == NGNN_REDUCE_SUM) return by_red(std::integral_constant<int, NGNN_REDUCE_SUM>{});
     return by_red(std::integral_constant<int, NGNN_REDUCE_MAX>{});
+#endif
 }
 
 // ---- narrow-mode neighbour term: out[d, :Fo] += reduce_{e into d} z[col[e], :Fo]
@@ -1095,14 +1230,14 @@ __global__ __launch_bounds__(256) void k_gcn_agg(const float *__restrict__ z, in
                 for (int u = 0; u < NA_UNR; ++u)
                     if (e + u < end) acc += v[u];
             }
-            const uint32_t h = epi.drop.thresh ? lowbias32(rk + static_cast<uint32_t>(c4)) : 0u;
+            const uint32_t k4 = epi.drop.thresh ? epi.drop.keep4(rk, static_cast<uint32_t>(c4)) : 0xfu;
             v4f o;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int c = 4 * c4 + j;
                 float y = acc[j] + ((bias && c < Fo) ? bias[c] : 0.0f);
                 bool zero = epi.relu && y < 0.0f;  // NaN passes, like torch.relu
-                if (epi.drop.thresh) zero = zero || ((h >> (8 * j)) & 0xffu) < epi.drop.thresh;
+                if (epi.drop.thresh) zero = zero || !((k4 >> j) & 1u);
                 o[j] = zero ? 0.0f : (epi.drop.thresh ? y * epi.drop.scale : y);
             }
             float *op = out + static_cast<int64_t>(d) * ldo + 4 * c4;
@@ -1135,7 +1270,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      int *rc, int64_t ldw, void *wl_ws, size_t wl_ws_bytes,
                      const float *const *x_dev, bool exact, float *z, int64_t ldz,
                      const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
-                     const int32_t *col_x, bool x_bf16, bool w_bf16) {
+                     const int32_t *col_x, bool x_bf16, bool w_bf16, bool wl_prepacked) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -1171,6 +1306,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     if (no_root) C = T4 = kpad = 0;
     // bf16-exact weights (NGNN_W_BF16): a one-part image (MEAN / SUM kernels)
     const bool w1 = w_bf16 && x3 && !no_root && reduce != NGNN_REDUCE_MAX;
+    // (development builds hold the fp32 split-bf16 MEAN kernels only)
+    if (NGNN_RT_FAST_BUILD && (!x3 || x_bf16 || w1 || reduce != NGNN_REDUCE_MEAN)) return 0;
     const size_t frag_kb = static_cast<size_t>(KG) * 64 * sizeof(v4f);  // one fp32 m-tile, all of K
     // one m-tile of the root image: X3 3 parts (1 with w1) x C chunks x 1 KiB + the tail
     const size_t root_kb = x3 ? (static_cast<size_t>((w1 ? 1 : 3) * C) * 64 * 16 +
@@ -1229,8 +1366,10 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                     *rc = NGNN_E_WORKSPACE;
                     return 1;
                 }
-                const int prc = ngnn_pack_weight(static_cast<const float *>(wl_packed), ldw, Fo, K,
-                                                 wl_ws, st);
+                // (NGNN_WL_PREPACKED: the producer packed this step's W_l there)
+                const int prc = wl_prepacked ? 0
+                                             : ngnn_pack_weight(static_cast<const float *>(wl_packed),
+                                                                ldw, Fo, K, wl_ws, st);
                 if (prc) {
                     *rc = prc;
                     return 1;
@@ -1302,7 +1441,9 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     const bool want_narrow = (reduce & NGNN_FWD_NARROW) != 0;
     const bool x_bf16 = (reduce & NGNN_X_BF16) != 0;
     const bool w_bf16 = (reduce & NGNN_W_BF16) != 0;
-    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW | NGNN_X_BF16 | NGNN_W_BF16);
+    const bool wl_prepacked = (reduce & NGNN_WL_PREPACKED) != 0;
+    reduce &= ~(NGNN_MATH_EXACT_F32 | NGNN_FWD_NARROW | NGNN_X_BF16 | NGNN_W_BF16 |
+                NGNN_WL_PREPACKED);
     // bf16 rows: the split-bf16 root term and the fused path only
     if (x_bf16 && (exact || want_narrow)) return NGNN_E_SHAPE;
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
@@ -1329,7 +1470,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
                              nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x, false,
-                             w_bf16)) {
+                             w_bf16, false)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -1348,7 +1489,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
                           ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16,
-                          w_bf16))
+                          w_bf16, wl_prepacked))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

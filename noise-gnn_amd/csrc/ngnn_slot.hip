@@ -8,6 +8,9 @@
 //                       padding row gets more than ceil(n_pad / (n_cap - N))
 //   labels [0, B)       copied
 //   *n_valid = N        (the forward kernels skip rows >= N)
+//   optional: a pack job -- one weight matrix (the layer-0 W_l) written in
+//   ngnn_pack_weight's fragment order, so the captured step's forward reads
+//   it prepacked (NGNN_WL_PREPACKED) instead of issuing a pack launch;
 //   optional: the target-grouped CSR of the padded edges (rowptr int32
 //   [n_cap + 1] by lower bound over the non-decreasing targets, col int32
 //   [e_cap]), so the captured step needs no CSR-build launches; and the
@@ -27,7 +30,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
     int32_t *__restrict__ n_valid, int32_t *__restrict__ rowptr, int32_t *__restrict__ col,
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
     uint32_t gen, int32_t *__restrict__ n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-    int32_t *__restrict__ colx, int vec) {
+    int32_t *__restrict__ colx, int vec, const float *__restrict__ pk_w, int64_t pk_ldw, int pk_fo,
+    int pk_k, float *__restrict__ pk_dst) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
@@ -123,6 +127,20 @@ __global__ __launch_bounds__(256) void k_slot_load(
         if (m && (threadIdx.x & 63) == 0)
             atomicMax(reinterpret_cast<unsigned long long *>(r_next), static_cast<unsigned long long>(m));
     }
+    if (pk_dst) {
+        // pack job: pk_dst = ngnn_pack_weight(pk_w) -- the layout
+        // [NT][KG][64 lanes][4]: lane l, element i of fragment (m, kg) holds
+        // W[16 m + (l & 15)][16 kg + 4 (l >> 4) + i], zero outside Fo x K
+        const int KG = (pk_k + 15) >> 4, NT = (pk_fo + 15) >> 4;
+        const int64_t total = static_cast<int64_t>(NT) * KG * 256;
+        for (int64_t i = tid; i < total; i += nthr) {
+            const int64_t f = i >> 8;
+            const int l = static_cast<int>((i >> 2) & 63), j = static_cast<int>(i & 3);
+            const int m = static_cast<int>(f / KG), kg = static_cast<int>(f - static_cast<int64_t>(m) * KG);
+            const int n = 16 * m + (l & 15), k = 16 * kg + 4 * (l >> 4) + j;
+            pk_dst[i] = (n < pk_fo && k < pk_k) ? pk_w[static_cast<int64_t>(n) * pk_ldw + k] : 0.0f;
+        }
+    }
     if (tid == 0) {
         *n_valid = static_cast<int32_t>(N);
         if (n_edge_rows)  // rows past the last target have no in-edges
@@ -148,7 +166,8 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int32_t *slot_rowptr, int32_t *slot_col, uint64_t *seed_state,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
                               int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
-                              int32_t *slot_colx, void *stream) {
+                              int32_t *slot_colx, const float *pack_w, int64_t pack_ldw,
+                              int64_t pack_fo, int64_t pack_k, float *pack_dst, void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
@@ -162,11 +181,15 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     NGNN_RETURN_IF((slot_rowptr == nullptr) != (slot_col == nullptr), NGNN_E_ARG);
     const int vec = (F % 4 == 0) && (ldx % 4 == 0) && (ld_slot % 4 == 0) && aligned(x, 16) &&
                     aligned(slot_x, 16);
-    const int64_t work = std::max<int64_t>({x_dev ? 0 : N * F / 4, e_cap, n_cap + 1, B, 1});
+    NGNN_RETURN_IF(pack_dst && (!pack_w || pack_fo <= 0 || pack_k <= 0 || pack_ldw < pack_k ||
+                                !fits_i32(pack_fo) || !fits_i32(pack_k)), NGNN_E_ARG);
+    const int64_t pack_n = pack_dst ? ceil_div(pack_fo, 16) * ceil_div(pack_k, 16) * 256 : 0;
+    const int64_t work = std::max<int64_t>({x_dev ? 0 : N * F / 4, e_cap, n_cap + 1, B, pack_n, 1});
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, 256), 4096));
     hipLaunchKernelGGL(k_slot_load, dim3(grid), dim3(256), 0, as_stream(stream), x, ldx, N, F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
                        n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
-                       xrow, xrow_dev, slot_colx, vec);
+                       xrow, xrow_dev, slot_colx, vec, pack_w, pack_ldw, static_cast<int>(pack_fo),
+                       static_cast<int>(pack_k), pack_dst);
     return launch_status();
 }

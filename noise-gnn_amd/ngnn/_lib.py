@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -24,6 +24,7 @@ MATH_EXACT_F32 = 0x100  # OR-ed into ngnn_sage_fwd_raw's reduce (include/ngnn.h)
 FWD_NARROW = 0x200      # same: output layer aggregated in the F_out-wide space
 X_BF16 = 0x400          # same: x rows are bf16 (read as bf16, widened exactly)
 W_BF16 = 0x800          # same: weights are bf16-exact (one split part)
+WL_PREPACKED = 0x1000   # same: ws already holds ngnn_pack_weight(wl)
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one
@@ -50,6 +51,8 @@ SIGNATURES = {
     "ngnn_seed_xent_workspace_bytes": (_sz, [_i64]),
     "ngnn_seed_xent_fwd": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _sz, _p]),
     "ngnn_seed_xent_bwd": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _i64, _p]),
+    "ngnn_seed_xent_fwd_grad": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _p, _sz,
+                                       _p]),
     "ngnn_ct_loss_workspace_bytes": (_sz, [_i64]),
     "ngnn_ct_loss_fwd": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _i64, _p,
                                 _p, _p, _p, _sz, _p, _p]),
@@ -58,7 +61,7 @@ SIGNATURES = {
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                               _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p, _p,
-                              _p, _p]),
+                              _p, _p, _i64, _i64, _i64, _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),

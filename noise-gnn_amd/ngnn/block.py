@@ -114,6 +114,8 @@ class Block:
         self.xrow_dev = None
         self.x_rows = 0
         self.col_x = None  # int32 col mapped through n_id (the slot load writes it)
+        # (W_l parameter, ngnn_pack_weight(W_l) kept current by a producer) or None
+        self.wl_prepacked = None
 
     @property
     def rowptr(self):
@@ -161,6 +163,7 @@ class _BlockCache:
             blk.n_edge_rows_dev = hint[8]
             if hint[9] is not None:
                 blk.xrow_dev, blk.x_rows, blk.col_x = hint[9]
+            blk.wl_prepacked = hint[10]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -187,7 +190,8 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
                     n_active: int | None = None, n_rows_dev: torch.Tensor | None = None,
                     csr: CSR | None = None, seed_dev: torch.Tensor | None = None,
                     x_dev: torch.Tensor | None = None, r_next=None,
-                    n_edge_rows_dev: torch.Tensor | None = None, xrow=None) -> None:
+                    n_edge_rows_dev: torch.Tensor | None = None, xrow=None,
+                    wl_prepacked=None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
     later rows have none) -- only used for roofline accounting.  n_rows_dev:
     device int32 scalar bounding the real rows of a padded slot.  csr: a
@@ -199,11 +203,14 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     n_edge_rows_dev: device int32 holding n_active for a changing batch.
     xrow: (device word, table rows, col_x): the producer stores the address of
     the batch's n_id in the word when x_dev points at the whole feature table
-    (fused x[n_id] gather), 0 otherwise, and keeps col_x = n_id[col] (int32)."""
+    (fused x[n_id] gather), 0 otherwise, and keeps col_x = n_id[col] (int32).
+    wl_prepacked: (W_l parameter, buffer) -- the producer keeps the buffer =
+    ngnn_pack_weight(W_l) current (the slot load's pack job)."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
-                                  n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev, xrow)
+                                  n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev, xrow,
+                                  wl_prepacked)
 
 
 def _drop_hint(key):
@@ -216,7 +223,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11]
+    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

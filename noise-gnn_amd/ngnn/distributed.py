@@ -107,26 +107,39 @@ class GradAllReduce:
 
     def pack(self):
         """grads -> bucket (stream-ordered copies, none for gradients that are
-        already bucket views; capturable in a HIP graph)."""
+        already bucket views; capturable in a HIP graph).  Gradients that are
+        not views -- a bf16 model's (autograd narrows the fused backward's
+        fp32 gradients to the parameters' dtype), or accumulated ones -- move
+        in ONE multi-tensor copy (torch._foreach_copy_, widening bf16 exactly)
+        instead of a launch per tensor."""
+        dst, src = [], []
         for p, v in zip(self.params, self.views):
             if p.grad is None:
                 v.zero_()
             elif not self._aliased(p, v):
-                v.copy_(p.grad)
+                dst.append(v)
+                src.append(p.grad)
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def allreduce(self):
         """The one collective: SUM over ranks (RCCL over xGMI with nccl)."""
         dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=self.group)
 
     def unpack(self):
-        """bucket / world -> grads (capturable)."""
+        """bucket / world -> grads (capturable; one multi-tensor copy back,
+        rounding to bf16 where the parameter is bf16)."""
         world = dist.get_world_size(self.group)
         self.bucket.div_(world)
+        dst, src = [], []
         for p, v in zip(self.params, self.views):
             if p.grad is None:
                 p.grad = v if p.dtype == v.dtype else v.to(p.dtype)
             elif not self._aliased(p, v):
-                p.grad.copy_(v)
+                dst.append(p.grad)
+                src.append(v)
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def __call__(self):
         if not self.active():

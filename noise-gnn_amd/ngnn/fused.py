@@ -158,7 +158,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
                    seed_dev: torch.Tensor | None = None,
                    x_dev: torch.Tensor | None = None, span: str = "sage_fwd",
                    narrow: bool = False, xrow_dev: torch.Tensor | None = None,
-                   x_rows: int = 0, w_bf16: bool = False) -> torch.Tensor:
+                   x_rows: int = 0, w_bf16: bool = False,
+                   wl_packed: torch.Tensor | None = None) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
     supplies the shape.  xrow_dev (with x_dev): device word holding the
@@ -168,7 +169,8 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     wide) instead of x (K wide) -- the output layer's form (no agg_out then).
     w_bf16: the weights hold bf16-exact values (a bf16 model's parameters,
     widened): NGNN_W_BF16, a one-part split image (same sums, fewer MFMAs and
-    wider column slices)."""
+    wider column slices).  wl_packed: ngnn_pack_weight(wl) kept current by a
+    producer (NGNN_WL_PREPACKED: no pack launch when W_l streams from L2)."""
     N, K = x.shape
     Fo = wl.shape[0]
     if x.dtype == torch.bfloat16 and not bf16_rows_ok(x, narrow):
@@ -216,6 +218,10 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
+    prepacked = 0
+    if (wl_packed is not None and not narrow and xk is x and wl_.data_ptr() == wl.data_ptr()
+            and wl_packed.numel() * 4 >= lib.ngnn_pack_weight_bytes(Fo, K)):
+        ws, prepacked = wl_packed, _lib.WL_PREPACKED
     with _timing.span(span, nbytes, flops, mfma_s) as rec:
         # raw weights straight into the row-tile kernel; packed fallback otherwise
         # rows >= n_active have no in-edges (a sampler-built block): dense kernel
@@ -227,12 +233,12 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
             _lib.ptr(block.col_x) if xrow_dev is not None else None,
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0)
-            | (_lib.X_BF16 if xb else 0) | (_lib.W_BF16 if w1 else 0),
+            | (_lib.X_BF16 if xb else 0) | (_lib.W_BF16 if w1 else 0) | prepacked,
             _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out),
             agg_out.stride(0) if agg_out is not None else xk.size(1),
-            _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
+            _lib.ptr(ws), ws.numel() * ws.element_size(), _lib.stream_handle(x.device))
         if rc == _lib.E_SHAPE and xb and x_dev is None:
             # bf16 rows outside the bf16 envelope: the fp32 path on widened rows
             return sage_layer_fwd(x.float(), block, reduce, wl, bl, wr, relu, p_drop, seed,
@@ -337,6 +343,18 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
     return out
 
 
+def const_bounds(dev, L: int, R: int) -> torch.Tensor:
+    """The stack backward's read-only row-bound array (L + 1 words = R), cached
+    per (device, L, R).  A graph producer creates it BEFORE capture (else the
+    first captured backward records its fill as a node of every replay)."""
+    key = (dev, "bnd", L, int(R))
+    bnd = _ws.get(key)
+    if bnd is None:
+        bnd = torch.full((L + 1,), int(R), dtype=torch.int32, device=dev)
+        _ws[key] = bnd
+    return bnd
+
+
 def _dgrad_fused_ok(Fo: int, K: int) -> bool:
     """ngnn_sage_dgrad_fused (per target row, VALU products, W_r and W_l in
     LDS) only while both weights fit its LDS: a wave re-reads the whole of W
@@ -359,6 +377,10 @@ class _SAGEStack(torch.autograd.Function):
             relu, p_i, seed_i = not last, (0.0 if last else p_drop), seed + 7919 * i
             x_dev = block.x_dev if i == 0 else None
             xrow = dict(xrow_dev=block.xrow_dev, x_rows=block.x_rows) if i == 0 else {}
+            pk = block.wl_prepacked
+            if (pk is not None and i == 0 and wr is not None
+                    and pk[0].data_ptr() == wl.data_ptr() and pk[0].shape == wl.shape):
+                xrow["wl_packed"] = pk[1]
             if wr is None and h.size(1) > wl.shape[0]:
                 # GCN layer narrowing its input: transform first (PyG's order),
                 # no saved aggregate (rebuilt for the rows backward needs)
@@ -416,11 +438,7 @@ class _SAGEStack(torch.autograd.Function):
             bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
                              dtype=torch.int32, device=dev)
         else:  # read-only: a cached constant (no fill launch per step)
-            key = (dev, "bnd", L, int(rows_hint))
-            bnd = _ws.get(key)
-            if bnd is None:
-                bnd = torch.full((L + 1,), int(rows_hint), dtype=torch.int32, device=dev)
-                _ws[key] = bnd
+            bnd = const_bounds(dev, L, int(rows_hint))
         bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
         if pre_top:
             bp[L - 1] = block.r_next[0].data_ptr()
@@ -567,6 +585,34 @@ def sage_stack_supported(model, x) -> bool:
     return True
 
 
+class _ConvCall:
+    """A single conv run as a one-layer stack: no dropout (the reference
+    wrapper applies relu / F.dropout itself, sage.py:35-38)."""
+    dropout = 0.0
+    training = False
+
+
+def conv_supported(conv, x) -> bool:
+    return (x.is_cuda and x.dtype in _IO_DTYPES and x.dim() == 2
+            and all(p.dtype in _IO_DTYPES for p in conv.parameters()))
+
+
+def sage_conv(conv, x, block: Block) -> torch.Tensor:
+    """SAGEConv.forward (PyG 2.5.1 semantics, sage.py:34) as a one-layer fused
+    stack: forward on the row-tile kernel (aggregate saved), backward =
+    weight gradient + input gradient kernels; the input gradient covers every
+    row (the wrapper's relu / dropout backward reads all of it)."""
+    aggr = "sum" if conv.aggr == "add" else conv.aggr
+    params = [conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight]
+    return _run_stack(_ConvCall, x, block, 0, None, params, aggr, keep_bf16_x=True)
+
+
+def gcn_conv(conv, x, block: Block) -> torch.Tensor:
+    """GCNConv(normalize=False).forward (convolution.py:31) as a one-layer
+    fused GCN stack (W_r = 0, sum aggregation)."""
+    return _run_stack(_ConvCall, x, block, 0, None, [conv.lin.weight, conv.bias, None], "sum")
+
+
 def zero_copy_ok(model, n_rows: int, in_dim: int, table_rows: int = 0) -> bool:
     """Can a HIP-graph slot hand this model's layer 0 the batch's feature rows
     in place (ngnn_sage_fwd_raw's x_dev)?  Only the fused SAGE stack reads
@@ -574,6 +620,11 @@ def zero_copy_ok(model, n_rows: int, in_dim: int, table_rows: int = 0) -> bool:
     buffer offsets over the slot's rows (x, the output, the saved aggregate).
     table_rows > 0: the rows are gathered from a feature table of that many
     rows (fused x[n_id]; the weight gradient then needs it under 2 GiB)."""
+    # only this package's fused stacks read the slot's x through x_dev; any
+    # other model (e.g. a reference wrapper around ngnn convs) reads the slot
+    from .models import SAGE, SimpleGCN
+    if not isinstance(model, (SAGE, SimpleGCN)):
+        return False
     if not isinstance(getattr(model, "convs", None), torch.nn.ModuleList):
         return False
     if getattr(model, "use_bn", False):

@@ -82,6 +82,9 @@ class GraphedTrainStep:
         self._split_reduce = False
         self._one = None
         self.zero_copy = True
+        # (layer-0 W_l, its packed image): the slot load packs the weight's
+        # current values, the captured forward reads them prepacked
+        self._pack = None
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -149,6 +152,10 @@ class GraphedTrainStep:
             _lib.ptr(self.x_dev) if zero_copy else None, _lib.ptr(self.r_next), self._next_gen(),
             _lib.ptr(self.n_edge_rows), _lib.ptr(xrow), _lib.ptr(xrow_word),
             _lib.ptr(self.col_x) if xrow_word is not None else None,
+            # pack job: layer 0's W_l in fragment order for the captured forward
+            *((_lib.ptr(self._pack[0]), self._pack[0].stride(0), self._pack[0].shape[0],
+               self._pack[0].shape[1], _lib.ptr(self._pack[1])) if self._pack is not None
+              else (None, 0, 0, 0, None)),
             _lib.stream_handle(self.x.device)), "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
 
@@ -163,9 +170,11 @@ class GraphedTrainStep:
         out = self.model(self.x, self.ei)
         self.out = out  # the captured step's logits (static: rewritten by every replay)
         loss = self.loss_fn(out, self.y, self.B)
-        # a persistent d(loss) = 1 instead of backward()'s ones_like fill launch
+        # a persistent d(loss) = 1 instead of backward()'s ones_like fill
+        # launch; marked, so the loss backward needs no scale launch either
         if self._one is None or self._one.shape != loss.shape:
-            self._one = torch.ones_like(loss)
+            from .losses import unit_grad
+            self._one = unit_grad(loss)
         loss.backward(self._one)
         return loss
 
@@ -214,12 +223,21 @@ class GraphedTrainStep:
         self.x_rows = table_rows if self.zero_copy else 0
         if self.x_rows:
             self.col_x = torch.zeros(self.e_cap, dtype=torch.int32, device=self.x.device)
+        self._pack = _prepack_target(self.model)
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
                         x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B),
                         n_edge_rows_dev=self.n_edge_rows,
-                        xrow=(self.xrow_dev, self.x_rows, self.col_x) if self.x_rows else None)
+                        xrow=(self.xrow_dev, self.x_rows, self.col_x) if self.x_rows else None,
+                        wl_prepacked=self._pack)
+        if self._pack is not None:  # the capture's own forward reads it: pack it now
+            self.load(x, edge_index, y)
         self.opt.zero_grad(set_to_none=True)
+        # the backward's constant row-bound array: created now, not inside the capture
+        convs = getattr(self.model, "convs", None)
+        if convs is not None:
+            from .fused import const_bounds
+            const_bounds(self.x.device, len(convs), self.B)
         # data parallel: the bucket pack is the tail of the first graph and the
         # unpack (/ world) the head of the second, so between the replays the
         # host issues only the one all-reduce
@@ -264,6 +282,20 @@ class GraphedTrainStep:
             self.reducer()
         self.g_opt.replay()
         return self.loss
+
+
+def _prepack_target(model):
+    """(W_l, packed buffer) of layer 0 when the model is a fused SAGE stack
+    with fp32 weights (a bf16 model's weights are widened copies: no stable
+    address), else None."""
+    from .fused import pack_weight
+    from .models import SAGE
+    if not isinstance(model, SAGE) or getattr(model, "use_bn", False):
+        return None
+    w = model.convs[0].lin_l.weight
+    if w.dtype != torch.float32 or not w.is_cuda or w.stride(1) != 1:
+        return None
+    return (w, torch.zeros_like(pack_weight(w.detach())))
 
 
 def slot_size(batch_size: int, fanouts, margin_rows: int = 1024):

@@ -2,14 +2,20 @@
 
 ``seed_cross_entropy(out, y, batch_size)`` == ``F.cross_entropy(out[:batch_size],
 y[:batch_size])`` -- the loss of the reference's training loop
-(pipeline.py:158) -- in two launches (forward, backward) instead of the
-softmax / nll / slice-backward / fill chain.  The input gradient is a
-view of a cached buffer whose rows >= batch_size are zero and stay zero (only
-rows < batch_size are ever written), and it tells the SAGE stack's backward
-how many leading rows can be nonzero (``_ngnn_nonzero_rows``), so that
-backward skips its row-extent scan.
+(pipeline.py:158) -- instead of the softmax / nll / slice-backward / fill
+chain.  When the logits need a gradient, ONE launch
+(``ngnn_seed_xent_fwd_grad``) writes the loss and the unit-scale gradient;
+the backward then costs nothing when its incoming gradient is the training
+step's persistent unit tensor (``unit_grad``, marked ``_ngnn_unit``) and one
+launch otherwise.  The input gradient is a view of a zero-initialised
+buffer whose rows >= batch_size stay zero (only rows < batch_size are ever
+written), and it tells the SAGE stack's backward how many leading rows can
+be nonzero (``_ngnn_nonzero_rows``), so that backward skips its row-extent
+scan.
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 
@@ -17,6 +23,46 @@ from . import _lib
 
 _zero_rows: dict = {}
 _ws: dict = {}
+_free_grads: dict = {}  # (dev, C, B) -> zero-row gradient buffers not held by a pending node
+
+
+def unit_grad(loss: torch.Tensor) -> torch.Tensor:
+    """A ones tensor shaped like `loss` that the loss backward recognises as 1
+    (no scale launch): for a training step's loss.backward(unit_grad(loss)),
+    kept by the caller and never modified."""
+    one = torch.ones_like(loss)
+    one._ngnn_unit = True
+    return one
+
+
+def _take_grad_buffer(dev, n: int, c: int, b: int) -> torch.Tensor:
+    """A zero-row [>= n, c] gradient buffer for ONE pending loss node: two
+    forwards before one backward (several losses per step) get different
+    buffers.  Returned to the pool by the node's backward (or when its graph
+    is freed without one)."""
+    key = (dev, c, b)
+    pool = _free_grads.setdefault(key, [])
+    while pool:
+        buf = pool.pop()
+        if buf.size(0) >= n:
+            return buf
+    return torch.zeros(max(n, 1), c, dtype=torch.float32, device=dev)
+
+
+def _give_back(key, buf) -> None:
+    _free_grads.setdefault(key, []).append(buf)
+
+
+class _GradHold:
+    """Owns a taken gradient buffer until backward hands it back (weakref
+    finalizer: also when the autograd graph is dropped unused)."""
+
+    def __init__(self, key, buf):
+        self.buf = buf
+        self._fin = weakref.finalize(self, _give_back, key, buf)
+
+    def release(self):
+        self._fin()
 
 
 def _workspace(dev, B: int) -> torch.Tensor:
@@ -53,11 +99,24 @@ class _SeedXent(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=x.device)
         count = torch.empty((), dtype=torch.float32, device=x.device)
         ws = _workspace(x.device, B)
-        _lib.check(_lib.load().ngnn_seed_xent_fwd(
-            _lib.ptr(x), x.stride(0), B, x.size(1), _lib.ptr(yy), int(ignore_index),
-            _lib.ptr(loss), _lib.ptr(count), _lib.ptr(ws), ws.numel(),
-            _lib.stream_handle(x.device)), "ngnn_seed_xent_fwd")
-        ctx.ws = ws  # holds the row log-sum-exps for the backward (same stream)
+        lib = _lib.load()
+        ctx.hold = None
+        if ctx.needs_input_grad[0]:
+            # loss + the unit-scale gradient in one launch
+            key = (x.device, x.size(1), B)
+            hold = _GradHold(key, _take_grad_buffer(x.device, logits.size(0), x.size(1), B))
+            dx = hold.buf
+            _lib.check(lib.ngnn_seed_xent_fwd_grad(
+                _lib.ptr(x), x.stride(0), B, x.size(1), _lib.ptr(yy), int(ignore_index),
+                _lib.ptr(loss), _lib.ptr(count), _lib.ptr(dx), dx.stride(0), _lib.ptr(ws),
+                ws.numel(), _lib.stream_handle(x.device)), "ngnn_seed_xent_fwd_grad")
+            ctx.hold = hold
+        else:
+            _lib.check(lib.ngnn_seed_xent_fwd(
+                _lib.ptr(x), x.stride(0), B, x.size(1), _lib.ptr(yy), int(ignore_index),
+                _lib.ptr(loss), _lib.ptr(count), _lib.ptr(ws), ws.numel(),
+                _lib.stream_handle(x.device)), "ngnn_seed_xent_fwd")
+        ctx.ws = ws
         ctx.save_for_backward(x, yy, count)
         ctx.B, ctx.ignore, ctx.n = B, int(ignore_index), logits.size(0)
         return loss
@@ -65,8 +124,20 @@ class _SeedXent(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, yy, count = ctx.saved_tensors
+        hold = ctx.hold
+        if hold is not None:
+            # the gradient rows the forward wrote (unit scale); the buffer goes
+            # back to the pool -- stream order protects it until its consumer
+            # (this backward pass) has read it
+            dx = hold.buf[:ctx.n]
+            ctx.hold = None
+            hold.release()
+            if getattr(g, "_ngnn_unit", False):
+                dx._ngnn_nonzero_rows = ctx.B  # rows >= B are zero: the SAGE backward's row bound
+                return dx, None, None, None
+        else:
+            dx = _grad_buffer(x.device, ctx.n, x.size(1), ctx.B)
         g = g.contiguous()
-        dx = _grad_buffer(x.device, ctx.n, x.size(1), ctx.B)
         _lib.check(_lib.load().ngnn_seed_xent_bwd(
             _lib.ptr(x), x.stride(0), ctx.B, x.size(1), _lib.ptr(yy), ctx.ignore, _lib.ptr(ctx.ws),
             _lib.ptr(g), _lib.ptr(count), _lib.ptr(dx), dx.stride(0), _lib.stream_handle(x.device)),

@@ -10,7 +10,10 @@ imports (``sage.py:4``, ``convolution.py:4``):
   out = sum_{j->i} (x W^T)_j + bias                  (convolution.py:19-23, :31)
 
 ``forward`` also accepts a prebuilt :class:`ngnn.block.Block` in place of
-``edge_index`` (the model wrappers build one per mini-batch).
+``edge_index`` (the model wrappers build one per mini-batch).  On the GPU
+(float32 / bfloat16) each conv is ONE autograd node over the hand-written
+kernels (ngnn.fused: a one-layer fused stack), so a reference wrapper that
+imports these classes instead of PyG's trains without library GEMMs.
 """
 from __future__ import annotations
 
@@ -78,21 +81,23 @@ class SAGEConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         block = get_block(edge_index, x.size(0))
-        if x.dtype == torch.bfloat16 or self.lin_l.weight.dtype == torch.bfloat16:
-            # bf16 storage, fp32 arithmetic (the kernels are fp32)
-            out = (F.linear(segment_aggregate(x.float(), block, self.aggr), self.lin_l.weight.float(),
-                            self.lin_l.bias.float())
-                   + F.linear(x.float(), self.lin_r.weight.float()))
-            return out.to(x.dtype)
+        from . import fused
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p.requires_grad for p in self.parameters()))
-        if not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2:
+        if (not needs_grad and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+                and self.lin_l.weight.dtype == torch.float32):
             # inference (e.g. SAGE.inference, sage.py:52): one fused launch
-            from .fused import sage_layer_fwd
             aggr = "sum" if self.aggr == "add" else self.aggr
             xc = x if x.stride(1) == 1 else x.contiguous()
-            return sage_layer_fwd(xc, block, aggr, self.lin_l.weight, self.lin_l.bias,
-                                  self.lin_r.weight, relu=False, p_drop=0.0, seed=0)
+            return fused.sage_layer_fwd(xc, block, aggr, self.lin_l.weight, self.lin_l.bias,
+                                        self.lin_r.weight, relu=False, p_drop=0.0, seed=0)
+        if fused.conv_supported(self, x):
+            # the per-conv drop-in (INTEGRATION.md option A: the reference's own
+            # wrapper, sage.py:33-39, with this class in place of PyG's): one
+            # autograd node on the hand-written kernels -- fused gather +
+            # split-bf16 MFMA forward, MFMA weight gradient, narrow-space input
+            # gradient -- no library GEMM; relu / dropout stay the wrapper's
+            return fused.sage_conv(self, x, block)
         out = self.lin_l(segment_aggregate(x, block, self.aggr))
         return out + self.lin_r(x)
 
@@ -118,10 +123,11 @@ class GCNConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index) -> torch.Tensor:
         block = get_block(edge_index, x.size(0))
-        if x.dtype == torch.bfloat16 or self.lin.weight.dtype == torch.bfloat16:
-            # bf16 storage, fp32 arithmetic (the kernels are fp32)
-            h = F.linear(x.float(), self.lin.weight.float())
-            return (segment_aggregate(h, block, "sum") + self.bias.float()).to(x.dtype)
+        from . import fused
+        if fused.conv_supported(self, x):
+            # per-conv drop-in (convolution.py:29-35 with this class in place of
+            # PyG's): one autograd node on the hand-written kernels
+            return fused.gcn_conv(self, x, block)
         h = self.lin(x)
         return segment_aggregate(h, block, "sum") + self.bias
 

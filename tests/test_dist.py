@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, dtype="f32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     try:
@@ -41,21 +41,31 @@ def _worker(rank, world, port, q):
         # gradient all-reduce == mean of per-rank gradients
         torch.manual_seed(0)
         model = pyg_ref.SAGE(6, 8, 3, 2, dropout=0.0)
+        if dtype == "bf16":  # BASELINE config #3's model dtype
+            model = model.to(torch.bfloat16)
+        elif dtype == "mixed":  # bf16 and fp32 parameters in one bucket
+            model.convs[0].to(torch.bfloat16)
         g = torch.Generator().manual_seed(100)
         data = [(torch.randn(20, 6, generator=g), torch.randint(0, 20, (2, 60), generator=g),
                  torch.randint(0, 3, (20,), generator=g)) for _ in range(world)]
         local_grads = []
+        def fwd(x, ei):
+            if dtype == "f32":
+                return model(x, ei)
+            h = model.convs[0](x.to(model.convs[0].lin_l.weight.dtype), ei).relu()
+            return model.convs[1](h.to(model.convs[1].lin_l.weight.dtype), ei).float()
         for (x, ei, y) in data:
             model.zero_grad()
-            torch.nn.functional.cross_entropy(model(x, ei)[:5], y[:5]).backward()
+            torch.nn.functional.cross_entropy(fwd(x, ei)[:5], y[:5]).backward()
             local_grads.append([p.grad.clone() for p in model.parameters()])
-        want = [sum(gs) / world for gs in zip(*local_grads)]
+        # the bucket's arithmetic: widen, sum in fp32, / world, round to the parameter dtype
+        want = [(sum(g.float() for g in gs) / world).to(gs[0].dtype) for gs in zip(*local_grads)]
         model.zero_grad()
         x, ei, y = data[rank]
-        torch.nn.functional.cross_entropy(model(x, ei)[:5], y[:5]).backward()
+        torch.nn.functional.cross_entropy(fwd(x, ei)[:5], y[:5]).backward()
         GradAllReduce(model.parameters())()
-        ok_grad = all(torch.allclose(p.grad, w_, atol=1e-6) for p, w_ in
-                      zip(model.parameters(), want))
+        ok_grad = all(p.grad.dtype == w_.dtype and torch.allclose(p.grad.float(), w_.float(), atol=1e-6)
+                      for p, w_ in zip(model.parameters(), want))
         q.put((rank, ok_shard, ok_grad, mine.numel()))
         dist.barrier()
         dist.destroy_process_group()
@@ -64,11 +74,15 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(120)
-def test_gloo_world2_sharding_and_grad_allreduce():
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "mixed"])
+def test_gloo_world2_sharding_and_grad_allreduce(dtype):
+    """f32, a bf16 model (BASELINE config #3 under data parallelism) and a
+    mixed one: the bf16 gradients go through the fp32 bucket (one
+    multi-tensor copy each way) and come back rounded to bf16."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, dtype)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in procs]

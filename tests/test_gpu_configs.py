@@ -1,21 +1,25 @@
-"""Parity at the exact BASELINE.json configurations.
+"""Parity at the exact BASELINE.json configurations, through what bench.py
+times.
 
-Each test runs the product path at the config's real model dimensions and
-fanout on a full-size synthetic graph (datasets are not downloadable; the
-graphs have the published node / edge / feature / class counts) and checks it
-against the CPU oracle (oracle/pyg_ref.py: the PyG 2.5.1 op sequence):
+Each test runs the benched step -- ngnn.graphs.GraphedTrainStep: slot load,
+one captured forward (fused layer kernels, hash dropout), seed-row cross
+entropy, bounded backward, Adam -- in TRAIN mode at the config's real model
+dimensions and fanout on a full-size synthetic graph (datasets are not
+downloadable; the graphs have the published node / edge / feature / class
+counts), and checks it against the CPU oracle (oracle/pyg_ref.py: the PyG
+2.5.1 op sequence) with the replay's dropout masks rebuilt on the host:
 
-* the headline path itself -- GraphedTrainStep (zero-copy slot, captured
-  forward + bounded backward + Adam, hash dropout) -- on a full
-  ogbn-products [15,10] bs 1024 block: logits, every gradient and the
-  post-step parameters;
-* ogbn-arxiv SAGE(128,256,40) [15,10] bs 1024, train mode;
-* Amazon-Computers SAGE(767,512,10) max [10,5], 300 seeds (K % 4 != 0);
-* ogbn-products SAGE(100,256,256,47) bf16 [20,15,10] bs 1024 in the graph
-  slot (slot rows x 256 fp32 > 2 GiB: the 64-row kernel and the slot copy),
-  bf16 against the fp32 oracle at the SURVEY 8(c) bf16 tolerance, on the
-  seed rows and a row sample through the oracle's receptive field;
-* a CitationFull-Cora-width layer stack SAGE(8710,512,70).
+* the headline: ogbn-products SAGE(100,256,47) [15,10] bs 1024 (zero-copy
+  slot): logits, loss, every gradient, post-step parameters;
+* config #2, ogbn-arxiv SAGE(128,256,40) [15,10] bs 1024: the same;
+* config #3, ogbn-products SAGE(100,256,256,47) bf16 [20,15,10] bs 1024:
+  seed-row logits, loss and every gradient through the seeds' receptive
+  field, a row sample's logits, post-step parameters -- bf16 against the
+  fp32 oracle at the SURVEY 8(c) bf16 tolerance 2e-2;
+* config #5, Amazon-Computers SAGE(767,512,10) max [10,5], 300 seeds
+  (K % 4 != 0: the slot copies the rows): logits, then the backward layer
+  by layer on the step's own per-layer tensors (near-tied maxima);
+* config #1's widths, a CitationFull-Cora SAGE(8710,512,70) [10,5] bs 512.
 
 Tolerances as tests/test_gpu_fused.py: outputs 1e-5, input gradients
 rtol 1e-4 / atol 1e-5, weight gradients 1e-4; bf16 2e-2.
@@ -117,56 +121,127 @@ def test_headline_graph_step_full_products_block():
         assert (p - init[k]).abs().max() <= 1e-3 + 1e-6, k
 
 
+def _graph_step(model, b, warm, fanout, bs, in_dim, lr=1e-3):
+    """The benched step: GraphedTrainStep (slot load + one captured forward,
+    seed-row cross entropy, bounded backward, Adam) on block b after a
+    capture (warm-up state restored) on block `warm`.  Returns the step, its
+    loss and the slot's dropout seed of that replay."""
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.optim import Adam
+    opt = Adam(model.parameters(), lr=lr)
+    n_cap, e_cap = slot_size(bs, fanout)
+    step = GraphedTrainStep(model, opt, bs, n_cap, e_cap, in_dim, DEV)
+    step.capture(warm.x, warm.edge_index, warm.y)
+    loss = step(b.x, b.edge_index, b.y)
+    torch.cuda.synchronize()
+    return step, loss, int(step.seed_state.item()) & (2**64 - 1)
+
+
+def _slot_masks(seed_state, N, hidden, p, L):
+    """The dropout keep masks of a graph replay (layer i keyed by the slot
+    seed: (7919 i) ^ seed_state)."""
+    return [dropout_keep((7919 * i) ^ seed_state, N, hidden, p).float() for i in range(L - 1)]
+
+
+def _check_adam_step(mine, ref, init, lr=1e-3, bf16=False):
+    """Post-step parameters against torch's Adam on the oracle's gradients.
+    At step 1 the update is lr * g / (|g| + eps): compared where |g| is well
+    away from 0 (elsewhere a tiny gradient difference may flip a 1e-3 step);
+    bf16 parameters within one bf16 rounding of the oracle's update."""
+    o_ref = torch.optim.Adam(ref.parameters(), lr=lr)
+    o_ref.step()
+    for k, q in ref.named_parameters():
+        p = dict(mine.named_parameters())[k].detach().float().cpu()
+        sure = q.grad.abs() > (1e-3 if bf16 else 1e-4) * max(1.0, float(q.grad.abs().max()))
+        want = q.detach()
+        if bf16:
+            want = want.to(torch.bfloat16).float()
+            tol = want.abs() * 2.0**-7 + 1e-6
+            assert ((p - want).abs() <= tol)[sure].all(), k
+        else:
+            torch.testing.assert_close(p[sure], want[sure], rtol=0, atol=2e-6, msg=k)
+        # |step| <= lr (plus, for bf16, the rounding of the new value)
+        bound = lr + 1e-6 + (torch.maximum(init[k].abs(), p.abs()) * 2.0**-7 if bf16 else 0.0)
+        assert ((p - init[k]).abs() <= bound).all(), k
+
+
 @pytest.mark.timeout(300)
-def test_config_arxiv_15_10_bs1024():
+def test_config_arxiv_graph_step():
+    """BASELINE config #2: ogbn-arxiv SAGE(128,256,40), [15,10] bs 1024, fp32,
+    through the benched graph step in train mode (dropout 0.5): logits of
+    every row, loss, every gradient and the post-step parameters."""
     from ngnn.loader import sample_block
     g = _graph("ogbn-arxiv")
     b = sample_block(g, g.train_idx[:1024], [15, 10], seed=3)
+    warm = sample_block(g, g.train_idx[1024:2048], [15, 10], seed=4)
     torch.manual_seed(1)
-    mine = ngnn.SAGE(128, 256, 40, 2, dropout=0.5).to(DEV)
-    _eager_vs_oracle(b, mine, 256, train=True, aggr="mean", check_dx=True)
+    mine = ngnn.SAGE(128, 256, 40, 2, dropout=0.5).to(DEV).train()
+    init = {k: v.detach().cpu().clone() for k, v in mine.state_dict().items()}
+    step, loss, seed_state = _graph_step(mine, b, warm, [15, 10], 1024, 128)
+    assert step.zero_copy
+    N = b.num_nodes
+    out = step.out[:N].cpu()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
+    ref = _MaskedSAGE(128, 256, 40, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 256, 0.5, 2))
+    ref.load_state_dict(init)
+    out_r = ref(b.x.cpu(), b.edge_index.cpu())
+    loss_r = F.cross_entropy(out_r[:1024], b.y[:1024].cpu())
+    loss_r.backward()
+    torch.testing.assert_close(out, out_r.detach(), **OUT)
+    assert abs(float(loss) - float(loss_r)) < 1e-5
+    for k, q in ref.named_parameters():
+        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+    _check_adam_step(mine, ref, init)
 
 
 @pytest.mark.timeout(300)
-def test_config_computers_max_10_5():
-    """K = 767 (not a multiple of 4), max aggregator, the config's full batch.
+def test_config_computers_max_graph_step():
+    """BASELINE config #5: Amazon-Computers SAGE(767,512,10) max, [10,5], the
+    config's full batch of 300 seeds, through the benched graph step in
+    train mode (K = 767: not a multiple of 4, so the slot copies the rows).
 
-    Forward end to end at 1e-5.  The max gradient goes to the argmax
+    Logits of every row at 1e-5.  The max gradient goes to the argmax
     neighbour, and fp32 rounding differences between the GPU's and the CPU's
-    layer-0 outputs (~1e-6) flip near-tied maxima (~1e6 (row, feature) pairs
-    here), so the backward is pinned LAYER BY LAYER on identical inputs: the
-    oracle's layer-1 backward runs on the GPU's layer-1 input, the oracle's
-    layer-0 backward on the GPU's layer-0 output gradient."""
+    layer-0 outputs (~1e-6) flip near-tied maxima, so the backward is pinned
+    LAYER BY LAYER on identical inputs: the captured step's own per-layer
+    tensors (the debug hook's clones, recorded into the graph and rewritten
+    by every replay) feed the oracle's layer backward.  Post-step parameters
+    against torch's Adam on the GPU gradients' oracle counterparts."""
     from ngnn import fused
     from ngnn.loader import sample_block
     g = _graph("computers")
     b = sample_block(g, g.train_idx, [10, 5], seed=5)
+    warm = sample_block(g, g.train_idx, [10, 5], seed=6)
     assert b.batch_size == 300
     torch.manual_seed(2)
     mine = ngnn.SAGE(767, 512, 10, 2, dropout=0.5, aggr="max").to(DEV).train()
-    torch.manual_seed(99)
-    s = int(torch.randint(0, 2**62, (1,)).item())
-    torch.manual_seed(99)
+    init = {k: v.detach().cpu().clone() for k, v in mine.state_dict().items()}
     fused._debug_grads = []
     try:
-        out = mine(b.x, b.edge_index)
-        F.cross_entropy(out[:300], b.y[:300]).backward()
-        dbg = {i: (dy.cpu(), hin.cpu()) for i, dy, _, hin in fused._debug_grads}
+        step, loss, seed_state = _graph_step(mine, b, warm, [10, 5], 300, 767)
+        captured = fused._debug_grads[-2:]  # the captured backward's entries (layers 1, 0)
+        dbg = {i: (dy.cpu(), hin.cpu()) for i, dy, _, hin in captured}
     finally:
         fused._debug_grads = None
+    assert sorted(dbg) == [0, 1]
     N = b.num_nodes
-    mask = dropout_keep(s, N, 512, 0.5).float()
+    out = step.out[:N].cpu()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
+    mask = _slot_masks(seed_state, N, 512, 0.5, 2)[0]
     ref = _MaskedSAGE(767, 512, 10, 2, dropout=0.5, aggr="max", masks=[mask])
-    ref.load_state_dict({k: v.cpu() for k, v in mine.state_dict().items()})
+    ref.load_state_dict(init)
     x, ei, y = b.x.cpu(), b.edge_index.cpu(), b.y[:300].cpu()
     with torch.no_grad():
-        torch.testing.assert_close(out.cpu(), ref(x, ei), **OUT)
-    grads = {k: p.grad.cpu() for k, p in mine.named_parameters()}
+        out_r = ref(x, ei)
+    torch.testing.assert_close(out, out_r, **OUT)
+    assert abs(float(loss) - float(F.cross_entropy(out_r[:300], y))) < 1e-5
+    # the layer-1 input the step saw is the oracle's layer-0 output (1e-5)
+    with torch.no_grad():
+        h0 = ref.convs[0](x, ei).relu() * mask * dropout_scale(0.5)
+    torch.testing.assert_close(dbg[1][1][:N], h0, **OUT)
     # layer 1 on the GPU's layer-1 input
-    h1 = dbg[1][1].clone().requires_grad_(True)
+    h1 = dbg[1][1][:N].clone().requires_grad_(True)
     F.cross_entropy(ref.convs[1](h1, ei)[:300], y).backward()
-    # d(layer-1 input): the bounded backward writes rows < R' = max(R, 1 + max
-    # source of the edges into rows < R) only -- the oracle is zero past them
     src, dst = ei
     rn = max(300, int(src[dst < 300].max()) + 1)
     assert not h1.grad[rn:].any()
@@ -178,18 +253,36 @@ def test_config_computers_max_10_5():
     h0.backward(torch.cat([dbg[0][0][:rn], torch.zeros(N - rn, 512)]))
     for n, q in ref.convs[0].named_parameters():
         torch.testing.assert_close(grads[f"convs.0.{n}"], q.grad, **WGRAD, msg=n)
+    _check_adam_step(mine, ref, init)
 
 
 @pytest.mark.timeout(300)
-def test_config_cora_width_stack():
-    """CitationFull-Cora widths: 8,710 features -> 512 -> 70 (config_cora.yml
-    fanout [10,5], bs 512) on a Cora-sized synthetic graph."""
+def test_config_cora_width_graph_step():
+    """BASELINE config #1's layer widths: CitationFull-Cora SAGE(8710,512,70)
+    (config_cora.yml fanout [10,5], bs 512) on a Cora-sized synthetic graph,
+    through the graph step in train mode (K = 8,710: the W_r image exceeds
+    the LDS, the 64-row kernel's path)."""
     from ngnn.loader import sample_block
     g = _graph("cora")
     b = sample_block(g, g.train_idx[:512], [10, 5], seed=9)
+    warm = sample_block(g, g.train_idx[512:1024], [10, 5], seed=10)
     torch.manual_seed(3)
-    mine = ngnn.SAGE(8710, 512, 70, 2, dropout=0.5).to(DEV)
-    _eager_vs_oracle(b, mine, 512, train=True, aggr="mean")
+    mine = ngnn.SAGE(8710, 512, 70, 2, dropout=0.5).to(DEV).train()
+    init = {k: v.detach().cpu().clone() for k, v in mine.state_dict().items()}
+    step, loss, seed_state = _graph_step(mine, b, warm, [10, 5], 512, 8710)
+    N = b.num_nodes
+    out = step.out[:N].cpu()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
+    ref = _MaskedSAGE(8710, 512, 70, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 512, 0.5, 2))
+    ref.load_state_dict(init)
+    out_r = ref(b.x.cpu(), b.edge_index.cpu())
+    loss_r = F.cross_entropy(out_r[:512], b.y[:512].cpu())
+    loss_r.backward()
+    torch.testing.assert_close(out, out_r.detach(), **OUT)
+    assert abs(float(loss) - float(loss_r)) < 1e-5
+    for k, q in ref.named_parameters():
+        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+    _check_adam_step(mine, ref, init)
 
 
 def _receptive_rows(ei, rows, hops):
@@ -205,10 +298,11 @@ def _receptive_rows(ei, rows, hops):
     return sets[::-1]
 
 
-def _oracle_rows(ref, x, ei, rows):
+def _oracle_rows(ref, x, ei, rows, masks=None, scale=1.0):
     """The oracle's outputs for `rows` only, computed through their receptive
     field (layer l over the rows layer l+1 needs, with every edge into them):
-    the same values as the full-block forward on those rows."""
+    the same values as the full-block forward on those rows.  masks: the
+    hidden layers' dropout keep masks over the whole block (row-indexed)."""
     L = len(ref.convs)
     sets = _receptive_rows(ei, rows, L)
     src, dst = ei
@@ -224,42 +318,61 @@ def _oracle_rows(ref, x, ei, rows):
         h = conv(h, torch.stack([pos[src[e]], pos[dst[e]]]))[pos[need]]
         if i != L - 1:
             h = h.relu()
+            if masks is not None:
+                h = h * masks[i][need] * scale
         have = need
     return h
 
 
 @pytest.mark.timeout(400)
-def test_config_products_3layer_bf16_graph_slot():
-    """ogbn-products SAGE(100,256,256,47) in bf16, [20,15,10] bs 1024, through
-    the graph step (eval-mode forward of the captured model on the slot): the
-    slot's rows x 256 fp32 exceed the row-tile kernel's 2 GiB buffer range,
-    so this is the large-block path.  bf16 against the fp32 oracle (2e-2),
-    seed rows and a row sample, through their receptive field."""
-    from ngnn.graphs import GraphedTrainStep, slot_size
+def test_config_products_3layer_bf16_graph_step():
+    """BASELINE config #3: ogbn-products SAGE(100,256,256,47) in bf16,
+    [20,15,10] bs 1024, through the benched graph step in TRAIN mode
+    (dropout 0.5, hash masks from the slot seed).  Against the fp32 oracle
+    (bf16 storage at the module boundary: features, parameters, logits,
+    gradients) at the SURVEY 8(c) bf16 tolerance 2e-2:
+
+    * logits of the seed rows and of a row sample, through their receptive
+      field (the oracle over the whole 1.5 M-row block is not needed: the
+      loss reads the seed rows, whose receptive field IS the block's
+      training-relevant part);
+    * the loss and every parameter gradient (seed-row loss back-propagated
+      through that receptive field: exactly the full block's gradients),
+      elementwise at 2e-2 of the tensor's largest magnitude;
+    * the post-step parameters within one bf16 rounding of torch's Adam."""
     from ngnn.loader import sample_block
-    from ngnn.optim import Adam
     g = _graph("ogbn-products")
     g.x = g.x.to(torch.bfloat16)
     b = sample_block(g, g.train_idx[:1024], [20, 15, 10], seed=11)
+    warm = sample_block(g, g.train_idx[1024:2048], [20, 15, 10], seed=12)
     torch.manual_seed(4)
-    mine = ngnn.SAGE(100, 256, 47, 3, dropout=0.0).to(DEV).to(torch.bfloat16).train()
+    mine = ngnn.SAGE(100, 256, 47, 3, dropout=0.5).to(DEV).to(torch.bfloat16).train()
     init = {k: v.detach().float().cpu().clone() for k, v in mine.state_dict().items()}
-    opt = Adam(mine.parameters(), lr=1e-3)
-    n_cap, e_cap = slot_size(1024, [20, 15, 10])
-    step = GraphedTrainStep(mine, opt, 1024, n_cap, e_cap, 100, DEV)
-    step.capture(b.x, b.edge_index, b.y)
-    step(b.x, b.edge_index, b.y)
-    torch.cuda.synchronize()
+    step, loss, seed_state = _graph_step(mine, b, warm, [20, 15, 10], 1024, 100)
     N = b.num_nodes
     out = step.out[:N].float().cpu()
-    ref = pyg_ref.SAGE(100, 256, 47, 3, dropout=0.0).eval()
-    ref.load_state_dict(init)
-    gen = torch.Generator().manual_seed(0)
-    rows = torch.unique(torch.cat([torch.arange(1024), torch.randint(1024, N, (3000,), generator=gen)]))
-    with torch.no_grad():
-        want = _oracle_rows(ref, b.x.float().cpu(), b.edge_index.cpu(), rows)
-    torch.testing.assert_close(out[rows], want, rtol=2e-2, atol=2e-2)
     assert torch.isfinite(out).all()
+    grads = {k: p.grad.detach().float().cpu().clone() for k, p in mine.named_parameters()}
+    masks = _slot_masks(seed_state, N, 256, 0.5, 3)
+    ref = pyg_ref.SAGE(100, 256, 47, 3, dropout=0.5)
+    ref.load_state_dict(init)
+    x, ei = b.x.float().cpu(), b.edge_index.cpu()
+    seeds = torch.arange(1024)
+    out_r = _oracle_rows(ref, x, ei, seeds, masks, dropout_scale(0.5))
+    loss_r = F.cross_entropy(out_r, b.y[:1024].cpu())
+    loss_r.backward()
+    BF = dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(out[:1024], out_r.detach(), **BF)
+    assert abs(float(loss) - float(loss_r)) < 2e-2 * max(1.0, abs(float(loss_r)))
+    for k, q in ref.named_parameters():
+        torch.testing.assert_close(grads[k], q.grad, rtol=2e-2,
+                                   atol=2e-2 * float(q.grad.abs().max()), msg=k)
+    gen = torch.Generator().manual_seed(0)
+    rows = torch.unique(torch.randint(1024, N, (3000,), generator=gen))
+    with torch.no_grad():
+        want = _oracle_rows(ref, x, ei, rows, masks, dropout_scale(0.5))
+    torch.testing.assert_close(out[rows], want, **BF)
+    _check_adam_step(mine, ref, init, bf16=True)
 
 
 def test_3layer_h256_backward_gemm_scatter_path():

@@ -34,16 +34,23 @@ def _lowbias32(x):
 
 
 def dropout_keep(seed, n_rows, n_cols, p):
-    """Host replica of ngnn_device.h::Dropout: one hash per column quad,
-    keep <=> byte (col % 4) >= ceil(p * 256)."""
+    """Host replica of ngnn_device.h::Dropout.  Byte mode (thresh != 128): one
+    hash per column quad, keep <=> byte (col % 4) >= ceil(p * 256).  Bit mode
+    (p = 0.5): keep <=> bit c & 31 of the hash of word c >> 5."""
     s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
     thresh = dropout_thresh(p)
     r = np.arange(n_rows, dtype=np.uint64)[:, None]
     c = np.arange(n_cols, dtype=np.uint64)[None, :]
     rk = _lowbias32(r ^ s0) ^ s1
-    h = _lowbias32((rk + (c >> np.uint64(2))) & M32)
-    byte = (h >> (np.uint64(8) * (c & np.uint64(3)))) & np.uint64(0xFF)
-    return torch.from_numpy(byte >= np.uint64(thresh))
+    u = np.uint64
+    if thresh == 128:
+        word = c >> u(5)
+        bit = c & u(31)
+        h = _lowbias32((rk + word) & M32)
+        return torch.from_numpy(((h >> bit) & u(1)) == u(1))
+    h = _lowbias32((rk + (c >> u(2))) & M32)
+    byte = (h >> (u(8) * (c & u(3)))) & u(0xFF)
+    return torch.from_numpy(byte >= u(thresh))
 
 
 def dropout_thresh(p):

@@ -320,7 +320,7 @@ def test_slot_load_csr_equals_lower_bound(case):
         _lib.ptr(x), x.stride(0), N, F, _lib.ptr(ei) if E else None, max(E, 0), E, _lib.ptr(y), 8,
         _lib.ptr(sx), sx.stride(0), n_cap, _lib.ptr(sei), e_cap, _lib.ptr(sy), _lib.ptr(nv),
         _lib.ptr(rowptr), _lib.ptr(col), None, None, None, 0, None, None, None, None,
-        _lib.stream_handle(DEV)), "ngnn_slot_load")
+        None, 0, 0, 0, None, _lib.stream_handle(DEV)), "ngnn_slot_load")
     torch.cuda.synchronize()
     n_pad, span = e_cap - E, n_cap - N
     pad = N + (torch.arange(n_pad) * span) // max(n_pad, 1) if n_pad else torch.zeros(0, dtype=torch.int64)
@@ -347,3 +347,31 @@ def test_slot_rejects_unsorted_targets():
     perm = torch.randperm(b.edge_index.size(1), device=DEV)
     with pytest.raises(ValueError, match="target-sorted"):
         step.load(b.x, b.edge_index[:, perm], b.y)
+
+
+@pytest.mark.parametrize("fo,k", [(256, 100), (47, 256), (5, 3), (600, 64)])
+def test_slot_pack_job_equals_pack_weight(fo, k):
+    """ngnn_slot_load's pack job writes exactly ngnn_pack_weight's fragment
+    layout (zero padding included) of the weight's current values."""
+    from ngnn import _lib
+    from ngnn.fused import pack_weight
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(fo + k)
+    w = torch.randn(fo, k + 3, generator=g).to(DEV)[:, :k]  # row stride k + 3
+    dst = torch.full((lib.ngnn_pack_weight_bytes(fo, k) // 4,), 7.0, device=DEV)
+    N, F, n_cap = 4, 4, 8
+    x = torch.zeros(N, F, device=DEV)
+    y = torch.zeros(1, dtype=torch.int64, device=DEV)
+    sx = torch.zeros(n_cap, F, device=DEV)
+    sy = torch.zeros(1, dtype=torch.int64, device=DEV)
+    sei = torch.zeros(2, 2, dtype=torch.int64, device=DEV)
+    ei = torch.tensor([[0, 1], [0, 1]], device=DEV)
+    nv = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _lib.check(lib.ngnn_slot_load(
+        _lib.ptr(x), F, N, F, _lib.ptr(ei), 2, 2, _lib.ptr(y), 1, _lib.ptr(sx), F, n_cap,
+        _lib.ptr(sei), 2, _lib.ptr(sy), _lib.ptr(nv), None, None, None, None, None, 0, None,
+        None, None, None, _lib.ptr(w), w.stride(0), fo, k, _lib.ptr(dst),
+        _lib.stream_handle(DEV)), "ngnn_slot_load")
+    want = pack_weight(w)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, want)
