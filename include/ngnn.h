@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 11
+#define NGNN_ABI_VERSION 12
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -63,8 +63,8 @@ extern "C" {
  * bf16 [*, ldx] (ldx in elements, a multiple of 4; 16-B aligned base).  The
  * rows are read as bf16 -- half the bytes of the fp32 layout -- and widened
  * exactly: the split-bf16 root term needs one part (3 products), the gather
- * sums in fp32.  Outputs and agg_out stay fp32.  Not with NGNN_MATH_EXACT_F32
- * or NGNN_FWD_NARROW (NGNN_E_SHAPE: convert x and call again). */
+ * sums in fp32.  Outputs (unless NGNN_OUT_BF16), z and agg_out stay fp32.  Not
+ * with NGNN_MATH_EXACT_F32 (NGNN_E_SHAPE: convert x and call again). */
 #define NGNN_X_BF16 0x400
 /* flag OR-ed into ngnn_sage_fwd_raw's `reduce`: the weights (W_r, and W_l of
  * NGNN_FWD_NARROW) hold bf16-exact values -- a bf16 model's parameters
@@ -81,6 +81,13 @@ extern "C" {
  * load, ngnn_slot_load's pack job), so a layer whose W_l streams from L2
  * issues no pack launch of its own; ignored when W_l is staged in LDS. */
 #define NGNN_WL_PREPACKED 0x1000
+/* flag OR-ed into ngnn_sage_fwd_raw's `reduce`: `out` holds bf16 [n_rows,
+ * ldo] (ldo in elements, a multiple of 4; 8-B aligned), each output rounded to
+ * nearest even after bias, ReLU and dropout -- a bf16 model's hidden
+ * activations, which the reference's bf16 layer stores in bf16 too.  Whole
+ * 16-column output tiles only; not with NGNN_FWD_NARROW or the wide path
+ * (NGNN_E_SHAPE: call without and convert). */
+#define NGNN_OUT_BF16 0x2000
 
 /* dtypes */
 #define NGNN_F32 0
@@ -123,7 +130,9 @@ int ngnn_csr_build(const int64_t *keys, const int64_t *vals, int64_t E, int64_t 
  * SUM : edge-order fp32 sum; MEAN: sum / max(deg,1) (IEEE division);
  * MAX : NaN-propagating max, empty rows -> 0 (scatter_reduce amax,
  *       include_self=False on a zero tensor).
- * Replaces PyG MessagePassing.propagate (gather x_j + utils.scatter) [ext]. */
+ * Replaces PyG MessagePassing.propagate (gather x_j + utils.scatter) [ext].
+ * dtype NGNN_BF16: x holds bf16 rows (F, ldx multiples of 4; 8-B aligned),
+ * widened exactly; out stays fp32. */
 int ngnn_seg_agg_fwd(const void *x, int64_t ldx, int64_t F, const int32_t *rowptr,
                      const int32_t *col, int64_t n_dst, int reduce, int dtype,
                      void *out, int64_t ldo, void *stream);
@@ -288,9 +297,16 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * host value): rows at or past it have no in-edges (NGNN_FWD_NARROW's
  * gather stops there; NeighborLoader numbers the rows that receive edges
  * first).  Pass n_rows when unknown.
+ * Wide layers (ngnn_sage_wide_preferred: K % 4 != 0, or F_out needing more
+ * than four LDS column slices -- Amazon-Computers' 767 -> 512 layer) with
+ * plain fp32 rows run as an aggregate launch over rows < n_edge_rows (into
+ * agg_out, else ws) + a 2-D tiled exact-fp32 MFMA dual GEMM (ngnn_wide.hip).
  * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes (calls sharing
  * a ws must be stream-ordered). */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
+/* 1 when ngnn_sage_fwd_raw runs a [K -> Fo] layer on the wide path (exact:
+ * the NGNN_MATH_EXACT_F32 mode), else 0. */
+int ngnn_sage_wide_preferred(int64_t K, int64_t Fo, int exact);
 int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *xrow,
                       const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx, int64_t K,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
@@ -343,12 +359,16 @@ size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K);
  * ngnn_sage_fwd_raw's x_dev). */
 /* h_idx / h_idx_dev (nullable; the device word overrides): row r of h is
  * row h_idx[r] of h, a table of h_rows rows (< 2 GiB) -- layer 0 under the
- * fused x[n_id] gather (see ngnn_sage_fwd_raw's xrow).  h_bf16: h holds bf16
- * (a bf16 model's layer input, as ngnn_sage_fwd_raw's NGNN_X_BF16; K and ldh
- * multiples of 4), widened exactly when staged. */
+ * fused x[n_id] gather (see ngnn_sage_fwd_raw's xrow).  bf16_flags: bit 0
+ * (NGNN_WG_H_BF16) h holds bf16 (a bf16 model's layer input, as
+ * ngnn_sage_fwd_raw's NGNN_X_BF16; K and ldh multiples of 4); bit 1
+ * (NGNN_WG_Y_BF16) the mask rows y hold bf16 (a bf16 model's hidden
+ * activations, NGNN_OUT_BF16); both widened exactly when staged. */
+#define NGNN_WG_H_BF16 1
+#define NGNN_WG_Y_BF16 2
 int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy, float yscale,
                     const float *h, const float *const *h_dev, const int64_t *h_idx,
-                    const int64_t *const *h_idx_dev, int64_t h_rows, int h_bf16, int64_t ldh,
+                    const int64_t *const *h_idx_dev, int64_t h_rows, int bf16_flags, int64_t ldh,
                     const float *agg, int64_t ld_agg, const int32_t *rowptr, int64_t n_rows,
                     const int32_t *r_ptr,
                     int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
@@ -461,6 +481,11 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * model's fp32 logits handed back in bf16 (Tensor.to(torch.bfloat16), the
  * `SAGE.forward` return dtype of a bf16 model).  src 16-B, dst 8-B aligned. */
 int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream);
+/* dst[r, :F] = float(src[r, :F]) (bf16 -> fp32, exact) for rows r <
+ * min(n_rows, *n_rows_dev) (n_rows_dev nullable): the rows of a bf16 model's
+ * activations a backward kernel reads as an fp32 mask. */
+int ngnn_widen_bf16_rows(const void *src, int64_t lds, int64_t F, int64_t n_rows,
+                         const int32_t *n_rows_dev, float *dst, int64_t ldd, void *stream);
 int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
                    const int32_t *dtypes, float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,

@@ -133,6 +133,41 @@ __global__ __launch_bounds__(256) void k_seg_agg_fwd(const float *__restrict__ x
     }
 }
 
+// bf16 input rows (a bf16 model's activations): one wave per target row,
+// lanes over 4-column quads (8-B loads), widened exactly and reduced in edge
+// order in fp32 -- the sequence of the fp32 kernel on the widened rows.
+template <int RED>
+__global__ __launch_bounds__(256) void k_seg_agg_fwd_bf16(const uint16_t *__restrict__ x, int64_t ldx,
+                                                          int F, const int32_t *__restrict__ rowptr,
+                                                          const int32_t *__restrict__ col, int n_dst,
+                                                          float *__restrict__ out, int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (row >= n_dst) return;
+    const int beg = rowptr[row], end = rowptr[row + 1];
+    for (int f = 4 * lane; f < F; f += 256) {
+        float4 acc = splat<4>(RED == NGNN_REDUCE_MAX ? -INFINITY : 0.0f);
+        for (int e = beg; e < end; ++e) {
+            const int64_t j = col[e];
+            const uint2 w = *reinterpret_cast<const uint2 *>(x + j * ldx + f);
+            const float4 v{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                           __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+            reduce_into<4, RED>(acc, v);
+        }
+        const int deg = end - beg;
+        if (RED == NGNN_REDUCE_MEAN) {
+            const float cnt = static_cast<float>(deg > 1 ? deg : 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) comp<4>(acc, i) = comp<4>(acc, i) / cnt;
+        } else if (RED == NGNN_REDUCE_MAX && deg == 0) {
+            acc = splat<4>(0.0f);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (f + i < F) out[row * ldo + f + i] = comp<4>(acc, i);
+    }
+}
+
 // ------------------------------------------------- backward, sum / mean
 // grad_x[j] = sum_{e: src_e = j} g[dst_e] (/ deg(dst_e) for mean), over the
 // transposed CSR (rowptr_t, col_t = targets) in edge order.
@@ -368,7 +403,7 @@ using namespace ngnn;
 extern "C" int ngnn_seg_agg_fwd(const void *x, int64_t ldx, int64_t F, const int32_t *rowptr,
                                 const int32_t *col, int64_t n_dst, int reduce, int dtype, void *out,
                                 int64_t ldo, void *stream) {
-    NGNN_RETURN_IF(dtype != NGNN_F32, NGNN_E_DTYPE);
+    NGNN_RETURN_IF(dtype != NGNN_F32 && dtype != NGNN_BF16, NGNN_E_DTYPE);
     NGNN_RETURN_IF(reduce < NGNN_REDUCE_SUM || reduce > NGNN_REDUCE_MAX, NGNN_E_ARG);
     NGNN_RETURN_IF(F < 0 || n_dst < 0 || !rowptr, NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < F || ldo < F, NGNN_E_SHAPE);
@@ -376,6 +411,22 @@ extern "C" int ngnn_seg_agg_fwd(const void *x, int64_t ldx, int64_t F, const int
     if (F == 0 || n_dst == 0) return NGNN_OK;
     // col may be NULL when the block has no edges (rowptr is all zeros then)
     NGNN_RETURN_IF(!x || !out, NGNN_E_ARG);
+    if (dtype == NGNN_BF16) {  // bf16 rows: F and ldx multiples of 4, 8-B aligned
+        NGNN_RETURN_IF(F % 4 != 0 || ldx % 4 != 0 || !aligned(x, 8), NGNN_E_SHAPE);
+        const unsigned g = static_cast<unsigned>(ceil_div(n_dst, 4));
+        const uint16_t *xb = static_cast<const uint16_t *>(x);
+        float *of = static_cast<float *>(out);
+        if (reduce == NGNN_REDUCE_MEAN)
+            hipLaunchKernelGGL(k_seg_agg_fwd_bf16<NGNN_REDUCE_MEAN>, dim3(g), dim3(256), 0,
+                               as_stream(stream), xb, ldx, (int)F, rowptr, col, (int)n_dst, of, ldo);
+        else if (reduce == NGNN_REDUCE_SUM)
+            hipLaunchKernelGGL(k_seg_agg_fwd_bf16<NGNN_REDUCE_SUM>, dim3(g), dim3(256), 0,
+                               as_stream(stream), xb, ldx, (int)F, rowptr, col, (int)n_dst, of, ldo);
+        else
+            hipLaunchKernelGGL(k_seg_agg_fwd_bf16<NGNN_REDUCE_MAX>, dim3(g), dim3(256), 0,
+                               as_stream(stream), xb, ldx, (int)F, rowptr, col, (int)n_dst, of, ldo);
+        return launch_status();
+    }
     const int vec = pick_vec(F, {{x, ldx}, {out, ldo}});
     const int lpr = pick_lpr(F, vec);
     const unsigned grid = static_cast<unsigned>(ceil_div(n_dst, 256 / lpr));

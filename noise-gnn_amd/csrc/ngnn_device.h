@@ -15,6 +15,7 @@ __device__ __forceinline__ T gload(const T *p, int64_t i) {
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // ---- raw buffer access (LLVM intrinsics by name).  A resource covers
 // [base, base + bytes) (word3 = 0x00020000: raw, 32-bit element format for
@@ -23,11 +24,11 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ v4f buf_load4(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 __device__ float buf_load1(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
 __device__ int buf_load1i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
-typedef int i32x2 __attribute__((ext_vector_type(2)));
 __device__ i32x2 buf_load2i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
 __device__ i32x4 buf_load4i(i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void buf_store4(v4f v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
 __device__ void buf_store1(float v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
+__device__ void buf_store2i(i32x2 v, i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v2i32");
 
 __device__ __forceinline__ i32x4 make_rsrc(const void *p, uint32_t bytes) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);
@@ -174,6 +175,22 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      float *z = nullptr, int64_t ldz = 0, const int64_t *xrow = nullptr,
                      const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
                      const int32_t *col_x = nullptr, bool x_bf16 = false,
-                     bool w_bf16 = false, bool wl_prepacked = false);
+                     bool w_bf16 = false, bool wl_prepacked = false, bool agg_pre = false,
+                     bool out_bf16 = false);
+
+// Wide-layer forward (ngnn_wide.hip): an aggregate launch into agg_out (or
+// the workspace) + a 2-D tiled fp32-MFMA dual GEMM.  Raw [F_out, K] weights.
+bool sage_wide_preferred(int64_t K, int64_t Fo, bool exact);
+size_t sage_wide_workspace_bytes(int64_t K, int64_t n_rows);
+int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                        const int32_t *n_rows_dev, int64_t n_edge_rows,
+                        const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
+                        int reduce, float *agg, int64_t ld_agg, hipStream_t st);
+int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                  const int32_t *n_rows_dev, int64_t n_edge_rows, const int32_t *n_edge_rows_dev,
+                  const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,
+                  const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
+                  int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
+                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st);
 
 }  // namespace ngnn

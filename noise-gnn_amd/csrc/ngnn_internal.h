@@ -31,4 +31,6 @@ inline bool aligned(const void *p, size_t a) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+int num_cus();  // compute units of the current device (cached; ngnn_sage_rt.hip)
+
 }  // namespace ngnn

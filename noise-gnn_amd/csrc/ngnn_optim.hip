@@ -20,13 +20,28 @@ struct AdamTensors {
     float *p[kMaxT];  // fp32, or bf16 when bf[k] (update in fp32, stored rounded)
     const float *g[kMaxT];
     int bf[kMaxT];
+    int vec[kMaxT];  // p, g, m, v aligned for 4-element vector accesses
     float *m[kMaxT];
     float *v[kMaxT];
     int64_t off[kMaxT + 1];  // prefix sums of numel
-    int64_t boff[kMaxT + 1];  // prefix sums of workgroups (ceil(numel / 256) per tensor)
+    int64_t boff[kMaxT + 1];  // prefix sums of virtual workgroups (ceil(numel / kAdamChunk))
     int n;
 };
 
+constexpr int kAdamVec = 4;                   // elements per thread
+constexpr int kAdamChunk = 256 * kAdamVec;    // elements per virtual workgroup
+
+__device__ __forceinline__ float bf16_bits_to_f(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ uint32_t f_to_bf16_bits(float f) {  // RNE, NaN -> 0x7FC0
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// grid-stride over virtual workgroups of kAdamChunk elements (boff counts
+// them per tensor): a few hundred workgroups, 16-B loads of 4 elements, and
+// as many ticket atomics as workgroups (one per virtual workgroup serialised
+// on the ticket's L2 channel: 40 us for Amazon-Computers' 1.6 M parameters)
 __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__ step,
                                               uint32_t *__restrict__ ticket, float lr, float b1,
                                               float b2, float eps, float wd) {
@@ -34,31 +49,72 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
     const float bc1 = 1.0f - powf(b1, t);
     const float bc2s = sqrtf(1.0f - powf(b2, t));
     const float step_size = lr / bc1;
-    // workgroup -> tensor: uniform (scalar loads of the tensor's pointers,
-    // no per-lane search and dependent pointer loads)
-    int k = 0;
-    while (k + 1 < T.n && static_cast<int64_t>(blockIdx.x) >= T.boff[k + 1]) ++k;
-    const int64_t j = (static_cast<int64_t>(blockIdx.x) - T.boff[k]) * blockDim.x + threadIdx.x;
-    if (j < T.off[k + 1] - T.off[k]) {
-        float g, p;
-        if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
-            g = __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(T.g[k])[j]);
-            p = __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(T.p[k])[j]);
-        } else {
-            g = T.g[k][j];
-            p = T.p[k][j];
-        }
+    auto upd = [&](float g, float &p, float &m, float &v) {
         if (wd != 0.0f) g = g + wd * p;
-        float m = T.m[k][j];
-        float v = T.v[k][j];
         m = m + (1.0f - b1) * (g - m);
         v = b2 * v + (1.0f - b2) * g * g;
         const float denom = sqrtf(v) / bc2s + eps;
         p = p - step_size * (m / denom);
-        T.m[k][j] = m;
-        T.v[k][j] = v;
-        if (T.bf[k]) reinterpret_cast<__hip_bfloat16 *>(T.p[k])[j] = __float2bfloat16(p);
-        else T.p[k][j] = p;
+    };
+    const int64_t nvb = T.boff[T.n];
+    int k = 0;
+    for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+        // virtual workgroup -> tensor: uniform (scalar loads of its pointers)
+        while (k + 1 < T.n && vb >= T.boff[k + 1]) ++k;
+        const int64_t n = T.off[k + 1] - T.off[k];
+        const int64_t j = (vb - T.boff[k]) * kAdamChunk + threadIdx.x * kAdamVec;
+        if (j >= n) continue;
+        float *mp = T.m[k] + j, *vp = T.v[k] + j;
+        if (T.vec[k] && j + kAdamVec <= n) {  // aligned base, j % 4 == 0
+            float4 m4 = *reinterpret_cast<const float4 *>(mp);
+            float4 v4 = *reinterpret_cast<const float4 *>(vp);
+            float g[4], p[4];
+            if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
+                const uint2 gb = *reinterpret_cast<const uint2 *>(
+                    reinterpret_cast<const uint16_t *>(T.g[k]) + j);
+                const uint2 pb = *reinterpret_cast<const uint2 *>(
+                    reinterpret_cast<const uint16_t *>(T.p[k]) + j);
+                g[0] = bf16_bits_to_f(gb.x & 0xffffu); g[1] = bf16_bits_to_f(gb.x >> 16);
+                g[2] = bf16_bits_to_f(gb.y & 0xffffu); g[3] = bf16_bits_to_f(gb.y >> 16);
+                p[0] = bf16_bits_to_f(pb.x & 0xffffu); p[1] = bf16_bits_to_f(pb.x >> 16);
+                p[2] = bf16_bits_to_f(pb.y & 0xffffu); p[3] = bf16_bits_to_f(pb.y >> 16);
+            } else {
+                const float4 g4 = *reinterpret_cast<const float4 *>(T.g[k] + j);
+                const float4 p4 = *reinterpret_cast<const float4 *>(T.p[k] + j);
+                g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
+                p[0] = p4.x; p[1] = p4.y; p[2] = p4.z; p[3] = p4.w;
+            }
+            upd(g[0], p[0], m4.x, v4.x);
+            upd(g[1], p[1], m4.y, v4.y);
+            upd(g[2], p[2], m4.z, v4.z);
+            upd(g[3], p[3], m4.w, v4.w);
+            *reinterpret_cast<float4 *>(mp) = m4;
+            *reinterpret_cast<float4 *>(vp) = v4;
+            if (T.bf[k]) {
+                const uint2 o{f_to_bf16_bits(p[0]) | (f_to_bf16_bits(p[1]) << 16),
+                              f_to_bf16_bits(p[2]) | (f_to_bf16_bits(p[3]) << 16)};
+                *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(T.p[k]) + j) = o;
+            } else {
+                *reinterpret_cast<float4 *>(T.p[k] + j) = float4{p[0], p[1], p[2], p[3]};
+            }
+        } else {  // the tensor's ragged tail, or an unaligned view
+            for (int64_t e = j; e < min(j + kAdamVec, n); ++e) {
+                float g, p;
+                if (T.bf[k]) {
+                    g = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.g[k])[e]);
+                    p = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.p[k])[e]);
+                } else {
+                    g = T.g[k][e];
+                    p = T.p[k][e];
+                }
+                float m = T.m[k][e], v = T.v[k][e];
+                upd(g, p, m, v);
+                T.m[k][e] = m;
+                T.v[k][e] = v;
+                if (T.bf[k]) reinterpret_cast<uint16_t *>(T.p[k])[e] = static_cast<uint16_t>(f_to_bf16_bits(p));
+                else T.p[k][e] = p;
+            }
+        }
     }
     if (ticket) {
         // every workgroup has read *step (its value fed the loop above) before
@@ -107,13 +163,17 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
             NGNN_RETURN_IF(dtypes && dtypes[base + k] != NGNN_F32 && dtypes[base + k] != NGNN_BF16,
                            NGNN_E_DTYPE);
             T.v[k] = exp_avg_sqs[base + k];
+            const size_t pa = T.bf[k] ? 8 : 16;  // 4 elements of p and g
+            T.vec[k] = aligned(T.p[k], pa) && aligned(T.g[k], pa) && aligned(T.m[k], 16) &&
+                       aligned(T.v[k], 16);
             T.off[k + 1] = T.off[k] + numels[base + k];
         }
         if (T.off[T.n] == 0) continue;
         T.boff[0] = 0;
-        for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], 256);
+        for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], kAdamChunk);
         NGNN_RETURN_IF(T.boff[T.n] > (int64_t{1} << 31) - 1, NGNN_E_RANGE);
-        const unsigned grid = static_cast<unsigned>(T.boff[T.n]);
+        // at most 2 workgroups per CU: the rest is the grid-stride loop
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(T.boff[T.n], 2 * num_cus()));
         hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
                            eps, weight_decay);
         const int rc = launch_status();
@@ -171,5 +231,42 @@ extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 4), 256), 2048));
     hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, as_stream(stream), src,
                        static_cast<uint16_t *>(dst), n);
+    return launch_status();
+}
+
+// ---- bf16 rows -> fp32 rows [0, min(n_rows, *n_rows_dev)) x F (a bf16 model's
+// activations widened for the backward kernels that read fp32 masks, rows
+// below a device-side bound only); exact.
+namespace ngnn {
+namespace {
+__global__ __launch_bounds__(256) void k_widen_bf16_rows(const uint16_t *__restrict__ src, int64_t lds,
+                                                         int F, int n_rows,
+                                                         const int32_t *__restrict__ n_rows_dev,
+                                                         float *__restrict__ dst, int64_t ldd) {
+    int rows = n_rows;
+    if (n_rows_dev) rows = min(rows, *n_rows_dev);
+    const int64_t total = static_cast<int64_t>(rows) * F;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total; i += stride) {
+        const int64_t r = i / F;
+        const int c = static_cast<int>(i - r * F);
+        dst[r * ldd + c] = __uint_as_float(static_cast<uint32_t>(src[r * lds + c]) << 16);
+    }
+}
+}  // namespace
+}  // namespace ngnn
+
+extern "C" int ngnn_widen_bf16_rows(const void *src, int64_t lds, int64_t F, int64_t n_rows,
+                                    const int32_t *n_rows_dev, float *dst, int64_t ldd,
+                                    void *stream) {
+    using namespace ngnn;
+    NGNN_RETURN_IF(F < 0 || n_rows < 0 || lds < F || ldd < F, NGNN_E_ARG);
+    NGNN_RETURN_IF(!fits_i32(F) || !fits_i32(n_rows), NGNN_E_RANGE);
+    if (F == 0 || n_rows == 0) return NGNN_OK;
+    NGNN_RETURN_IF(!src || !dst, NGNN_E_ARG);
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_rows * F, 256), 4096));
+    hipLaunchKernelGGL(k_widen_bf16_rows, dim3(grid), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t *>(src), lds, static_cast<int>(F),
+                       static_cast<int>(n_rows), n_rows_dev, dst, ldd);
     return launch_status();
 }

@@ -51,8 +51,9 @@ __device__ __forceinline__ int wgrad_slices(int R, int S) {
 // "has in-edges" test (rowptr: the saved aggregate of an edgeless row is never
 // written) are applied when the registers are written to LDS, so no load
 // waits on another.  Needs ld * 64 * 4 < 2^31 (host-checked).
-template <int COLS, bool VEC, bool MASK, bool DEG, bool BF = false>
-struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
+template <int COLS, bool VEC, int MASK, bool DEG, bool BF = false>
+struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded); MASK: 0
+                // none, 1 fp32 mask rows, 2 bf16 mask rows (a bf16 model's activations)
     static constexpr int W = VEC ? 4 : 1;
     static constexpr int CPR = COLS / W;               // loads per row
     static constexpr int N = WG_BM * CPR / 512;        // loads per thread
@@ -63,7 +64,9 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
     // make every load wait at once (the next chunk's loads must stay in
     // flight under this chunk's MFMAs)
     i32x2 raw[BF && VEC ? N : 1];
-    T m[MASK ? N : 1];
+    T m[MASK == 1 ? N : 1];
+    i32x2 mraw[MASK == 2 && VEC ? N : 1];  // bf16 mask quads, widened in store()
+    float mh[MASK == 2 && !VEC ? N : 1];
     int d0[DEG ? N : 1], d1[DEG ? N : 1];
 
     // ridx (nullable): row r of the operand is row ridx[r] of src, a table of
@@ -79,7 +82,9 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
         const i32x4 rs = ridx ? make_rsrc(sb, static_cast<uint32_t>(src_rows * ld * EB))
                              : make_rsrc(sb + c0 * ld * EB, nr * static_cast<uint32_t>(ld) * EB);
         i32x4 rm = rs, rp = rs;
-        if (MASK) rm = make_rsrc(mask + c0 * ldm, nr * static_cast<uint32_t>(ldm) * 4u);
+        constexpr uint32_t MB = MASK == 2 ? 2u : 4u;
+        if (MASK) rm = make_rsrc(reinterpret_cast<const char *>(mask) + c0 * ldm * MB,
+                                 nr * static_cast<uint32_t>(ldm) * MB);
         if (DEG) rp = make_rsrc(rowptr + c0, (nr + 1u) * 4u);
 #pragma unroll
         for (int u = 0; u < N; ++u) {
@@ -105,9 +110,17 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
                 v[u] = buf_load1(rs, vo, 0, 0);
             }
             if (MASK) {
-                const int mo = kok ? (r * static_cast<int>(ldm) + k) * 4 : kBufOOB;
-                if constexpr (VEC) m[u] = buf_load4(rm, mo, 0, 0);
-                else m[u] = buf_load1(rm, mo, 0, 0);
+                const int mo = kok ? (r * static_cast<int>(ldm) + k) * static_cast<int>(MB) : kBufOOB;
+                if constexpr (MASK == 2 && VEC) {
+                    mraw[u] = buf_load2i(rm, mo, 0, 0);
+                } else if constexpr (MASK == 2) {
+                    const int w = buf_load1i(rm, mo & ~3, 0, 0);
+                    mh[u] = __int_as_float((mo & 2) ? (w & static_cast<int>(0xffff0000u)) : (w << 16));
+                } else if constexpr (VEC) {
+                    m[u] = buf_load4(rm, mo, 0, 0);
+                } else {
+                    m[u] = buf_load1(rm, mo, 0, 0);
+                }
             }
             if (DEG) {
                 d0[u] = buf_load1i(rp, r * 4, 0, 0);
@@ -125,7 +138,11 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded)
             if constexpr (BF && VEC) w = bf16x4_to_f32(raw[u]);
             else w = v[u];
             float *wf = reinterpret_cast<float *>(&w);
-            const float *mf = reinterpret_cast<const float *>(&m[MASK ? u : 0]);
+            T mv;
+            if constexpr (MASK == 2 && VEC) mv = bf16x4_to_f32(mraw[u]);
+            else if constexpr (MASK == 2) mv = mh[u];
+            else mv = m[MASK ? u : 0];
+            const float *mf = reinterpret_cast<const float *>(&mv);
 #pragma unroll
             for (int i = 0; i < W; ++i) {
                 float x = wf[i];
@@ -180,7 +197,7 @@ __device__ __forceinline__ void wgrad_mfma_dispatch(int ktn, v4f (&acc)[NTW][KTW
 // matrix split the (4) Fo tiles of the workgroup; else they split the K tiles.
 // Slice s owns rows [rb, re) (R split into S ranges on 4-row boundaries, so
 // every used slice gets the same work +-4 rows), walked in 64-row chunks.
-template <int NTW, int KTW, bool SPLIT_N, bool VZ, int VH, bool MASK>
+template <int NTW, int KTW, bool SPLIT_N, bool VZ, int VH, int MASK>
 __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
     const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
     float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
@@ -538,9 +555,14 @@ __global__ __launch_bounds__(256) void k_dgrad_fused(
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float *z = sdz[wave];
     const int R = min(n_rows, *r_ptr);
+    // work item = (target row d, 64-column chunk): a few hundred seed rows
+    // still fill the chip (one wave per row ran the 512-wide chunks of
+    // Amazon-Computers' hidden layer back to back: 80 us for 300 rows)
+    const int nch = (K + 63) >> 6;
+    const int64_t items = static_cast<int64_t>(R) * nch;
     const float *wr = wr_g, *wl = wl_g;
     if (LDS_W) {
-        if (static_cast<int64_t>(blockIdx.x) * 4 >= R) return;  // no rows for this workgroup
+        if (static_cast<int64_t>(blockIdx.x) * 4 >= items) return;  // no work for this workgroup
         const int n4 = (Fo * K) >> 2;  // Fo K % 4 == 0 on this path
         float4 *s4 = reinterpret_cast<float4 *>(sw);
         const float4 *r4 = reinterpret_cast<const float4 *>(wr_g);
@@ -553,7 +575,8 @@ __global__ __launch_bounds__(256) void k_dgrad_fused(
         wr = sw;
         wl = sw + Fo * K;
     }
-    for (int64_t d = blockIdx.x * 4 + wave; d < R; d += gridDim.x * 4) {
+    for (int64_t w = blockIdx.x * 4 + wave; w < items; w += gridDim.x * 4) {
+        const int64_t d = w / nch;
         for (int n = lane; n < Fo; n += 64) {
             float v = dy[d * ldy + n];
             if (y) v = (y[d * ldyy + n] > 0.0f) ? v * yscale : 0.0f;
@@ -563,7 +586,8 @@ __global__ __launch_bounds__(256) void k_dgrad_fused(
         __builtin_amdgcn_wave_barrier();
         const int beg = rowptr[d], end = rowptr[d + 1];
         const float cnt = static_cast<float>(end - beg);
-        for (int f0 = 0; f0 < K; f0 += 64) {
+        do {  // (continue: this lane is done with the item)
+            const int f0 = static_cast<int>(w - d * nch) * 64;
             const int f = f0 + lane;
             const bool act = f < K;
             const int fc = act ? f : 0;
@@ -600,7 +624,7 @@ __global__ __launch_bounds__(256) void k_dgrad_fused(
                 if (RED == NGNN_REDUCE_MAX && !(h[j * ldh + f] == a)) continue;
                 atomicAdd(dh + j * ldd + f, v);
             }
-        }
+        } while (0);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // done reading z
         __builtin_amdgcn_wave_barrier();
     }
@@ -854,7 +878,7 @@ extern "C" size_t ngnn_sage_wgrad_workspace_bytes(int64_t Fo, int64_t K) {
 
 template <int NTW, int KTW, bool SPLIT_N>
 static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, int vh, const float *dy, int64_t ldy,
-                         const float *y, int64_t ldyy, float yscale, const float *h,
+                         const float *y, int64_t ldyy, bool y_bf16, float yscale, const float *h,
                          const float *const *h_dev, int64_t ldh, const int64_t *h_idx,
                          const int64_t *const *h_idx_dev, int64_t h_rows, const float *agg,
                          int64_t ld_agg, const int32_t *rowptr, const int32_t *r_ptr, int Fo, int K,
@@ -868,8 +892,9 @@ static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, int vh, const float
     using T = std::true_type;
     using F = std::false_type;
     auto with_mask = [&](auto vz_c, auto vh_c) {
-        if (y) go(vz_c, vh_c, T{});
-        else go(vz_c, vh_c, F{});
+        if (y && y_bf16) go(vz_c, vh_c, std::integral_constant<int, 2>{});
+        else if (y) go(vz_c, vh_c, std::integral_constant<int, 1>{});
+        else go(vz_c, vh_c, std::integral_constant<int, 0>{});
     };
     using V0 = std::integral_constant<int, 0>;
     using V1 = std::integral_constant<int, 1>;
@@ -888,7 +913,7 @@ static void launch_wgrad(dim3 grid, hipStream_t st, bool vz, int vh, const float
 extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int64_t ldyy,
                                float yscale, const float *h, const float *const *h_dev,
                                const int64_t *h_idx, const int64_t *const *h_idx_dev, int64_t h_rows,
-                               int h_bf16, int64_t ldh, const float *agg, int64_t ld_agg,
+                               int bf16_flags, int64_t ldh, const float *agg, int64_t ld_agg,
                                const int32_t *rowptr, int64_t n_rows, const int32_t *r_ptr,
                                int64_t Fo, int64_t K, float *dwl, float *dbl, float *dwr, void *ws,
                                size_t ws_bytes, void *stream) {
@@ -902,6 +927,9 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     NGNN_RETURN_IF(ldy > (1 << 22) || ldh > (1 << 22) || ld_agg > (1 << 22) ||
                    (y && ldyy > (1 << 22)) || Fo * K > (int64_t{1} << 28), NGNN_E_RANGE);
     NGNN_RETURN_IF(!ws || ws_bytes < ngnn_sage_wgrad_workspace_bytes(Fo, K), NGNN_E_WORKSPACE);
+    // bf16_flags: 1 h rows bf16, 2 mask rows y bf16
+    const int h_bf16 = bf16_flags & 1;
+    const bool y_bf16 = (bf16_flags & 2) != 0;
     // indexed h (the feature table under the fused x[n_id] gather): 32-bit
     // offsets over the whole table
     NGNN_RETURN_IF((h_idx || h_idx_dev) && (h_rows <= 0 || h_rows * ldh * 4 >= (int64_t{1} << 31)),
@@ -912,7 +940,7 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
                    NGNN_E_SHAPE);
     // 16-B staging per operand pair: dz (+ its mask y) and h / agg
     const bool vz = (Fo % 4 == 0) && (ldy % 4 == 0) && aligned(dy, 16) &&
-                    (!y || ((ldyy % 4 == 0) && aligned(y, 16)));
+                    (!y || ((ldyy % 4 == 0) && aligned(y, y_bf16 ? 8 : 16)));
     const int vh = h_bf16 ? 2
                           : ((K % 4 == 0) && (ldh % 4 == 0) && (ld_agg % 4 == 0) &&
                              (h_dev || aligned(h, 16)) && aligned(agg, 16));  // h_dev: 16-B aligned by contract
@@ -925,7 +953,7 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
         1, std::min<int64_t>(ceil_div(n_rows, WG_BM), std::max<int64_t>(1, S_MAX / (gy * gz)))));
     const dim3 grid(S, static_cast<unsigned>(gy), static_cast<unsigned>(gz));
     const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
-#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, yscale, h, h_dev, ldh, h_idx, h_idx_dev, \
+#define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, y_bf16, yscale, h, h_dev, ldh, h_idx, h_idx_dev, \
                      h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf
     if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
     else if (NT == 1) launch_wgrad<1, 2, false>(NGNN_WG_ARGS);
@@ -1089,7 +1117,7 @@ extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *
     const bool lds_w = ((Fo * K) % 4 == 0) && aligned(wl, 16) && aligned(wr, 16) &&
                        wbytes + sizeof(float) * 4 * FD_MAXF <= 150 * 1024;
     const unsigned g = static_cast<unsigned>(
-        std::min<int64_t>(ceil_div(n_rows, 4), lds_w ? dgrad_num_cus() : 1024));
+        std::min<int64_t>(ceil_div(n_rows * ceil_div(K, 64), 4), lds_w ? dgrad_num_cus() : 1024));
     auto go = [&](auto red_c, auto lds_c) {
         constexpr int RED_ = decltype(red_c)::value;
         constexpr bool L_ = decltype(lds_c)::value;

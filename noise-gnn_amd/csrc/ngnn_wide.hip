@@ -1,0 +1,410 @@
+// Wide SAGEConv layer forward for gfx950: layers whose weight image does not
+// fit the row-tile kernel's LDS for more than two column slices -- Amazon-
+// Computers' 767 -> 512 max layer (config_amazon.yml:11-14), where the
+// row-tile kernel would re-read x in 16 slices and the 64-row kernel ran
+// 128 workgroups on 256 CUs (460 us, 12 % of the f32 MFMA peak).
+//
+// Same contract as one SAGEConv layer of sage.py:33-39 (PyG 2.5.1
+// SAGEConv.forward + relu + F.dropout):
+//     out = act( b + x W_r^T + [deg > 0] agg(x) W_l^T )
+// as TWO launches:
+//   k_wide_agg   one wave per target row with in-edges: agg[d] = mean / sum /
+//                max over its in-neighbours, walked in edge order (the fp32
+//                sequence of ngnn_seg_agg_fwd: bit-identical aggregate), written
+//                to the caller's saved-aggregate buffer (the backward's input);
+//   k_wide_gemm  a 2-D tiled dual GEMM over [x | agg] . [W_r ; W_l]^T on exact
+//                fp32 MFMA (v_mfma_f32_16x16x4_f32, like the 64-row kernel),
+//                64 rows x 128 output columns per 256-thread workgroup, K staged
+//                through double-buffered LDS 32 at a time (one barrier per
+//                stage), the next stage's global loads in flight during the
+//                current stage's MFMAs; tiles past the rows with in-edges skip
+//                the W_l half.  Epilogue from the accumulators: bias, ReLU,
+//                hash dropout (the same keys as every other forward kernel),
+//                16-B stores (a lane holds 4 consecutive columns of one row).
+//   Persistent workgroups over the LIVE tiles (device row count), tile t =
+//   blockIdx + j gridDim with the grid a multiple of 8: each XCD (linear id %
+//   8) keeps to fixed column tiles, so its L2 holds only its slice of W.
+//
+// Roofline: flops 2 N K F_out + 2 N_edge K F_out on the
+// 157.3 TF f32 MFMA peak; bytes x (N K 4) + gathered rows (E K 4) + agg write
+// and re-read (2 N_edge K 4) + out (N F_out 4).
+#include <algorithm>
+
+#include "ngnn_device.h"
+
+namespace ngnn {
+namespace {
+
+constexpr int WBM = 64;        // rows per tile
+constexpr int WBN = 128;       // output columns per tile
+constexpr int WKC = 32;        // k per LDS stage
+constexpr int WLD = WKC + 4;   // LDS row stride (floats): 16 rows hit 16 distinct 4-bank groups
+constexpr int WSTAGE = (WBM + WBN) * WLD;  // floats per stage buffer
+constexpr int WXU = WBM * WKC / 256;       // x / agg loads per thread per stage (8)
+constexpr int WWU = WBN * WKC / 256;       // weight loads per thread per stage (16)
+
+// ---- aggregate rows [0, min(n_rows, *n_rows_dev, *n_edge_dev)): one wave
+// per row, lane owns columns p0 + lane + 64 c (c < NC); neighbour ids loaded
+// 64 at a time and broadcast; two neighbour rows in flight, reduced in order.
+template <int RED, int NC>
+__global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, int64_t ldx, int K,
+                                                  const int32_t *__restrict__ rowptr,
+                                                  const int32_t *__restrict__ col, int n_rows,
+                                                  const int32_t *__restrict__ n_rows_dev,
+                                                  const int32_t *__restrict__ n_edge_dev,
+                                                  float *__restrict__ agg, int64_t ld_agg,
+                                                  int n_cap, int round16) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int rows = n_rows;
+    if (n_edge_dev) rows = min(rows, *n_edge_dev);
+    // round16: rows up to the end of the last 16-row tile with in-edges (the
+    // row-tile kernel reads the aggregate of whole tiles; those rows have no
+    // in-edges and get 0)
+    if (round16) rows = (rows + 15) & ~15;
+    rows = min(rows, n_cap);
+    if (n_rows_dev) rows = min(rows, *n_rows_dev);
+    const float init = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
+    for (int64_t d = static_cast<int64_t>(blockIdx.x) * 4 + wave; d < rows; d += gridDim.x * 4) {
+        const int beg = rowptr[d], end = rowptr[d + 1];
+        for (int p0 = 0; p0 < K; p0 += 64 * NC) {
+            float acc[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = init;
+            for (int eb = beg; eb < end; eb += 64) {
+                const int n = min(64, end - eb);
+                const int myc = lane < n ? col[eb + lane] : 0;
+                int k = 0;
+                for (; k + 2 <= n; k += 2) {
+                    const int64_t j0 = __shfl(myc, k), j1 = __shfl(myc, k + 1);
+                    float v0[NC], v1[NC];
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        const int f = p0 + lane + 64 * c;
+                        v0[c] = f < K ? x[j0 * ldx + f] : 0.0f;
+                        v1[c] = f < K ? x[j1 * ldx + f] : 0.0f;
+                    }
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        if (RED == NGNN_REDUCE_MAX) {
+                            acc[c] = nanmax(acc[c], v0[c]);
+                            acc[c] = nanmax(acc[c], v1[c]);
+                        } else {
+                            acc[c] = acc[c] + v0[c];
+                            acc[c] = acc[c] + v1[c];
+                        }
+                    }
+                }
+                if (k < n) {
+                    const int64_t j0 = __shfl(myc, k);
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        const int f = p0 + lane + 64 * c;
+                        const float v = f < K ? x[j0 * ldx + f] : 0.0f;
+                        acc[c] = (RED == NGNN_REDUCE_MAX) ? nanmax(acc[c], v) : acc[c] + v;
+                    }
+                }
+            }
+            const int deg = end - beg;
+            const float cnt = static_cast<float>(deg > 1 ? deg : 1);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int f = p0 + lane + 64 * c;
+                if (f >= K) continue;
+                float v = acc[c];
+                if (RED == NGNN_REDUCE_MEAN) v = v / cnt;
+                if (RED == NGNN_REDUCE_MAX && deg == 0) v = 0.0f;
+                agg[d * ld_agg + f] = v;
+            }
+        }
+    }
+}
+
+struct WideArgs {
+    const float *x;
+    int64_t ldx;
+    const float *agg;  // NULL: no neighbour term
+    int64_t ld_agg;
+    const float *wr;   // NULL: no root term (GCNConv's aggregate-first form)
+    const float *wl;
+    int64_t ldw;
+    int K, Fo, n_rows, n_edge;
+    const int32_t *n_rows_dev, *n_edge_dev;
+    float *out;
+    int64_t ldo;
+    Epi epi;
+    const uint64_t *seed_dev;
+    int n_ct;  // column tiles
+};
+
+template <bool VOUT>
+__global__ __launch_bounds__(256, 2) void k_wide_gemm(WideArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * WSTAGE];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int rows = a.n_rows;
+    if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
+    int erows = min(a.n_edge, rows);
+    if (a.n_edge_dev) erows = min(erows, *a.n_edge_dev);
+    const int nK = (a.K + WKC - 1) / WKC;
+    const int c_root = a.wr ? nK : 0;  // root stages
+    // live tiles (device row count); tile t = row tile t / n_ct, column tile
+    // t % n_ct.  Persistent workgroups take t = blockIdx.x + j gridDim.x; the
+    // grid is a multiple of 8, so with n_ct | 8 every tile an XCD (linear id
+    // % 8) runs has the same column tile(s): that XCD's L2 holds only its
+    // slice of W, and the row tiles with in-edges (first in a NeighborLoader
+    // block, twice the stages) spread over every workgroup.
+    const int n_live = ((rows + WBM - 1) / WBM) * a.n_ct;
+
+    float xr[WXU], wreg[WWU];
+    // wave tile: 64 output columns (4 MFMA m-tiles) x 32 rows (2 n-tiles)
+    const int wn = (wave & 1) * 64, wm = (wave >> 1) * 32;
+    const int i16 = lane & 15, q = lane >> 4;
+    Dropout drop = a.epi.drop;
+    if (a.seed_dev) drop.reseed(*a.seed_dev);
+
+    for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
+        const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
+        const int r0 = rt * WBM, n0 = ct * WBN;
+        const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);  // + neighbour stages
+        auto load = [&](int c) {
+            const bool nb = c >= c_root;
+            const int kc = (nb ? c - c_root : c) * WKC;
+            const float *src = nb ? a.agg : a.x;
+            const int64_t ld = nb ? a.ld_agg : a.ldx;
+            const int rlim = nb ? erows : rows;
+            const float *w = nb ? a.wl : a.wr;
+#pragma unroll
+            for (int u = 0; u < WXU; ++u) {
+                const int idx = u * 256 + tid, r = idx >> 5, k = idx & 31;
+                xr[u] = (r0 + r < rlim && kc + k < a.K) ? src[(r0 + r) * ld + kc + k] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < WWU; ++u) {
+                const int idx = u * 256 + tid, n = idx >> 5, k = idx & 31;
+                wreg[u] = (n0 + n < a.Fo && kc + k < a.K)
+                              ? w[static_cast<int64_t>(n0 + n) * a.ldw + kc + k]
+                              : 0.0f;
+            }
+        };
+        auto store = [&](float *s) {
+#pragma unroll
+            for (int u = 0; u < WXU; ++u) {
+                const int idx = u * 256 + tid;
+                s[(idx >> 5) * WLD + (idx & 31)] = xr[u];
+            }
+#pragma unroll
+            for (int u = 0; u < WWU; ++u) {
+                const int idx = u * 256 + tid;
+                s[(WBM + (idx >> 5)) * WLD + (idx & 31)] = wreg[u];
+            }
+        };
+        v4f acc[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
+
+        if (nch > 0) {
+            load(0);
+            store(lds);
+            __syncthreads();
+        }
+        for (int c = 0; c < nch; ++c) {
+            const bool more = c + 1 < nch;
+            if (more) load(c + 1);  // in flight during this stage's MFMAs
+            const float *s = lds + (c & 1) * WSTAGE;
+            // k mapping inside a stage: lane group q takes k = 8 q + step, so
+            // each operand is two ds_read_b128 per tile for all 8 steps
+            v4f wa[4][2], xb[2][2];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float *p = s + (WBM + wn + mt * 16 + i16) * WLD + 8 * q;
+                wa[mt][0] = *reinterpret_cast<const v4f *>(p);
+                wa[mt][1] = *reinterpret_cast<const v4f *>(p + 4);
+            }
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const float *p = s + (wm + nt * 16 + i16) * WLD + 8 * q;
+                xb[nt][0] = *reinterpret_cast<const v4f *>(p);
+                xb[nt][1] = *reinterpret_cast<const v4f *>(p + 4);
+            }
+#pragma unroll
+            for (int st = 0; st < 8; ++st)
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            wa[mt][st >> 2][st & 3], xb[nt][st >> 2][st & 3], acc[mt][nt], 0, 0, 0);
+            if (more) store(lds + ((c + 1) & 1) * WSTAGE);
+            __syncthreads();
+        }
+
+        // ---- epilogue: lane holds columns n0 + wn + 16 mt + 4 q + (0..3) of
+        // row r0 + wm + 16 nt + i16
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int r = r0 + wm + nt * 16 + i16;
+            if (r >= rows) continue;
+            const uint32_t rk = drop.row_key(static_cast<uint32_t>(r));
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int c0 = n0 + wn + mt * 16 + 4 * q;
+                if (c0 >= a.Fo) continue;
+                const uint32_t kb =
+                    drop.thresh ? drop.keep4(rk, static_cast<uint32_t>(a.epi.col_base + c0) >> 2) : 0xfu;
+                v4f v = acc[mt][nt];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float e = v[j];
+                    if (a.epi.bias && c0 + j < a.Fo) e += a.epi.bias[c0 + j];
+                    if (a.epi.relu) e = (e < 0.0f) ? 0.0f : e;  // NaN passes, like torch.relu
+                    if (drop.thresh) e = ((kb >> j) & 1u) ? e * drop.scale : 0.0f;
+                    v[j] = e;
+                }
+                float *o = a.out + static_cast<int64_t>(r) * a.ldo + c0;
+                if (VOUT && c0 + 4 <= a.Fo) {
+                    *reinterpret_cast<v4f *>(o) = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (c0 + j < a.Fo) o[j] = v[j];
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// The row-tile kernel holds the W_r image of its whole column slice in LDS
+// and re-reads x once per slice: the wide path takes a layer when F_out needs
+// more than four such slices (or none fits), or K is not a multiple of 4 (the
+// row-tile kernel reads 16-B column quads; the caller pads K when that keeps
+// it within two slices, fused.pad_k_ok).  Its f32 MFMA rate is 1/2.7 of the
+// row-tile kernel's split-bf16 root term, so moderately sliced layers (the
+// 256 -> 256 hidden layer: 3 slices) stay on the row-tile kernel.
+bool sage_wide_preferred(int64_t K, int64_t Fo, bool exact) {
+    if (K % 4 != 0) return true;
+    const int64_t KG = ceil_div(K, 16);
+    int64_t C = K / 32, T4 = ceil_div(K % 32, 4);
+    if (T4 > 3) {  // X3_TAIL_MAX (ngnn_sage_rt.hip): the tail becomes a padded chunk
+        C += 1;
+        T4 = 0;
+    }
+    const int64_t img = exact ? KG * 64 * 16 : 3 * C * 64 * 16 + T4 * 64 * 4;
+    const int64_t cap = 160 * 1024 - 1024 - 256;
+    int ntw = 0;
+    for (int c : {16, 8, 6, 4, 3, 2})
+        if (c * img <= cap) {
+            ntw = c;
+            break;
+        }
+    return ntw == 0 || ceil_div(Fo, 16 * ntw) > 4;
+}
+
+size_t sage_wide_workspace_bytes(int64_t K, int64_t n_rows) {
+    return static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * static_cast<size_t>(K) * sizeof(float);
+}
+
+int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                  const int32_t *n_rows_dev, int64_t n_edge_rows, const int32_t *n_edge_rows_dev,
+                  const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,
+                  const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
+                  int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
+                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st) {
+    const int64_t n_edge = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
+    float *agg = nullptr;
+    int64_t lda = ld_agg;
+    if (wl && n_edge > 0) {
+        if (agg_out) {
+            agg = agg_out;
+        } else {
+            NGNN_RETURN_IF(!ws || ws_bytes < sage_wide_workspace_bytes(K, n_edge) || !aligned(ws, 4),
+                           NGNN_E_WORKSPACE);
+            agg = static_cast<float *>(ws);
+            lda = K;
+        }
+        const unsigned ga = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_edge, 4), 8 * num_cus()));
+        auto launch_agg = [&](auto red_c, auto nc_c) {
+            hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
+                               dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
+                               static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, lda,
+                               static_cast<int>(n_rows), 0);
+        };
+        auto by_nc = [&](auto red_c) {
+            if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
+            else if (K <= 512) launch_agg(red_c, std::integral_constant<int, 8>{});
+            else launch_agg(red_c, std::integral_constant<int, 12>{});  // (> 768: passes of 768)
+        };
+        if (reduce == NGNN_REDUCE_MEAN) by_nc(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
+        else if (reduce == NGNN_REDUCE_SUM) by_nc(std::integral_constant<int, NGNN_REDUCE_SUM>{});
+        else by_nc(std::integral_constant<int, NGNN_REDUCE_MAX>{});
+        const int rc = launch_status();
+        if (rc) return rc;
+    }
+    WideArgs a;
+    a.x = x;
+    a.ldx = ldx;
+    a.agg = agg;
+    a.ld_agg = lda;
+    a.wr = wr;
+    a.wl = wl;
+    a.ldw = ldw;
+    a.K = static_cast<int>(K);
+    a.Fo = static_cast<int>(Fo);
+    a.n_rows = static_cast<int>(n_rows);
+    a.n_edge = static_cast<int>(n_edge);
+    a.n_rows_dev = n_rows_dev;
+    a.n_edge_dev = n_edge_rows_dev;
+    a.out = out;
+    a.ldo = ldo;
+    a.epi = Epi{bias, relu, make_dropout(p_drop, seed), 0};
+    a.seed_dev = seed_dev;
+    a.n_ct = static_cast<int>(ceil_div(Fo, WBN));
+    const int64_t tiles = ceil_div(n_rows, WBM) * a.n_ct;
+    NGNN_RETURN_IF(tiles > INT32_MAX, NGNN_E_RANGE);
+    // persistent: two workgroups per CU (55 KiB LDS, 178 VGPRs each), a
+    // multiple of 8 (one per XCD in turn)
+    const int64_t grid = std::max<int64_t>(8, std::min<int64_t>(ceil_div(tiles, 8) * 8, 2 * num_cus()));
+    const bool vout = (ldo % 4 == 0) && aligned(out, 16);
+    if (vout)
+        hipLaunchKernelGGL(k_wide_gemm<true>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_wide_gemm<false>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, a);
+    return launch_status();
+}
+
+}  // namespace ngnn
+
+namespace ngnn {
+// The aggregate of rows [0, ceil16(min(n_edge_rows, *n_edge_rows_dev))) into
+// agg (ld_agg), for the row-tile kernel's pre-aggregated max layers.
+int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
+                        const int32_t *n_rows_dev, int64_t n_edge_rows,
+                        const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
+                        int reduce, float *agg, int64_t ld_agg, hipStream_t st) {
+    const int64_t n_edge = std::max<int64_t>(0, std::min(ceil_div(n_edge_rows, 16) * 16, n_rows));
+    if (n_edge == 0) return NGNN_OK;
+    const unsigned ga = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_edge, 4), 8 * num_cus()));
+    auto launch_agg = [&](auto red_c, auto nc_c) {
+        hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
+                           dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
+                           static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, ld_agg,
+                           static_cast<int>(n_rows), 1);
+    };
+    auto by_nc = [&](auto red_c) {
+        if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
+        else if (K <= 512) launch_agg(red_c, std::integral_constant<int, 8>{});
+        else launch_agg(red_c, std::integral_constant<int, 12>{});
+    };
+    if (reduce == NGNN_REDUCE_MEAN) by_nc(std::integral_constant<int, NGNN_REDUCE_MEAN>{});
+    else if (reduce == NGNN_REDUCE_SUM) by_nc(std::integral_constant<int, NGNN_REDUCE_SUM>{});
+    else by_nc(std::integral_constant<int, NGNN_REDUCE_MAX>{});
+    return launch_status();
+}
+}  // namespace ngnn
+
+extern "C" int ngnn_sage_wide_preferred(int64_t K, int64_t Fo, int exact) {
+    if (K <= 0 || Fo <= 0) return 0;
+    return ngnn::sage_wide_preferred(K, Fo, exact != 0) ? 1 : 0;
+}

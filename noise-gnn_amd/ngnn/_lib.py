@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -25,6 +25,7 @@ FWD_NARROW = 0x200      # same: output layer aggregated in the F_out-wide space
 X_BF16 = 0x400          # same: x rows are bf16 (read as bf16, widened exactly)
 W_BF16 = 0x800          # same: weights are bf16-exact (one split part)
 WL_PREPACKED = 0x1000   # same: ws already holds ngnn_pack_weight(wl)
+OUT_BF16 = 0x2000   # same: out rows bf16 (a bf16 model's hidden activations)
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one
@@ -66,6 +67,7 @@ SIGNATURES = {
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
     "ngnn_sage_fwd_raw_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "ngnn_sage_wide_preferred": (_int, [_i64, _i64, _int]),
     "ngnn_sage_fwd_raw": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int, _p, _p,
                                  _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
@@ -76,6 +78,7 @@ SIGNATURES = {
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
     "ngnn_cast_f32_bf16": (_int, [_p, _p, _i64, _p]),
+    "ngnn_widen_bf16_rows": (_int, [_p, _i64, _i64, _i64, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _int, _i64, _p,
                                _i64, _p, _i64,
                                _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),

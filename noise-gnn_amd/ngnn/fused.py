@@ -159,7 +159,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
                    x_dev: torch.Tensor | None = None, span: str = "sage_fwd",
                    narrow: bool = False, xrow_dev: torch.Tensor | None = None,
                    x_rows: int = 0, w_bf16: bool = False,
-                   wl_packed: torch.Tensor | None = None) -> torch.Tensor:
+                   wl_packed: torch.Tensor | None = None, out_bf16: bool = False) -> torch.Tensor:
     """One fused SAGEConv(+relu+dropout) layer, no autograd.  x_dev: device
     word holding the address of x's rows (zero-copy graph slot); x then only
     supplies the shape.  xrow_dev (with x_dev): device word holding the
@@ -170,17 +170,24 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
     w_bf16: the weights hold bf16-exact values (a bf16 model's parameters,
     widened): NGNN_W_BF16, a one-part split image (same sums, fewer MFMAs and
     wider column slices).  wl_packed: ngnn_pack_weight(wl) kept current by a
-    producer (NGNN_WL_PREPACKED: no pack launch when W_l streams from L2)."""
+    producer (NGNN_WL_PREPACKED: no pack launch when W_l streams from L2).
+    out_bf16: return bf16 rows (NGNN_OUT_BF16, a bf16 model's hidden
+    activations, rounded in the epilogue); fp32 when the layer's kernel
+    cannot (narrow / wide / partial 16-column tiles)."""
     N, K = x.shape
     Fo = wl.shape[0]
-    if x.dtype == torch.bfloat16 and not bf16_rows_ok(x, narrow):
+    if x.dtype == torch.bfloat16 and (not bf16_rows_ok(x, narrow) or (
+            x_dev is None and _lib.load().ngnn_sage_wide_preferred(K, Fo, int(_exact_f32)))):
+        # (the wide path reads fp32 rows: bf16 rows widened, exactly)
         x = x.float()
     xb = x.dtype == torch.bfloat16  # bf16 rows read as such (NGNN_X_BF16)
-    out = torch.empty(N, Fo, dtype=torch.float32, device=x.device)
+    out_bf16 = out_bf16 and not narrow and Fo % 16 == 0
+    out = torch.empty(N, Fo, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
     root = wr is not None  # (None: GCNConv's aggregate-first form, no root term)
     # algorithmic bytes: x + gathered rows + col + rowptr + out;  flops: root GEMM on
     # every row + neighbour GEMM on rows with in-edges (0 if not known: conservative)
-    nbytes = (N * K + block.E * K) * (2 if xb else 4) + (block.E + N * Fo) * 4 + (N + 1) * 4
+    nbytes = ((N * K + block.E * K) * (2 if xb else 4) + block.E * 4 + N * Fo * (2 if out_bf16 else 4)
+              + (N + 1) * 4)
     n_e = int(block.n_active or 0)
     flops = 2 * N * K * Fo * root + 2 * n_e * K * Fo
     # ideal matrix-core time of the instruction mix (DESIGN.md section 5): the
@@ -217,6 +224,12 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         wr_ = _pad_cols(wr_, K4) if root else None
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
+    if (not xb and x_dev is None and xrow_dev is None and not (narrow and agg_out is None)
+            and lib.ngnn_sage_wide_preferred(xk.size(1), Fo, int(_exact_f32))):
+        # the wide path (ngnn_wide.hip): exact f32 MFMA throughout, and the
+        # aggregate of the rows with in-edges written then re-read
+        mfma_s = flops / (MFMA_F32_TFS * 1e12)
+        nbytes += 2 * n_e * K * 4
     ws = _workspace(x.device, "sage_fwd", lib.ngnn_sage_fwd_raw_workspace_bytes(K, Fo, N), zero=True)
     prepacked = 0
     if (wl_packed is not None and not narrow and xk is x and wl_.data_ptr() == wl.data_ptr()
@@ -233,12 +246,18 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
             _lib.ptr(block.col_x) if xrow_dev is not None else None,
             _lib.REDUCE[reduce] | (_lib.MATH_EXACT_F32 if _exact_f32 else 0)
             | (_lib.FWD_NARROW if (narrow and agg_out is None) else 0)
-            | (_lib.X_BF16 if xb else 0) | (_lib.W_BF16 if w1 else 0) | prepacked,
+            | (_lib.X_BF16 if xb else 0) | (_lib.W_BF16 if w1 else 0) | prepacked
+            | (_lib.OUT_BF16 if out_bf16 else 0),
             _lib.ptr(wl_), _lib.ptr(wr_), wl_.stride(0), _lib.ptr(bl), Fo,
             _lib.ptr(out), out.stride(0), int(relu), float(p_drop), seed & (2**64 - 1),
             _lib.ptr(seed_dev), _lib.ptr(agg_out),
             agg_out.stride(0) if agg_out is not None else xk.size(1),
             _lib.ptr(ws), ws.numel() * ws.element_size(), _lib.stream_handle(x.device))
+        if rc == _lib.E_SHAPE and out_bf16:
+            # this layer's kernel writes fp32 rows only
+            return sage_layer_fwd(x, block, reduce, wl, bl, wr, relu, p_drop, seed, agg_out,
+                                  seed_dev, x_dev, span, narrow, xrow_dev, x_rows, w_bf16,
+                                  wl_packed, out_bf16=False)
         if rc == _lib.E_SHAPE and xb and x_dev is None:
             # bf16 rows outside the bf16 envelope: the fp32 path on widened rows
             return sage_layer_fwd(x.float(), block, reduce, wl, bl, wr, relu, p_drop, seed,
@@ -259,9 +278,10 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
 
 def bf16_rows_ok(x: torch.Tensor, narrow: bool = False) -> bool:
     """Can the row-tile kernel read these bf16 rows directly (NGNN_X_BF16)?
-    Split-bf16 root term (not the exact-fp32 mode), not a narrow layer, rows
-    of a multiple of 4 elements on 8-B boundaries, a 16-B aligned base."""
-    return (x.dtype == torch.bfloat16 and not _exact_f32 and not narrow and x.dim() == 2
+    Split-bf16 root term (not the exact-fp32 mode), rows of a multiple of 4
+    elements on 8-B boundaries, a 16-B aligned base (narrow layers too: the
+    output layer reading a bf16 model's hidden activations)."""
+    return (x.dtype == torch.bfloat16 and not _exact_f32 and x.dim() == 2
             and x.stride(1) == 1 and x.size(1) % 4 == 0 and x.stride(0) % 4 == 0
             and x.data_ptr() % 16 == 0)
 
@@ -311,6 +331,10 @@ def gcn_transform_first(x, block: Block, w, b, relu: bool, p_drop: float, seed: 
     GCNConv [ext]): z = x W^T on the row-tile kernel (no bias, no epilogue),
     then ngnn_gcn_agg_fwd: out = act(sum_{j->i} z_j + b) -- the form for
     F_in > F_out (the gather runs at the narrower width)."""
+    if x.dtype != torch.float32:  # this launch reads fp32 rows (no NGNN_X_BF16 here)
+        if x_dev is not None:
+            raise _lib.NGNNError("transform-first GCN layer on a zero-copy non-fp32 input")
+        x = x.float()
     N, K = x.shape
     Fo = w.shape[0]
     ldz = _pad16(Fo)
@@ -393,10 +417,16 @@ class _SAGEStack(torch.autograd.Function):
                 narrow = (wr is not None and last and i > 0
                           and narrow_ok(reduce, h.size(1), wl.shape[0], False, 0.0))
                 agg = None if narrow else agg_buffer(h.size(0), h.size(1), h.device, wl.shape[0])
+                # a bf16 model's hidden activations are bf16 rows (as the
+                # reference's bf16 layers produce them): half the bytes written
+                # here and read by the next layer and the backward.  (MAX keeps
+                # fp32: its backward tie test reads the layer input; GCN stacks
+                # keep fp32 too: their transform-first layers read fp32 rows.)
                 h = sage_layer_fwd(h, block, reduce, wl, bl, wr, relu=relu, p_drop=p_i,
                                    seed=seed_i, agg_out=agg, seed_dev=seed_dev, x_dev=x_dev,
                                    span=f"sage_fwd_l{i}", narrow=narrow, w_bf16=w_bf16,
-                                   **xrow)
+                                   out_bf16=(w_bf16 and not last and reduce != "max"
+                                             and wr is not None), **xrow)
             acts.append(h)
             aggs.append(agg)
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
@@ -464,6 +494,7 @@ class _SAGEStack(torch.autograd.Function):
             Fo, K = wl.shape
             hidden = i != L - 1
             ymask = y_out if hidden else None
+            y_bf16 = ymask is not None and ymask.dtype == torch.bfloat16
             yscale = dropout_scale(p) if (hidden and p > 0.0) else 1.0
             # gradient buffers: the data-parallel bucket's views when the caller
             # registered them (a fresh view each time, so autograd adopts it as
@@ -485,8 +516,9 @@ class _SAGEStack(torch.autograd.Function):
                 with _timing.span("sage_agg_seed_rows", 0, 0):
                     _lib.check(lib.ngnn_seg_agg_fwd(
                         _lib.ptr(h_in), h_in.stride(0), K, _lib.ptr(block.rowptr),
-                        _lib.ptr(block.col), R, red, _lib.F32, _lib.ptr(agg), agg.stride(0),
-                        stream), "ngnn_seg_agg_fwd")
+                        _lib.ptr(block.col), R, red,
+                        _lib.BF16 if h_in.dtype == torch.bfloat16 else _lib.F32, _lib.ptr(agg),
+                        agg.stride(0), stream), "ngnn_seg_agg_fwd")
             wsb = lib.ngnn_sage_wgrad_workspace_bytes(Fo, K)
             ws = _workspace(dev, "wgrad", wsb)
             with _timing.span("sage_wgrad", 0, 0):  # row bound is device-side: no host count
@@ -495,7 +527,9 @@ class _SAGEStack(torch.autograd.Function):
                     ymask.stride(0) if ymask is not None else Fo, yscale, _lib.ptr(h_in),
                     _lib.ptr(block.x_dev) if i == 0 else None,
                     None, _lib.ptr(block.xrow_dev) if i == 0 else None,
-                    block.x_rows if i == 0 else 0, int(h_in.dtype == torch.bfloat16), h_in.stride(0), _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
+                    block.x_rows if i == 0 else 0,
+                    int(h_in.dtype == torch.bfloat16) | (2 if y_bf16 else 0), h_in.stride(0),
+                    _lib.ptr(agg), agg.stride(0), _lib.ptr(block.rowptr), N,
                     bptr(i + 1), Fo, K, _lib.ptr(dwl), _lib.ptr(dbl), _lib.ptr(dwr),
                     _lib.ptr(ws), ws.numel(), stream)
             _lib.check(rc, "ngnn_sage_wgrad")
@@ -506,6 +540,14 @@ class _SAGEStack(torch.autograd.Function):
                 _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
                                                        bptr(i + 1), None, bptr(i), block.E, stream),
                            "ngnn_block_prefix_stats")
+            if y_bf16:
+                # the input-gradient kernels read an fp32 mask: widen its rows
+                # below the output-gradient bound (device-side)
+                ym = _workspace(dev, "ymask_f32", N * Fo * 4).view(torch.float32)[:N * Fo].view(N, Fo)
+                _lib.check(lib.ngnn_widen_bf16_rows(_lib.ptr(ymask), ymask.stride(0), Fo, N,
+                                                    bptr(i + 1), _lib.ptr(ym), Fo, stream),
+                           "ngnn_widen_bf16_rows")
+                ymask = ym
             if not deterministic and Fo < K and reduce in ("sum", "mean"):
                 # narrow-space path: scatter dz (Fo wide), then one MFMA pass
                 dh = torch.empty(N, K, dtype=torch.float32, device=dev)

@@ -175,6 +175,54 @@ def test_narrow_output_layer_matches_oracle(K, Fo, reduce):
         torch.testing.assert_close(got, want, **OUT)
 
 
+@pytest.mark.parametrize("K,Fo", [(767, 512), (768, 1024), (767, 40), (1030, 300), (250, 513)])
+@pytest.mark.parametrize("reduce", ["max", "mean", "sum"])
+def test_wide_layer_matches_oracle(K, Fo, reduce):
+    """The wide path (ngnn_wide.hip: aggregate launch + 2-D tiled fp32-MFMA
+    dual GEMM; Amazon-Computers' 767 -> 512 max layer): output with bias,
+    ReLU and hash dropout against the oracle with the host-replicated mask,
+    the saved aggregate bit-identical to the C oracle's edge-order sums, rows
+    past the edge-row bound (no in-edges) on the root term alone, and the
+    device-side row bound honoured (rows past it untouched)."""
+    from ngnn import _lib
+    from ngnn.fused import agg_buffer
+    if not _lib.load().ngnn_sage_wide_preferred(K, Fo, 0):
+        pytest.skip("shape stays on the row-tile kernel")
+    N, p, seed = 1100, 0.5, 77
+    g = torch.Generator().manual_seed(K + Fo)
+    ei = rand_block(K * 5 + Fo, N, 6000)
+    ei = ei[:, ei[1] < 700]  # rows >= 700 receive no edges
+    x = torch.randn(N, K, generator=g)
+    conv = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
+    with torch.no_grad():
+        pre = conv(x, ei).relu()
+    keep = dropout_keep(seed, N, Fo, p)
+    want = pre * keep * dropout_scale(p)
+    blk = Block(ei.to(DEV), N)
+    blk.n_active = 700
+    agg = agg_buffer(N, K, DEV, Fo)
+    agg.fill_(float("nan"))
+    got = sage_layer_fwd(x.to(DEV), blk, reduce, conv.lin_l.weight.to(DEV),
+                         conv.lin_l.bias.to(DEV), conv.lin_r.weight.to(DEV), relu=True,
+                         p_drop=p, seed=seed, agg_out=agg).cpu()
+    torch.testing.assert_close(got, want, **OUT)
+    want_agg = c_agg.agg_fwd(x.numpy(), ei.numpy(), N, reduce)[:700]
+    assert torch.equal(agg[:700].cpu(), torch.from_numpy(want_agg))
+    # device row bound (a graph slot's row count: the layer's input has 900
+    # rows, every edge source among them), no saved-aggregate buffer
+    ei2 = ei[:, ei[0] < 900]
+    with torch.no_grad():
+        want2 = conv(x[:900], ei2).relu() * keep[:900] * dropout_scale(p)
+    nrd = torch.tensor([900], dtype=torch.int32, device=DEV)
+    blk2 = Block(ei2.to(DEV), N)
+    blk2.n_active = 700
+    blk2.n_rows_dev = nrd
+    got2 = sage_layer_fwd(x.to(DEV), blk2, reduce, conv.lin_l.weight.to(DEV),
+                          conv.lin_l.bias.to(DEV), conv.lin_r.weight.to(DEV), relu=True,
+                          p_drop=p, seed=seed).cpu()
+    torch.testing.assert_close(got2[:900], want2, **OUT)
+
+
 class _MaskedSAGE(pyg_ref.SAGE):
     """Oracle SAGE whose dropout uses given keep masks (one per hidden layer)."""
 
@@ -504,7 +552,10 @@ def test_bf16_rows_equal_widened_rows(K, Fo, reduce):
         o = sage_layer_fwd(x, *args, relu=True, p_drop=0.25, seed=99, agg_out=agg)
         outs.append((o.cpu(), agg.cpu()))
     assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    # the saved aggregate is defined on rows with in-edges (the backward never
+    # reads the others; a pre-aggregated max layer writes them as 0)
+    has = torch.bincount(ei[1], minlength=N) > 0
+    assert torch.equal(outs[0][1][has], outs[1][1][has])
     with torch.no_grad():
         pre = conv(xb.float(), ei).relu()
     keep = dropout_keep(99, N, Fo, 0.25)
@@ -597,3 +648,52 @@ def test_cast_f32_bf16_equals_torch(n):
     torch.cuda.synchronize()
     want = x.to(torch.bfloat16)
     assert torch.equal(y.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.parametrize("layers,train", [(2, False), (3, False), (3, True)])
+def test_bf16_activations_equal_rounded_fp32_rows(layers, train):
+    """A bf16 model's hidden activations are stored as bf16 rows
+    (NGNN_OUT_BF16 epilogue; the next layer reads them with NGNN_X_BF16, the
+    output layer in narrow mode; the backward's weight gradient reads them as
+    bf16 h and bf16 mask rows, the seed-row aggregate rebuild as bf16, the
+    input-gradient kernels through ngnn_widen_bf16_rows).  Against the same
+    stack whose hidden layers write fp32 rows then rounded to the same bf16
+    values: logits bitwise, parameter gradients equal up to the input-gradient
+    scatter's atomic order (one bf16 rounding)."""
+    from ngnn import fused
+    from ngnn.loader import sample_block, synthetic_graph
+    graph = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.01)
+    graph.x = graph.x.to(torch.bfloat16)
+    b = sample_block(graph, graph.train_idx[:512], [10, 8, 5][:layers], seed=2)
+    torch.manual_seed(5)
+    m = ngnn.SAGE(100, 256, 47, layers, dropout=0.5).to(DEV).to(torch.bfloat16)
+    m.train(train)
+    orig = fused.sage_layer_fwd
+    calls = []
+
+    def rounded_fp32_rows(*a, **k):
+        want = k.get("out_bf16", False)
+        calls.append(want)
+        k["out_bf16"] = False
+        h = orig(*a, **k)
+        return h.bfloat16().float() if want else h
+
+    res = []
+    for patch in (False, True):
+        fused.sage_layer_fwd = rounded_fp32_rows if patch else orig
+        try:
+            m.zero_grad(set_to_none=True)
+            torch.manual_seed(42)
+            out = m(b.x, b.edge_index)
+            F.cross_entropy(out[:512].float(), b.y[:512]).backward()
+            torch.cuda.synchronize()
+        finally:
+            fused.sage_layer_fwd = orig
+        res.append((out.detach().float().cpu(),
+                    {k: p.grad.detach().float().cpu().clone() for k, p in m.named_parameters()}))
+    assert calls.count(True) == layers - 1  # every hidden layer asked for bf16 rows
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[0][1]:
+        # (bf16 gradients: a different atomic order may move one rounding)
+        torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=2.0**-8,
+                                   atol=2.0**-8 * float(res[1][1][k].abs().max()), msg=k)

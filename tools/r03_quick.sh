@@ -1,25 +1,35 @@
 #!/bin/bash
-# Quick GPU check: GPU tests, then the computers config and the headline bench.
+# One GPU call: a pytest subset (PYTEST_K, else all -m gpu), then the benches in BENCHES
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-T=${TAG:-q}
+T=${TAG:-r03q}
 O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
-step() {  # name timeout cmd...: stop the call on a crash / timeout
+step() {
   local n=$1 t=$2; shift 2
   timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
   echo "[$n] rc=$rc" | tee -a $O/status.txt
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step pytest_gpu 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread
-tail -1 $O/pytest_gpu.log
-for b in ${BENCHES:-computers headline}; do
-  case $b in
-    computers) step bench_computers 300 python3 bench.py --no-cpu-baseline --dataset computers --fanout 10,5 --batch-size 300 --hidden 512 --aggr max ;;
-    headline) step bench_headline 300 python3 bench.py --no-cpu-baseline ;;
-    p3_f32) step bench_p3_f32 400 python3 bench.py --no-cpu-baseline --fanout 20,15,10 --steps 20 --warmup 5 ;;
-    p3_bf16) step bench_p3_bf16 400 python3 bench.py --no-cpu-baseline --fanout 20,15,10 --steps 20 --warmup 5 --dtype bf16 ;;
+if [ -n "${PYTEST_K:-}" ]; then
+  step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$PYTEST_K"
+  tail -5 $O/pytest.log
+fi
+for c in ${BENCHES:-}; do
+  case $c in
+    headline) A="" ;;
+    computers) A="--dataset computers --fanout 10,5 --batch-size 300 --hidden 512 --aggr max" ;;
+    arxiv) A="--dataset ogbn-arxiv" ;;
+    p3_f32) A="--fanout 20,15,10 --steps 20 --warmup 5" ;;
+    p3_bf16) A="--fanout 20,15,10 --dtype bf16 --steps 20 --warmup 5" ;;
+    gcn) A="--module gcn" ;;
   esac
-  tail -1 $O/bench_$b.log 2>/dev/null | cut -c1-400
+  step bench_$c 400 python3 bench.py --no-cpu-baseline $A
+  tail -1 $O/bench_$c.log | cut -c1-400
+  if [ "${PROF:-0}" = 1 ]; then
+    step prof_$c 400 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-epoch --timer none $A
+    python3 tools/trace_step.py $O/prof_$c/run_kernel_trace.csv --marker k_slot_load --skip 8 --steps 10 > $O/step_$c.txt 2>&1
+    head -24 $O/step_$c.txt
+  fi
 done
 echo done
