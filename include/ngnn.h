@@ -295,7 +295,8 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * weights only, not with NGNN_FWD_NARROW).
  * n_edge_rows / n_edge_rows_dev (device int, nullable, min'd with the
  * host value): rows at or past it have no in-edges (NGNN_FWD_NARROW's
- * gather stops there; NeighborLoader numbers the rows that receive edges
+ * gather stops there, and the row-tile kernel runs the tiles past it on its
+ * root-term-only loop; NeighborLoader numbers the rows that receive edges
  * first).  Pass n_rows when unknown.
  * Wide layers (ngnn_sage_wide_preferred: K % 4 != 0, or F_out needing more
  * than four LDS column slices -- Amazon-Computers' 767 -> 512 layer) with

@@ -176,7 +176,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const int64_t *const *xrow_dev = nullptr, int64_t x_rows = 0,
                      const int32_t *col_x = nullptr, bool x_bf16 = false,
                      bool w_bf16 = false, bool wl_prepacked = false, bool agg_pre = false,
-                     bool out_bf16 = false);
+                     bool out_bf16 = false, int64_t n_edge_rows = -1,
+                     const int32_t *n_edge_rows_dev = nullptr);
 
 // Wide-layer forward (ngnn_wide.hip): an aggregate launch into agg_out (or
 // the workspace) + a 2-D tiled fp32-MFMA dual GEMM.  Raw [F_out, K] weights.

@@ -193,7 +193,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const float *const *x_dev, bool exact, float *z, int64_t ldz,
                      const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
                      const int32_t *col_x, bool x_bf16, bool w_bf16, bool wl_prepacked,
-                     bool agg_pre, bool out_bf16) {
+                     bool agg_pre, bool out_bf16, int64_t n_edge_rows,
+                     const int32_t *n_edge_rows_dev) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -302,6 +303,9 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         }
         a.NT = NT;
         a.NT1 = NT1;
+        // (unknown: every row may have in-edges -- no root-only phase)
+        a.n_edge = static_cast<int>(n_edge_rows < 0 ? n_rows : std::min(n_edge_rows, n_rows));
+        a.n_edge_dev = n_edge_rows_dev;
         a.wz_raw = narrow ? static_cast<const float *>(wl_packed) : nullptr;
         a.z = z;
         a.ldz = ldz;
@@ -310,7 +314,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.ldo = ldo;
         a.vec_out = (Fo_c % 4 == 0) && (ldo % 4 == 0) && aligned(a.out, out_bf16 ? 8 : 16);
         a.out_bf16 = out_bf16;
-        if (out_bf16 && !(a.vec_out && Fo_c % 16 == 0)) {  // bf16 rows: whole 16-column tiles only
+        if (out_bf16 && !(a.vec_out && Fo_c % 16 == 0 && w1)) {  // bf16 rows: whole 16-column tiles of a one-part-image layer
             *rc = NGNN_E_SHAPE;
             return 1;
         }
@@ -396,7 +400,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
                              nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x, x_bf16,
-                             w_bf16, false)) {
+                             w_bf16, false, false, false, n_edge_rows, n_edge_rows_dev)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -434,7 +438,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
                           ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16,
-                          w_bf16, wl_prepacked, agg_pre, out_bf16))
+                          w_bf16, wl_prepacked, agg_pre, out_bf16, n_edge_rows, n_edge_rows_dev))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

@@ -3,6 +3,7 @@
 // instantiation units (ngnn_rt_tu.hip).  See ngnn_sage_rt.hip for the design.
 #pragma once
 #include <cstdlib>
+#include <type_traits>
 
 #include "ngnn_device.h"
 
@@ -25,6 +26,9 @@
 #endif
 #ifndef NGNN_RT_DBG_NOLOAD
 #define NGNN_RT_DBG_NOLOAD 0
+#endif
+#ifndef NGNN_RT_DBG_CONTIG
+#define NGNN_RT_DBG_CONTIG 0  // (diagnostic) output stores at tile-contiguous offsets (wrong layout)
 #endif
 #ifndef NGNN_RT_FAST_BUILD
 #define NGNN_RT_FAST_BUILD 0  // (development builds) 1: the fp32 MEAN kernels only
@@ -114,6 +118,10 @@ struct RtArgs {
     // z = x W_l^T [n_rows, ldz] (the neighbour term is aggregated afterwards
     // in the F_out-wide space); NT1 == NT otherwise
     int NT1;
+    // rows with in-edges all lie below min(n_edge, *n_edge_dev) (n_edge_dev may
+    // be null); the tiles past it run the root-term-only loop
+    int n_edge;
+    const int32_t *n_edge_dev;
     const float *wz_raw;
     float *z;
     int64_t ldz;
@@ -600,24 +608,31 @@ __device__ __forceinline__ int bit_mask_at(uint32_t w, int b) {
     }
 }
 
-// epilogue: lane holds output features m*16 + 4q .. +3 of row r.  Stores go
-// through a buffer resource (rows past n_rows are dropped by the range);
-// `vec` (uniform): F_out a multiple of 16 with 16-B aligned rows -- one
-// 16-B store per m-tile, no per-lane predicates.  Branch-free.
+// epilogue: lane holds output features m*16 + 4q .. +3 of row r; acc already
+// holds b + x W^T (the accumulators start from the bias, read from LDS at the
+// top of the tile, so the epilogue reads nothing).  Stores go through a
+// buffer resource (rows past n_rows are dropped by the range); padded tiles
+// (m >= NT) store past the range (dropped, no branch).  VEC:
+// F_out a multiple of 16 with 16-B aligned rows -- one 16-B store per m-tile
+// at immediate offset 64 m from one per-tile address.  OB: bf16 rows (8-B
+// stores).  NAR: narrow mode -- tiles [NT1, NT) are z = x W_l^T rows (their
+// bias is 0; a uniform branch per tile m).  The per-tile dispatch picks one
+// of these copies once per tile; inside, no branches besides NAR's.
 // DM (dropout mode, ngnn_device.h): 0 none; 1 byte mode -- the lane's four
 // columns f .. f+3 (f = col_base + 16 m + 4 q, col_base a multiple of 16) are
 // one hash quad, pb + 4 m; 2 bit mode (p = 0.5) -- column c is bit c & 31 of
 // hash word c >> 5, so two consecutive 16-column tiles share one word and the
 // lane's four bits of tile m sit at 16 (gc & 1) + 4 q (gc = the global
 // 16-column tile): one shift per tile, then four immediate bit fields.  In
-// bit mode sbias holds 2 b: the survivor scale 2 is folded into the bias
-// add, fma(acc, 2, 2 b) == 2 (acc + b) bitwise, and ReLU is an INTEGER max
+// bit mode the survivor scale 2 is exact (2 acc), and ReLU is an INTEGER max
 // with 0 (a pre-activation with the sign bit set -- negative, -0.0 or a
 // negative-signed NaN -- gives +0.0; a positive NaN passes), then one AND
-// with the keep mask: ~4 VALU per element instead of ~9.
-template <int NTW, int DM, bool RELU, bool VEC>
+// with the keep mask: 3.5 VALU per element.
+template <int NTW, int DM, bool RELU, bool VEC, bool OB, bool NAR, bool ODD = false>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
-                                         i32x4 zr, const float *sbias, int r, int rl, int q) {
+                                         i32x4 zr, int r, int rl, int q) {
+    static_assert(!NAR || (DM == 0 && !RELU && !OB), "narrow: the output layer's plain form");
+    static_assert(!OB || VEC, "bf16 rows: whole 16-column tiles");
     // orsrc / zr: the tile's output / z rows (rl = row in the tile); r, the
     // global row, keys the dropout hash
     const uint32_t thresh = a.epi.drop.thresh;
@@ -626,38 +641,44 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     const uint32_t pb = DM == 1 ? rk + static_cast<uint32_t>((a.epi.col_base + 4 * q) >> 2) : 0u;
     const int cb16 = a.epi.col_base >> 4;  // global 16-column tile of m = 0 (uniform)
     uint32_t hw = 0;                       // bit mode: the current hash word
-    const int ob = a.out_bf16;  // (uniform) 2-byte output elements
-    const int obase = rl * static_cast<int>(a.ldo) * (ob ? 2 : 4);
+    const int obase = rl * static_cast<int>(a.ldo) * (OB ? 2 : 4) + (OB ? 8 : 16) * q;
     // re-materialised per call: the per-tile-index tests below must not be
     // hoisted out of the tile loop as SGPR lane masks (they spill)
     int NT = a.NT, NT1 = a.NT1;
     asm volatile("" : "+s"(NT));
     asm volatile("" : "+s"(NT1));
+    // narrow: z tile m (>= NT1) at zbase + 64 m, the same immediate as out's
+    const int zbase = NAR ? rl * static_cast<int>(a.ldz) * 4 + 16 * q - 64 * NT1 : 0;
 #pragma unroll
     for (int m = 0; m < NTW; ++m) {
-        if (m >= NT) continue;  // padded tiles (uniform)
-        if (m >= NT1) {         // narrow mode: z = x W_l^T rows, no epilogue
-            buf_store4(acc[m], zr, (rl * static_cast<int>(a.ldz) + (m - NT1) * 16 + 4 * q) * 4, 0, 0);
+        // padded tiles (m >= NT, uniform): the store offset past the range
+        // (dropped).  NB the range check covers voffset + imm only, never the
+        // scalar soffset -- a "past the range" soffset would still write.
+        // (select, then + the tile's immediate: kOOB + 64 m stays past every range)
+        const bool live = m < NT;
+        if (NAR && m >= NT1) {  // (uniform branch) z rows: 16-B stores, no epilogue
+            buf_store4(acc[m], zr, (live ? zbase : kOOB) + 64 * m, 0, 0);
             continue;
         }
-        const int f = m * 16 + 4 * q;
-        const v4f b = *reinterpret_cast<const v4f *>(sbias + f);
         const int gc = cb16 + m;  // global 16-column tile (uniform)
-        uint32_t hs = 0;          // bit mode: this lane's four bits of tile m in bits 0..3
+        // (ODD: cb16 is odd -- the tile parity, hence where a new hash word
+        // starts, is compile-time: no branch)
+        const int par = (m + (ODD ? 1 : 0)) & 1;  // (a constant after unrolling)
+        uint32_t hs = 0;  // bit mode: this lane's four bits of tile m in bits 0..3
         if (DM == 2) {
-            if (m == 0 || (gc & 1) == 0) hw = lowbias32(rk + static_cast<uint32_t>(gc >> 1));
-            hs = hw >> (((gc & 1) << 4) + 4 * q);
+            if (m == 0 || par == 0) hw = lowbias32(rk + static_cast<uint32_t>(gc >> 1));
+            hs = hw >> ((par << 4) + 4 * q);
         }
         const uint32_t h = DM == 1 ? lowbias32(pb + 4u * m) : 0u;
         v4f v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (DM == 2) {
-                int yi = __float_as_int(__builtin_fmaf(acc[m][j], 2.0f, b[j]));
+                int yi = __float_as_int(acc[m][j] * 2.0f);
                 if (RELU) yi = max(yi, 0);
                 v[j] = __int_as_float(yi & bit_mask_at(hs, j));
             } else {
-                const float y = acc[m][j] + b[j];
+                const float y = acc[m][j];
                 // y < 0 (ReLU; NaN passes, like torch.relu) or a dropped column -> 0
                 bool zero = RELU && y < 0.0f;
                 if (DM == 1) zero = zero || ((h >> (8 * j)) & 0xffu) < thresh;
@@ -665,20 +686,23 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
             }
         }
         if (NGNN_RT_DBG_NOSTORE && v[0] != 1234.5f) continue;
-        if (VEC && ob) {  // 4 bf16 (hardware RNE), one 8-B store
+        if (OB) {  // 4 bf16 (hardware RNE), one 8-B store
             typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
             const bf16x2 p0{static_cast<__bf16>(v[0]), static_cast<__bf16>(v[1])};
             const bf16x2 p1{static_cast<__bf16>(v[2]), static_cast<__bf16>(v[3])};
             i32x2 w;
             w.x = __builtin_bit_cast(int, p0);
             w.y = __builtin_bit_cast(int, p1);
-            buf_store2i(w, orsrc, obase + 2 * f, 0, 0);
+            buf_store2i(w, orsrc, (live ? obase : kOOB) + 32 * m, 0, 0);
+        } else if (VEC && NGNN_RT_DBG_CONTIG) {  // (diagnostic: tile-contiguous 1-KiB stores)
+            buf_store4(v, orsrc, (live ? (rl + 16 * q) * 16 : kOOB) + 1024 * m, 0, 0);
         } else if (VEC) {
-            buf_store4(v, orsrc, obase + 4 * f, 0, 0);
+            buf_store4(v, orsrc, (live ? obase : kOOB) + 64 * m, 0, 0);
         } else {
+            const int f = m * 16 + 4 * q;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                buf_store1(v[j], orsrc, f + j < a.Fo ? obase + 4 * (f + j) : kOOB, 0, 0);
+                buf_store1(v[j], orsrc, (live && f + j < a.Fo) ? obase + 4 * (16 * m + j) : kOOB, 0, 0);
         }
     }
 }
@@ -808,10 +832,9 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         }
         if (WL_LDS && !have_l)
             for (int i = threadIdx.x; i < nfr; i += RT_WAVES * 64) swl[i] = z;
-        // (bit-mode dropout folds its survivor scale 2 into the bias add: 2 b)
-        const float bsc = a.epi.drop.thresh == 128u ? 2.0f : 1.0f;
+        // (the accumulators' initial value; 0 past F_out and on narrow z tiles)
         for (int i = threadIdx.x; i < NTW * 16; i += RT_WAVES * 64)
-            sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] * bsc : 0.0f;
+            sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] : 0.0f;
     }
     __syncthreads();
 
@@ -839,7 +862,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // that drew them finishing last.  (A chip-wide counter in global memory
     // serialises ~10k same-address atomics: measured 2x slower.)  A wave
     // claims its next tile when it starts the current one.
-    auto claim = [&]() -> int {
+    auto claim = [&]() __attribute__((always_inline)) -> int {
         int j = 0;
         if ((threadIdx.x & 63) == 0) j = atomicAdd(&s_next_tile, 1);
         return static_cast<int>(blockIdx.x) +
@@ -875,7 +898,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // inside its branch): with one multiply after the join, the wait for
     // the n_id load sat at the join and every tile paid a vmcnt(0) -- a drain
     // of the previous tile's output stores -- even without the fused gather.
-    auto row_off = [&](int rr) -> uint32_t {
+    auto row_off = [&](int rr) __attribute__((always_inline)) -> uint32_t {
         if (rr >= n_rows) return static_cast<uint32_t>(kOOB);
         uint32_t o;
         if (xrow) {
@@ -894,14 +917,14 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // empty asm, so nothing derived from them is hoisted and kept live across
     // the tile loop: such invariants were the VGPR spills, and their reloads
     // drained the prefetch with a vmcnt(0))
-    auto lane_ids = [&](int &lane_, int &q_, int &rl_) {
+    auto lane_ids = [&](int &lane_, int &q_, int &rl_) __attribute__((always_inline)) {
         int l = static_cast<int>(threadIdx.x) & 63;
         asm volatile("" : "+v"(l));
         lane_ = l;
         q_ = l >> 4;
         rl_ = l & 15;
     };
-    auto prefetch = [&](int tn, uint32_t roff_tn) {
+    auto prefetch = [&](int tn, uint32_t roff_tn) __attribute__((always_inline)) {
         int lane, q, rl;
         lane_ids(lane, q, rl);
         (void)lane;
@@ -941,7 +964,86 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) asm volatile("" : "+v"(xtn[s2]));
         asm volatile("" : "+v"(nbeg), "+v"(nend));
     }
-    for (; t < n_tiles; t = tnext, ++kt) {
+    // ---- the tile epilogue: one branch-free copy per tile form (uniform
+    // dispatch); acc holds b + x W_r^T (+ agg W_l^T)
+    auto tile_epilogue = [&](const v4f (&acc)[NTW], int t, int r, int rl, int q) __attribute__((always_inline)) {
+        const i32x4 orsrc = a.out_bf16 ? tile_rsrc2(a.out, a.ldo, a.Fo, t, n_rows)
+                                       : tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
+        const i32x4 zr = a.z ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
+        // one branch-free epilogue copy per tile form (uniform dispatch)
+        auto epi = [&](auto dm_c, auto relu_c, auto ob_c, auto nar_c) __attribute__((always_inline)) {
+            constexpr int DMv = decltype(dm_c)::value;
+            constexpr bool RELUv = decltype(relu_c)::value, OBv = decltype(ob_c)::value;
+            constexpr bool NARv = decltype(nar_c)::value;
+            if (DMv == 2 && ((a.epi.col_base >> 4) & 1))
+                epilogue<NTW, DMv, RELUv, VEC, OBv, NARv, true>(acc, a, orsrc, zr, r, rl, q);
+            else
+                epilogue<NTW, DMv, RELUv, VEC, OBv, NARv, false>(acc, a, orsrc, zr, r, rl, q);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        using D0 = std::integral_constant<int, 0>;
+        using D1 = std::integral_constant<int, 1>;
+        using D2 = std::integral_constant<int, 2>;
+        // narrow mode (the output layer: split-bf16, W_l not a neighbour term)
+        constexpr bool CAN_NAR = X3 && WLM == 0 && RED != NGNN_REDUCE_MAX;
+        // bf16 hidden rows: a bf16 model's layers (one-part weight images)
+        constexpr bool CAN_OB = W1 && VEC;
+        auto by_drop = [&](auto ob_c) __attribute__((always_inline)) {
+            if (a.epi.drop.thresh == 128u) {  // bit mode
+                if (a.epi.relu) epi(D2{}, T{}, ob_c, F{});
+                else epi(D2{}, F{}, ob_c, F{});
+            } else if (a.epi.drop.thresh) {
+                if (a.epi.relu) epi(D1{}, T{}, ob_c, F{});
+                else epi(D1{}, F{}, ob_c, F{});
+            } else if (a.epi.relu) {
+                epi(D0{}, T{}, ob_c, F{});
+            } else {
+                epi(D0{}, F{}, ob_c, F{});
+            }
+        };
+        if (CAN_NAR && a.NT1 < a.NT) {
+            if constexpr (CAN_NAR) epi(D0{}, F{}, F{}, T{});
+        } else if (CAN_OB && a.out_bf16) {
+            if constexpr (CAN_OB) by_drop(T{});
+        } else {
+            by_drop(F{});
+        }
+    };
+    // the accumulators start from the bias (one LDS read per output tile,
+    // one wait): b + x W_r^T (+ agg W_l^T), no bias add in the epilogue
+    auto init_acc = [&](v4f (&acc)[NTW], int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int m = 0; m < NTW; ++m) acc[m] = *reinterpret_cast<const v4f *>(sbias + 16 * m + 4 * q);
+    };
+    // X3 fp32 tail steps (the K % 32 columns past the bf16 chunks): every
+    // W value of a step read from LDS before its MFMAs (one wait, not one per
+    // pair of output tiles)
+    auto tail_mfma = [&](v4f (&acc)[NTW], const float (&xt)[X3_TAIL_MAX], int q, int lane) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) {
+            if (s2 < a.T4) {
+                float wt[NTW];
+#pragma unroll
+                for (int m = 0; m < NTW; ++m) wt[m] = swt[(s2 * NTW + m) * 64 + lane];
+                const float xv = __int_as_float(__float_as_int(xt[s2]) & lt_mask(32 * a.C + 4 * s2 + q, a.K));
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < NTW; ++m)
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[m], xv, acc[m], 0, 0, 0);
+            }
+        }
+    };
+    // tiles from t2 on have no in-edges (rows >= the block's edge-row bound,
+    // NeighborLoader's order): phase 2 below, a root-term-only loop (X3)
+    int t2 = n_tiles;
+    if (X3 && !NGNN_RT_STATIC) {
+        int ne = have_l ? a.n_edge : 0;  // (no neighbour term in the kernel: every tile)
+        if (a.n_edge_dev) ne = min(ne, *a.n_edge_dev);
+        t2 = min(n_tiles, (max(ne, 0) + RT_ROWS - 1) / RT_ROWS);
+        if (nchunk > 2) t2 = n_tiles;  // (phase 2 covers 1 or 2 chunks)
+    }
+    for (; t < t2; t = tnext, ++kt) {
 #if NGNN_RT_STATIC
         tnext = tile_of(kt + 1);
         (void)claim;
@@ -957,24 +1059,12 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         const int r = t * RT_ROWS + rl;
         const int beg = nbeg, deg = (nend - nbeg) & nmask;
         const int maxdeg = have_l ? rowgroup_max16(deg) : 0;
+        // the accumulators start from the bias (one LDS read per output tile,
+        // one wait): b + x W_r^T (+ agg W_l^T), no bias add in the epilogue
         v4f acc[NTW];
-#pragma unroll
-        for (int m = 0; m < NTW; ++m) acc[m] = v4f{0.f, 0.f, 0.f, 0.f};
-        if (X3) {
-            // fp32 tail steps (the K % 32 columns past the bf16 chunks) first,
-            // while the prefetched tail values are still this tile's
-#pragma unroll
-            for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) {
-                if (s2 < a.T4) {
-                    const float xv = __int_as_float(__float_as_int(xtn[s2]) &
-                                                    lt_mask(32 * a.C + 4 * s2 + q, a.K));
-#pragma unroll
-                    for (int m = 0; m < NTW; ++m)
-                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(swt[(s2 * NTW + m) * 64 + lane], xv,
-                                                                      acc[m], 0, 0, 0);
-                }
-            }
-        }
+        init_acc(acc, q);
+        // (X3: the tail first, while the prefetched tail values are still this tile's)
+        if (X3) tail_mfma(acc, xtn, q, lane);
 
         // ---- root term: x[r] . W_r^T, chunk by chunk; chunk c+1 (or, in the
         // last chunk, the next tile's chunk 0 and row bounds) loads behind
@@ -1039,24 +1129,87 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             }
         }
 
-        // ---- epilogue (bias, relu, dropout and the stores)
-        const i32x4 orsrc = a.out_bf16 ? tile_rsrc2(a.out, a.ldo, a.Fo, t, n_rows)
-                                       : tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
-        const i32x4 zr = a.z ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
-        if (a.epi.drop.thresh == 128u) {  // bit mode (sbias holds 2 b)
-            if (a.epi.relu)
-                epilogue<NTW, 2, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
-            else
-                epilogue<NTW, 2, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
-        } else if (a.epi.drop.thresh) {
-            if (a.epi.relu)
-                epilogue<NTW, 1, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
-            else
-                epilogue<NTW, 1, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
-        } else if (a.epi.relu) {
-            epilogue<NTW, 0, true, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
-        } else {
-            epilogue<NTW, 0, false, VEC>(acc, a, orsrc, zr, sbias, r, rl, q);
+        // ---- epilogue (relu, dropout and the stores; the bias is in acc)
+        tile_epilogue(acc, t, r, rl, q);
+    }
+
+    // ---- phase 2 (X3): the tiles without in-edges.  The same tail, root
+    // term and epilogue, with the x fragments ping-ponged between two
+    // register sets by STEP (one 128-column chunk of one tile): step s runs on
+    // set s % 2 while step s + 1 (the tile's next chunk, or the next tile's
+    // first) loads into the other.  The chunk count is a compile-time NCH (1:
+    // K <= 140, 2: K <= 268; wider layers stay in phase 1) and the loop body
+    // spans a whole number of steps per set (2 tiles for NCH = 1, 1 for 2), so
+    // every step's set and position is fixed: no register copy, and the wait
+    // for a tile's prefetched fragments counts the previous tile's 16 output
+    // stores as younger (no store drain per tile).  With phase 1's one
+    // loop-carried set the compiler copied the prefetch into it -- waiting
+    // for it -- right before every epilogue.
+    if constexpr (X3 && !NGNN_RT_STATIC) {
+        auto phase2 = [&](auto nch_c) __attribute__((always_inline)) {
+            constexpr int NCH = decltype(nch_c)::value;
+            constexpr int TPB = (NCH % 2) ? 2 : 1;  // tiles per loop body
+            v4f xb[RT_KC];
+            float xtb[X3_TAIL_MAX] = {0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < RT_KC; ++g) xb[g] = v4f{0.f, 0.f, 0.f, 0.f};
+            // settle tile t's fragments (in flight from phase 1's prefetch, or
+            // the first one): a wave entering here straight from the start
+            // has no stores behind them, and the compiler's wait at a loop
+            // head takes the fewest younger memory ops over the entry paths
+#pragma unroll
+            for (int g = 0; g < RT_KC; ++g) asm volatile("" : "+v"(xn[g]));
+#pragma unroll
+            for (int s2 = 0; s2 < X3_TAIL_MAX; ++s2) asm volatile("" : "+v"(xtn[s2]));
+            uint32_t roff = roff_n;  // tile t's row offset
+            v4f acc[NTW];
+            // tile u of the loop body (compile-time u: every step's register
+            // set is fixed); false when the wave has no tiles left
+            auto one_tile = [&](auto u_c) __attribute__((always_inline)) -> bool {
+                constexpr int U = decltype(u_c)::value;
+                int lane, q, rl;
+                lane_ids(lane, q, rl);
+                const int tn = claim();
+                const uint32_t roff_tn = row_off(tn * RT_ROWS + rl);
+                init_acc(acc, q);
+                if constexpr ((U * NCH) % 2 == 0) tail_mfma(acc, xtn, q, lane);
+                else tail_mfma(acc, xtb, q, lane);
+                const int kq8 = a.K - (32 * (a.C - 1) + 8 * q);
+                auto chunk = [&](auto c_c, v4f (&xcur)[RT_KC], v4f (&xnxt)[RT_KC],
+                                 float (&xtnxt)[X3_TAIL_MAX]) __attribute__((always_inline)) {
+                    constexpr int C_ = decltype(c_c)::value;
+                    if constexpr (C_ + 1 < NCH) {
+                        load_x<true, XB>(xnxt, xr, roff, (C_ + 1) * RT_KC * 16, q);
+                    } else {  // the next tile's chunk 0 and tail (past the end: reads 0)
+                        load_x<true, XB>(xnxt, xr, roff_tn, 0, q);
+                        load_xt<XB>(xtnxt, a, xr, roff_tn, q);
+                    }
+                    mfma_group_x3<NTW, XB, W1>(acc, xcur, sw3, pst, 4 * C_, min(4, a.C - 4 * C_),
+                                               a.kpad && C_ == NCH - 1, kq8, lane);
+                };
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                // step s = U NCH + c runs on set s % 2 (xn even, xb odd)
+                if constexpr ((U * NCH) % 2 == 0) chunk(I0{}, xn, xb, xtb);
+                else chunk(I0{}, xb, xn, xtn);
+                if constexpr (NCH == 2) {
+                    if constexpr ((U * NCH + 1) % 2 == 0) chunk(I1{}, xn, xb, xtb);
+                    else chunk(I1{}, xb, xn, xtn);
+                }
+                tile_epilogue(acc, t, t * RT_ROWS + rl, rl, q);
+                t = tn;
+                roff = roff_tn;
+                return t < n_tiles;
+            };
+            while (one_tile(std::integral_constant<int, 0>{})) {
+                if constexpr (TPB == 2) {
+                    if (!one_tile(std::integral_constant<int, 1>{})) break;
+                }
+            }
+        };
+        if (t < n_tiles) {
+            if (nchunk == 1) phase2(std::integral_constant<int, 1>{});
+            else phase2(std::integral_constant<int, 2>{});
         }
     }
 }

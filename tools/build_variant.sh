@@ -1,13 +1,14 @@
 #!/bin/bash
-# Build an A/B variant of libngnn.so with extra -D flags into ablib/<name>.so
-# usage: tools/build_variant.sh NAME "-DFOO=1 ..."
+# Build an A/B variant of libngnn.so with extra -D flags into ablib/<name>.so:
+# the in-tree build's objects are reused, the row-tile kernel units are
+# rebuilt with the flags.  usage: tools/build_variant.sh NAME "-DFOO=1 ..."
 set -eu
 cd "$(dirname "$0")/../noise-gnn_amd/csrc"
 n=$1; shift
-mkdir -p ../../ablib build_$n
-for f in *.hip *.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -I../../include -I. "$@" -c $f -o build_$n/$f.o &
-done
-wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ablib/$n.so build_$n/*.o
+rm -rf build_$n && mkdir -p build_$n ../../ablib
+cp -p build/*.o build_$n/
+rm -f build_$n/ngnn_rt_*.o build_$n/ngnn_sage_rt.hip.o ${RM_OBJS:-}
+make -s -j8 OBJ=build_$n OUT=../../ablib/_$n EXTRA="$*" >/dev/null
+mv ../../ablib/_$n/libngnn.so ../../ablib/$n.so && rmdir ../../ablib/_$n
 rm -rf build_$n
+echo "built ablib/$n.so"
