@@ -214,8 +214,39 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         run()
+    res = {"seq": [], "step": [], "cold": [], "warm": []}
+    # "seq" -- the in-step figure: R timed batches as ONE graph of [slot load,
+    # layer-0 launch] pairs minus a graph of the R slot loads alone, divided by
+    # R (each launch right after its batch's slot load, back to back as in the
+    # step; no event sits next to a single launch)
+    R = min(len(timed), 20)
+    try:
+        gs = []
+        for with_l0 in (True, False):
+            gg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gg):
+                for b in timed[:R]:
+                    gstep.load(b.x, b.edge_index, b.y, zero_copy=gstep.zero_copy,
+                               batch_size=b.batch_size)
+                    if with_l0:
+                        run()
+            gs.append(gg)
+        tt = {0: [], 1: []}
+        for _ in range(3):
+            for i, gg in enumerate(gs):
+                gg.replay()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                gg.replay()
+                e1.record()
+                e1.synchronize()
+                tt[i].append(e0.elapsed_time(e1) * 1e3)
+        res["seq"].append((sorted(tt[0])[1] - sorted(tt[1])[1]) / R)
+        del gs
+    except Exception:  # (a capture this build refuses: the per-launch figures only)
+        res["seq"] = []
     flush = torch.empty(flush_mb << 20, dtype=torch.uint8, device=x.device)
-    res = {"step": [], "cold": [], "warm": []}
     for b in timed:
         for cond in ("step", "cold"):  # (step first: the cold run leaves the rows resident)
             gstep.load(b.x, b.edge_index, b.y, zero_copy=gstep.zero_copy, batch_size=b.batch_size)
@@ -368,7 +399,7 @@ def main():
             # launch from the eager records of those batches
             timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
             l0 = l0_launch_us(gstep, model, args.aggr, timed)
-            ms = l0["step"] * 1e-3 * n
+            ms = l0.get("seq", l0["step"]) * 1e-3 * n
         t = ms * 1e-3
         gbs = nbytes / t / 1e9
         tfs = flops / t / 1e12
@@ -390,17 +421,24 @@ def main():
             "traffic": traffic, "traffic_src": traffic_src, "launches": n,
             "avg_us": round(1e3 * ms / n, 2),
             "timed_in": "timed region (eager)" if not graph else (
+                "in-step sequence: HIP events around one replay of a graph of 20 timed batches' "
+                "[slot load, layer-0 forward] pairs minus one of the 20 slot loads alone, / 20 "
+                "(each launch right after its batch's slot load, back to back, as in the step: "
+                "compare rocprof's in-step average of the layer-0 kernels); alg. bytes/flops per "
+                "launch from an eager pass over the same batches" if (l0 and "seq" in l0) else
                 "HIP events around a graph replay of this one launch on each timed batch, right "
                 "after that batch's slot load (as in the step), over all timed batches after the "
                 "timed region; alg. bytes/flops per launch from an eager pass over the same "
                 "batches" if l0 is not None else
                 "eager pass over the timed batches, right after the graph replays"),
+            "avg_us_single": None if l0 is None else round(l0["step"], 2),
             "avg_us_cold": None if l0 is None else round(l0["cold"], 2),
             "avg_us_warm": None if l0 is None else round(l0["warm"], 2),
             "cold_warm_note": None if l0 is None else (
-                "avg_us: after the slot load as in the step; cold: after a 512 MiB write "
-                "(L2 and MALL hold none of the input); warm: an immediate second launch on the "
-                "same batch (partly MALL-resident)"),
+                "avg_us: the in-step sequence (timed_in); single: events around one replay of "
+                "the launch alone right after its slot load (includes the graph-launch gap); "
+                "cold: the same after a 512 MiB write (L2 and MALL hold none of the input); "
+                "warm: an immediate second launch on the same batch (partly MALL-resident)"),
             "avg_us_eager_pass": None if eager_us is None else round(eager_us, 2),
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),

@@ -177,7 +177,10 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const int32_t *col_x = nullptr, bool x_bf16 = false,
                      bool w_bf16 = false, bool wl_prepacked = false, bool agg_pre = false,
                      bool out_bf16 = false, int64_t n_edge_rows = -1,
-                     const int32_t *n_edge_rows_dev = nullptr);
+                     const int32_t *n_edge_rows_dev = nullptr, void *img_ws = nullptr);
+// the tail of ngnn_sage_fwd_raw's workspace that holds a slice's prebuilt
+// X3 root image (ngnn_root.hip: k_x3_image)
+constexpr size_t kImgWsBytes = 160 * 1024;
 
 // Wide-layer forward (ngnn_wide.hip): an aggregate launch into agg_out (or
 // the workspace) + a 2-D tiled fp32-MFMA dual GEMM.  Raw [F_out, K] weights.
@@ -186,7 +189,8 @@ size_t sage_wide_workspace_bytes(int64_t K, int64_t n_rows);
 int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                         const int32_t *n_rows_dev, int64_t n_edge_rows,
                         const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
-                        int reduce, float *agg, int64_t ld_agg, hipStream_t st);
+                        int reduce, float *agg, int64_t ld_agg, hipStream_t st,
+                        const float *const *x_dev = nullptr);
 int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const int32_t *n_rows_dev, int64_t n_edge_rows, const int32_t *n_edge_rows_dev,
                   const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,

@@ -42,6 +42,8 @@
 // Bytes per launch: 4*(N*K + E*K + E + N + 1 + N*F_out) (x, gathered rows,
 // col, rowptr, out) + the optional saved aggregate; flops 2*N*K*F_out +
 // 2*N_edge_rows*K*F_out.
+#include <cstdlib>
+
 #include "ngnn_sage_rt_kern.h"
 
 namespace ngnn {
@@ -194,7 +196,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                      const int64_t *xrow, const int64_t *const *xrow_dev, int64_t x_rows,
                      const int32_t *col_x, bool x_bf16, bool w_bf16, bool wl_prepacked,
                      bool agg_pre, bool out_bf16, int64_t n_edge_rows,
-                     const int32_t *n_edge_rows_dev) {
+                     const int32_t *n_edge_rows_dev, void *img_ws) {
     // (with x_dev the run-time address must be 16-B aligned, as torch's are)
     if (K % 4 != 0 || ldx % 4 != 0 || (!x_dev && !aligned(x, 16))) return 0;
     if (ldw && (ldw % 4 != 0 || !aligned(wr_packed, 16) || (wl_packed && !aligned(wl_packed, 16))))
@@ -306,6 +308,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         // (unknown: every row may have in-edges -- no root-only phase)
         a.n_edge = static_cast<int>(n_edge_rows < 0 ? n_rows : std::min(n_edge_rows, n_rows));
         a.n_edge_dev = n_edge_rows_dev;
+        a.root_split = 0;
         a.wz_raw = narrow ? static_cast<const float *>(wl_packed) : nullptr;
         a.z = z;
         a.ldz = ldz;
@@ -333,7 +336,40 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.col_x = (xrow || xrow_dev) ? col_x : nullptr;
         a.x_bf16 = x_bf16;
         a.w1 = w1;
+        // the split-bf16 root image built once (k_x3_image) into img_ws and
+        // DMA-copied by every workgroup (else each workgroup builds it)
+        a.img = nullptr;
+        if (x3 && !no_root && img_ws && x3_image_bytes(NTW, C, T4, w1) <= kImgWsBytes) {
+            *rc = build_image(a, NTW, img_ws, st);
+            if (*rc) return 1;
+        }
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
+        // the tiles past the edge-row bound on k_root (ngnn_root.hip) when an
+        // instantiation covers this layer: k_sage_rt takes the tiles with
+        // in-edges (none in narrow mode), then k_root the rest
+        const bool vec = a.vec_out && (a.Fo == a.NT * 16);
+        const int form = (x3 && !NGNN_RT_STATIC && !no_root) ? rt_form(a, NTW, vec) : 0;
+        // policy (NGNN_ROOT, read once): 1 (default) k_root for layers with no
+        // in-kernel neighbour term (narrow mode: every tile); 2 also split the
+        // layers with edge tiles (k_sage_rt edge tiles, then k_root -- measured
+        // slower on products layer 0: the edge tiles alone then hold the GPU
+        // ~48 us, in one launch they overlap the root tiles); 0 never
+        static const int policy = [] {
+            const char *e = std::getenv("NGNN_ROOT");
+            return e ? std::atoi(e) : 1;
+        }();
+        const bool want_root = policy == 2 || (policy == 1 && !a.wl);
+        if (form && want_root && launch_root(a, NTW, form, vec, st, true) == NGNN_OK) {
+            if (a.wl) {
+                a.root_split = 1;
+                *rc = dispatch_rt(NTW, a, reduce, wl_lds, x3, n_tiles, lds, st);
+                if (*rc) return 1;
+                a.root_split = 0;
+            }
+            *rc = launch_root(a, NTW, form, vec, st);
+            if (*rc) return 1;
+            continue;
+        }
         *rc = dispatch_rt(NTW, a, reduce, wl_lds, x3, n_tiles, lds, st);
         if (*rc) return 1;
     }
@@ -352,7 +388,8 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64
     const size_t wide = (sage_wide_preferred(K, Fo, false) || sage_wide_preferred(K, Fo, true))
                             ? sage_wide_workspace_bytes(K, n_rows)
                             : 0;
-    return std::max({ngnn_pack_weight_bytes(Fo, K), z, wide});
+    // + the prebuilt root image at the workspace's tail (kImgWsBytes)
+    return std::max({ngnn_pack_weight_bytes(Fo, K), z, wide}) + kImgWsBytes;
 }
 
 extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *xrow,
@@ -393,6 +430,20 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     // narrow mode (MEAN / SUM): the neighbour term aggregated in the F_out-wide
     // space (z = x W_l^T, then a gather of z), no saved aggregate
     const int64_t ldz = ceil_div(Fo, 16) * 16;
+    // the root image's region: the workspace's last kImgWsBytes (16-B aligned)
+    // when the rest still holds z (narrow) / a packed W_l
+    const size_t head = want_narrow ? static_cast<size_t>(n_rows) * ldz * sizeof(float)
+                                    : ngnn_pack_weight_bytes(Fo, K);
+    void *img_ws = nullptr;
+    // (NGNN_IMG=0, read once: every workgroup builds its image -- A/B only)
+    static const bool img_on = [] {
+        const char *e = std::getenv("NGNN_IMG");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (img_on && ws && aligned(ws, 16) && ws_bytes >= head + kImgWsBytes + 16) {
+        const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - kImgWsBytes) & ~uintptr_t(15);
+        img_ws = reinterpret_cast<void *>(e);
+    }
     if (want_narrow && wl && reduce != NGNN_REDUCE_MAX && !agg_out && !relu && !(p_drop > 0.0f) &&
         ws && aligned(ws, 16) &&
         ws_bytes >= static_cast<size_t>(n_rows) * ldz * sizeof(float)) {
@@ -400,7 +451,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         if (sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo,
                              out, ldo, relu, p_drop, seed, seed_dev, nullptr, K, st, &rc, ldw,
                              nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x, x_bf16,
-                             w_bf16, false, false, false, n_edge_rows, n_edge_rows_dev)) {
+                             w_bf16, false, false, false, n_edge_rows, n_edge_rows_dev, img_ws)) {
             if (rc) return rc;
             const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
             const unsigned grid = static_cast<unsigned>(
@@ -428,17 +479,26 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     // row-tile kernel's edge tiles then read densely -- its in-kernel gather
     // walks 16-row tiles one 128-column chunk at a time (Amazon-Computers'
     // 512 -> 10 layer: 67 us for ~3k rows with in-edges)
-    const bool agg_pre = reduce == NGNN_REDUCE_MAX && wl && agg_out && x && !x_dev && !xrow &&
-                         !xrow_dev && !x_bf16 && K >= 256 && ld_agg % 4 == 0 && aligned(agg_out, 16);
+    // NGNN_AGGPRE (read once; A/B): 1 -- mean / sum layers too (layer 0 of
+    // products: its 16.2 k rows with in-edges gathered at full occupancy
+    // instead of inside the row-tile kernel, one wave per 16-row tile)
+    static const int aggpre_all = [] {
+        const char *e = std::getenv("NGNN_AGGPRE");
+        return e ? std::atoi(e) : 0;
+    }();
+    const bool agg_pre = (reduce == NGNN_REDUCE_MAX ? K >= 256 : aggpre_all == 1) && wl && agg_out &&
+                         (x || x_dev) && !xrow && !xrow_dev && !x_bf16 && ld_agg % 4 == 0 &&
+                         aligned(agg_out, 16);
     if (agg_pre) {
         rc = sage_wide_aggregate(x, ldx, K, n_rows, n_rows_dev, n_edge_rows, n_edge_rows_dev, rowptr,
-                                 col, reduce, agg_out, ld_agg, st);
+                                 col, reduce, agg_out, ld_agg, st, x_dev);
         if (rc) return rc;
     }
     if (!sage_fwd_rowtile(x, ldx, K, n_rows, n_rows_dev, rowptr, col, reduce, wl, wr, bias, Fo, out,
                           ldo, relu, p_drop, seed, seed_dev, agg_out, ld_agg, st, &rc, ldw, ws,
                           ws_bytes, x_dev, exact, nullptr, 0, xrow, xrow_dev, x_rows, col_x, x_bf16,
-                          w_bf16, wl_prepacked, agg_pre, out_bf16, n_edge_rows, n_edge_rows_dev))
+                          w_bf16, wl_prepacked, agg_pre, out_bf16, n_edge_rows, n_edge_rows_dev,
+                          img_ws))
         return NGNN_E_SHAPE;  // outside the row-tile envelope: pack + ngnn_sage_fwd
     return rc;
 }

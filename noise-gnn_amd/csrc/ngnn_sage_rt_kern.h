@@ -122,6 +122,13 @@ struct RtArgs {
     // be null); the tiles past it run the root-term-only loop
     int n_edge;
     const int32_t *n_edge_dev;
+    // 1: the tiles past the edge-row bound belong to k_root (ngnn_root.hip,
+    // launched after this kernel): stop there
+    int root_split;
+    // non-null: the X3 root image (sw3 + tail, the LDS layout) prebuilt in
+    // global memory by k_x3_image -- the prologue copies it by LDS-DMA
+    // instead of every workgroup splitting W_r from scattered row reads
+    const v4f *img;
     const float *wz_raw;
     float *z;
     int64_t ldz;
@@ -628,7 +635,7 @@ __device__ __forceinline__ int bit_mask_at(uint32_t w, int b) {
 // with 0 (a pre-activation with the sign bit set -- negative, -0.0 or a
 // negative-signed NaN -- gives +0.0; a positive NaN passes), then one AND
 // with the keep mask: 3.5 VALU per element.
-template <int NTW, int DM, bool RELU, bool VEC, bool OB, bool NAR, bool ODD = false>
+template <int NTW, int DM, bool RELU, bool VEC, bool OB, bool NAR, bool ODD = false, bool NARF = false>
 __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a, i32x4 orsrc,
                                          i32x4 zr, int r, int rl, int q) {
     static_assert(!NAR || (DM == 0 && !RELU && !OB), "narrow: the output layer's plain form");
@@ -648,7 +655,7 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     asm volatile("" : "+s"(NT));
     asm volatile("" : "+s"(NT1));
     // narrow: z tile m (>= NT1) at zbase + 64 m, the same immediate as out's
-    const int zbase = NAR ? rl * static_cast<int>(a.ldz) * 4 + 16 * q - 64 * NT1 : 0;
+    const int zbase = NAR ? rl * static_cast<int>(a.ldz) * 4 + 16 * q - 64 * (NARF ? NTW / 2 : NT1) : 0;
 #pragma unroll
     for (int m = 0; m < NTW; ++m) {
         // padded tiles (m >= NT, uniform): the store offset past the range
@@ -656,7 +663,8 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
         // scalar soffset -- a "past the range" soffset would still write.
         // (select, then + the tile's immediate: kOOB + 64 m stays past every range)
         const bool live = m < NT;
-        if (NAR && m >= NT1) {  // (uniform branch) z rows: 16-B stores, no epilogue
+        // (uniform branch; NARF: NT1 = NTW / 2, compile-time) z rows: 16-B stores, no epilogue
+        if (NAR && (NARF ? m >= NTW / 2 : m >= NT1)) {
             buf_store4(acc[m], zr, (live ? zbase : kOOB) + 64 * m, 0, 0);
             continue;
         }
@@ -707,6 +715,90 @@ __device__ __forceinline__ void epilogue(const v4f (&acc)[NTW], const RtArgs &a,
     }
 }
 
+// The split-bf16 root image in LDS: W_r split into three bf16 parts (one
+// with W1), one lane fragment (8 consecutive k of one output row) per slot,
+// [NP][C][NTW][64] bf16x8, then the fp32 tail [T4][NTW][64]; rows past F_out
+// / columns past K are zero.  Image row n: W_r row n (tiles < NT1), W_l row
+// n - 16 NT1 (narrow mode's tiles [NT1, NT)), nothing for padded tiles (>= NT)
+// or rows past F_out of either half.  All nthreads threads of the workgroup.
+template <int NTW, bool W1>
+__device__ __forceinline__ void build_x3_image(const RtArgs &a, bf16x8 *sw3, float *swt, int pst,
+                                               int nthreads) {
+    auto wrow = [&](int n) -> const float * {
+        if (n >= 16 * a.NT) return nullptr;
+        const bool zt = n >= 16 * a.NT1;
+        const int nn = zt ? n - 16 * a.NT1 : n;
+        const float *base = zt ? a.wz_raw : a.wr_raw;
+        if (nn >= a.Fo || base == nullptr) return nullptr;
+        return base + static_cast<int64_t>(nn) * a.ldw;
+    };
+    // BATCH slots per thread in flight: their global loads issue together
+    // (one L2 round trip per batch, not one per slot -- with 256 threads and
+    // a 3,072-slot image the one-at-a-time loop cost ~10 us per launch)
+    constexpr int BATCH = 8;
+    for (int s0 = threadIdx.x; s0 < pst; s0 += nthreads * BATCH) {
+        v4f lo[BATCH], hi[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            const int sl = s0 + u * nthreads;
+            const int l = sl & 63, mt = (sl >> 6) % NTW, cc = (sl >> 6) / NTW;
+            const int n = mt * 16 + (l & 15), k = 32 * cc + 8 * (l >> 4);
+            lo[u] = v4f{0.f, 0.f, 0.f, 0.f};
+            hi[u] = v4f{0.f, 0.f, 0.f, 0.f};
+            const float *row = sl < pst ? wrow(n) : nullptr;
+            if (row) {
+                const float *src = row + k;
+                if (k + 8 <= a.K) {
+                    lo[u] = gload(reinterpret_cast<const v4f *>(src), 0);
+                    hi[u] = gload(reinterpret_cast<const v4f *>(src + 4), 0);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        lo[u][j] = k + j < a.K ? gload(src, j) : 0.0f;
+                        hi[u][j] = k + 4 + j < a.K ? gload(src, 4 + j) : 0.0f;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            const int sl = s0 + u * nthreads;
+            if (sl >= pst) break;
+            bf16x8 p1, p2, p3;
+            split3(lo[u], hi[u], p1, p2, p3);
+            sw3[sl] = p1;
+            if (!W1) {
+                sw3[pst + sl] = p2;
+                sw3[2 * pst + sl] = p3;
+            }
+        }
+    }
+    const int ntail = a.T4 * NTW * 64;
+    for (int sl = threadIdx.x; sl < ntail; sl += nthreads) {
+        const int l = sl & 63, mt = (sl >> 6) % NTW, st = (sl >> 6) / NTW;
+        const int n = mt * 16 + (l & 15), k = 32 * a.C + 4 * st + (l >> 4);
+        const float *row = wrow(n);
+        swt[sl] = (row && k < a.K) ? row[k] : 0.0f;
+    }
+}
+
+// LDS-DMA copy of a prebuilt image into LDS: the bf16 parts (nv v4f, a
+// multiple of 64: one 1-KiB wave-instruction per 64) and the fp32 tail (nt
+// floats, a multiple of 64: 256-B dword pieces) right behind them, every
+// wave's copies in flight at once (the caller waits vmcnt(0) and barriers)
+__device__ __forceinline__ void dma_image(v4f *dst, const v4f *src, int nv, int nt, int nwaves) {
+    const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int ln = threadIdx.x & 63;
+    for (int c = wv; c < nv / 64; c += nwaves)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 64 + ln),
+                                         (__attribute__((address_space(3))) void *)(dst + c * 64), 16, 0, 0);
+    const float *ts = reinterpret_cast<const float *>(src + nv);
+    float *td = reinterpret_cast<float *>(dst + nv);
+    for (int c = wv; c < nt / 64; c += nwaves)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(ts + c * 64 + ln),
+                                         (__attribute__((address_space(3))) void *)(td + c * 64), 4, 0, 0);
+}
+
 // WLM: W_l source -- 0 streamed from L2 (packed fragments), 1 in LDS.  (A
 // raw-layout L2 stream that saves the pack launch measured slower: 0.373 vs
 // 0.355 ms/step on products, the extra address VALU spills the L0 kernel.)
@@ -738,56 +830,8 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     const int ln = threadIdx.x & 63;
     {
         const int nch = a.NT * a.KG;  // valid 1-KiB fp32 fragments per matrix
-        if (X3) {
-            // W_r split into three bf16 parts, one lane fragment (8 consecutive
-            // k of one output row) per slot; rows past F_out / columns past K
-            // are zero
-            // image row n: W_r row n (tiles < NT1), W_l row n - 16 NT1 (narrow
-            // mode's tiles [NT1, NT)), nothing for padded tiles (>= NT) or
-            // rows past F_out of either half
-            auto wrow = [&](int n) -> const float * {
-                if (n >= 16 * a.NT) return nullptr;
-                const bool zt = n >= 16 * a.NT1;
-                const int nn = zt ? n - 16 * a.NT1 : n;
-                const float *base = zt ? a.wz_raw : a.wr_raw;
-                if (nn >= a.Fo || base == nullptr) return nullptr;
-                return base + static_cast<int64_t>(nn) * a.ldw;
-            };
-            const int nslot = pst;
-            for (int sl = threadIdx.x; sl < nslot; sl += RT_WAVES * 64) {
-                const int l = sl & 63, mt = (sl >> 6) % NTW, cc = (sl >> 6) / NTW;
-                const int n = mt * 16 + (l & 15), k = 32 * cc + 8 * (l >> 4);
-                v4f lo{0.f, 0.f, 0.f, 0.f}, hi{0.f, 0.f, 0.f, 0.f};
-                const float *row = wrow(n);
-                if (row) {
-                    const float *src = row + k;
-                    if (k + 8 <= a.K) {
-                        lo = *reinterpret_cast<const v4f *>(src);
-                        hi = *reinterpret_cast<const v4f *>(src + 4);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            lo[j] = k + j < a.K ? src[j] : 0.0f;
-                            hi[j] = k + 4 + j < a.K ? src[4 + j] : 0.0f;
-                        }
-                    }
-                }
-                bf16x8 p1, p2, p3;
-                split3(lo, hi, p1, p2, p3);
-                sw3[sl] = p1;
-                if (!W1) {
-                    sw3[pst + sl] = p2;
-                    sw3[2 * pst + sl] = p3;
-                }
-            }
-            const int ntail = a.T4 * NTW * 64;
-            for (int sl = threadIdx.x; sl < ntail; sl += RT_WAVES * 64) {
-                const int l = sl & 63, mt = (sl >> 6) % NTW, st = (sl >> 6) / NTW;
-                const int n = mt * 16 + (l & 15), k = 32 * a.C + 4 * st + (l >> 4);
-                const float *row = wrow(n);
-                swt[sl] = (row && k < a.K) ? row[k] : 0.0f;
-            }
-        }
+        if (X3 && a.img) dma_image(lds, a.img, NP * pst, a.T4 * NTW * 64, RT_WAVES);
+        else if (X3) build_x3_image<NTW, W1>(a, sw3, swt, pst, RT_WAVES * 64);
         // fp32 images by LDS-DMA, 1 KiB (one n-tile x k-group fragment) per
         // wave-instruction, all in flight at once; padding tiles zeroed.
         // X3: only W_l (when it lives in LDS); otherwise W_r and W_l.
@@ -807,6 +851,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                     (const __attribute__((address_space(1))) void *)(a.wl + so),
                     (__attribute__((address_space(3))) void *)(swl + d), 16, 0, 0);
         }
+        if (X3 && a.img) __builtin_amdgcn_s_waitcnt(0);  // (the image's LDS-DMAs landed)
         if (a.ldw && (!X3 || (WL_LDS && have_l))) {
             // raw weights: lanes outside F_out x K loaded row 0 / column 0 --
             // zero those slots once this wave's LDS-DMAs have landed
@@ -837,10 +882,14 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
             sbias[i] = (a.epi.bias && i < a.Fo) ? a.epi.bias[i] : 0.0f;
     }
     __syncthreads();
+#ifdef NGNN_DBG_PROLOGUE_ONLY
+    if (a.K != 1234567) return;  // (diagnostic: the image build alone)
+#endif
 
     const int wave = wv;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
+    n_rows = __builtin_amdgcn_readfirstlane(n_rows);  // (provably uniform: scalar resources)
     const int n_tiles = (n_rows + RT_ROWS - 1) / RT_ROWS;
     // 128-column groups of the root term: X3 covers 32 C columns (at least
     // one group, which also carries the next tile's prefetch); fp32 all of K
@@ -966,6 +1015,10 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     }
     // ---- the tile epilogue: one branch-free copy per tile form (uniform
     // dispatch); acc holds b + x W_r^T (+ agg W_l^T)
+    // narrow mode (the output layer: split-bf16, W_l not a neighbour term);
+    // bf16 hidden rows (a bf16 model's layers: one-part weight images)
+    constexpr bool CAN_NAR = X3 && WLM == 0 && RED != NGNN_REDUCE_MAX;
+    constexpr bool CAN_OB = W1 && VEC;
     auto tile_epilogue = [&](const v4f (&acc)[NTW], int t, int r, int rl, int q) __attribute__((always_inline)) {
         const i32x4 orsrc = a.out_bf16 ? tile_rsrc2(a.out, a.ldo, a.Fo, t, n_rows)
                                        : tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
@@ -985,10 +1038,6 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         using D0 = std::integral_constant<int, 0>;
         using D1 = std::integral_constant<int, 1>;
         using D2 = std::integral_constant<int, 2>;
-        // narrow mode (the output layer: split-bf16, W_l not a neighbour term)
-        constexpr bool CAN_NAR = X3 && WLM == 0 && RED != NGNN_REDUCE_MAX;
-        // bf16 hidden rows: a bf16 model's layers (one-part weight images)
-        constexpr bool CAN_OB = W1 && VEC;
         auto by_drop = [&](auto ob_c) __attribute__((always_inline)) {
             if (a.epi.drop.thresh == 128u) {  // bit mode
                 if (a.epi.relu) epi(D2{}, T{}, ob_c, F{});
@@ -1036,12 +1085,28 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     };
     // tiles from t2 on have no in-edges (rows >= the block's edge-row bound,
     // NeighborLoader's order): phase 2 below, a root-term-only loop (X3)
+    // phase 2's epilogue form is fixed per launch (its loop holds ONE
+    // straight-line epilogue: with the per-tile form dispatch inside the loop
+    // the compiler's waits at the tile head stopped counting the previous
+    // tile's stores as younger and drained them every tile).  Forms:
+    // 1 bit-mode dropout + ReLU, 2 ReLU, 3 plain, 4 narrow; +4: bf16 rows.
+    // Other forms (byte-mode dropout, odd column slices) run in phase 1.
+    int p2form = 0;
+    if (CAN_NAR && a.NT1 < a.NT) {
+        // (phase 2's narrow epilogue splits out / z tiles at NTW / 2)
+        if (a.NT == NTW && 2 * a.NT1 == NTW) p2form = 4;
+    } else {
+        const bool odd = (a.epi.col_base >> 4) & 1;
+        if (a.epi.drop.thresh == 128u && a.epi.relu && !odd) p2form = 1;
+        else if (a.epi.drop.thresh == 0u && a.epi.relu) p2form = 2;
+        else if (a.epi.drop.thresh == 0u && !a.epi.relu) p2form = 3;
+        if (p2form && CAN_OB && a.out_bf16) p2form = p2form == 3 ? 0 : p2form + 4;
+    }
     int t2 = n_tiles;
-    if (X3 && !NGNN_RT_STATIC) {
+    if (X3 && !NGNN_RT_STATIC && ((p2form && nchunk <= 2) || a.root_split)) {  // (phase 2 covers 1 or 2 chunks)
         int ne = have_l ? a.n_edge : 0;  // (no neighbour term in the kernel: every tile)
         if (a.n_edge_dev) ne = min(ne, *a.n_edge_dev);
-        t2 = min(n_tiles, (max(ne, 0) + RT_ROWS - 1) / RT_ROWS);
-        if (nchunk > 2) t2 = n_tiles;  // (phase 2 covers 1 or 2 chunks)
+        t2 = __builtin_amdgcn_readfirstlane(min(n_tiles, (max(ne, 0) + RT_ROWS - 1) / RT_ROWS));
     }
     for (; t < t2; t = tnext, ++kt) {
 #if NGNN_RT_STATIC
@@ -1133,6 +1198,8 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
         tile_epilogue(acc, t, r, rl, q);
     }
 
+    if (a.root_split) return;  // (k_root runs the rest)
+
     // ---- phase 2 (X3): the tiles without in-edges.  The same tail, root
     // term and epilogue, with the x fragments ping-ponged between two
     // register sets by STEP (one 128-column chunk of one tile): step s runs on
@@ -1146,8 +1213,12 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
     // loop-carried set the compiler copied the prefetch into it -- waiting
     // for it -- right before every epilogue.
     if constexpr (X3 && !NGNN_RT_STATIC) {
-        auto phase2 = [&](auto nch_c) __attribute__((always_inline)) {
+        auto phase2 = [&](auto nch_c, auto form_c) __attribute__((always_inline)) {
             constexpr int NCH = decltype(nch_c)::value;
+            constexpr int FORM = decltype(form_c)::value;
+            constexpr int FB = FORM > 4 ? FORM - 4 : FORM;  // the form without bf16 rows
+            constexpr int DM = FB == 1 ? 2 : 0;
+            constexpr bool RELU = FB == 1 || FB == 2, OB = FORM > 4, NAR = FB == 4;
             constexpr int TPB = (NCH % 2) ? 2 : 1;  // tiles per loop body
             v4f xb[RT_KC];
             float xtb[X3_TAIL_MAX] = {0.f, 0.f, 0.f};
@@ -1196,7 +1267,12 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                     if constexpr ((U * NCH + 1) % 2 == 0) chunk(I1{}, xn, xb, xtb);
                     else chunk(I1{}, xb, xn, xtn);
                 }
-                tile_epilogue(acc, t, t * RT_ROWS + rl, rl, q);
+                {
+                    const i32x4 orsrc = OB ? tile_rsrc2(a.out, a.ldo, a.Fo, t, n_rows)
+                                           : tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
+                    const i32x4 zr = NAR ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
+                    epilogue<NTW, DM, RELU, VEC, OB, NAR, false, NAR>(acc, a, orsrc, zr, t * RT_ROWS + rl, rl, q);
+                }
                 t = tn;
                 roff = roff_tn;
                 return t < n_tiles;
@@ -1207,9 +1283,24 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                 }
             }
         };
-        if (t < n_tiles) {
-            if (nchunk == 1) phase2(std::integral_constant<int, 1>{});
-            else phase2(std::integral_constant<int, 2>{});
+        auto run = [&](auto form_c) __attribute__((always_inline)) {
+            if (nchunk == 1) phase2(std::integral_constant<int, 1>{}, form_c);
+            else phase2(std::integral_constant<int, 2>{}, form_c);
+        };
+        if (t < n_tiles) {  // (p2form != 0: t2 < n_tiles only then)
+            using IC1 = std::integral_constant<int, 1>;
+            using IC2 = std::integral_constant<int, 2>;
+            using IC3 = std::integral_constant<int, 3>;
+            if (p2form == 1) run(IC1{});
+            else if (p2form == 2) run(IC2{});
+            else if (p2form == 3) run(IC3{});
+            else if (CAN_NAR && p2form == 4) {
+                if constexpr (CAN_NAR) run(std::integral_constant<int, 4>{});
+            } else if (CAN_OB && p2form == 5) {
+                if constexpr (CAN_OB) run(std::integral_constant<int, 5>{});
+            } else if (CAN_OB && p2form == 6) {
+                if constexpr (CAN_OB) run(std::integral_constant<int, 6>{});
+            }
         }
     }
 }
@@ -1273,6 +1364,17 @@ int dispatch_rt_red(const RtArgs &a, bool wl_lds, bool x3, int n_tiles, size_t l
 #define NGNN_RT_FOR_EACH(X) \
     X(2, 0) X(2, 1) X(2, 2) X(3, 0) X(3, 1) X(3, 2) X(4, 0) X(4, 1) X(4, 2) \
     X(6, 0) X(6, 1) X(6, 2) X(8, 0) X(8, 1) X(8, 2) X(16, 0) X(16, 1) X(16, 2)
+// k_root (ngnn_root.hip): the tiles past the edge-row bound on the
+// one-wave-per-SIMD root-term kernel; NGNN_E_SHAPE when no instantiation
+// covers (NTW, C, T4, the epilogue form, bf16 flags) -- nothing launched
+int launch_root(const RtArgs &a, int ntw, int form, bool vec, hipStream_t st, bool dry = false);
+// the epilogue form of a launch (1 bit-mode dropout + ReLU, 2 ReLU, 3 plain,
+// 4 narrow, 5 / 6: 1 / 2 with bf16 rows), 0 for forms without a
+// root-term-only loop
+int rt_form(const RtArgs &a, int ntw, bool vec);
+// bytes of a slice's prebuilt X3 image (ngnn_root.hip) and its build launch
+size_t x3_image_bytes(int ntw, int C, int T4, bool w1);
+int build_image(RtArgs &a, int ntw, void *dst, hipStream_t st);
 #define NGNN_RT_FN(N, R) dispatch_rt_n##N##_r##R
 #define NGNN_RT_DECLARE(N, R) \
     int NGNN_RT_FN(N, R)(const RtArgs &a, bool wl_lds, bool x3, int n_tiles, size_t lds, hipStream_t st);

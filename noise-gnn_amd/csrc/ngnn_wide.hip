@@ -53,8 +53,10 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
                                                   const int32_t *__restrict__ n_rows_dev,
                                                   const int32_t *__restrict__ n_edge_dev,
                                                   float *__restrict__ agg, int64_t ld_agg,
-                                                  int n_cap, int round16) {
+                                                  int n_cap, int round16,
+                                                  const float *const *x_dev) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (x_dev) x = gload(x_dev, 0);  // (a graph slot's batch address, read at run time)
     int rows = n_rows;
     if (n_edge_dev) rows = min(rows, *n_edge_dev);
     // round16: rows up to the end of the last 16-row tile with in-edges (the
@@ -329,7 +331,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                                dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                                static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, lda,
-                               static_cast<int>(n_rows), 0);
+                               static_cast<int>(n_rows), 0, nullptr);
         };
         auto by_nc = [&](auto red_c) {
             if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
@@ -382,7 +384,8 @@ namespace ngnn {
 int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                         const int32_t *n_rows_dev, int64_t n_edge_rows,
                         const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
-                        int reduce, float *agg, int64_t ld_agg, hipStream_t st) {
+                        int reduce, float *agg, int64_t ld_agg, hipStream_t st,
+                        const float *const *x_dev) {
     const int64_t n_edge = std::max<int64_t>(0, std::min(ceil_div(n_edge_rows, 16) * 16, n_rows));
     if (n_edge == 0) return NGNN_OK;
     const unsigned ga = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_edge, 4), 8 * num_cus()));
@@ -390,7 +393,7 @@ int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                            dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                            static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, ld_agg,
-                           static_cast<int>(n_rows), 1);
+                           static_cast<int>(n_rows), 1, x_dev);
     };
     auto by_nc = [&](auto red_c) {
         if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});

@@ -295,7 +295,14 @@ def _prepack_target(model):
     w = model.convs[0].lin_l.weight
     if w.dtype != torch.float32 or not w.is_cuda or w.stride(1) != 1:
         return None
-    return (w, torch.zeros_like(pack_weight(w.detach())))
+    # the packed W_l at the buffer's head; the layer's workspace size (its
+    # tail holds the kernel's prebuilt root image) -- the buffer IS the
+    # captured forward's workspace
+    from . import _lib
+    Fo, K = w.shape
+    n = max(pack_weight(w.detach()).numel(),
+            -(-_lib.load().ngnn_sage_fwd_raw_workspace_bytes(K, Fo, 0) // 4) + 16)
+    return (w, torch.zeros(n, dtype=torch.float32, device=w.device))
 
 
 def slot_size(batch_size: int, fanouts, margin_rows: int = 1024):

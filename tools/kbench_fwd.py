@@ -64,6 +64,7 @@ def main():
                                    agg_out=agg_)
             return f
         empty = Block(torch.empty(2, 0, dtype=torch.long, device=dev), N)
+        empty.n_active = 0  # no row has in-edges (the kernel's root-term-only loop)
         def run_narrow():
             def f():
                 sage_layer_fwd(x, blk, "mean", wl, bl, wr, relu=False, p_drop=0.0, seed=7,
