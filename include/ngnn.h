@@ -303,7 +303,9 @@ int ngnn_sage_fwd(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
  * plain fp32 rows run as an aggregate launch over rows < n_edge_rows (into
  * agg_out, else ws) + a 2-D tiled exact-fp32 MFMA dual GEMM (ngnn_wide.hip).
  * ws: ngnn_sage_fwd_raw_workspace_bytes(K, Fo, n_rows) bytes (calls sharing
- * a ws must be stream-ordered). */
+ * a ws must be stream-ordered); its last 160 KiB hold the launch's prebuilt
+ * split-bf16 root image (k_x3_image) when the rest still fits the z rows /
+ * packed W_l -- a smaller ws makes every workgroup build the image itself. */
 size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64_t n_rows);
 /* 1 when ngnn_sage_fwd_raw runs a [K -> Fo] layer on the wide path (exact:
  * the NGNN_MATH_EXACT_F32 mode), else 0. */
