@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 12
+#define NGNN_ABI_VERSION 13
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -319,6 +319,38 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
                       int64_t Fo, float *out, int64_t ldo, int relu, float p_drop, uint64_t seed,
                       const uint64_t *seed_dev, float *agg_out, int64_t ld_agg, void *ws,
                       size_t ws_bytes, void *stream);
+
+/* Two-layer SAGE forward of the headline shape in three launches
+ * (ngnn_fwd2.hip): sage.py:33-39 for
+ * SAGE(K0, 256, F1, num_layers=2) -- conv0 -> relu -> dropout -> conv1 --
+ * replacing two ngnn_sage_fwd_raw calls (the second with NGNN_FWD_NARROW).
+ * Shape envelope (ngnn_sage2_supported): 96 < K0 <= 128, K0 % 4 == 0, hidden
+ * H == 256, 32 < F1 <= 48, reduce MEAN or SUM.  Weights are the raw PyG
+ * Linear matrices (lin_l / lin_r of each conv, rows of ldw0 / ldw1 floats).
+ *   h   [n_rows, ldh]  = dropout(relu(b0 + x W_r0^T + agg(x) W_l0^T)); only
+ *        rows < min(h_rows, *h_rows_dev) are written (the rows a bounded
+ *        backward reads: pass n_rows to write all);
+ *   agg0 [n_rows, ld_agg] = the layer-0 neighbour aggregate of the rows of
+ *        the 16-row tiles below n_edge_rows (the backward's saved aggregate;
+ *        bit-identical to ngnn_seg_agg_fwd);
+ *   out [n_rows, ldo]  = b1 + h W_r1^T + agg(h) W_l1^T (logits, every row).
+ * Rows at or past min(n_edge_rows, *n_edge_rows_dev) must have no in-edges
+ * (NeighborLoader numbers the rows that receive edges first; pass n_rows
+ * when unknown).  x_dev (nullable): device word holding x's address (graph
+ * slot), x then unused.  Arithmetic: H2 (two fp16 parts per operand after
+ * power-of-two scaling, three MFMA products), inside the fp32 parity bars.
+ * ws: ngnn_sage2_workspace_bytes(K0, F1, n_rows), 256-B aligned. */
+int ngnn_sage2_supported(int64_t K0, int64_t H, int64_t F1, int reduce);
+size_t ngnn_sage2_workspace_bytes(int64_t K0, int64_t F1, int64_t n_rows);
+int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t ldx, int64_t K0,
+                   int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
+                   const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
+                   int reduce, const float *wl0, const float *bl0, const float *wr0,
+                   int64_t ldw0, int64_t H, const float *wl1, const float *bl1,
+                   const float *wr1, int64_t ldw1, int64_t F1, float p_drop, uint64_t seed,
+                   const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
+                   const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
+                   int64_t ldo, void *ws, size_t ws_bytes, void *stream);
 
 /* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
  * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The

@@ -15,6 +15,10 @@
 namespace ngnn {
 namespace {
 
+// the one-launch forward + gradient recounts the labels per workgroup
+// (B^2 / 4 reads): above this many seed rows the O(B) three-launch path
+constexpr int64_t kXentFusedMaxB = 4096;
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(256) void k_xent_bwd(const float *__restrict__ x, i
     // workspace (two losses per step, co-teaching) may have overwritten it
     (void)ws;
     const float lse = row_lse(xr, C, lane);
-    const float scale = *g / *count;
+    const float scale = (g ? *g : 1.0f) / *count;  // (g NULL: the unit scale of loss.backward())
     for (int c = lane; c < C; c += 64) {
         const float p = expf(xr[c] - lse);
         dr[c] = scale * (p - (c == t ? 1.0f : 0.0f));
@@ -122,6 +126,17 @@ __global__ __launch_bounds__(256) void k_xent_bwd(const float *__restrict__ x, i
 // order, and the LAST workgroup to finish (a device ticket) adds the
 // workgroup sums in a fixed order: loss = sum / count, deterministic.
 // ws: partial sums [gridDim.x] floats; ticket (uint32, zero between calls).
+// Every workgroup reads all B labels, so the count costs B^2 / 4 label reads
+// in all: the host takes this kernel only for B <= kXentFusedMaxB (the
+// training step's seed rows) and the three-launch O(B) path above it.
+// The hand-off is the measured gfx950 form of MI355X_MICROARCH.md ("Valid
+// forms", first table row): every partial an agent-scope (sc1) store drained
+// by s_waitcnt vmcnt(0) before ONE agent-scope atomic add per workgroup, the
+// last adder reads every partial with agent-scope (sc1) loads.  It leans on
+// gfx9's vmcnt counting stores and on sc1 codegen, hence the target check.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "k_xent_fused's fence-free hand-off is verified for gfx950 only"
+#endif
 __global__ __launch_bounds__(256) void k_xent_fused(const float *__restrict__ x, int64_t ld, int B,
                                                     int C, const int64_t *__restrict__ y,
                                                     int64_t ignore, float *__restrict__ part,
@@ -364,6 +379,18 @@ extern "C" int ngnn_seed_xent_fwd_grad(const float *logits, int64_t ld, int64_t 
     NGNN_RETURN_IF(!fits_i32(B) || !fits_i32(C), NGNN_E_RANGE);
     NGNN_RETURN_IF(ws_bytes < ngnn_seed_xent_workspace_bytes(B) || !aligned(ws, 16), NGNN_E_WORKSPACE);
     float *w = static_cast<float *>(ws);
+    hipStream_t st = as_stream(stream);
+    if (B > kXentFusedMaxB) {
+        // large seed sets (a full-batch loader): rows, fixed-order sum, then the
+        // gradient rows at unit scale -- O(B) label reads
+        const unsigned grid = static_cast<unsigned>(ceil_div(B, 4));
+        hipLaunchKernelGGL(k_xent_rows, dim3(grid), dim3(256), 0, st, logits, ld, (int)B, (int)C, y,
+                           ignore_index, w);
+        hipLaunchKernelGGL(k_xent_sum, dim3(1), dim3(256), 0, st, w, (int)B, loss, count);
+        hipLaunchKernelGGL(k_xent_bwd, dim3(grid), dim3(256), 0, st, logits, ld, (int)B, (int)C, y,
+                           ignore_index, w, nullptr, count, dlogits, ldd);
+        return launch_status();
+    }
     // the ticket sits past the row-loss area of ngnn_seed_xent_fwd (3 B floats)
     uint32_t *ticket = reinterpret_cast<uint32_t *>(w + 3 * B);
     hipLaunchKernelGGL(k_xent_fused, dim3(static_cast<unsigned>(ceil_div(B, 4))), dim3(256), 0,

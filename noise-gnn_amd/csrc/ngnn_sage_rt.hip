@@ -178,6 +178,23 @@ __global__ __launch_bounds__(256) void k_gcn_agg(const float *__restrict__ z, in
 
 }  // namespace
 
+// out[d, :Fo] += mean / sum_{e into d} z[col[e], :Fo] for the rows with
+// in-edges (the narrow output layer's neighbour term; also ngnn_fwd2.hip)
+int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *rowptr, const int32_t *col,
+                      int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
+                      const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st) {
+    const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
+    const unsigned grid = static_cast<unsigned>(
+        std::max<int64_t>(1, std::min<int64_t>(4 * num_cus(), ceil_div(rows, 16))));
+    if (reduce == NGNN_REDUCE_MEAN)
+        hipLaunchKernelGGL(k_narrow_agg<true>, dim3(grid), dim3(256), 0, st, z, ldz, static_cast<int>(Fo),
+                           rowptr, col, static_cast<int>(n_rows), n_rows_dev, n_edge_rows_dev, out, ldo);
+    else
+        hipLaunchKernelGGL(k_narrow_agg<false>, dim3(grid), dim3(256), 0, st, z, ldz, static_cast<int>(Fo),
+                           rowptr, col, static_cast<int>(n_rows), n_rows_dev, n_edge_rows_dev, out, ldo);
+    return launch_status();
+}
+
 // Returns 1 and stores the launch status in *rc when the row-tile kernel
 // takes this call, 0 when the shape is outside its envelope (the caller then
 // runs the 64-row kernel).  Envelope: no input mask, K % 4 == 0 with 16-B
@@ -453,18 +470,8 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
                              nullptr, 0, x_dev, exact, z, ldz, xrow, xrow_dev, x_rows, col_x, x_bf16,
                              w_bf16, false, false, false, n_edge_rows, n_edge_rows_dev, img_ws)) {
             if (rc) return rc;
-            const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
-            const unsigned grid = static_cast<unsigned>(
-                std::max<int64_t>(1, std::min<int64_t>(4 * num_cus(), ceil_div(rows, 16))));
-            if (reduce == NGNN_REDUCE_MEAN)
-                hipLaunchKernelGGL(k_narrow_agg<true>, dim3(grid), dim3(256), 0, st, z, ldz,
-                                   static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows),
-                                   n_rows_dev, n_edge_rows_dev, out, ldo);
-            else
-                hipLaunchKernelGGL(k_narrow_agg<false>, dim3(grid), dim3(256), 0, st, z, ldz,
-                                   static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows),
-                                   n_rows_dev, n_edge_rows_dev, out, ldo);
-            return launch_status();
+            return narrow_agg_launch(z, ldz, Fo, rowptr, col, n_rows, n_rows_dev, n_edge_rows,
+                                     n_edge_rows_dev, reduce, out, ldo, st);
         }
     }
     // wide layers (the row-tile kernel's weight image too large for its LDS,

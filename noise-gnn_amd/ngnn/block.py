@@ -199,7 +199,9 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     seed_dev: device uint64 dropout seed the producer advances per batch.
     x_dev: device word the producer fills with the address of the feature
     rows the layer-0 kernels must read (zero-copy slot).  r_next: (device int32,
-    R): the producer keeps ngnn_block_prefix_stats' bound for R there.
+    R[, trusted]): the producer keeps ngnn_block_prefix_stats' bound for R
+    there; trusted: the step's loss reads rows < R only, so a forward may keep
+    hidden rows below that bound alone (ngnn.fused.sage2_forward).
     n_edge_rows_dev: device int32 holding n_active for a changing batch.
     xrow: (device word, table rows, col_x): the producer stores the address of
     the batch's n_id in the word when x_dev points at the whole feature table

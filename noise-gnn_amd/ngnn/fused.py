@@ -388,6 +388,74 @@ def _dgrad_fused_ok(Fo: int, K: int) -> bool:
     return Fo <= 512 and 2 * Fo * K * 4 + 4 * 512 * 4 <= 150 * 1024
 
 
+# the two-layer weight-stationary forward (ngnn_sage2_fwd) for the shapes it
+# covers; False: always the per-layer kernels (A/B switch, tests)
+_use_fwd2 = True
+
+
+def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
+    """Does ngnn_sage2_fwd cover this stack?  SAGE(K0, 256, F1) with two
+    layers, mean/sum, fp32 rows and weights, a block whose rows with in-edges
+    are known to come first (a NeighborLoader block: hinted n_active or the
+    graph slot's device word), plain rows (no fused x[n_id] gather)."""
+    if not _use_fwd2 or _exact_f32 or w_bf16 or len(params) != 6 or reduce not in ("mean", "sum"):
+        return False
+    if any(q is None or q.dtype != torch.float32 for q in params):
+        return False
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 4:
+        return False
+    if block.xrow_dev is not None or (block.n_active is None and block.n_edge_rows_dev is None):
+        return False
+    wl0, _, wr0, wl1, _, wr1 = params
+    if wl0.shape != wr0.shape or wl1.shape != wr1.shape or wl1.shape[1] != wl0.shape[0]:
+        return False
+    return bool(_lib.load().ngnn_sage2_supported(x.size(1), wl0.shape[0], wl1.shape[0],
+                                                _lib.REDUCE[reduce]))
+
+
+def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev):
+    """(h, logits, layer-0 aggregate) of a two-layer stack in one call
+    (include/ngnn.h ngnn_sage2_fwd).  h holds the rows the bounded backward
+    reads: every row, or rows < R' when the graph slot vouches that the loss
+    reads rows < its B (block.r_next[2])."""
+    wl0, bl0, wr0, wl1, bl1, wr1 = (q.detach() for q in params)
+    if wl0.stride(1) != 1 or wr0.stride(0) != wl0.stride(0) or wr0.stride(1) != 1:
+        wl0, wr0 = wl0.contiguous(), wr0.contiguous()
+    if wl1.stride(1) != 1 or wr1.stride(0) != wl1.stride(0) or wr1.stride(1) != 1:
+        wl1, wr1 = wl1.contiguous(), wr1.contiguous()
+    bl0, bl1 = bl0.contiguous(), bl1.contiguous()
+    N, K0 = x.shape
+    H, F1 = wl0.shape[0], wl1.shape[0]
+    dev = x.device
+    lib = _lib.load()
+    h = torch.empty(N, H, dtype=torch.float32, device=dev)
+    out = torch.empty(N, F1, dtype=torch.float32, device=dev)
+    agg0 = agg_buffer(N, K0, dev, H)
+    ws = _workspace(dev, "sage2", lib.ngnn_sage2_workspace_bytes(K0, F1, N))
+    n_edge = N if block.n_active is None else min(int(block.n_active), N)
+    rn = block.r_next
+    h_rows_dev = rn[0] if (rn is not None and len(rn) > 2 and rn[2]) else None
+    n_e = int(block.n_active or 0)
+    # algorithmic bytes (DESIGN.md section 5b): x, gathered rows + col + rowptr,
+    # saved aggregate, nb written + read, h rows (all: upper bound), logits + z
+    # written, z gathered + logits read/written by the narrow aggregate
+    nbytes = 4 * (N * K0 + block.E * (K0 + 1) + (N + 1) + 2 * n_e * K0 + 2 * n_e * H + N * H
+                  + N * (F1 + 16 * (-(-F1 // 16))) + block.E * 16 * (-(-F1 // 16)) + 2 * n_e * F1)
+    flops = 2 * N * K0 * H + 2 * n_e * K0 * H + 4 * N * H * F1
+    mfma_s = 3 * flops / 2 / (16 * MFMA_F32_TFS * 1e12)  # three fp16 products per fp32 product
+    with _timing.span("sage_fwd2", nbytes, flops, mfma_s):
+        rc = lib.ngnn_sage2_fwd(
+            _lib.ptr(x), _lib.ptr(block.x_dev), x.stride(0), K0, N, _lib.ptr(block.n_rows_dev),
+            n_edge, _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.REDUCE[reduce], _lib.ptr(wl0), _lib.ptr(bl0), _lib.ptr(wr0), wl0.stride(0), H,
+            _lib.ptr(wl1), _lib.ptr(bl1), _lib.ptr(wr1), wl1.stride(0), F1, float(p_drop),
+            seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(h), h.stride(0), N, _lib.ptr(h_rows_dev),
+            _lib.ptr(agg0), agg0.stride(0), _lib.ptr(out), out.stride(0), _lib.ptr(ws),
+            ws.numel(), _lib.stream_handle(dev))
+    _lib.check(rc, "ngnn_sage2_fwd")
+    return h, out, agg0, h_rows_dev is not None
+
+
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
@@ -395,6 +463,12 @@ class _SAGEStack(torch.autograd.Function):
         L = len(params) // 3
         acts, aggs = [x], []
         h = x
+        ctx.h_partial = False
+        if L == 2 and sage2_ok(x, block, reduce, params, w_bf16):
+            h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, params, p_drop, seed, seed_dev)
+            acts += [h1, h]
+            aggs += [agg0, None]
+            L = 0  # (the per-layer loop below is skipped)
         for i in range(L):
             wl, bl, wr = params[3 * i:3 * i + 3]
             last = i == L - 1
@@ -429,7 +503,7 @@ class _SAGEStack(torch.autograd.Function):
                                              and wr is not None), **xrow)
             acts.append(h)
             aggs.append(agg)
-        ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, L
+        ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, len(params) // 3
         ctx.gouts = gouts  # _GradViews (buffers the weight gradients go into) or None
         ctx.save_for_backward(*acts, *aggs, *params)
         return h
@@ -470,6 +544,10 @@ class _SAGEStack(torch.autograd.Function):
         else:  # read-only: a cached constant (no fill launch per step)
             bnd = const_bounds(dev, L, int(rows_hint))
         bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
+        if ctx.h_partial and not pre_top:
+            # the forward wrote h only below the slot's R' (sage2_forward)
+            raise _lib.NGNNError("this backward needs hidden rows past the slot's bound: the loss "
+                                 "must read rows < the slot's batch size (seed_cross_entropy)")
         if pre_top:
             bp[L - 1] = block.r_next[0].data_ptr()
         bptr = lambda j: bp[j]  # noqa: E731

@@ -226,7 +226,7 @@ class GraphedTrainStep:
         self._pack = _prepack_target(self.model)
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
-                        x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B),
+                        x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B, self.loss_fn is seed_cross_entropy),
                         n_edge_rows_dev=self.n_edge_rows,
                         xrow=(self.xrow_dev, self.x_rows, self.col_x) if self.x_rows else None,
                         wl_prepacked=self._pack)

@@ -41,6 +41,33 @@ def test_abi_version_and_strerror():
     assert b"unknown" in lib.ngnn_strerror(-99)
 
 
+def test_docs_cite_the_current_abi():
+    """INTEGRATION.md's ctypes stub reads the header's version (no stale
+    literal), DESIGN.md states the current one, and every profiles/ file the
+    docs cite exists (the stub asserted 11 against ABI 12)."""
+    import glob
+    root = os.path.dirname(HEADER.rstrip("/")).rsplit("/include", 1)[0]
+    integ = open(os.path.join(root, "INTEGRATION.md")).read()
+    design = open(os.path.join(root, "DESIGN.md")).read()
+    assert not re.search(r"ngnn_abi_version\(\)\s*==\s*\d", integ)
+    assert "NGNN_ABI_VERSION" in integ
+    for v in re.findall(r"ABI v(\d+)", design):
+        assert int(v) == _lib.ABI_VERSION
+    # the stub's version probe, run as written against the built library
+    cwd = os.getcwd()
+    try:
+        os.chdir(root)
+        m = re.search(r'NGNN_ABI_VERSION = int\(re\.search\((.*?)\)\.group\(1\)\)', integ, re.S)
+        assert m, "the stub derives its version from the header"
+        ver = int(eval("re.search(" + m.group(1) + ").group(1)", {"re": re}))
+        assert ver == _lib.load().ngnn_abi_version()
+        for cite in set(re.findall(r"profiles/[A-Za-z0-9_.*\-]+", integ + design)):
+            if cite.endswith((".txt", ".csv", ".log", ".json")) or "*" in cite:
+                assert glob.glob(cite.rstrip(".,)")), f"cited but absent: {cite}"
+    finally:
+        os.chdir(cwd)
+
+
 def test_argument_errors_return_before_launch():
     lib = _lib.load()
     # bad reduce enum, bad dtype, ld < F, null pointers: no kernel is launched

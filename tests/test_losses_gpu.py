@@ -10,7 +10,10 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-@pytest.mark.parametrize("C,B", [(47, 256), (10, 256), (130, 256), (47, 5000)])
+# B <= 4096: the one-launch forward + gradient; larger (a full-batch seed
+# set): the O(B) three-launch path (the one-launch count is O(B^2))
+@pytest.mark.parametrize("C,B", [(47, 256), (10, 256), (130, 256), (47, 4096), (47, 5000),
+                                 (47, 100_000), (10, 200_000)])
 def test_value_and_grad(C, B):
     from ngnn.losses import seed_cross_entropy
     g = torch.Generator().manual_seed(C)
