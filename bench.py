@@ -68,7 +68,8 @@ def parse():
                          "x = graph.x[n_id] unmaterialized and the layer-0 kernels gather the "
                          "rows (graph replay) -- no copy in the loader, +6 us L0 forward and "
                          "+5 us L0 weight gradient in the step (scattered 400-B row reads)")
-    ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg",
+    ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg,"
+                                       "sage2_prep,sage2_edge,sage2_fwd,sage2_narrow",
                     help="comma list of kernel spans timed with HIP events in the timed region "
                          "('all', or 'none' for profiler runs)")
     return ap.parse_args()
@@ -179,7 +180,7 @@ def cpu_baseline(batches, args, layers):
                       f"oracle/pyg_ref.py"}
 
 
-def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
+def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512, dom: str = "sage_fwd_l0"):
     """Per-launch duration of the captured step's layer-0 kernel, measured
     with HIP events on the stream it runs on (events cannot be recorded
     inside the step's own graph on ROCm).  The launch is captured alone into a
@@ -194,8 +195,13 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
       partly MALL-resident: the round-2 figure's condition).
 
     Returns {condition: mean us over the batches}; each figure includes the
-    dispatch gap between an event and the kernel (about 1-2 us)."""
-    from ngnn import fused
+    dispatch gap between an event and the kernel (about 1-2 us).
+
+    dom "sage2_fwd": the two-layer forward's main launch (k_fwd2); its
+    predecessors in the step (weight images, the edge rows' aggregate + nb)
+    run right before it in every graph, and the "seq" figure subtracts a
+    graph that holds them too."""
+    from ngnn import _lib, fused
     from ngnn.block import get_block
     blk = get_block(gstep.ei, gstep.n_cap)
     c = model.convs[0]
@@ -204,16 +210,36 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
     agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])
     p = model.dropout if model.training else 0.0
     w1 = c.lin_l.weight.dtype == torch.bfloat16
+    pre = None
+    if dom == "sage2_fwd":
+        params = [q.detach() for cv in model.convs for q in (cv.lin_l.weight, cv.lin_l.bias,
+                                                            cv.lin_r.weight)]
+        bufs = fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev)
 
-    def run():
-        fused.sage_layer_fwd(x, blk, aggr, wl, bl, wr, relu=True, p_drop=p, seed=0, agg_out=agg,
-                             seed_dev=blk.seed_dev, x_dev=blk.x_dev, xrow_dev=blk.xrow_dev,
-                             x_rows=blk.x_rows, w_bf16=w1)
+        def pre():
+            fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev,
+                                stages=_lib.SAGE2_PREP | _lib.SAGE2_EDGE, bufs=bufs)
+
+        def run():
+            fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev,
+                                stages=_lib.SAGE2_MAIN, bufs=bufs)
+    else:
+        def run():
+            fused.sage_layer_fwd(x, blk, aggr, wl, bl, wr, relu=True, p_drop=p, seed=0, agg_out=agg,
+                                 seed_dev=blk.seed_dev, x_dev=blk.x_dev, xrow_dev=blk.xrow_dev,
+                                 x_rows=blk.x_rows, w_bf16=w1)
+    if pre is not None:
+        pre()
     run()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         run()
+    gpre = None
+    if pre is not None:
+        gpre = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gpre):
+            pre()
     res = {"seq": [], "step": [], "cold": [], "warm": []}
     # "seq" -- the in-step figure: R timed batches as ONE graph of [slot load,
     # layer-0 launch] pairs minus a graph of the R slot loads alone, divided by
@@ -228,6 +254,8 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
                 for b in timed[:R]:
                     gstep.load(b.x, b.edge_index, b.y, zero_copy=gstep.zero_copy,
                                batch_size=b.batch_size)
+                    if pre is not None:
+                        pre()
                     if with_l0:
                         run()
             gs.append(gg)
@@ -244,12 +272,18 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
                 tt[i].append(e0.elapsed_time(e1) * 1e3)
         res["seq"].append((sorted(tt[0])[1] - sorted(tt[1])[1]) / R)
         del gs
-    except Exception:  # (a capture this build refuses: the per-launch figures only)
+    except RuntimeError as e:  # a capture this build refuses: the per-launch figures only
         res["seq"] = []
+        print(f"[bench] in-step sequence timing unavailable: {e}", file=sys.stderr)
     flush = torch.empty(flush_mb << 20, dtype=torch.uint8, device=x.device)
+    hrows = []
     for b in timed:
         for cond in ("step", "cold"):  # (step first: the cold run leaves the rows resident)
             gstep.load(b.x, b.edge_index, b.y, zero_copy=gstep.zero_copy, batch_size=b.batch_size)
+            if cond == "step":  # the rows of h the step writes: the slot's R' (low word)
+                hrows.append(min(int(gstep.r_next.item()) & 0xFFFFFFFF, b.num_nodes))
+            if gpre is not None:
+                gpre.replay()
             if cond == "cold":
                 flush.fill_(cond == "cold")
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -265,7 +299,9 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512):
             if cond == "step":
                 res["warm"].append(evs[2].elapsed_time(evs[3]) * 1e3)
     del flush
-    return {k: sum(v) / len(v) for k, v in res.items() if v}
+    out = {k: sum(v) / len(v) for k, v in res.items() if v}
+    out["hrows"] = hrows
+    return out
 
 
 def _allreduce_name(world: int) -> str:
@@ -393,13 +429,17 @@ def main():
     if dom:
         name, (n, ms, nbytes, flops, mfma_s) = dom
         eager_us = 1e3 * ms / n
-        if graph and name == "sage_fwd_l0" and args.module == "sage":
+        if graph and name in ("sage_fwd_l0", "sage2_fwd") and args.module == "sage":
             # the same kernel on the same timed batches, each right after its
             # slot load (see l0_launch_us); algorithmic bytes / flops per
             # launch from the eager records of those batches
             timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
-            l0 = l0_launch_us(gstep, model, args.aggr, timed)
+            l0 = l0_launch_us(gstep, model, args.aggr, timed, dom=name)
             ms = l0.get("seq", l0["step"]) * 1e-3 * n
+            if name == "sage2_fwd":
+                # in the step h is written only below the slot's R' (the eager
+                # pass writes every row): the in-step algorithmic bytes
+                nbytes -= sum(4 * 256 * (bb.num_nodes - r) for bb, r in zip(timed, l0["hrows"]))
         t = ms * 1e-3
         gbs = nbytes / t / 1e9
         tfs = flops / t / 1e12

@@ -337,20 +337,32 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  * Rows at or past min(n_edge_rows, *n_edge_rows_dev) must have no in-edges
  * (NeighborLoader numbers the rows that receive edges first; pass n_rows
  * when unknown).  x_dev (nullable): device word holding x's address (graph
- * slot), x then unused.  Arithmetic: H2 (two fp16 parts per operand after
+ * slot), x then unused.  xrow / xrow_dev / x_rows / col_x: the fused
+ * x[n_id] gather, as ngnn_sage_fwd_raw's (x is the x_rows-row feature table,
+ * col_x = n_id[col]).  Arithmetic: H2 (two fp16 parts per operand after
  * power-of-two scaling, three MFMA products), inside the fp32 parity bars.
+ * stages: NGNN_SAGE2_ALL, or a subset in order (per-launch timing; the
+ * workspace carries the images, nb and z between stages): PREP the weight
+ * images, EDGE the aggregate + nb of the rows with in-edges, MAIN every
+ * row's layer 0 + layer-1 products, NARROW the z aggregate into out.
  * ws: ngnn_sage2_workspace_bytes(K0, F1, n_rows), 256-B aligned. */
+#define NGNN_SAGE2_PREP 1
+#define NGNN_SAGE2_EDGE 2
+#define NGNN_SAGE2_MAIN 4
+#define NGNN_SAGE2_NARROW 8
+#define NGNN_SAGE2_ALL 15
 int ngnn_sage2_supported(int64_t K0, int64_t H, int64_t F1, int reduce);
 size_t ngnn_sage2_workspace_bytes(int64_t K0, int64_t F1, int64_t n_rows);
-int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t ldx, int64_t K0,
+int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xrow,
+                   const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx, int64_t K0,
                    int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                    const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
-                   int reduce, const float *wl0, const float *bl0, const float *wr0,
+                   const int32_t *col_x, int reduce, const float *wl0, const float *bl0, const float *wr0,
                    int64_t ldw0, int64_t H, const float *wl1, const float *bl1,
                    const float *wr1, int64_t ldw1, int64_t F1, float p_drop, uint64_t seed,
                    const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
                    const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
-                   int64_t ldo, void *ws, size_t ws_bytes, void *stream);
+                   int64_t ldo, int stages, void *ws, size_t ws_bytes, void *stream);
 
 /* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
  * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The

@@ -81,6 +81,28 @@ __device__ __forceinline__ float amax4(v4f v) {
     return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
 
+// cross-lane max of non-negative floats (their bit patterns order as ints),
+// on VALU only (no LDS round trip): DPP inside a 16-lane row, the gfx950
+// permlane swaps across rows
+__device__ __forceinline__ float max_xor16(float v) {  // lanes l and l ^ 16
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
+}
+__device__ __forceinline__ float max_xor32(float v) {  // lanes l and l ^ 32
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
+}
+__device__ __forceinline__ float max_row16(float v) {  // all 16 lanes of the row
+    int x = __float_as_int(v);
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));  // row_mirror
+    return __int_as_float(x);
+}
+
 // three-product H2 MFMA: acc += (a1 + a2)(b1 + b2) - a2 b2, smallest first
 __device__ __forceinline__ v4f mfma_h2(half8 a1, half8 a2, half8 b1, half8 b2, v4f acc) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, b1, acc, 0, 0, 0);
@@ -191,6 +213,10 @@ struct G2Args {
     int n_edge;
     const int32_t *n_edge_dev;
     const int32_t *rowptr, *col;
+    // fused x[n_id] gather: x is the feature table (x_rows rows) and col_x =
+    // n_id[col] (the slot load writes it); null: x holds the block's rows
+    const int32_t *col_x;
+    int64_t x_rows;
     int mean;
     const half8 *img_l0;
     const int *exps;
@@ -225,8 +251,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     __builtin_amdgcn_s_waitcnt(0);  // (this wave's image DMAs landed)
     __syncthreads();
     const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
-    const int64_t xbytes = (static_cast<int64_t>(n_rows) - 1) * a.ldx * 4 + a.K0 * 4;
-    const i32x4 xr = make_rsrc_u(xb, static_cast<uint32_t>(n_rows > 0 ? xbytes : 0));
+    const int32_t *colg = a.col_x ? a.col_x : a.col;  // the gather's source rows
+    const int64_t xrows = a.col_x ? a.x_rows : static_cast<int64_t>(n_rows);
+    const int64_t xbytes = (xrows - 1) * a.ldx * 4 + a.K0 * 4;
+    const i32x4 xr = make_rsrc_u(xb, static_cast<uint32_t>(xrows > 0 ? xbytes : 0));
     const i32x4 ar = make_rsrc(a.agg, static_cast<uint32_t>(a.cap_rows * a.ld_agg * 4));
     const i32x4 nr = make_rsrc(a.nb, static_cast<uint32_t>(a.cap_rows * F2_HID * 4));
     const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
@@ -235,9 +263,8 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
         const int r = t * F2_ROWS + rl;
         const int beg = r < n_rows ? a.rowptr[r] : 0;
         const int deg = r < n_rows ? a.rowptr[r + 1] - beg : 0;
-        int maxdeg = deg;
-        for (int o = 1; o < 16; o <<= 1) maxdeg = max(maxdeg, __shfl_xor(maxdeg, o));
-        maxdeg = __builtin_amdgcn_readfirstlane(maxdeg);
+        // (the 16 rows' max degree: every row group holds the same 16 values)
+        const int maxdeg = __builtin_amdgcn_readfirstlane(__float_as_int(max_row16(__int_as_float(deg))));
         // column offsets of the lane's 2 C0 pieces (past K0: out of range)
         int coff[2 * C0];
 #pragma unroll
@@ -253,7 +280,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
             // rows, F2_NB per round trip
             int cw[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) cw[j] = e0 + j < deg ? gload(a.col, beg + e0 + j) : -1;
+            for (int j = 0; j < 16; ++j) cw[j] = e0 + j < deg ? gload(colg, beg + e0 + j) : -1;
 #pragma unroll
             for (int b4 = 0; b4 < 16; b4 += F2_NB) {
                 if (e0 + b4 >= maxdeg) break;
@@ -288,8 +315,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
 #pragma unroll
         for (int p = 0; p < 2 * C0; ++p)
             buf_store4(acc[p], ar, (coff[p] >= 0 && arow != kOOB2) ? arow + coff[p] : kOOB2, 0, 0);
-        amax = fmaxf(amax, __shfl_xor(amax, 16));
-        amax = fmaxf(amax, __shfl_xor(amax, 32));
+        amax = max_xor32(max_xor16(amax));
         const int ea = h2_exp(amax);
         half8 b1[C0], b2[C0];
 #pragma unroll
@@ -316,6 +342,12 @@ struct F2Args {
     const float *const *x_dev;
     int64_t ldx;
     int K0;
+    // fused x[n_id] gather: row r of the block is row xrow[r] of x (the
+    // feature table, x_rows rows); the device word xrow_dev (graph slot, 0:
+    // plain rows) overrides xrow; both null: identity
+    const int64_t *xrow;
+    const int64_t *const *xrow_dev;
+    int64_t x_rows;
     int n_rows;
     const int32_t *n_rows_dev;
     int n_edge;
@@ -397,8 +429,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     if (ntj == 0) return;  // (uniform over the workgroup)
 
     const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
-    const int64_t xbytes = (static_cast<int64_t>(n_rows) - 1) * a.ldx * 4 + a.K0 * 4;
-    const i32x4 xr = make_rsrc_u(xb, static_cast<uint32_t>(n_rows > 0 ? xbytes : 0));
+    const int64_t *xrow = a.xrow_dev ? gload(a.xrow_dev, 0) : a.xrow;
+    const int64_t xrows = xrow ? a.x_rows : static_cast<int64_t>(n_rows);
+    const int64_t xbytes = (xrows - 1) * a.ldx * 4 + a.K0 * 4;
+    const i32x4 xr = make_rsrc_u(xb, static_cast<uint32_t>(xrows > 0 ? xbytes : 0));
     const int ne16 = (ne + F2_ROWS - 1) / F2_ROWS * F2_ROWS;
     const i32x4 nbr = make_rsrc(a.nb, static_cast<uint32_t>(static_cast<int64_t>(min<int64_t>(ne16, a.cap_rows)) * F2_HID * 4));
     const i32x4 hrs = make_rsrc(a.h, static_cast<uint32_t>(static_cast<int64_t>(hr) * a.ldh * 4));
@@ -413,7 +447,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     auto xload = [&](int j) __attribute__((always_inline)) -> v4f {
         const int row = tile_of(j) * F2_ROWS + srow;
         const bool ok = j < ntj && row < n_rows && scol;
-        return buf_load4(xr, ok ? static_cast<int>(static_cast<uint32_t>(row) * ld4 + 16u * sslot) : kOOB2, 0, 0);
+        // (fused gather: the row's feature-table index; a dependent load, with
+        // four tiles in flight its latency overlaps the tiles in between)
+        const uint32_t src = (xrow && ok) ? static_cast<uint32_t>(gload(xrow, row)) : static_cast<uint32_t>(row);
+        return buf_load4(xr, ok ? static_cast<int>(src * ld4 + 16u * sslot) : kOOB2, 0, 0);
     };
     // nb of the lane's 8 columns (rows past the edge tiles read 0)
     auto nbload = [&](int j, v4f (&nbv)[2]) __attribute__((always_inline)) {
@@ -425,9 +462,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     };
     // row max over the tile row's 32 lanes, scale, split, parts into LDS
     auto split = [&](v4f v, int buf) __attribute__((always_inline)) {
-        float m = amax4(v);
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float m = max_xor16(max_row16(amax4(v)));  // the tile row's 32 lanes
         const int e = h2_exp(m);
         const v4f vs = ldexp4(v, e);
         half4 p1, p2;
@@ -481,9 +516,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, 0);
         // layer 1: this wave's 32 rows of K -- the B fragment is the lane's own
         // 8 values of h (k order 4q + i, 16 + 4q + i: the image matches)
-        float m = fmaxf(amax4(hv[0]), amax4(hv[1]));
-        m = fmaxf(m, __shfl_xor(m, 16));
-        m = fmaxf(m, __shfl_xor(m, 32));
+        const float m = max_xor32(max_xor16(fmaxf(amax4(hv[0]), amax4(hv[1]))));  // lanes rl + 16 q
         const int eh = h2_exp(m);
         half8 h1, h2;
         h2_split(ldexp4(hv[0], eh), ldexp4(hv[1], eh), h1, h2);
@@ -622,22 +655,26 @@ extern "C" size_t ngnn_sage2_workspace_bytes(int64_t K0, int64_t F1, int64_t n_r
     return ws2_layout(K0, F1, n_rows).total + 256;
 }
 
-extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t ldx, int64_t K0,
+extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xrow,
+                              const int64_t *const *xrow_dev, int64_t x_rows, int64_t ldx, int64_t K0,
                               int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                               const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
-                              int reduce, const float *wl0, const float *bl0, const float *wr0,
+                              const int32_t *col_x, int reduce, const float *wl0, const float *bl0, const float *wr0,
                               int64_t ldw0, int64_t H, const float *wl1, const float *bl1,
                               const float *wr1, int64_t ldw1, int64_t F1, float p_drop, uint64_t seed,
                               const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
                               const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
-                              int64_t ldo, void *ws, size_t ws_bytes, void *stream) {
+                              int64_t ldo, int stages, void *ws, size_t ws_bytes, void *stream) {
     NGNN_RETURN_IF(!ngnn_sage2_supported(K0, H, F1, reduce), NGNN_E_SHAPE);
     NGNN_RETURN_IF(n_rows < 0 || n_edge_rows < 0 || h_rows < 0, NGNN_E_ARG);
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
+    NGNN_RETURN_IF(stages <= 0 || stages > NGNN_SAGE2_ALL, NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < K0 || ldx % 4 != 0 || ldw0 < K0 || ldw1 < H || ldh < H || ldh % 4 != 0 ||
                        ld_agg < K0 || ld_agg % 4 != 0 || ldo < F1,
                    NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(n_rows), NGNN_E_RANGE);
+    const bool indexed = xrow || xrow_dev;
+    NGNN_RETURN_IF(indexed && (x_rows <= 0 || !col_x), NGNN_E_ARG);
     if (n_rows == 0) return NGNN_OK;
     NGNN_RETURN_IF((!x && !x_dev) || !rowptr || !col || !wl0 || !bl0 || !wr0 || !wl1 || !bl1 || !wr1 ||
                        !h || !agg0 || !out || !ws,
@@ -647,7 +684,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
                    NGNN_E_ALIGN);
     // 32-bit buffer offsets: every operand under 3.75 GiB
     const int64_t lim = 0xF0000000ll - 4096;
-    NGNN_RETURN_IF(n_rows * ldx * 4 > lim || n_rows * ldh * 4 > lim || n_rows * ld_agg * 4 > lim ||
+    NGNN_RETURN_IF(std::max(n_rows, indexed ? x_rows : 0) * ldx * 4 > lim || n_rows * ldh * 4 > lim || n_rows * ld_agg * 4 > lim ||
                        n_rows * ldo * 4 > lim || n_rows * F2_HID * 4 > lim,
                    NGNN_E_RANGE);
     const Ws2 L = ws2_layout(K0, F1, n_rows);
@@ -665,7 +702,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
     const int64_t cap_rows = ceil_div(n_rows, 16) * 16;
     // the saved aggregate's and nb's rows: whole edge tiles (NB: agg0 must hold
     // ceil16(n_edge) rows when they exceed n_rows -- capped at n_rows here)
-    {
+    if (stages & NGNN_SAGE2_PREP) {
         P2Args p{wr0, wl0, ldw0, static_cast<int>(K0), C0, wr1, wl1, ldw1, static_cast<int>(F1), NT1,
                  img_r0, img_l0, img_1, exps};
         hipLaunchKernelGGL(k_prep2, dim3(3), dim3(1024), 0, st, p);
@@ -673,7 +710,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
         if (rc) return rc;
     }
     const int ncu = num_cus();
-    if (n_edge_rows > 0) {
+    if ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0) {
         G2Args g;
         g.x = x;
         g.x_dev = x_dev;
@@ -685,6 +722,8 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
         g.n_edge_dev = n_edge_rows_dev;
         g.rowptr = rowptr;
         g.col = col;
+        g.col_x = indexed ? col_x : nullptr;
+        g.x_rows = x_rows;
         g.mean = reduce == NGNN_REDUCE_MEAN;
         g.img_l0 = img_l0;
         g.exps = exps;
@@ -698,12 +737,15 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
         if (C0 == 4) rc = launch_edge_nb<4>(g, grid, st);
         if (rc) return rc;
     }
-    {
+    if (stages & NGNN_SAGE2_MAIN) {
         F2Args f;
         f.x = x;
         f.x_dev = x_dev;
         f.ldx = ldx;
         f.K0 = static_cast<int>(K0);
+        f.xrow = xrow;
+        f.xrow_dev = xrow_dev;
+        f.x_rows = x_rows;
         f.n_rows = static_cast<int>(n_rows);
         f.n_rows_dev = n_rows_dev;
         f.n_edge = static_cast<int>(std::min(n_edge_rows, n_rows));
@@ -736,6 +778,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, int64_t
         }
         if (rc) return rc;
     }
+    if (!(stages & NGNN_SAGE2_NARROW)) return NGNN_OK;
     return narrow_agg_launch(z, ldz, F1, rowptr, col, n_rows, n_rows_dev, n_edge_rows, n_edge_rows_dev, reduce,
                              out, ldo, st);
 }

@@ -26,6 +26,7 @@ X_BF16 = 0x400          # same: x rows are bf16 (read as bf16, widened exactly)
 W_BF16 = 0x800          # same: weights are bf16-exact (one split part)
 WL_PREPACKED = 0x1000   # same: ws already holds ngnn_pack_weight(wl)
 OUT_BF16 = 0x2000   # same: out rows bf16 (a bf16 model's hidden activations)
+SAGE2_PREP, SAGE2_EDGE, SAGE2_MAIN, SAGE2_NARROW, SAGE2_ALL = 1, 2, 4, 8, 15  # ngnn_sage2_fwd stages
 F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/ngnn.h one to one
@@ -74,9 +75,10 @@ SIGNATURES = {
                                  _sz, _p]),
     "ngnn_sage2_supported": (_int, [_i64, _i64, _i64, _int]),
     "ngnn_sage2_workspace_bytes": (_sz, [_i64, _i64, _i64]),
-    "ngnn_sage2_fwd": (_int, [_p, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _int, _p, _p, _p, _i64,
+    "ngnn_sage2_fwd": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int,
+                              _p, _p, _p, _i64,
                               _i64, _p, _p, _p, _i64, _i64, ctypes.c_float, ctypes.c_uint64, _p, _p,
-                              _i64, _i64, _p, _p, _i64, _p, _i64, _p, _sz, _p]),
+                              _i64, _i64, _p, _p, _i64, _p, _i64, _int, _p, _sz, _p]),
     "ngnn_gcn_agg_fwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _int, ctypes.c_float,
                                 ctypes.c_uint64, _p, _p, _i64, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),

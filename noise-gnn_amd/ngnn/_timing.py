@@ -71,6 +71,12 @@ class KernelTimer:
         return out
 
 
+def timing() -> bool:
+    """Is a KernelTimer active (callers then split multi-launch calls into
+    one timed span per launch)?"""
+    return _active is not None
+
+
 @contextlib.contextmanager
 def span(name: str, nbytes: int, flops: int = 0, mfma_s: float = 0.0):
     t = _active

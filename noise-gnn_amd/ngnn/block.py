@@ -206,8 +206,9 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     xrow: (device word, table rows, col_x): the producer stores the address of
     the batch's n_id in the word when x_dev points at the whole feature table
     (fused x[n_id] gather), 0 otherwise, and keeps col_x = n_id[col] (int32).
-    wl_prepacked: (W_l parameter, buffer) -- the producer keeps the buffer =
-    ngnn_pack_weight(W_l) current (the slot load's pack job)."""
+    wl_prepacked: (W_l parameter, buffer[, state]) -- the producer keeps the
+    buffer = ngnn_pack_weight(W_l) current (the slot load's pack job); state
+    (ngnn.graphs.PackState): the pack is current only while state.armed."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,

@@ -397,14 +397,14 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
     """Does ngnn_sage2_fwd cover this stack?  SAGE(K0, 256, F1) with two
     layers, mean/sum, fp32 rows and weights, a block whose rows with in-edges
     are known to come first (a NeighborLoader block: hinted n_active or the
-    graph slot's device word), plain rows (no fused x[n_id] gather)."""
+    graph slot's device word); plain rows or the slot's fused x[n_id]."""
     if not _use_fwd2 or _exact_f32 or w_bf16 or len(params) != 6 or reduce not in ("mean", "sum"):
         return False
     if any(q is None or q.dtype != torch.float32 for q in params):
         return False
     if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 4:
         return False
-    if block.xrow_dev is not None or (block.n_active is None and block.n_edge_rows_dev is None):
+    if block.n_active is None and block.n_edge_rows_dev is None:
         return False
     wl0, _, wr0, wl1, _, wr1 = params
     if wl0.shape != wr0.shape or wl1.shape != wr1.shape or wl1.shape[1] != wl0.shape[0]:
@@ -413,11 +413,14 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
                                                 _lib.REDUCE[reduce]))
 
 
-def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev):
-    """(h, logits, layer-0 aggregate) of a two-layer stack in one call
-    (include/ngnn.h ngnn_sage2_fwd).  h holds the rows the bounded backward
-    reads: every row, or rows < R' when the graph slot vouches that the loss
-    reads rows < its B (block.r_next[2])."""
+def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev,
+                  stages: int | None = None, bufs=None):
+    """(h, logits, layer-0 aggregate, h partial?) of a two-layer stack in one
+    call (include/ngnn.h ngnn_sage2_fwd).  h holds the rows the bounded
+    backward reads: every row, or rows < R' when the graph slot vouches that
+    the loss reads rows < its B (block.r_next[2]).  stages / bufs (bench.py's
+    per-launch timing): a subset of the launches, on the (h, out, agg0) of an
+    earlier call."""
     wl0, bl0, wr0, wl1, bl1, wr1 = (q.detach() for q in params)
     if wl0.stride(1) != 1 or wr0.stride(0) != wl0.stride(0) or wr0.stride(1) != 1:
         wl0, wr0 = wl0.contiguous(), wr0.contiguous()
@@ -428,31 +431,49 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     H, F1 = wl0.shape[0], wl1.shape[0]
     dev = x.device
     lib = _lib.load()
-    h = torch.empty(N, H, dtype=torch.float32, device=dev)
-    out = torch.empty(N, F1, dtype=torch.float32, device=dev)
-    agg0 = agg_buffer(N, K0, dev, H)
+    if bufs is None:
+        h = torch.empty(N, H, dtype=torch.float32, device=dev)
+        out = torch.empty(N, F1, dtype=torch.float32, device=dev)
+        agg0 = agg_buffer(N, K0, dev, H)
+    else:
+        h, out, agg0 = bufs[:3]
     ws = _workspace(dev, "sage2", lib.ngnn_sage2_workspace_bytes(K0, F1, N))
     n_edge = N if block.n_active is None else min(int(block.n_active), N)
     rn = block.r_next
     h_rows_dev = rn[0] if (rn is not None and len(rn) > 2 and rn[2]) else None
     n_e = int(block.n_active or 0)
-    # algorithmic bytes: x, gathered rows + col + rowptr,
-    # saved aggregate, nb written + read, h rows (all: upper bound), logits + z
-    # written, z gathered + logits read/written by the narrow aggregate
-    nbytes = 4 * (N * K0 + block.E * (K0 + 1) + (N + 1) + 2 * n_e * K0 + 2 * n_e * H + N * H
-                  + N * (F1 + 16 * (-(-F1 // 16))) + block.E * 16 * (-(-F1 // 16)) + 2 * n_e * F1)
-    flops = 2 * N * K0 * H + 2 * n_e * K0 * H + 4 * N * H * F1
-    mfma_s = 3 * flops / 2 / (16 * MFMA_F32_TFS * 1e12)  # three fp16 products per fp32 product
-    with _timing.span("sage_fwd2", nbytes, flops, mfma_s):
-        rc = lib.ngnn_sage2_fwd(
-            _lib.ptr(x), _lib.ptr(block.x_dev), x.stride(0), K0, N, _lib.ptr(block.n_rows_dev),
-            n_edge, _lib.ptr(block.n_edge_rows_dev), _lib.ptr(block.rowptr), _lib.ptr(block.col),
-            _lib.REDUCE[reduce], _lib.ptr(wl0), _lib.ptr(bl0), _lib.ptr(wr0), wl0.stride(0), H,
+    args = [_lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev), int(block.x_rows),
+            x.stride(0), K0, N, _lib.ptr(block.n_rows_dev), n_edge, _lib.ptr(block.n_edge_rows_dev),
+            _lib.ptr(block.rowptr), _lib.ptr(block.col),
+            _lib.ptr(block.col_x) if block.xrow_dev is not None else None, _lib.REDUCE[reduce], _lib.ptr(wl0), _lib.ptr(bl0), _lib.ptr(wr0), wl0.stride(0), H,
             _lib.ptr(wl1), _lib.ptr(bl1), _lib.ptr(wr1), wl1.stride(0), F1, float(p_drop),
-            seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(h), h.stride(0), N, _lib.ptr(h_rows_dev),
-            _lib.ptr(agg0), agg0.stride(0), _lib.ptr(out), out.stride(0), _lib.ptr(ws),
-            ws.numel(), _lib.stream_handle(dev))
-    _lib.check(rc, "ngnn_sage2_fwd")
+            seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(h), h.stride(0), N,
+            _lib.ptr(h_rows_dev), _lib.ptr(agg0), agg0.stride(0), _lib.ptr(out), out.stride(0)]
+    tail = [_lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)]
+    if stages is not None or not _timing.timing():
+        _lib.check(lib.ngnn_sage2_fwd(*args, _lib.SAGE2_ALL if stages is None else stages, *tail),
+                   "ngnn_sage2_fwd")
+        return h, out, agg0, h_rows_dev is not None
+    # timed: one span per launch.  Algorithmic bytes / flops per launch
+    # (DESIGN.md section 5b); n_e = rows with in-edges (0 when not told: lower bound)
+    C0p = 32 * (-(-K0 // 32))  # K0 padded to the fp16 chunks the MFMAs run
+    ldz = 16 * (-(-F1 // 16))
+    h_rows = N  # (upper bound: under the slot's bound fewer rows are written)
+    f16 = 16 * MFMA_F32_TFS * 1e12  # fp16 MFMA peak; three products per fp32-equivalent product
+    stages = [
+        ("sage2_prep", _lib.SAGE2_PREP, 4 * 3 * H * K0 + 8 * 2 * H * F1, 0, 0.0),
+        ("sage2_edge", _lib.SAGE2_EDGE,
+         4 * (block.E * (K0 + 1) + n_e * (K0 + 1) + n_e * K0 + n_e * H),
+         2 * n_e * K0 * H, 3 * 2 * n_e * C0p * H / f16),
+        ("sage2_fwd", _lib.SAGE2_MAIN,
+         4 * (N * K0 + n_e * H + h_rows * H + N * F1 + N * ldz),
+         2 * N * K0 * H + 4 * N * H * F1, 3 * (2 * N * C0p * H + 2 * N * H * 2 * ldz) / f16),
+        ("sage2_narrow", _lib.SAGE2_NARROW, 4 * (block.E * (ldz + 1) + 2 * n_e * F1 + n_e + 1), 0, 0.0),
+    ]
+    for name, st, nbytes, flops, mfma_s in stages:
+        with _timing.span(name, nbytes, flops, mfma_s):
+            rc = lib.ngnn_sage2_fwd(*args, st, *tail)
+        _lib.check(rc, "ngnn_sage2_fwd")
     return h, out, agg0, h_rows_dev is not None
 
 
@@ -476,9 +497,11 @@ class _SAGEStack(torch.autograd.Function):
             x_dev = block.x_dev if i == 0 else None
             xrow = dict(xrow_dev=block.xrow_dev, x_rows=block.x_rows) if i == 0 else {}
             pk = block.wl_prepacked
-            if (pk is not None and i == 0 and wr is not None
+            if (pk is not None and i == 0 and wr is not None and (len(pk) < 3 or pk[2].armed)
                     and pk[0].data_ptr() == wl.data_ptr() and pk[0].shape == wl.shape):
                 xrow["wl_packed"] = pk[1]
+                if len(pk) > 2:
+                    pk[2].armed = False  # one forward per load (graphs.PackState)
             if wr is None and h.size(1) > wl.shape[0]:
                 # GCN layer narrowing its input: transform first (PyG's order),
                 # no saved aggregate (rebuilt for the rows backward needs)

@@ -158,6 +158,8 @@ class GraphedTrainStep:
               else (None, 0, 0, 0, None)),
             _lib.stream_handle(self.x.device)), "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
+        if self._pack is not None:  # this load packed the current W_l: one forward may use it
+            self._pack[2].armed = True
 
     def _next_gen(self) -> int:
         self._gen += 1
@@ -276,6 +278,8 @@ class GraphedTrainStep:
         count when it is short of the captured B (see load)."""
         self.load(x, edge_index, y, zero_copy=self.zero_copy, batch_size=batch_size)
         self.g_fb.replay()
+        if self._pack is not None:  # the replayed forward consumed this load's pack
+            self._pack[2].armed = False
         if self._split_reduce:
             self.reducer.allreduce()
         elif self.reducer is not None:
@@ -302,7 +306,21 @@ def _prepack_target(model):
     Fo, K = w.shape
     n = max(pack_weight(w.detach()).numel(),
             -(-_lib.load().ngnn_sage_fwd_raw_workspace_bytes(K, Fo, 0) // 4) + 16)
-    return (w, torch.zeros(n, dtype=torch.float32, device=w.device))
+    return (w, torch.zeros(n, dtype=torch.float32, device=w.device), PackState())
+
+
+class PackState:
+    """Validity of the slot's packed W_l: armed by every load() (whose slot
+    kernel packed the weight's values of that moment), consumed by the one
+    forward that reads it (ngnn.fused._SAGEStack).  A later eager forward over
+    the slot -- after an optimizer step, without a new load(), e.g. the
+    warm-up's second step -- packs W_l itself instead of reading a stale pack
+    (ADVICE r3).  Graph replays are unaffected: each follows its own load."""
+
+    __slots__ = ("armed",)
+
+    def __init__(self):
+        self.armed = False
 
 
 def slot_size(batch_size: int, fanouts, margin_rows: int = 1024):

@@ -121,6 +121,53 @@ def test_headline_graph_step_full_products_block():
         assert (p - init[k]).abs().max() <= 1e-3 + 1e-6, k
 
 
+@pytest.mark.timeout(300)
+def test_headline_graph_step_fused_row_gather_vs_oracle():
+    """the headline step with the fused x[n_id] gather
+    (NeighborLoader(gather_features=False): the batch hands the resident
+    feature table + n_id; layer 0's kernels and weight gradient read table
+    rows n_id[r]) against the oracle on the MATERIALIZED rows -- logits of
+    every row, loss, every gradient, post-step parameters."""
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import IndexedRows, sample_block
+    from ngnn.optim import Adam
+    g = _graph("ogbn-products")
+    b = sample_block(g, g.train_idx[:1024], [15, 10], seed=17)
+    b2 = sample_block(g, g.train_idx[1024:2048], [15, 10], seed=18)
+    N = b.num_nodes
+    torch.manual_seed(3)
+    mine = ngnn.SAGE(100, 256, 47, 2, dropout=0.5).to(DEV).train()
+    init = {k: v.detach().cpu().clone() for k, v in mine.state_dict().items()}
+    opt = Adam(mine.parameters(), lr=1e-3)
+    n_cap, e_cap = slot_size(1024, [15, 10])
+    step = GraphedTrainStep(mine, opt, 1024, n_cap, e_cap, 100, DEV)
+    step.capture(IndexedRows(g.x, b2.n_id), b2.edge_index, b2.y)
+    assert step.zero_copy and step.x_rows == g.num_nodes
+    loss = step(IndexedRows(g.x, b.n_id), b.edge_index, b.y)
+    torch.cuda.synchronize()
+    out = step.out[:N].cpu()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
+    seed_state = int(step.seed_state.item()) & (2**64 - 1)
+    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5,
+                      masks=[dropout_keep(seed_state, N, 256, 0.5).float()])
+    ref.load_state_dict(init)
+    xm = g.x[b.n_id].cpu()  # the materialized rows
+    assert torch.equal(xm, b.x.cpu())
+    out_r = ref(xm, b.edge_index.cpu())
+    loss_r = F.cross_entropy(out_r[:1024], b.y[:1024].cpu())
+    loss_r.backward()
+    torch.testing.assert_close(out, out_r.detach(), **OUT)
+    assert abs(float(loss) - float(loss_r)) < 1e-5
+    for k, q in ref.named_parameters():
+        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+    o_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    o_ref.step()
+    for k, q in ref.named_parameters():
+        p = dict(mine.named_parameters())[k].detach().cpu()
+        sure = q.grad.abs() > 1e-4
+        torch.testing.assert_close(p[sure], q.detach()[sure], rtol=0, atol=2e-6, msg=k)
+
+
 def _graph_step(model, b, warm, fanout, bs, in_dim, lr=1e-3):
     """The benched step: GraphedTrainStep (slot load + one captured forward,
     seed-row cross entropy, bounded backward, Adam) on block b after a

@@ -375,3 +375,27 @@ def test_slot_pack_job_equals_pack_weight(fo, k):
     want = pack_weight(w)
     torch.cuda.synchronize()
     assert torch.equal(dst, want)
+
+
+def test_slot_prepacked_wl_never_stale():
+    """the slot's packed layer-0 W_l is valid for the one forward
+    after each load() only.  An eager forward over the slot after a replay
+    (whose Adam changed W_l, no new load) must pack W_l itself: it equals a
+    forward of the same model on an unhinted copy of the batch."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import sample_block, synthetic_graph
+    from ngnn.optim import Adam
+    g = synthetic_graph("ogbn-products", DEV, seed=1, scale=0.02)
+    b = sample_block(g, g.train_idx[:256], [15, 10, 5], seed=3)
+    torch.manual_seed(5)
+    model = ngnn.SAGE(100, 256, 47, 3, dropout=0.0).to(DEV)  # per-layer path: layer 0 streams W_l
+    opt = Adam(model.parameters(), lr=1e-2)
+    n_cap, e_cap = slot_size(256, [15, 10, 5])
+    step = GraphedTrainStep(model, opt, 256, n_cap, e_cap, 100, DEV)
+    step.capture(b.x, b.edge_index, b.y)
+    step(b.x, b.edge_index, b.y)  # load (packs W_l), replay (Adam moves W_l)
+    with torch.no_grad():
+        got = model(step.x, step.ei)[:b.num_nodes]
+        want = model(b.x.clone(), b.edge_index.clone())
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
