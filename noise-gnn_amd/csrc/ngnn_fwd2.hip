@@ -41,6 +41,7 @@
 //              products, the cross-wave sum; then k_narrow_agg (ngnn_sage_rt.hip)
 //              adds mean_j z_j to the rows with in-edges.
 #include <algorithm>
+#include <type_traits>
 
 #include "ngnn_device.h"
 
@@ -130,35 +131,48 @@ struct P2Args {
     int *exps;      // [0] W_r0, [1] W_l0, [2] [W_r1 | W_l1]
 };
 
-// block 0: W_r0, block 1: W_l0, block 2: layer 1.  max |w| over the matrix,
-// its exponent, then every image slot (8 values of one lane, both parts).
-__global__ __launch_bounds__(1024) void k_prep2(P2Args a) {
-    __shared__ float sred[16];
-    const int mat = blockIdx.x;
+// blockIdx.y: 0 W_r0, 1 W_l0, 2 layer 1.  Every block reduces its matrix's
+// max |w| itself (16-B loads, all in flight: ~100 KB per matrix from L2) --
+// no cross-block hand-off -- then writes its share of the image slots (8
+// values of one lane, both parts).
+constexpr int P2_THREADS = 256;
+constexpr int P2_U = 32;  // float4 loads per thread for the max: 32 x 256 = 256 x 128 / 4 (K0 <= 128)
+__global__ __launch_bounds__(P2_THREADS) void k_prep2(P2Args a) {
+    __shared__ float sred[P2_THREADS / 64];
+    const int mat = blockIdx.y;
     float m = 0.0f;
-    if (mat < 2) {
-        const float *w = mat == 0 ? a.wr0 : a.wl0;
-        for (int i = threadIdx.x; i < F2_HID * a.K0; i += blockDim.x) {
-            const int n = i / a.K0, k = i - n * a.K0;
-            m = fmaxf(m, fabsf(w[n * a.ldw0 + k]));
+    {
+        // the matrix as float4 quads (rows are 16-B aligned: K0 and ldw % 4 == 0)
+        const int q0 = mat < 2 ? a.K0 / 4 : F2_HID / 4;  // quads per row
+        const int nr = mat < 2 ? F2_HID : 2 * a.F1;
+        const int nq = nr * q0;
+        v4f t[P2_U];
+#pragma unroll
+        for (int u = 0; u < P2_U; ++u) {
+            const int i = u * P2_THREADS + static_cast<int>(threadIdx.x);
+            const int rr = i / q0, c = i - rr * q0;
+            const float *row;
+            if (mat < 2) row = (mat == 0 ? a.wr0 : a.wl0) + static_cast<int64_t>(min(rr, F2_HID - 1)) * a.ldw0;
+            else {
+                const int z = rr >= a.F1;
+                row = (z ? a.wl1 : a.wr1) + static_cast<int64_t>(min(rr - z * a.F1, a.F1 - 1)) * a.ldw1;
+            }
+            t[u] = i < nq ? *reinterpret_cast<const v4f *>(row + 4 * c) : v4f{0.f, 0.f, 0.f, 0.f};
         }
-    } else {
-        for (int i = threadIdx.x; i < 2 * a.F1 * F2_HID; i += blockDim.x) {
-            const int z = i >= a.F1 * F2_HID;
-            const int ii = i - z * a.F1 * F2_HID, o = ii / F2_HID, k = ii - o * F2_HID;
-            m = fmaxf(m, fabsf((z ? a.wl1 : a.wr1)[o * a.ldw1 + k]));
-        }
+#pragma unroll
+        for (int u = 0; u < P2_U; ++u) m = fmaxf(m, amax4(t[u]));
     }
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = m;
     __syncthreads();
     m = 0.0f;
-    for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) m = fmaxf(m, sred[i]);
+#pragma unroll
+    for (int i = 0; i < P2_THREADS / 64; ++i) m = fmaxf(m, sred[i]);
     const int e = h2_exp(m);
-    if (threadIdx.x == 0) a.exps[mat] = e;
+    if (threadIdx.x == 0 && blockIdx.x == 0) a.exps[mat] = e;
     const int C0 = a.C0, MT1 = 2 * a.NT1;
     const int nslot = mat == 0 ? F2_WAVES * 2 * C0 * 64 : mat == 1 ? (F2_HID / 16) * C0 * 64 : F2_WAVES * MT1 * 64;
-    for (int s = threadIdx.x; s < nslot; s += blockDim.x) {
+    for (int s = blockIdx.x * P2_THREADS + threadIdx.x; s < nslot; s += gridDim.x * P2_THREADS) {
         const int l = s & 63, f = s >> 6, m16 = l & 15, q = l >> 4;
         float v[8];
         int dst;
@@ -370,8 +384,11 @@ struct F2Args {
     int F1;
 };
 
-// DM: dropout mode (0 none, 1 byte, 2 bit: Dropout in ngnn_device.h).
-template <int C0, int NT1, int DM>
+// DM: dropout mode (0 none, 1 byte, 2 bit: Dropout in ngnn_device.h).  XR:
+// the fused x[n_id] gather (rows through n_id, whose loads run two tiles
+// ahead of the row loads: a dependent index load next to them made every
+// tile wait vmcnt(0) -- a drain of the prefetches and the previous stores)
+template <int C0, int NT1, int DM, bool XR>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     constexpr int MT1 = 2 * NT1;
     constexpr int PSTR = 32 * C0 + 8;        // halves per row of a parts buffer (+16 B pad)
@@ -401,10 +418,14 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     v4f b0v[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) b0v[mt] = *reinterpret_cast<const v4f *>(a.b0 + 32 * wv + 16 * mt + 4 * q);
-    // reduce item of this lane (lanes < NIT): output tile mt1, lane lnn of it
+    // reduce item of this lane (lanes < NIT): output tile mt1, lane lnn of it;
+    // items [0, 64 NT1) are out's tiles, the rest z's -- waves 0-3 take out,
+    // waves 4-7 z (NIT = 16 NT1 items per wave), so the store form is
+    // wave-uniform (no exec-divergent store branches: their varying VMEM
+    // counts made the compiler's waits conservative)
     const int item = wv * NIT + (ln < NIT ? ln : 0);
     const int rmt = item >> 6, rln = item & 63;
-    const int rzt = rmt >= NT1;
+    const int rzt = __builtin_amdgcn_readfirstlane(wv) >= F2_WAVES / 2;
     const int rcol = 16 * (rmt - rzt * NT1) + 4 * (rln >> 4);  // first output column of the item
     v4f b1v{0.f, 0.f, 0.f, 0.f};
     if (!rzt) {
@@ -429,8 +450,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     if (ntj == 0) return;  // (uniform over the workgroup)
 
     const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
-    const int64_t *xrow = a.xrow_dev ? gload(a.xrow_dev, 0) : a.xrow;
+    const int64_t *xrow = !XR ? nullptr : a.xrow_dev ? gload(a.xrow_dev, 0) : a.xrow;
     const int64_t xrows = xrow ? a.x_rows : static_cast<int64_t>(n_rows);
+    // (XR: n_id through a buffer resource -- a word of 0 means plain rows)
+    const i32x4 ir = make_rsrc_u(xrow, static_cast<uint32_t>(xrow ? static_cast<int64_t>(n_rows) * 8 : 0));
     const int64_t xbytes = (xrows - 1) * a.ldx * 4 + a.K0 * 4;
     const i32x4 xr = make_rsrc_u(xb, static_cast<uint32_t>(xrows > 0 ? xbytes : 0));
     const int ne16 = (ne + F2_ROWS - 1) / F2_ROWS * F2_ROWS;
@@ -444,12 +467,16 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     const int srow = 2 * wv + (ln >> 5), sslot = ln & 31;
     const bool scol = 4 * sslot < a.K0 && sslot < 8 * C0;
     auto tile_of = [&](int j) { return b + j * G; };
-    auto xload = [&](int j) __attribute__((always_inline)) -> v4f {
+    // XR: the split row's feature-table index (low word of n_id; rows past
+    // the block read 0 and are masked at use)
+    auto iload = [&](int j) __attribute__((always_inline)) -> int {
+        const int row = tile_of(j) * F2_ROWS + srow;
+        return buf_load1i(ir, row < n_rows ? row * 8 : kOOB2, 0, 0);
+    };
+    auto xload = [&](int j, int idx) __attribute__((always_inline)) -> v4f {
         const int row = tile_of(j) * F2_ROWS + srow;
         const bool ok = j < ntj && row < n_rows && scol;
-        // (fused gather: the row's feature-table index; a dependent load, with
-        // four tiles in flight its latency overlaps the tiles in between)
-        const uint32_t src = (xrow && ok) ? static_cast<uint32_t>(gload(xrow, row)) : static_cast<uint32_t>(row);
+        const uint32_t src = (XR && xrow) ? static_cast<uint32_t>(idx) : static_cast<uint32_t>(row);
         return buf_load4(xr, ok ? static_cast<int>(src * ld4 + 16u * sslot) : kOOB2, 0, 0);
     };
     // nb of the lane's 8 columns (rows past the edge tiles read 0)
@@ -548,41 +575,97 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     };
 
     // ---- pipeline: x of 4 tiles in flight (registers, one buffer per tile
-    // residue mod 4), nb one tile ahead; per tile j: split(j + 1), compute(j),
-    // ONE barrier, reduce(j).  Double-buffered parts and partials make the
-    // single barrier sufficient.
+    // residue mod 4); per tile j: split(j + 1), compute(j), ONE barrier,
+    // reduce(j).  Double-buffered parts and partials make the single barrier
+    // sufficient.
+    //
+    // vmcnt counts vector-memory ops IN ORDER, so a load consumed soon after
+    // its issue forces every older one -- the x prefetches -- to land with
+    // it.  Hence: (1) the edge tiles (nb, loaded one tile ahead) run in a
+    // phase of their own (the first ~4 tiles of a workgroup), the other tiles
+    // in a phase without nb loads; (2) XR's n_id loads run four tiles ahead
+    // of the row loads that use them; (3) loads pending at a phase entry are
+    // SETTLED first -- the compiler's wait for a loop-carried load takes the
+    // fewest younger memory ops over the paths into the loop, and a load left
+    // pending on the entry path made every in-loop wait a near drain of the
+    // prefetches and the previous tiles' stores (vmcnt(4) instead of ~20).
     v4f xv[4];
+    int ixr[4] = {0, 0, 0, 0};  // XR: n_id of tile j + 5 at step j (slot j % 4)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xv[i] = xload(i);
+    for (int i = 0; i < 4; ++i) xv[i] = xload(i, XR ? iload(i) : 0);
     v4f nbv[2][2];
     nbload(0, nbv[0]);
     split(xv[0], 0);
-    xv[0] = xload(4);
+    xv[0] = xload(4, XR ? iload(4) : 0);
+    if (XR) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ixr[i] = iload(5 + i);
+    }
+    auto settle = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(xv[i]), "+v"(ixr[i]));
+        asm volatile("" : "+v"(nbv[0][0]), "+v"(nbv[0][1]), "+v"(nbv[1][0]), "+v"(nbv[1][1]));
+    };
+    settle();
     lds_barrier();
-    auto step = [&](auto u_c, int j) __attribute__((always_inline)) {
-        constexpr int U = decltype(u_c)::value;  // j % 4
-        constexpr int B = U & 1;                 // j % 2
-        if (j + 1 < ntj) split(xv[(U + 1) & 3], B ^ 1);
-        xv[(U + 1) & 3] = xload(j + 5);
-        nbload(j + 1, nbv[B ^ 1]);
-        compute(j, B, nbv[B]);
+    auto step = [&](auto u_c, auto nb_c, int j) __attribute__((always_inline)) {
+        constexpr int U = decltype(u_c)::value;   // j % 4
+        constexpr int B = U & 1;                  // j % 2
+        constexpr bool NB = decltype(nb_c)::value;  // an edge tile phase
+        // (unconditional: past the last tile it splits zeros into a parts
+        // buffer no one reads -- a skipped split left that register's load
+        // pending on one path, and the compiler then drained vmcnt before
+        // reusing the register)
+        split(xv[(U + 1) & 3], B ^ 1);
+        xv[(U + 1) & 3] = xload(j + 5, ixr[U]);
+        if (XR) ixr[U] = iload(j + 9);
+        if (NB) {
+            nbload(j + 1, nbv[B ^ 1]);
+            compute(j, B, nbv[B]);
+        } else {
+            const v4f zz[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+            compute(j, B, zz);
+        }
         lds_barrier();
         reduce(j, B);
     };
-    for (int j = 0; j < ntj; j += 4) {
-        step(std::integral_constant<int, 0>{}, j);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    // this workgroup's edge tiles: j < ntj_e, rounded up to a multiple of 4
+    // (the ring position); tiles past the edge rows in it read nb = 0
+    const int n_et = ne16 / F2_ROWS;
+    const int ntj_e = min(ntj, 4 * ((max(0, (n_et - b + G - 1) / G) + 3) / 4));
+    int j = 0;
+    for (; j < ntj_e; j += 4) {
+        step(I0{}, std::true_type{}, j);
         if (j + 1 >= ntj) break;
-        step(std::integral_constant<int, 1>{}, j + 1);
+        step(I1{}, std::true_type{}, j + 1);
         if (j + 2 >= ntj) break;
-        step(std::integral_constant<int, 2>{}, j + 2);
+        step(I2{}, std::true_type{}, j + 2);
         if (j + 3 >= ntj) break;
-        step(std::integral_constant<int, 3>{}, j + 3);
+        step(I3{}, std::true_type{}, j + 3);
     }
+    if (j >= ntj) return;
+    settle();  // (the x rows in flight: settled once at the phase change)
+    // whole trips of 4 steps with no exits inside (an exit between steps
+    // gave the compiler's wait analysis a short path into the loop head:
+    // vmcnt(2) there, a near drain every 4 tiles), then the remainder
+    for (; j + 4 <= ntj; j += 4) {
+        step(I0{}, std::false_type{}, j);
+        step(I1{}, std::false_type{}, j + 1);
+        step(I2{}, std::false_type{}, j + 2);
+        step(I3{}, std::false_type{}, j + 3);
+    }
+    if (j < ntj) step(I0{}, std::false_type{}, j);
+    if (j + 1 < ntj) step(I1{}, std::false_type{}, j + 1);
+    if (j + 2 < ntj) step(I2{}, std::false_type{}, j + 2);
 }
 
-template <int C0, int NT1, int DM>
+template <int C0, int NT1, int DM, bool XR>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
-    auto fn = k_fwd2<C0, NT1, DM>;
+    auto fn = k_fwd2<C0, NT1, DM, XR>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 8) * 2 + 2 * F2_ROWS * 4;
     static bool attr_set = false;  // benign race: idempotent
@@ -669,17 +752,18 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     NGNN_RETURN_IF(n_rows < 0 || n_edge_rows < 0 || h_rows < 0, NGNN_E_ARG);
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
     NGNN_RETURN_IF(stages <= 0 || stages > NGNN_SAGE2_ALL, NGNN_E_ARG);
-    NGNN_RETURN_IF(ldx < K0 || ldx % 4 != 0 || ldw0 < K0 || ldw1 < H || ldh < H || ldh % 4 != 0 ||
+    NGNN_RETURN_IF(ldx < K0 || ldx % 4 != 0 || ldw0 < K0 || ldw0 % 4 != 0 || ldw1 < H || ldw1 % 4 != 0 || ldh < H || ldh % 4 != 0 ||
                        ld_agg < K0 || ld_agg % 4 != 0 || ldo < F1,
                    NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(n_rows), NGNN_E_RANGE);
     const bool indexed = xrow || xrow_dev;
     NGNN_RETURN_IF(indexed && (x_rows <= 0 || !col_x), NGNN_E_ARG);
     if (n_rows == 0) return NGNN_OK;
-    NGNN_RETURN_IF((!x && !x_dev) || !rowptr || !col || !wl0 || !bl0 || !wr0 || !wl1 || !bl1 || !wr1 ||
+    NGNN_RETURN_IF((!x && !x_dev) || !rowptr || (!col && n_edge_rows > 0) || !wl0 || !bl0 || !wr0 || !wl1 || !bl1 || !wr1 ||
                        !h || !agg0 || !out || !ws,
                    NGNN_E_ARG);
     NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(agg0, 16) || !aligned(bl0, 16) ||
+                       !aligned(wr0, 16) || !aligned(wl0, 16) || !aligned(wr1, 16) || !aligned(wl1, 16) ||
                        !aligned(ws, 256),
                    NGNN_E_ALIGN);
     // 32-bit buffer offsets: every operand under 3.75 GiB
@@ -705,7 +789,8 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     if (stages & NGNN_SAGE2_PREP) {
         P2Args p{wr0, wl0, ldw0, static_cast<int>(K0), C0, wr1, wl1, ldw1, static_cast<int>(F1), NT1,
                  img_r0, img_l0, img_1, exps};
-        hipLaunchKernelGGL(k_prep2, dim3(3), dim3(1024), 0, st, p);
+        // (F2_WAVES * 2 * C0 * 64 = 4,096 slots of the largest image: 16 blocks each)
+        hipLaunchKernelGGL(k_prep2, dim3(16, 3), dim3(P2_THREADS), 0, st, p);
         const int rc = launch_status();
         if (rc) return rc;
     }
@@ -772,10 +857,13 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, tiles)));
         const int dm = f.drop.thresh == 0 ? 0 : f.drop.thresh == 128u ? 2 : 1;
         int rc = NGNN_E_SHAPE;
-        if (C0 == 4 && NT1 == 3) {
-            rc = dm == 2 ? launch_fwd2<4, 3, 2>(f, grid, st)
-                         : dm == 1 ? launch_fwd2<4, 3, 1>(f, grid, st) : launch_fwd2<4, 3, 0>(f, grid, st);
-        }
+        auto go = [&](auto xr_c) {
+            constexpr bool XRv = decltype(xr_c)::value;
+            return dm == 2   ? launch_fwd2<4, 3, 2, XRv>(f, grid, st)
+                   : dm == 1 ? launch_fwd2<4, 3, 1, XRv>(f, grid, st)
+                             : launch_fwd2<4, 3, 0, XRv>(f, grid, st);
+        };
+        if (C0 == 4 && NT1 == 3) rc = indexed ? go(std::true_type{}) : go(std::false_type{});
         if (rc) return rc;
     }
     if (!(stages & NGNN_SAGE2_NARROW)) return NGNN_OK;
