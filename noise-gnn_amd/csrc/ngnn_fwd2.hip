@@ -30,17 +30,17 @@
 // parity bars (outputs 1e-5) with half the MFMAs of the 3 x bf16 split.  The
 // accumulators are unscaled with v_ldexp (exact).
 //
-// Three launches, all on the caller's stream:
-//   k_prep2    the weight images (fp16 parts in fragment order) and the
-//              per-matrix exponents; one workgroup per matrix;
+// Two launches (plus the narrow neighbour term), all on the caller's stream;
+// each loads its weight slices into registers itself (per-wave scales):
 //   k_edge_nb  rows with in-edges (NeighborLoader numbers them first): the
 //              neighbour aggregate in edge order (bit-identical to
 //              ngnn_seg_agg_fwd; it is the backward's saved aggregate), then
-//              nb = agg W_l0^T on MFMA with W_l0's image in LDS;
+//              nb = agg W_l0^T on MFMA, W_l0's slices in registers;
 //   k_fwd2     every row: layer 0's root term + nb + epilogue, layer 1's
 //              products, the cross-wave sum; then k_narrow_agg (ngnn_sage_rt.hip)
 //              adds mean_j z_j to the rows with in-edges.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ngnn_device.h"
@@ -54,7 +54,6 @@ typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 constexpr int F2_WAVES = 8;    // workgroup: 8 waves x 32 hidden columns = 256
 constexpr int F2_HID = 256;    // hidden width of the fused shape
 constexpr int F2_ROWS = 16;    // rows per tile (one MFMA n-block)
-constexpr int F2_NB = 4;       // neighbour rows in flight per lane (k_edge_nb)
 constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
 
 // e with max|v| 2^e in [2^14, 2^15) (0 -> 15; inf / NaN rows stay inf / NaN)
@@ -117,103 +116,47 @@ __device__ __forceinline__ v4f mfma_h2(half8 a1, half8 a2, half8 b1, half8 b2, v
 // the compiler from moving memory accesses across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// ---------------------------------------------------------------- k_prep2
-struct P2Args {
-    const float *wr0, *wl0;  // [256, K0], row stride ldw0
-    int64_t ldw0;
-    int K0, C0;
-    const float *wr1, *wl1;  // [F1, 256], row stride ldw1
-    int64_t ldw1;
-    int F1, NT1;
-    half8 *img_r0;  // k_fwd2: [8 w][2 mt][C0][2 p][64]
-    half8 *img_l0;  // k_edge_nb: [16 mt][C0][2 p][64] (its LDS image)
-    half8 *img_1;   // k_fwd2: [8 w][2 NT1][2 p][64]
-    int *exps;      // [0] W_r0, [1] W_l0, [2] [W_r1 | W_l1]
-};
+// ---------------------------------------------------------------- weight slices
+// Every wave loads its slice of a weight matrix straight from the fp32
+// weights into A-fragment registers at launch (~100 KB per matrix per
+// workgroup, L2-resident after the first workgroups): lane (m, q) of a
+// fragment holds 8 values of one weight row (two 16-B loads), scaled by the
+// wave's OWN power of two (max |w| over the wave's slice) and split into the
+// two fp16 parts.  Per-wave scales are exact to undo: every product is
+// unscaled per wave before any cross-wave sum -- so there is no weight-prep
+// launch and no cross-workgroup hand-off (a round-3 design had both).
+__device__ __forceinline__ v4f wload4(const float *row, int k, int kmax, bool ok) {
+    return (ok && k < kmax) ? *reinterpret_cast<const v4f *>(row + k) : v4f{0.f, 0.f, 0.f, 0.f};
+}
 
-// blockIdx.y: 0 W_r0, 1 W_l0, 2 layer 1.  Every block reduces its matrix's
-// max |w| itself (16-B loads, all in flight: ~100 KB per matrix from L2) --
-// no cross-block hand-off -- then writes its share of the image slots (8
-// values of one lane, both parts).
-constexpr int P2_THREADS = 256;
-constexpr int P2_U = 32;  // float4 loads per thread for the max: 32 x 256 = 256 x 128 / 4 (K0 <= 128)
-__global__ __launch_bounds__(P2_THREADS) void k_prep2(P2Args a) {
-    __shared__ float sred[P2_THREADS / 64];
-    const int mat = blockIdx.y;
-    float m = 0.0f;
-    {
-        // the matrix as float4 quads (rows are 16-B aligned: K0 and ldw % 4 == 0)
-        const int q0 = mat < 2 ? a.K0 / 4 : F2_HID / 4;  // quads per row
-        const int nr = mat < 2 ? F2_HID : 2 * a.F1;
-        const int nq = nr * q0;
-        v4f t[P2_U];
+// max of a non-negative float over the wave
+__device__ __forceinline__ float wave_max(float v) { return max_xor32(max_xor16(max_row16(v))); }
+
+// layer 0's slice of wave wv: rows 32 wv + 16 mt + m of w ([256, K0], row
+// stride ldw), k = 32 c + 8 q .. + 7; returns the wave's exponent
+template <int C0>
+__device__ __forceinline__ int load_w0_slice(const float *w, int64_t ldw, int K0, int wv, int ln,
+                                             half8 (&frag)[2][C0][2]) {
+    const int q = ln >> 4, m = ln & 15;
+    v4f t[2][C0][2];
+    float mx = 0.0f;
 #pragma unroll
-        for (int u = 0; u < P2_U; ++u) {
-            const int i = u * P2_THREADS + static_cast<int>(threadIdx.x);
-            const int rr = i / q0, c = i - rr * q0;
-            const float *row;
-            if (mat < 2) row = (mat == 0 ? a.wr0 : a.wl0) + static_cast<int64_t>(min(rr, F2_HID - 1)) * a.ldw0;
-            else {
-                const int z = rr >= a.F1;
-                row = (z ? a.wl1 : a.wr1) + static_cast<int64_t>(min(rr - z * a.F1, a.F1 - 1)) * a.ldw1;
+    for (int mt = 0; mt < 2; ++mt) {
+        const float *row = w + static_cast<int64_t>(32 * wv + 16 * mt + m) * ldw;
+#pragma unroll
+        for (int c = 0; c < C0; ++c)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                t[mt][c][p] = wload4(row, 32 * c + 8 * q + 4 * p, K0, true);
+                mx = fmaxf(mx, amax4(t[mt][c][p]));
             }
-            t[u] = i < nq ? *reinterpret_cast<const v4f *>(row + 4 * c) : v4f{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < P2_U; ++u) m = fmaxf(m, amax4(t[u]));
     }
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = m;
-    __syncthreads();
-    m = 0.0f;
+    const int e = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
-    for (int i = 0; i < P2_THREADS / 64; ++i) m = fmaxf(m, sred[i]);
-    const int e = h2_exp(m);
-    if (threadIdx.x == 0 && blockIdx.x == 0) a.exps[mat] = e;
-    const int C0 = a.C0, MT1 = 2 * a.NT1;
-    const int nslot = mat == 0 ? F2_WAVES * 2 * C0 * 64 : mat == 1 ? (F2_HID / 16) * C0 * 64 : F2_WAVES * MT1 * 64;
-    for (int s = blockIdx.x * P2_THREADS + threadIdx.x; s < nslot; s += gridDim.x * P2_THREADS) {
-        const int l = s & 63, f = s >> 6, m16 = l & 15, q = l >> 4;
-        float v[8];
-        int dst;
-        half8 *img;
-        if (mat < 2) {
-            int n, c;
-            if (mat == 0) {  // f = (w 2 + mt) C0 + c
-                c = f % C0;
-                const int wm = f / C0;  // w 2 + mt
-                n = 16 * wm + m16;      // = 32 w + 16 mt + m16
-            } else {  // f = mt C0 + c
-                c = f % C0;
-                n = 16 * (f / C0) + m16;
-            }
-            const float *w = (mat == 0 ? a.wr0 : a.wl0) + static_cast<int64_t>(n) * a.ldw0;
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = 32 * c + 8 * q + j;
-                v[j] = k < a.K0 ? w[k] : 0.0f;
-            }
-            dst = f * 2;
-            img = mat == 0 ? a.img_r0 : a.img_l0;
-        } else {  // f = w MT1 + mt1; k order of the h fragment: 4q + j, 16 + 4q + j - 4
-            const int w = f / MT1, mt1 = f - w * MT1;
-            const int zt = mt1 >= a.NT1;
-            const int o = 16 * (mt1 - zt * a.NT1) + m16;
-            const float *row = (zt ? a.wl1 : a.wr1) + static_cast<int64_t>(o) * a.ldw1;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = 32 * w + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
-                v[j] = o < a.F1 ? row[k] : 0.0f;
-            }
-            dst = f * 2;
-            img = a.img_1;
-        }
-        v4f lo{v[0], v[1], v[2], v[3]}, hi{v[4], v[5], v[6], v[7]};
-        half8 p1, p2;
-        h2_split(ldexp4(lo, e), ldexp4(hi, e), p1, p2);
-        img[dst * 64 + l] = p1;
-        img[(dst + 1) * 64 + l] = p2;
-    }
+        for (int c = 0; c < C0; ++c) h2_split(ldexp4(t[mt][c][0], e), ldexp4(t[mt][c][1], e), frag[mt][c][0], frag[mt][c][1]);
+    return e;
 }
 
 // ---------------------------------------------------------------- k_edge_nb
@@ -232,38 +175,43 @@ struct G2Args {
     const int32_t *col_x;
     int64_t x_rows;
     int mean;
-    const half8 *img_l0;
-    const int *exps;
+    const float *wl0;  // [256, K0], row stride ldw0
+    int64_t ldw0;
     float *agg;  // saved aggregate [>= rows of the edge tiles, ld_agg]
     int64_t ld_agg;
     float *nb;   // [>= rows of the edge tiles, 256]
     int64_t cap_rows;  // rows of agg / nb
 };
 
-// One wave per 16-row tile of the rows with in-edges.  Lane (rl, q) gathers
-// columns 32 c + 8 q .. + 7 (c < C0) of its row's neighbours -- already the
-// B-fragment layout of the MFMA -- F2_NB neighbours per round trip, summed in
-// edge order from +0.0 (padded slots read 0), / max(deg, 1) for mean: the fp32
-// sequence of ngnn_seg_agg_fwd.  Then nb = agg W_l0^T (16 m-tiles, W_l0's
-// image in LDS), unscaled, 16-B stores.
+constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip for fanouts <= 16)
+
+// The rows with in-edges, 16-row tiles, one workgroup (8 waves) per CU
+// walking its tiles.  Per tile: every wave gathers TWO rows (32 lanes x 4
+// columns per row: the x split layout of k_fwd2), all of a row's neighbours
+// in one round trip (their ids were fetched during the previous tile, the
+// row pointers two tiles ahead), sums them in edge order from +0.0 and
+// divides by max(deg, 1) for mean -- the fp32 sequence of ngnn_seg_agg_fwd
+// (the saved aggregate is bit-identical to it); stores the aggregate, splits
+// it into fp16 parts in LDS; after one barrier every wave multiplies the tile
+// by ITS 32 columns of W_l0 (slice in registers) and stores nb, unscaled.
 template <int C0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
-    extern __shared__ __attribute__((aligned(16))) half8 simg[];  // [16][C0][2][64]
-    constexpr int NFR = (F2_HID / 16) * C0 * 2;
+    constexpr int PSTR = 32 * C0 + 8;
+    constexpr int XPB = 2 * F2_ROWS * PSTR;
+    __shared__ __attribute__((aligned(16))) _Float16 sxp[2 * XPB];
+    __shared__ int serow[2 * F2_ROWS];
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-    const int ln = threadIdx.x & 63;
-    for (int f = wv; f < NFR; f += F2_WAVES)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(a.img_l0 + f * 64 + ln),
-                                         (__attribute__((address_space(3))) void *)(simg + f * 64), 16, 0, 0);
+    const int ln = threadIdx.x & 63, q = ln >> 4, rl = ln & 15;
     int n_rows = a.n_rows;
     if (a.n_rows_dev) n_rows = min(n_rows, *a.n_rows_dev);
     int ne = min(a.n_edge, n_rows);
     if (a.n_edge_dev) ne = min(ne, *a.n_edge_dev);
     n_rows = __builtin_amdgcn_readfirstlane(n_rows);
     const int n_tiles = __builtin_amdgcn_readfirstlane((max(ne, 0) + F2_ROWS - 1) / F2_ROWS);
-    const int eW = a.exps[1];
-    __builtin_amdgcn_s_waitcnt(0);  // (this wave's image DMAs landed)
-    __syncthreads();
+    const int G = gridDim.x, b = blockIdx.x;
+    const int ntj = n_tiles > b ? (n_tiles - 1 - b) / G + 1 : 0;
+    if (ntj == 0) return;  // (uniform over the workgroup)
+
     const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
     const int32_t *colg = a.col_x ? a.col_x : a.col;  // the gather's source rows
     const int64_t xrows = a.col_x ? a.x_rows : static_cast<int64_t>(n_rows);
@@ -272,81 +220,104 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     const i32x4 ar = make_rsrc(a.agg, static_cast<uint32_t>(a.cap_rows * a.ld_agg * 4));
     const i32x4 nr = make_rsrc(a.nb, static_cast<uint32_t>(a.cap_rows * F2_HID * 4));
     const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
-    const int q = ln >> 4, rl = ln & 15;
-    for (int t = static_cast<int>(blockIdx.x) * F2_WAVES + wv; t < n_tiles; t += gridDim.x * F2_WAVES) {
-        const int r = t * F2_ROWS + rl;
-        const int beg = r < n_rows ? a.rowptr[r] : 0;
-        const int deg = r < n_rows ? a.rowptr[r + 1] - beg : 0;
-        // (the 16 rows' max degree: every row group holds the same 16 values)
-        const int maxdeg = __builtin_amdgcn_readfirstlane(__float_as_int(max_row16(__int_as_float(deg))));
-        // column offsets of the lane's 2 C0 pieces (past K0: out of range)
-        int coff[2 * C0];
+    // gather lanes: row srow of the tile, columns 4 sslot .. + 3
+    const int srow = 2 * wv + (ln >> 5), sslot = ln & 31;
+    const bool scol = 4 * sslot < a.K0 && sslot < 8 * C0;
+    auto tile_row = [&](int j, int rr) { return (b + j * G) * F2_ROWS + rr; };
+    auto rowptr_of = [&](int j, int &beg, int &end) __attribute__((always_inline)) {
+        const int r = tile_row(j, srow);
+        const bool ok = j < ntj && r < n_rows;
+        beg = ok ? gload(a.rowptr, r) : 0;
+        end = ok ? gload(a.rowptr, r + 1) : 0;
+    };
+    auto ids_of = [&](int beg, int end, int e0, int (&cw)[G2_NB]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int p = 0; p < 2 * C0; ++p) {
-            const int k = 32 * (p >> 1) + 8 * q + 4 * (p & 1);
-            coff[p] = k < a.K0 ? 4 * k : -1;
+        for (int e = 0; e < G2_NB; ++e) cw[e] = beg + e0 + e < end ? gload(colg, beg + e0 + e) : -1;
+    };
+    auto rows_of = [&](const int (&cw)[G2_NB], v4f (&v)[G2_NB]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < G2_NB; ++e)
+            v[e] = buf_load4(xr, (cw[e] >= 0 && scol) ? static_cast<int>(static_cast<uint32_t>(cw[e]) * ld4 + 16u * sslot) : kOOB2,
+                             0, 0);
+    };
+
+    // index loads of the first tiles, then this wave's W_l0 slice
+    int begc, endc, begn, endn;
+    int cw[G2_NB];
+    rowptr_of(0, begc, endc);
+    ids_of(begc, endc, 0, cw);
+    rowptr_of(1, begn, endn);
+    half8 wl[2][C0][2];
+    const int eW = load_w0_slice<C0>(a.wl0, a.ldw0, a.K0, wv, ln, wl);
+
+    for (int j = 0; j < ntj; ++j) {
+        const int B = j & 1;
+        v4f v[G2_NB];
+        rows_of(cw, v);
+        // the next tile's ids, the row pointers of the one after
+        int cwn[G2_NB];
+        ids_of(begn, endn, 0, cwn);
+        int begm, endm;
+        rowptr_of(j + 2, begm, endm);
+        v4f acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < G2_NB; ++e) acc += v[e];
+        const int deg = endc - begc;
+        // (rare: rows with more than G2_NB neighbours -- one round trip each)
+        const int dmax = __builtin_amdgcn_readfirstlane(__float_as_int(wave_max(__int_as_float(deg))));
+        for (int e0 = G2_NB; e0 < dmax; e0 += G2_NB) {
+            int ce[G2_NB];
+            ids_of(begc, endc, e0, ce);
+            rows_of(ce, v);
+#pragma unroll
+            for (int e = 0; e < G2_NB; ++e) acc += v[e];
         }
-        v4f acc[2 * C0];
+        if (a.mean) {
+            const float dv = static_cast<float>(deg > 1 ? deg : 1);
 #pragma unroll
-        for (int p = 0; p < 2 * C0; ++p) acc[p] = v4f{0.f, 0.f, 0.f, 0.f};
-        for (int e0 = 0; e0 < maxdeg; e0 += 16) {
-            // the window's 16 neighbour ids first (one round trip), then the
-            // rows, F2_NB per round trip
-            int cw[16];
+            for (int i = 0; i < 4; ++i) acc[i] = acc[i] / dv;
+        }
+        const int r = tile_row(j, srow);
+        buf_store4(acc, ar, (r < n_rows && scol) ? r * static_cast<int>(a.ld_agg) * 4 + 16 * sslot : kOOB2, 0, 0);
+        {  // parts of the tile row (max over the row's 32 lanes)
+            const int e = h2_exp(max_xor16(max_row16(amax4(acc))));
+            const v4f vs = ldexp4(acc, e);
+            half4 p1, p2;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) cw[j] = e0 + j < deg ? gload(colg, beg + e0 + j) : -1;
-#pragma unroll
-            for (int b4 = 0; b4 < 16; b4 += F2_NB) {
-                if (e0 + b4 >= maxdeg) break;
-                v4f v[F2_NB][2 * C0];
-#pragma unroll
-                for (int u = 0; u < F2_NB; ++u) {
-                    const int idx = cw[b4 + u];
-                    const uint32_t ro = static_cast<uint32_t>(idx) * ld4;
-#pragma unroll
-                    for (int p = 0; p < 2 * C0; ++p)
-                        v[u][p] = buf_load4(xr, (idx >= 0 && coff[p] >= 0) ? static_cast<int>(ro + coff[p]) : kOOB2,
-                                            0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < F2_NB; ++u)
-#pragma unroll
-                    for (int p = 0; p < 2 * C0; ++p) acc[p] += v[u][p];
+            for (int i = 0; i < 4; ++i) {
+                const _Float16 hh = static_cast<_Float16>(vs[i]);
+                p1[i] = hh;
+                p2[i] = static_cast<_Float16>(vs[i] - static_cast<float>(hh));
             }
-        }
-        const float dv = static_cast<float>(deg > 1 ? deg : 1);
-        float amax = 0.0f;
-#pragma unroll
-        for (int p = 0; p < 2 * C0; ++p) {
-            if (a.mean) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc[p][i] = acc[p][i] / dv;
+            if (sslot < 8 * C0) {
+                _Float16 *d = sxp + B * XPB + srow * PSTR + 4 * sslot;
+                *reinterpret_cast<half4 *>(d) = p1;
+                *reinterpret_cast<half4 *>(d + F2_ROWS * PSTR) = p2;
             }
-            amax = fmaxf(amax, amax4(acc[p]));
+            if (sslot == 0) serow[B * F2_ROWS + srow] = e;
         }
-        // the saved aggregate (rows of the edge tiles, columns < K0)
-        const int arow = r < n_rows ? r * static_cast<int>(a.ld_agg) * 4 : kOOB2;
+        lds_barrier();
+        // nb of the tile, this wave's 32 columns
+        v4f o[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+        const _Float16 *xp = sxp + B * XPB + rl * PSTR + 8 * q;
 #pragma unroll
-        for (int p = 0; p < 2 * C0; ++p)
-            buf_store4(acc[p], ar, (coff[p] >= 0 && arow != kOOB2) ? arow + coff[p] : kOOB2, 0, 0);
-        amax = max_xor32(max_xor16(amax));
-        const int ea = h2_exp(amax);
-        half8 b1[C0], b2[C0];
+        for (int c = 0; c < C0; ++c) {
+            const half8 x1 = *reinterpret_cast<const half8 *>(xp + 32 * c);
+            const half8 x2 = *reinterpret_cast<const half8 *>(xp + F2_ROWS * PSTR + 32 * c);
 #pragma unroll
-        for (int c = 0; c < C0; ++c) h2_split(ldexp4(acc[2 * c], ea), ldexp4(acc[2 * c + 1], ea), b1[c], b2[c]);
-        const int un = -(eW + ea);
-        const int nrow = r < n_rows ? r * F2_HID * 4 + 16 * q : kOOB2;
-#pragma unroll 4
-        for (int mt = 0; mt < F2_HID / 16; ++mt) {
-            v4f o{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < C0; ++c) {
-                const half8 w1 = simg[((mt * C0 + c) * 2) * 64 + ln];
-                const half8 w2 = simg[((mt * C0 + c) * 2 + 1) * 64 + ln];
-                o = mfma_h2(w1, w2, b1[c], b2[c], o);
-            }
-            buf_store4(ldexp4(o, un), nr, nrow == kOOB2 ? kOOB2 : nrow + 64 * mt, 0, 0);
+            for (int mt = 0; mt < 2; ++mt) o[mt] = mfma_h2(wl[mt][c][0], wl[mt][c][1], x1, x2, o[mt]);
         }
+        const int un = -(eW + serow[B * F2_ROWS + rl]);
+        const int r2 = tile_row(j, rl);
+        const int no = r2 < a.cap_rows ? r2 * F2_HID * 4 + (32 * wv + 4 * q) * 4 : kOOB2;
+        buf_store4(ldexp4(o[0], un), nr, no, 0, 0);
+        buf_store4(ldexp4(o[1], un), nr, no == kOOB2 ? kOOB2 : no + 64, 0, 0);
+#pragma unroll
+        for (int e = 0; e < G2_NB; ++e) cw[e] = cwn[e];
+        begc = begn;
+        endc = endn;
+        begn = begm;
+        endn = endm;
     }
 }
 
@@ -368,8 +339,10 @@ struct F2Args {
     const int32_t *n_edge_dev;
     const float *nb;  // [rows of the edge tiles, 256] (k_edge_nb)
     int64_t cap_rows;
-    const half8 *img_r0, *img_1;
-    const int *exps;
+    const float *wr0;  // [256, K0], row stride ldw0
+    int64_t ldw0;
+    const float *wr1, *wl1;  // [F1, 256], row stride ldw1
+    int64_t ldw1;
     const float *b0, *b1;
     Dropout drop;
     const uint64_t *seed_dev;
@@ -385,10 +358,11 @@ struct F2Args {
 };
 
 // DM: dropout mode (0 none, 1 byte, 2 bit: Dropout in ngnn_device.h).  XR:
-// the fused x[n_id] gather (rows through n_id, whose loads run two tiles
-// ahead of the row loads: a dependent index load next to them made every
-// tile wait vmcnt(0) -- a drain of the prefetches and the previous stores)
-template <int C0, int NT1, int DM, bool XR>
+// the fused x[n_id] gather (rows through n_id, whose loads run four tiles
+// ahead of the row loads that use them).
+// DBG (profiling builds only, NGNN_FWD2_DBG): bit 0 skips the reduce, 1 the
+// layer-1 products, 2 layer 0's products, 3 the x split -- time attribution
+template <int C0, int NT1, int DM, bool XR, int DBG = 0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     constexpr int MT1 = 2 * NT1;
     constexpr int PSTR = 32 * C0 + 8;        // halves per row of a parts buffer (+16 B pad)
@@ -398,40 +372,44 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     v4f *spart = lds2;                                                   // [2][8][MT1][64]
     _Float16 *sxp = reinterpret_cast<_Float16 *>(lds2 + 2 * F2_WAVES * MT1 * 64);  // [2][2][16][PSTR]
     int *serow = reinterpret_cast<int *>(sxp + 2 * XPB);                // [2][16]
+    float *sb0 = reinterpret_cast<float *>(serow + 2 * F2_ROWS);        // [256] b0
+    float *sb1 = sb0 + F2_HID;                                          // [16 NT1] b1 (0 past F1)
 
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63, q = ln >> 4, rl = ln & 15;
+    // the biases in LDS (read per tile: registers are the scarce resource here)
+    if (threadIdx.x < F2_HID) sb0[threadIdx.x] = a.b0[threadIdx.x];
+    if (threadIdx.x < 16 * NT1) sb1[threadIdx.x] = static_cast<int>(threadIdx.x) < a.F1 ? a.b1[threadIdx.x] : 0.0f;
     // ---- this wave's weight slices, for the whole launch
     half8 wr[2][C0][2], w1[MT1][2];
+    const int eW0 = load_w0_slice<C0>(a.wr0, a.ldw0, a.K0, wv, ln, wr);
+    int eW1;
+    {
+        // layer 1: output rows 16 m1' + m of W_r1 (m1 < NT1) / W_l1 (the rest),
+        // K rows 32 wv + (4 q + j, 16 + 4 q + j): the order of the lane's h
+        v4f t[MT1][2];
+        float mx = 0.0f;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+        for (int m1 = 0; m1 < MT1; ++m1) {
+            const int zt = m1 >= NT1;
+            const int o = 16 * (m1 - zt * NT1) + rl;
+            const float *row = (zt ? a.wl1 : a.wr1) + static_cast<int64_t>(min(o, a.F1 - 1)) * a.ldw1;
+            t[m1][0] = wload4(row, 32 * wv + 4 * q, F2_HID, o < a.F1);
+            t[m1][1] = wload4(row, 32 * wv + 16 + 4 * q, F2_HID, o < a.F1);
+            mx = fmaxf(mx, fmaxf(amax4(t[m1][0]), amax4(t[m1][1])));
+        }
+        eW1 = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
-        for (int c = 0; c < C0; ++c)
-#pragma unroll
-            for (int p = 0; p < 2; ++p) wr[mt][c][p] = a.img_r0[((((wv * 2 + mt) * C0 + c) * 2) + p) * 64 + ln];
-#pragma unroll
-    for (int m = 0; m < MT1; ++m)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) w1[m][p] = a.img_1[((wv * MT1 + m) * 2 + p) * 64 + ln];
-    const int eW0 = __builtin_amdgcn_readfirstlane(a.exps[0]);
-    const int eW1 = __builtin_amdgcn_readfirstlane(a.exps[2]);
-    v4f b0v[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) b0v[mt] = *reinterpret_cast<const v4f *>(a.b0 + 32 * wv + 16 * mt + 4 * q);
+        for (int m1 = 0; m1 < MT1; ++m1) h2_split(ldexp4(t[m1][0], eW1), ldexp4(t[m1][1], eW1), w1[m1][0], w1[m1][1]);
+    }
     // reduce item of this lane (lanes < NIT): output tile mt1, lane lnn of it;
     // items [0, 64 NT1) are out's tiles, the rest z's -- waves 0-3 take out,
-    // waves 4-7 z (NIT = 16 NT1 items per wave), so the store form is
-    // wave-uniform (no exec-divergent store branches: their varying VMEM
-    // counts made the compiler's waits conservative)
+    // waves 4-7 z (NIT = 16 NT1 items per wave); both store 4 dwords a lane
+    // through a wave-uniform resource (one store form: no branch)
     const int item = wv * NIT + (ln < NIT ? ln : 0);
     const int rmt = item >> 6, rln = item & 63;
     const int rzt = __builtin_amdgcn_readfirstlane(wv) >= F2_WAVES / 2;
     const int rcol = 16 * (rmt - rzt * NT1) + 4 * (rln >> 4);  // first output column of the item
-    v4f b1v{0.f, 0.f, 0.f, 0.f};
-    if (!rzt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b1v[i] = rcol + i < a.F1 ? a.b1[rcol + i] : 0.0f;
-    }
     Dropout drop = a.drop;
     if (a.seed_dev) drop.reseed(*a.seed_dev);
 
@@ -459,8 +437,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     const int ne16 = (ne + F2_ROWS - 1) / F2_ROWS * F2_ROWS;
     const i32x4 nbr = make_rsrc(a.nb, static_cast<uint32_t>(static_cast<int64_t>(min<int64_t>(ne16, a.cap_rows)) * F2_HID * 4));
     const i32x4 hrs = make_rsrc(a.h, static_cast<uint32_t>(static_cast<int64_t>(hr) * a.ldh * 4));
-    const i32x4 ors = make_rsrc(a.out, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldo * 4));
-    const i32x4 zrs = make_rsrc(a.z, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldz * 4));
+    const i32x4 rrs = rzt ? make_rsrc(a.z, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldz * 4))
+                          : make_rsrc(a.out, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldo * 4));
+    const uint32_t rld4 = static_cast<uint32_t>(rzt ? a.ldz : a.ldo) * 4u;
+    const int rlim = rzt ? 16 * NT1 : a.F1;
     const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
 
     // ---- x split lanes: row srow of the tile, columns 4 sslot .. + 3
@@ -506,11 +486,12 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         }
         if (sslot == 0) serow[buf * F2_ROWS + srow] = e;
     };
-    // one tile: layer 0 (32 columns), epilogue, h rows, layer-1 partial
-    auto compute = [&](int j, int buf, const v4f (&nbv)[2]) __attribute__((always_inline)) {
-        const int t = tile_of(j);
-        const int r = t * F2_ROWS + rl;
-        v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+    // layer 0's products of one tile (its parts buffer), this wave's 32
+    // columns; s0 = the lane row's unscale 2^-(eW0 + e_row) (read here: the
+    // buffer's exponents are overwritten in the next step)
+    auto l0 = [&](int buf, v4f (&acc)[2], float &s0) __attribute__((always_inline)) {
+        acc[0] = v4f{0.f, 0.f, 0.f, 0.f};
+        acc[1] = v4f{0.f, 0.f, 0.f, 0.f};
         const _Float16 *xp = sxp + buf * XPB + rl * PSTR + 8 * q;
 #pragma unroll
         for (int c = 0; c < C0; ++c) {
@@ -519,18 +500,28 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma_h2(wr[mt][c][0], wr[mt][c][1], x1, x2, acc[mt]);
         }
-        const int un0 = -(eW0 + serow[buf * F2_ROWS + rl]);
-        // epilogue: b0 + x W_r0^T + nb, ReLU (NaN passes), dropout keyed by
-        // (global row, global column) exactly as every other forward kernel
+        s0 = __builtin_amdgcn_ldexpf(1.0f, -(eW0 + serow[buf * F2_ROWS + rl]));
+    };
+    // one tile after layer 0: epilogue, h rows, layer-1 partial into spart[buf]
+    auto finish = [&](int j, int buf, const v4f (&acc)[2], float s0, const v4f (&nbv)[2], auto nb_c)
+        __attribute__((always_inline)) {
+        constexpr bool NB = decltype(nb_c)::value;
+        const int r = tile_of(j) * F2_ROWS + rl;
+        // b0 + x W_r0^T (+ nb), ReLU (NaN passes), dropout keyed by (global
+        // row, global column) exactly as every other forward kernel.  The
+        // unscale rides the fma (acc s0 is exact: a power of two)
         const uint32_t rk = DM ? drop.row_key(static_cast<uint32_t>(r)) : 0u;
         const uint32_t hw = DM == 2 ? lowbias32(rk + static_cast<uint32_t>(wv)) : 0u;  // columns 32 wv .. + 31
-        v4f hv[2];
+        v4f hv[2], b0v[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) b0v[mt] = *reinterpret_cast<const v4f *>(sb0 + 32 * wv + 16 * mt + 4 * q);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
             const uint32_t hq = DM == 1 ? lowbias32(rk + static_cast<uint32_t>(8 * wv + 4 * mt + q)) : 0u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float y = __builtin_amdgcn_ldexpf(acc[mt][i], un0) + b0v[mt][i] + nbv[mt][i];
+                float y = __builtin_fmaf(acc[mt][i], s0, b0v[mt][i]);
+                if (NB) y += nbv[mt][i];
                 bool zero = y < 0.0f;
                 if (DM == 2) zero = zero || !((hw >> (16 * mt + 4 * q + i)) & 1u);
                 if (DM == 1) zero = zero || ((hq >> (8 * i)) & 0xffu) < drop.thresh;
@@ -542,13 +533,17 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, 0);
         buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, 0);
         // layer 1: this wave's 32 rows of K -- the B fragment is the lane's own
-        // 8 values of h (k order 4q + i, 16 + 4q + i: the image matches)
+        // 8 values of h (k order 4q + i, 16 + 4q + i: the slice matches)
         const float m = max_xor32(max_xor16(fmaxf(amax4(hv[0]), amax4(hv[1]))));  // lanes rl + 16 q
         const int eh = h2_exp(m);
         half8 h1, h2;
         h2_split(ldexp4(hv[0], eh), ldexp4(hv[1], eh), h1, h2);
         const int un1 = -(eW1 + eh);
         v4f *pp = spart + (buf * F2_WAVES + wv) * MT1 * 64 + ln;
+        if (DBG & 2) {
+            asm volatile("" : "+v"(h1), "+v"(h2) : "v"(un1));
+            return;
+        }
 #pragma unroll
         for (int m1 = 0; m1 < MT1; ++m1) {
             const v4f o = mfma_h2(w1[m1][0], w1[m1][1], h1, h2, v4f{0.f, 0.f, 0.f, 0.f});
@@ -556,50 +551,56 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         }
     };
     // the 8 partials of this lane's item, summed in wave order (+ b1), stored
-    auto reduce = [&](int j, int buf) __attribute__((always_inline)) {
+    // (jj < 0: the step before the first tile -- nothing live)
+    auto reduce = [&](int jj, int buf) __attribute__((always_inline)) {
         const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + rmt * 64 + rln;
         v4f s = pp[0];
 #pragma unroll
         for (int w = 1; w < F2_WAVES; ++w) s += pp[w * MT1 * 64];
-        const int row = tile_of(j) * F2_ROWS + (rln & 15);
-        const bool live = ln < NIT && row < n_rows;
-        if (rzt) {
-            const int zo = live ? static_cast<int>(static_cast<uint32_t>(row) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol : kOOB2;
-            buf_store4(s, zrs, zo, 0, 0);
-        } else {
-            s += b1v;
-            const int oo = static_cast<int>(static_cast<uint32_t>(row) * static_cast<uint32_t>(a.ldo) * 4u) + 4 * rcol;
+        if (!rzt) s += *reinterpret_cast<const v4f *>(sb1 + rcol);
+        const int row = tile_of(jj) * F2_ROWS + (rln & 15);
+        const bool live = jj >= 0 && ln < NIT && row < n_rows;
+        const int oo = static_cast<int>(static_cast<uint32_t>(row) * rld4) + 4 * rcol;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) buf_store1(s[i], ors, (live && rcol + i < a.F1) ? oo + 4 * i : kOOB2, 0, 0);
-        }
+        for (int i = 0; i < 4; ++i) buf_store1(s[i], rrs, (live && rcol + i < rlim) ? oo + 4 * i : kOOB2, 0, 0);
     };
 
-    // ---- pipeline: x of 4 tiles in flight (registers, one buffer per tile
-    // residue mod 4); per tile j: split(j + 1), compute(j), ONE barrier,
-    // reduce(j).  Double-buffered parts and partials make the single barrier
-    // sufficient.
+    // ---- software pipeline over the workgroup's tiles.  Step j:
+    //   reduce(j - 1)  -- partials of the previous tile (spart[(j-1)&1])
+    //   l0(j + 1)      -- MFMA on parts buffer (j+1)&1 (split last step)
+    //   finish(j)      -- VALU epilogue + layer-1 MFMA -> spart[j&1]
+    //   split(j + 2)   -- x rows from the register ring -> parts buffer j&1
+    //   ONE barrier
+    // so every step holds independent MFMA and VALU work for the scheduler
+    // (layer 0 of the next tile beside the epilogue of this one).  Buffer
+    // safety: parts buffer j&1 was last read by l0(j) in step j - 1, spart
+    // (j-1)&1 is rewritten in step j + 1 -- each behind a barrier.
     //
+    // x rows run four steps ahead in a register ring (slot = tile % 4).
     // vmcnt counts vector-memory ops IN ORDER, so a load consumed soon after
     // its issue forces every older one -- the x prefetches -- to land with
-    // it.  Hence: (1) the edge tiles (nb, loaded one tile ahead) run in a
-    // phase of their own (the first ~4 tiles of a workgroup), the other tiles
-    // in a phase without nb loads; (2) XR's n_id loads run four tiles ahead
-    // of the row loads that use them; (3) loads pending at a phase entry are
-    // SETTLED first -- the compiler's wait for a loop-carried load takes the
-    // fewest younger memory ops over the paths into the loop, and a load left
-    // pending on the entry path made every in-loop wait a near drain of the
-    // prefetches and the previous tiles' stores (vmcnt(4) instead of ~20).
+    // it.  Hence: the edge tiles (nb loaded one tile ahead, first in the
+    // step) run in a phase of their own; XR's n_id loads run four tiles ahead
+    // of the row loads that use them; loads pending at a phase entry are
+    // SETTLED first (the compiler's wait for a loop-carried load takes the
+    // fewest younger memory ops over the paths into the loop); the loops have
+    // no exits between steps.
     v4f xv[4];
-    int ixr[4] = {0, 0, 0, 0};  // XR: n_id of tile j + 5 at step j (slot j % 4)
+    int ixr[4] = {0, 0, 0, 0};  // XR: at step j, slot (j+2)&3 holds n_id of tile j + 6
 #pragma unroll
     for (int i = 0; i < 4; ++i) xv[i] = xload(i, XR ? iload(i) : 0);
     v4f nbv[2][2];
     nbload(0, nbv[0]);
+    nbv[1][0] = nbv[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
     split(xv[0], 0);
     xv[0] = xload(4, XR ? iload(4) : 0);
+    split(xv[1], 1);
+    xv[1] = xload(5, XR ? iload(5) : 0);
     if (XR) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ixr[i] = iload(5 + i);
+        ixr[2] = iload(6);
+        ixr[3] = iload(7);
+        ixr[0] = iload(8);
+        ixr[1] = iload(9);
     }
     auto settle = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -608,26 +609,39 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     };
     settle();
     lds_barrier();
+    v4f acc[2];
+    float s0;
+    l0(0, acc, s0);
+    lds_barrier();  // (every wave's reads of parts buffer 0 before step 0 rewrites it)
+    const v4f zz[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
     auto step = [&](auto u_c, auto nb_c, int j) __attribute__((always_inline)) {
-        constexpr int U = decltype(u_c)::value;   // j % 4
-        constexpr int B = U & 1;                  // j % 2
-        constexpr bool NB = decltype(nb_c)::value;  // an edge tile phase
-        // (unconditional: past the last tile it splits zeros into a parts
-        // buffer no one reads -- a skipped split left that register's load
-        // pending on one path, and the compiler then drained vmcnt before
-        // reusing the register)
-        split(xv[(U + 1) & 3], B ^ 1);
-        xv[(U + 1) & 3] = xload(j + 5, ixr[U]);
-        if (XR) ixr[U] = iload(j + 9);
-        if (NB) {
-            nbload(j + 1, nbv[B ^ 1]);
-            compute(j, B, nbv[B]);
+        constexpr int U = decltype(u_c)::value;     // j % 4
+        constexpr int B = U & 1;                    // j % 2
+        constexpr int S = (U + 2) & 3;              // ring slot of tile j + 2 (then j + 6)
+        constexpr bool NB = decltype(nb_c)::value;  // an edge-tile phase
+        if (NB) nbload(j + 1, nbv[B ^ 1]);
+        if (!(DBG & 1)) reduce(j - 1, B ^ 1);
+        v4f accn[2];
+        float s0n;
+        if (!(DBG & 4)) {
+            l0(B ^ 1, accn, s0n);
         } else {
-            const v4f zz[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-            compute(j, B, zz);
+            accn[0] = xv[0];
+            accn[1] = xv[1];
+            s0n = 1.0f;
         }
+        finish(j, B, acc, s0, NB ? nbv[B] : zz, nb_c);
+        if (!(DBG & 8)) {
+            split(xv[S], B);
+        } else {
+            asm volatile("" : "+v"(xv[S]));
+        }
+        xv[S] = xload(j + 6, ixr[S]);
+        if (XR) ixr[S] = iload(j + 10);
         lds_barrier();
-        reduce(j, B);
+        acc[0] = accn[0];
+        acc[1] = accn[1];
+        s0 = s0n;
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -638,36 +652,38 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     const int n_et = ne16 / F2_ROWS;
     const int ntj_e = min(ntj, 4 * ((max(0, (n_et - b + G - 1) / G) + 3) / 4));
     int j = 0;
+    bool done = false;
     for (; j < ntj_e; j += 4) {
         step(I0{}, std::true_type{}, j);
-        if (j + 1 >= ntj) break;
+        if (j + 1 >= ntj) { done = true; break; }
         step(I1{}, std::true_type{}, j + 1);
-        if (j + 2 >= ntj) break;
+        if (j + 2 >= ntj) { done = true; break; }
         step(I2{}, std::true_type{}, j + 2);
-        if (j + 3 >= ntj) break;
+        if (j + 3 >= ntj) { done = true; break; }
         step(I3{}, std::true_type{}, j + 3);
     }
-    if (j >= ntj) return;
-    settle();  // (the x rows in flight: settled once at the phase change)
-    // whole trips of 4 steps with no exits inside (an exit between steps
-    // gave the compiler's wait analysis a short path into the loop head:
-    // vmcnt(2) there, a near drain every 4 tiles), then the remainder
-    for (; j + 4 <= ntj; j += 4) {
-        step(I0{}, std::false_type{}, j);
-        step(I1{}, std::false_type{}, j + 1);
-        step(I2{}, std::false_type{}, j + 2);
-        step(I3{}, std::false_type{}, j + 3);
+    if (!done && j < ntj) {
+        settle();  // (the x rows in flight: settled once at the phase change)
+        // whole trips of 4 steps with no exits inside, then the remainder
+        for (; j + 4 <= ntj; j += 4) {
+            step(I0{}, std::false_type{}, j);
+            step(I1{}, std::false_type{}, j + 1);
+            step(I2{}, std::false_type{}, j + 2);
+            step(I3{}, std::false_type{}, j + 3);
+        }
+        if (j < ntj) step(I0{}, std::false_type{}, j);
+        if (j + 1 < ntj) step(I1{}, std::false_type{}, j + 1);
+        if (j + 2 < ntj) step(I2{}, std::false_type{}, j + 2);
     }
-    if (j < ntj) step(I0{}, std::false_type{}, j);
-    if (j + 1 < ntj) step(I1{}, std::false_type{}, j + 1);
-    if (j + 2 < ntj) step(I2{}, std::false_type{}, j + 2);
+    reduce(ntj - 1, (ntj - 1) & 1);  // (the last tile's partials: behind the last step's barrier)
 }
 
-template <int C0, int NT1, int DM, bool XR>
+template <int C0, int NT1, int DM, bool XR, int DBG = 0>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
-    auto fn = k_fwd2<C0, NT1, DM, XR>;
+    auto fn = k_fwd2<C0, NT1, DM, XR, DBG>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
-                       static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 8) * 2 + 2 * F2_ROWS * 4;
+                       static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 8) * 2 + 2 * F2_ROWS * 4 +
+                       (F2_HID + 16 * NT1) * 4;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -680,24 +696,17 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
 
 template <int C0>
 int launch_edge_nb(const G2Args &a, int grid, hipStream_t st) {
-    auto fn = k_edge_nb<C0>;
-    const size_t lds = static_cast<size_t>(F2_HID / 16) * C0 * 2 * 64 * 16;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(F2_WAVES * 64), lds, st, a);
+    hipLaunchKernelGGL(k_edge_nb<C0>, dim3(grid), dim3(F2_WAVES * 64), 0, st, a);
     return launch_status();
 }
 
-// workspace layout (16-B aligned pieces)
+// workspace layout (256-B aligned pieces)
 struct Ws2 {
-    size_t img_r0, img_l0, img_1, exps, nb, z, total;
+    size_t nb, z, total;
 };
 Ws2 ws2_layout(int64_t K0, int64_t F1, int64_t n_rows) {
-    const int64_t C0 = ceil_div(K0, 32), NT1 = ceil_div(F1, 16);
+    (void)K0;
+    const int64_t NT1 = ceil_div(F1, 16);
     Ws2 w;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -705,10 +714,6 @@ Ws2 ws2_layout(int64_t K0, int64_t F1, int64_t n_rows) {
         off += (bytes + 255) & ~size_t(255);
         return o;
     };
-    w.img_r0 = take(static_cast<size_t>(F2_WAVES) * 2 * C0 * 2 * 64 * 16);
-    w.img_l0 = take(static_cast<size_t>(F2_HID / 16) * C0 * 2 * 64 * 16);
-    w.img_1 = take(static_cast<size_t>(F2_WAVES) * 2 * NT1 * 2 * 64 * 16);
-    w.exps = take(16);
     const int64_t rows16 = ceil_div(std::max<int64_t>(n_rows, 1), 16) * 16;
     w.nb = take(static_cast<size_t>(rows16) * F2_HID * 4);
     w.z = take(static_cast<size_t>(rows16) * NT1 * 16 * 4);
@@ -776,24 +781,14 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     hipStream_t st = as_stream(stream);
     char *wsb = static_cast<char *>(ws);
     const int C0 = static_cast<int>(ceil_div(K0, 32)), NT1 = static_cast<int>(ceil_div(F1, 16));
-    half8 *img_r0 = reinterpret_cast<half8 *>(wsb + L.img_r0);
-    half8 *img_l0 = reinterpret_cast<half8 *>(wsb + L.img_l0);
-    half8 *img_1 = reinterpret_cast<half8 *>(wsb + L.img_1);
-    int *exps = reinterpret_cast<int *>(wsb + L.exps);
     float *nb = reinterpret_cast<float *>(wsb + L.nb);
     float *z = reinterpret_cast<float *>(wsb + L.z);
     const int64_t ldz = 16 * NT1;
     const int64_t cap_rows = ceil_div(n_rows, 16) * 16;
     // the saved aggregate's and nb's rows: whole edge tiles (NB: agg0 must hold
     // ceil16(n_edge) rows when they exceed n_rows -- capped at n_rows here)
-    if (stages & NGNN_SAGE2_PREP) {
-        P2Args p{wr0, wl0, ldw0, static_cast<int>(K0), C0, wr1, wl1, ldw1, static_cast<int>(F1), NT1,
-                 img_r0, img_l0, img_1, exps};
-        // (F2_WAVES * 2 * C0 * 64 = 4,096 slots of the largest image: 16 blocks each)
-        hipLaunchKernelGGL(k_prep2, dim3(16, 3), dim3(P2_THREADS), 0, st, p);
-        const int rc = launch_status();
-        if (rc) return rc;
-    }
+    // (NGNN_SAGE2_PREP: accepted, nothing to do -- the kernels load their
+    // weight slices themselves since ABI 13's first release)
     const int ncu = num_cus();
     if ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0) {
         G2Args g;
@@ -810,14 +805,14 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         g.col_x = indexed ? col_x : nullptr;
         g.x_rows = x_rows;
         g.mean = reduce == NGNN_REDUCE_MEAN;
-        g.img_l0 = img_l0;
-        g.exps = exps;
+        g.wl0 = wl0;
+        g.ldw0 = ldw0;
         g.agg = agg0;
         g.ld_agg = ld_agg;
         g.nb = nb;
         g.cap_rows = n_rows;  // (agg0 has n_rows rows; nb has cap_rows >= n_rows)
         const int tiles = static_cast<int>(ceil_div(g.n_edge, 16));
-        const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, ceil_div(tiles, F2_WAVES))));
+        const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, tiles)));
         int rc = NGNN_E_SHAPE;
         if (C0 == 4) rc = launch_edge_nb<4>(g, grid, st);
         if (rc) return rc;
@@ -837,9 +832,11 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         f.n_edge_dev = n_edge_rows_dev;
         f.nb = nb;
         f.cap_rows = cap_rows;
-        f.img_r0 = img_r0;
-        f.img_1 = img_1;
-        f.exps = exps;
+        f.wr0 = wr0;
+        f.ldw0 = ldw0;
+        f.wr1 = wr1;
+        f.wl1 = wl1;
+        f.ldw1 = ldw1;
         f.b0 = bl0;
         f.b1 = bl1;
         f.drop = make_dropout(p_drop, seed);
@@ -857,6 +854,22 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, tiles)));
         const int dm = f.drop.thresh == 0 ? 0 : f.drop.thresh == 128u ? 2 : 1;
         int rc = NGNN_E_SHAPE;
+#ifdef NGNN_FWD2_DBG_BUILD
+        if (const char *d = getenv("NGNN_FWD2_DBG")) {
+            const int v = atoi(d);
+            if (C0 == 4 && NT1 == 3 && dm == 2 && !indexed) {
+                switch (v) {
+                    case 1: return launch_fwd2<4, 3, 2, false, 1>(f, grid, st);
+                    case 2: return launch_fwd2<4, 3, 2, false, 2>(f, grid, st);
+                    case 3: return launch_fwd2<4, 3, 2, false, 3>(f, grid, st);
+                    case 4: return launch_fwd2<4, 3, 2, false, 4>(f, grid, st);
+                    case 8: return launch_fwd2<4, 3, 2, false, 8>(f, grid, st);
+                    case 15: return launch_fwd2<4, 3, 2, false, 15>(f, grid, st);
+                    default: break;
+                }
+            }
+        }
+#endif
         auto go = [&](auto xr_c) {
             constexpr bool XRv = decltype(xr_c)::value;
             return dm == 2   ? launch_fwd2<4, 3, 2, XRv>(f, grid, st)

@@ -15,7 +15,8 @@ for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True))
     for r in csv.DictReader(open(f)):
         if sub not in r["Kernel_Name"]:
             continue
-        k = (r["Kernel_Name"].split("(")[0][-40:], r["Counter_Name"])
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("ngnn::", "")
+        k = (name[-42:], r["Counter_Name"])
         agg[k] += float(r["Counter_Value"])
         disp[k].add((f, r["Dispatch_Id"]))
 for k in sorted(agg):
