@@ -50,6 +50,7 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 constexpr int F2_WAVES = 8;    // workgroup: 8 waves x 32 hidden columns = 256
 constexpr int F2_HID = 256;    // hidden width of the fused shape
@@ -196,7 +197,7 @@ constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip 
 // by ITS 32 columns of W_l0 (slice in registers) and stores nb, unscaled.
 template <int C0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
-    constexpr int PSTR = 32 * C0 + 8;
+    constexpr int PSTR = 32 * C0 + 16;  // 72 dwords = 8 mod 64 banks: conflict-free fragment reads
     constexpr int XPB = 2 * F2_ROWS * PSTR;
     __shared__ __attribute__((aligned(16))) _Float16 sxp[2 * XPB];
     __shared__ int serow[2 * F2_ROWS];
@@ -361,11 +362,12 @@ struct F2Args {
 // the fused x[n_id] gather (rows through n_id, whose loads run four tiles
 // ahead of the row loads that use them).
 // DBG (profiling builds only, NGNN_FWD2_DBG): bit 0 skips the reduce, 1 the
-// layer-1 products, 2 layer 0's products, 3 the x split -- time attribution
+// layer-1 products, 2 layer 0's products, 3 the x split, 4 the out / z
+// stores (offsets out of range) -- time attribution
 template <int C0, int NT1, int DM, bool XR, int DBG = 0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     constexpr int MT1 = 2 * NT1;
-    constexpr int PSTR = 32 * C0 + 8;        // halves per row of a parts buffer (+16 B pad)
+    constexpr int PSTR = 32 * C0 + 16;       // halves per parts row: 72 dwords = 8 mod 64 banks (conflict-free fragment reads)
     constexpr int XPB = 2 * F2_ROWS * PSTR;  // halves per x-parts buffer (2 parts)
     constexpr int NIT = MT1 * 8;             // reduce items per wave (MT1 x 64 over 8 waves)
     extern __shared__ __attribute__((aligned(16))) v4f lds2[];
@@ -374,6 +376,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     int *serow = reinterpret_cast<int *>(sxp + 2 * XPB);                // [2][16]
     float *sb0 = reinterpret_cast<float *>(serow + 2 * F2_ROWS);        // [256] b0
     float *sb1 = sb0 + F2_HID;                                          // [16 NT1] b1 (0 past F1)
+    float *sout = sb1 + 16 * NT1;                                       // [2][16 F1] out tiles, packed rows
 
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63, q = ln >> 4, rl = ln & 15;
@@ -404,8 +407,13 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     }
     // reduce item of this lane (lanes < NIT): output tile mt1, lane lnn of it;
     // items [0, 64 NT1) are out's tiles, the rest z's -- waves 0-3 take out,
-    // waves 4-7 z (NIT = 16 NT1 items per wave); both store 4 dwords a lane
-    // through a wave-uniform resource (one store form: no branch)
+    // waves 4-7 z (NIT = 16 NT1 items per wave).  z: one 16-B store a lane.
+    // out: its rows are F1 floats wide (188 B, not 16-B aligned), but a
+    // tile's 16 rows are ONE contiguous 16-B-aligned block of 64 F1 bytes --
+    // the sums go to an LDS staging tile in that packed order and leave, a
+    // step later, as contiguous 16-B stores (dword stores scattered over 16
+    // rows cost a third of the kernel).  One store instruction per wave and
+    // step either way.
     const int item = wv * NIT + (ln < NIT ? ln : 0);
     const int rmt = item >> 6, rln = item & 63;
     const int rzt = __builtin_amdgcn_readfirstlane(wv) >= F2_WAVES / 2;
@@ -437,10 +445,9 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     const int ne16 = (ne + F2_ROWS - 1) / F2_ROWS * F2_ROWS;
     const i32x4 nbr = make_rsrc(a.nb, static_cast<uint32_t>(static_cast<int64_t>(min<int64_t>(ne16, a.cap_rows)) * F2_HID * 4));
     const i32x4 hrs = make_rsrc(a.h, static_cast<uint32_t>(static_cast<int64_t>(hr) * a.ldh * 4));
-    const i32x4 rrs = rzt ? make_rsrc(a.z, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldz * 4))
-                          : make_rsrc(a.out, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldo * 4));
-    const uint32_t rld4 = static_cast<uint32_t>(rzt ? a.ldz : a.ldo) * 4u;
-    const int rlim = rzt ? 16 * NT1 : a.F1;
+    const i32x4 zrs = make_rsrc(a.z, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.ldz * 4));
+    const i32x4 ors = make_rsrc(a.out, static_cast<uint32_t>(static_cast<int64_t>(n_rows) * a.F1 * 4));
+    const int F1 = a.F1;
     const uint32_t ld4 = static_cast<uint32_t>(a.ldx) * 4u;
 
     // ---- x split lanes: row srow of the tile, columns 4 sslot .. + 3
@@ -493,14 +500,17 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         acc[0] = v4f{0.f, 0.f, 0.f, 0.f};
         acc[1] = v4f{0.f, 0.f, 0.f, 0.f};
         const _Float16 *xp = sxp + buf * XPB + rl * PSTR + 8 * q;
+        half8 xf[C0][2];  // every fragment read issued before the first MFMA
 #pragma unroll
         for (int c = 0; c < C0; ++c) {
-            const half8 x1 = *reinterpret_cast<const half8 *>(xp + 32 * c);
-            const half8 x2 = *reinterpret_cast<const half8 *>(xp + F2_ROWS * PSTR + 32 * c);
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma_h2(wr[mt][c][0], wr[mt][c][1], x1, x2, acc[mt]);
+            xf[c][0] = *reinterpret_cast<const half8 *>(xp + 32 * c);
+            xf[c][1] = *reinterpret_cast<const half8 *>(xp + F2_ROWS * PSTR + 32 * c);
         }
         s0 = __builtin_amdgcn_ldexpf(1.0f, -(eW0 + serow[buf * F2_ROWS + rl]));
+#pragma unroll
+        for (int c = 0; c < C0; ++c)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma_h2(wr[mt][c][0], wr[mt][c][1], xf[c][0], xf[c][1], acc[mt]);
     };
     // one tile after layer 0: epilogue, h rows, layer-1 partial into spart[buf]
     auto finish = [&](int j, int buf, const v4f (&acc)[2], float s0, const v4f (&nbv)[2], auto nb_c)
@@ -552,17 +562,48 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     };
     // the 8 partials of this lane's item, summed in wave order (+ b1), stored
     // (jj < 0: the step before the first tile -- nothing live)
-    auto reduce = [&](int jj, int buf) __attribute__((always_inline)) {
+    // reduce(jj): the summed partials of tile jj -- out waves stage them in
+    // sout[jj & 1] (+ b1), z waves keep them for their store
+    auto reduce = [&](int jj, int buf) __attribute__((always_inline)) -> v4f {
         const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + rmt * 64 + rln;
         v4f s = pp[0];
 #pragma unroll
         for (int w = 1; w < F2_WAVES; ++w) s += pp[w * MT1 * 64];
         if (!rzt) s += *reinterpret_cast<const v4f *>(sb1 + rcol);
-        const int row = tile_of(jj) * F2_ROWS + (rln & 15);
-        const bool live = jj >= 0 && ln < NIT && row < n_rows;
-        const int oo = static_cast<int>(static_cast<uint32_t>(row) * rld4) + 4 * rcol;
+        float *d = sout + (jj & 1) * F2_ROWS * F1 + (rln & 15) * F1 + rcol;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) buf_store1(s[i], rrs, (live && rcol + i < rlim) ? oo + 4 * i : kOOB2, 0, 0);
+        for (int i = 0; i < 4; ++i)
+            if (!rzt && ln < NIT && rcol + i < F1) d[i] = s[i];
+        return s;
+    };
+    // ONE 16-B store per wave: z waves the z item of tile jz (sum s), out
+    // waves piece p = threadIdx.x of the staged out tile jo (sout[jo & 1]:
+    // tile jo's 16 rows are 4 F1 contiguous 16-B pieces of out)
+    auto store = [&](int jz, v4f s, int jo) __attribute__((always_inline)) {
+        const int p = static_cast<int>(threadIdx.x);  // (out waves: < 256)
+        const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
+        const int zrow = tile_of(jz) * F2_ROWS + (rln & 15);
+        const int zo = (jz >= 0 && ln < NIT && zrow < n_rows)
+                           ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
+                           : kOOB2;
+        const int oo = (jo >= 0 && p < 4 * F1) ? tile_of(jo) * F2_ROWS * F1 * 4 + 16 * p : kOOB2;
+        buf_store4(rzt ? s : v, rzt ? zrs : ors, (DBG & 16) ? kOOB2 : rzt ? zo : oo, 0, 0);
+    };
+    // the workgroup's last tile jo, which may end inside a piece (n_rows not
+    // a multiple of 16): element stores for that piece
+    auto out_store_last = [&](int jo) __attribute__((always_inline)) {
+        if (rzt) return;
+        const int p = static_cast<int>(threadIdx.x);
+        const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
+        const int base = tile_of(jo) * F2_ROWS * F1 * 4;
+        const int nv = min(n_rows - tile_of(jo) * F2_ROWS, F2_ROWS) * F1;  // valid elements of the tile
+        if (4 * p + 4 <= nv) {
+            buf_store4(v, ors, base + 16 * p, 0, 0);
+        } else if (4 * p < nv) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4 * p + i < nv) buf_store1(v[i], ors, base + 16 * p + 4 * i, 0, 0);
+        }
     };
 
     // ---- software pipeline over the workgroup's tiles.  Step j:
@@ -576,114 +617,150 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     // safety: parts buffer j&1 was last read by l0(j) in step j - 1, spart
     // (j-1)&1 is rewritten in step j + 1 -- each behind a barrier.
     //
-    // x rows run four steps ahead in a register ring (slot = tile % 4).
+    // x rows are loaded two steps before their split (a 2-slot register ring).
     // vmcnt counts vector-memory ops IN ORDER, so a load consumed soon after
     // its issue forces every older one -- the x prefetches -- to land with
     // it.  Hence: the edge tiles (nb loaded one tile ahead, first in the
-    // step) run in a phase of their own; XR's n_id loads run four tiles ahead
+    // step) run in a phase of their own; XR's n_id loads run two steps ahead
     // of the row loads that use them; loads pending at a phase entry are
     // SETTLED first (the compiler's wait for a loop-carried load takes the
     // fewest younger memory ops over the paths into the loop); the loops have
     // no exits between steps.
-    v4f xv[4];
-    int ixr[4] = {0, 0, 0, 0};  // XR: at step j, slot (j+2)&3 holds n_id of tile j + 6
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xv[i] = xload(i, XR ? iload(i) : 0);
-    v4f nbv[2][2];
-    nbload(0, nbv[0]);
-    nbv[1][0] = nbv[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
-    split(xv[0], 0);
-    xv[0] = xload(4, XR ? iload(4) : 0);
-    split(xv[1], 1);
-    xv[1] = xload(5, XR ? iload(5) : 0);
-    if (XR) {
-        ixr[2] = iload(6);
-        ixr[3] = iload(7);
-        ixr[0] = iload(8);
-        ixr[1] = iload(9);
-    }
-    auto settle = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(xv[i]), "+v"(ixr[i]));
-        asm volatile("" : "+v"(nbv[0][0]), "+v"(nbv[0][1]), "+v"(nbv[1][0]), "+v"(nbv[1][1]));
-    };
-    settle();
-    lds_barrier();
-    v4f acc[2];
-    float s0;
-    l0(0, acc, s0);
-    lds_barrier();  // (every wave's reads of parts buffer 0 before step 0 rewrites it)
-    const v4f zz[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-    auto step = [&](auto u_c, auto nb_c, int j) __attribute__((always_inline)) {
-        constexpr int U = decltype(u_c)::value;     // j % 4
-        constexpr int B = U & 1;                    // j % 2
-        constexpr int S = (U + 2) & 3;              // ring slot of tile j + 2 (then j + 6)
-        constexpr bool NB = decltype(nb_c)::value;  // an edge-tile phase
-        if (NB) nbload(j + 1, nbv[B ^ 1]);
-        if (!(DBG & 1)) reduce(j - 1, B ^ 1);
-        v4f accn[2];
-        float s0n;
-        if (!(DBG & 4)) {
-            l0(B ^ 1, accn, s0n);
-        } else {
-            accn[0] = xv[0];
-            accn[1] = xv[1];
-            s0n = 1.0f;
+    // the whole pipeline, instantiated twice: LAG (waves 4-7) runs each step's
+    // two halves in the other order (MI355X_MICROARCH.md: stagger SIMD
+    // partners by wave number >= 4)
+    auto pipeline = [&](auto lag_c) __attribute__((always_inline)) {
+        constexpr bool LAG = decltype(lag_c)::value;
+        // x ring: at step j, xv[j&1] holds tile j + 2 and xv[~j&1] tile j + 3;
+        // XR: ixr[j&1] holds n_id of tile j + 4
+        v4f xv[2];
+        int ixr[2] = {0, 0};
+        xv[0] = xload(0, XR ? iload(0) : 0);
+        xv[1] = xload(1, XR ? iload(1) : 0);
+        v4f nbv[2];  // nb of the tile the next finish() takes (edge phase)
+        nbload(0, nbv);
+        split(xv[0], 0);
+        split(xv[1], 1);
+        xv[0] = xload(2, XR ? iload(2) : 0);
+        xv[1] = xload(3, XR ? iload(3) : 0);
+        if (XR) {
+            ixr[0] = iload(4);
+            ixr[1] = iload(5);
         }
-        finish(j, B, acc, s0, NB ? nbv[B] : zz, nb_c);
-        if (!(DBG & 8)) {
-            split(xv[S], B);
-        } else {
-            asm volatile("" : "+v"(xv[S]));
-        }
-        xv[S] = xload(j + 6, ixr[S]);
-        if (XR) ixr[S] = iload(j + 10);
+        auto settle = [&]() __attribute__((always_inline)) {
+            asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(ixr[0]), "+v"(ixr[1]));
+            asm volatile("" : "+v"(nbv[0]), "+v"(nbv[1]));
+        };
+        settle();
         lds_barrier();
-        acc[0] = accn[0];
-        acc[1] = accn[1];
-        s0 = s0n;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    // this workgroup's edge tiles: j < ntj_e, rounded up to a multiple of 4
-    // (the ring position); tiles past the edge rows in it read nb = 0
-    const int n_et = ne16 / F2_ROWS;
-    const int ntj_e = min(ntj, 4 * ((max(0, (n_et - b + G - 1) / G) + 3) / 4));
-    int j = 0;
-    bool done = false;
-    for (; j < ntj_e; j += 4) {
-        step(I0{}, std::true_type{}, j);
-        if (j + 1 >= ntj) { done = true; break; }
-        step(I1{}, std::true_type{}, j + 1);
-        if (j + 2 >= ntj) { done = true; break; }
-        step(I2{}, std::true_type{}, j + 2);
-        if (j + 3 >= ntj) { done = true; break; }
-        step(I3{}, std::true_type{}, j + 3);
-    }
-    if (!done && j < ntj) {
-        settle();  // (the x rows in flight: settled once at the phase change)
-        // whole trips of 4 steps with no exits inside, then the remainder
-        for (; j + 4 <= ntj; j += 4) {
-            step(I0{}, std::false_type{}, j);
-            step(I1{}, std::false_type{}, j + 1);
-            step(I2{}, std::false_type{}, j + 2);
-            step(I3{}, std::false_type{}, j + 3);
+        v4f acc[2];
+        float s0;
+        l0(0, acc, s0);
+        lds_barrier();  // (every wave's reads of parts buffer 0 before step 0 rewrites it)
+        const v4f zz[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+        auto step = [&](auto u_c, auto nb_c, int j) __attribute__((always_inline)) {
+            constexpr int U = decltype(u_c)::value;     // j % 4
+            constexpr int B = U & 1;                    // j % 2
+            constexpr bool NB = decltype(nb_c)::value;  // an edge-tile phase
+            v4f accn[2];
+            float s0n;
+            // front: layer 0 of the next tile (fragment reads + MFMA), then the
+            // reduce (LDS reads) and the store
+            auto front = [&]() __attribute__((always_inline)) {
+                if (!(DBG & 4)) {
+                    l0(B ^ 1, accn, s0n);
+                } else {
+                    accn[0] = xv[0];
+                    accn[1] = xv[1];
+                    s0n = 1.0f;  // (DBG only)
+                }
+                if (!(DBG & 1)) {
+                    // z of tile j - 1 / out of tile j - 2 (staged in step j - 1;
+                    // the buffers differ from this step's staging writes)
+                    const v4f rs = reduce(j - 1, B ^ 1);
+                    store(j - 1, rs, j - 2);
+                }
+            };
+            // back: the VALU-heavy epilogue + layer-1 products, the split, the loads
+            auto back = [&]() __attribute__((always_inline)) {
+                finish(j, B, acc, s0, NB ? nbv : zz, nb_c);
+                if (!(DBG & 8)) {
+                    split(xv[B], B);  // tile j + 2
+                } else {
+                    asm volatile("" : "+v"(xv[B]));
+                }
+                // nb of the next tile BEFORE the x load: its wait next step leaves
+                // the younger x loads in flight
+                if (NB) nbload(j + 1, nbv);
+                xv[B] = xload(j + 4, ixr[B]);
+                if (XR) ixr[B] = iload(j + 6);
+            };
+            // (the halves are independent within a step; SIMD partners -- waves
+            // w and w + 4 -- run them in opposite orders, so one's MFMAs meet the
+            // other's VALU instead of both stalling on the same phase)
+            if (!LAG) {
+                front();
+                back();
+            } else {
+                back();
+                front();
+            }
+            lds_barrier();
+            acc[0] = accn[0];
+            acc[1] = accn[1];
+            s0 = s0n;
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        // this workgroup's edge tiles: j < ntj_e, rounded up to a multiple of 4
+        // (the ring position); tiles past the edge rows in it read nb = 0
+        const int n_et = ne16 / F2_ROWS;
+        const int ntj_e = min(ntj, 4 * ((max(0, (n_et - b + G - 1) / G) + 3) / 4));
+        int j = 0;
+        bool done = false;
+        for (; j < ntj_e; j += 4) {
+            step(I0{}, std::true_type{}, j);
+            if (j + 1 >= ntj) { done = true; break; }
+            step(I1{}, std::true_type{}, j + 1);
+            if (j + 2 >= ntj) { done = true; break; }
+            step(I2{}, std::true_type{}, j + 2);
+            if (j + 3 >= ntj) { done = true; break; }
+            step(I3{}, std::true_type{}, j + 3);
         }
-        if (j < ntj) step(I0{}, std::false_type{}, j);
-        if (j + 1 < ntj) step(I1{}, std::false_type{}, j + 1);
-        if (j + 2 < ntj) step(I2{}, std::false_type{}, j + 2);
-    }
-    reduce(ntj - 1, (ntj - 1) & 1);  // (the last tile's partials: behind the last step's barrier)
+        if (!done && j < ntj) {
+            settle();  // (the x rows in flight: settled once at the phase change)
+            // whole trips of 4 steps with no exits inside, then the remainder
+            for (; j + 4 <= ntj; j += 4) {
+                step(I0{}, std::false_type{}, j);
+                step(I1{}, std::false_type{}, j + 1);
+                step(I2{}, std::false_type{}, j + 2);
+                step(I3{}, std::false_type{}, j + 3);
+            }
+            if (j < ntj) step(I0{}, std::false_type{}, j);
+            if (j + 1 < ntj) step(I1{}, std::false_type{}, j + 1);
+            if (j + 2 < ntj) step(I2{}, std::false_type{}, j + 2);
+        }
+        if (!(DBG & 1)) {
+            // z of the last tile, out of tile ntj - 2 (staged before the last
+            // barrier); then the last tile's out: staged, one more barrier
+            const v4f rs = reduce(ntj - 1, (ntj - 1) & 1);
+            store(ntj - 1, rs, ntj - 2);
+            lds_barrier();
+            out_store_last(ntj - 1);
+        }
+    };
+    if (wv >= F2_WAVES / 2) pipeline(std::true_type{});
+    else pipeline(std::false_type{});
 }
 
 template <int C0, int NT1, int DM, bool XR, int DBG = 0>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     auto fn = k_fwd2<C0, NT1, DM, XR, DBG>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
-                       static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 8) * 2 + 2 * F2_ROWS * 4 +
-                       (F2_HID + 16 * NT1) * 4;
+                       static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
+                       (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -758,7 +835,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
     NGNN_RETURN_IF(stages <= 0 || stages > NGNN_SAGE2_ALL, NGNN_E_ARG);
     NGNN_RETURN_IF(ldx < K0 || ldx % 4 != 0 || ldw0 < K0 || ldw0 % 4 != 0 || ldw1 < H || ldw1 % 4 != 0 || ldh < H || ldh % 4 != 0 ||
-                       ld_agg < K0 || ld_agg % 4 != 0 || ldo < F1,
+                       ld_agg < K0 || ld_agg % 4 != 0 || ldo != F1,
                    NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(n_rows), NGNN_E_RANGE);
     const bool indexed = xrow || xrow_dev;
@@ -767,7 +844,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     NGNN_RETURN_IF((!x && !x_dev) || !rowptr || (!col && n_edge_rows > 0) || !wl0 || !bl0 || !wr0 || !wl1 || !bl1 || !wr1 ||
                        !h || !agg0 || !out || !ws,
                    NGNN_E_ARG);
-    NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(agg0, 16) || !aligned(bl0, 16) ||
+    NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(out, 16) || !aligned(agg0, 16) || !aligned(bl0, 16) ||
                        !aligned(wr0, 16) || !aligned(wl0, 16) || !aligned(wr1, 16) || !aligned(wl1, 16) ||
                        !aligned(ws, 256),
                    NGNN_E_ALIGN);
@@ -865,6 +942,7 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
                     case 4: return launch_fwd2<4, 3, 2, false, 4>(f, grid, st);
                     case 8: return launch_fwd2<4, 3, 2, false, 8>(f, grid, st);
                     case 15: return launch_fwd2<4, 3, 2, false, 15>(f, grid, st);
+                    case 16: return launch_fwd2<4, 3, 2, false, 16>(f, grid, st);
                     default: break;
                 }
             }

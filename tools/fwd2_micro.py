@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 import ngnn  # noqa: E402
 from ngnn import _lib, fused  # noqa: E402
-from ngnn.block import Block  # noqa: E402
+from ngnn.block import get_block  # noqa: E402
 from ngnn.loader import sample_block, synthetic_graph  # noqa: E402
 
 
@@ -35,7 +35,7 @@ def main():
     torch.manual_seed(0)
     seeds = graph.train_idx[torch.randperm(graph.train_idx.numel(), device=dev)[:1024]]
     b = sample_block(graph, seeds, [15, 10], seed=1)
-    blk = Block(b.edge_index, b.num_nodes)
+    blk = get_block(b.edge_index, b.num_nodes)
     model = ngnn.SAGE(b.x.size(1), 256, 47, 2, dropout=0.5).to(dev)
     c0, c1 = model.convs
     params = [c0.lin_l.weight, c0.lin_l.bias, c0.lin_r.weight, c1.lin_l.weight, c1.lin_l.bias, c1.lin_r.weight]
