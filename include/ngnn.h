@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 13
+#define NGNN_ABI_VERSION 14
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -333,7 +333,9 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  *   agg0 [n_rows, ld_agg] = the layer-0 neighbour aggregate of the rows of
  *        the 16-row tiles below n_edge_rows (the backward's saved aggregate;
  *        bit-identical to ngnn_seg_agg_fwd);
- *   out [n_rows, ldo]  = b1 + h W_r1^T + agg(h) W_l1^T (logits, every row).
+ *   out [n_rows, F1]   = b1 + h W_r1^T + agg(h) W_l1^T (logits, every row;
+ *        rows packed: ldo == F1, out 16-B aligned -- a 16-row tile of out is
+ *        one contiguous block, stored as 16-B pieces).
  * Rows at or past min(n_edge_rows, *n_edge_rows_dev) must have no in-edges
  * (NeighborLoader numbers the rows that receive edges first; pass n_rows
  * when unknown).  x_dev (nullable): device word holding x's address (graph
@@ -342,9 +344,10 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  * col_x = n_id[col]).  Arithmetic: H2 (two fp16 parts per operand after
  * power-of-two scaling, three MFMA products), inside the fp32 parity bars.
  * stages: NGNN_SAGE2_ALL, or a subset in order (per-launch timing; the
- * workspace carries the images, nb and z between stages): PREP the weight
- * images, EDGE the aggregate + nb of the rows with in-edges, MAIN every
- * row's layer 0 + layer-1 products, NARROW the z aggregate into out.
+ * workspace carries nb and z between stages): EDGE the aggregate + nb of
+ * the rows with in-edges, MAIN every row's layer 0 + layer-1 products,
+ * NARROW the z aggregate into out; PREP is accepted and does nothing (the
+ * kernels load their weight slices themselves).
  * ws: ngnn_sage2_workspace_bytes(K0, F1, n_rows), 256-B aligned. */
 #define NGNN_SAGE2_PREP 1
 #define NGNN_SAGE2_EDGE 2
@@ -363,6 +366,36 @@ int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xro
                    const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
                    const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
                    int64_t ldo, int stages, void *ws, size_t ws_bytes, void *stream);
+
+/* Every weight gradient of the two-layer stack above in three launches
+ * (ngnn_bwd2.hip): the backward of sage.py:33-39 under
+ * loss.backward() when the loss reads logit rows < *r_ptr (the seed rows,
+ * pipeline.py:155-160), replacing ngnn_seg_agg_fwd + two ngnn_sage_wgrad +
+ * ngnn_sage_dgrad_lowdim.  With g[s] = sum over edges s -> d (d < R) of
+ * dy[d] (/ deg(d) for MEAN), over rows < R' = max(R, *rnext_ptr):
+ *   dW_l1 = g^T h, dW_r1 = dy^T h, db1 = sum dy            ([F1, 256], [F1])
+ *   dz0 = (dy W_r1 + g W_l1) * [h > 0] * yscale            (on chip only)
+ *   dW_l0 = dz0^T agg0, dW_r0 = dz0^T x, db0 = sum dz0     ([256, K0], [256])
+ * dy [*, ldy] (rows < R read), h [*, ldh] / agg0 [*, ld_agg] the forward's
+ * (rows < R' read; an edgeless row's aggregate counts as 0), x / x_dev /
+ * xrow / xrow_dev / x_rows as ngnn_sage2_fwd's (row r of layer 0's input).
+ * Arithmetic: two bf16 parts per fp32 operand, three MFMA products per
+ * product (relative ~2^-16), fp32 accumulation -- inside the weight-gradient
+ * bars.  F1 <= 48, 0 < K0 <= 128, K0 % 4 == 0; weights [F1, 256] rows of
+ * ldw1 floats.  ws: ngnn_sage2_bwd_workspace_bytes(n_rows, K0, F1), 256-B
+ * aligned, ZERO-FILLED before its first use (g's part is zero again on
+ * return; its offset depends on K0 and F1 only, so a zeroed workspace may be
+ * grown for more rows).  Float atomics
+ * build g: not bitwise reproducible run to run (as the reference's CUDA
+ * index_add_). */
+size_t ngnn_sage2_bwd_workspace_bytes(int64_t n_rows, int64_t K0, int64_t F1);
+int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, const float *wr1,
+                   int64_t ldw1, const float *h, int64_t ldh, float yscale, const float *x,
+                   const float *const *x_dev, const int64_t *xrow, const int64_t *const *xrow_dev,
+                   int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
+                   const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
+                   const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
+                   float *dwl0, float *dbl0, float *dwr0, void *ws, size_t ws_bytes, void *stream);
 
 /* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
  * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The

@@ -1,0 +1,542 @@
+// Backward of the two-layer forward (ngnn_sage2_fwd):
+// every weight gradient of SAGE(K0 -> 256 -> F1) from the top-layer output
+// gradient dy (rows < R, the seed rows the loss reads) in three launches.
+//
+// The reference's autograd (sage.py:33-39 under loss.backward(),
+// pipeline.py:155-160) computes, per layer, dW_l = dz^T agg, dW_r = dz^T h_in,
+// db = sum dz and the input gradient through the transposed aggregation.  For
+// the top layer the aggregation is linear, so with g = the mean/sum
+// aggregation of dy scattered onto its SOURCE rows (g[s] = sum_{d <- s} dy[d]
+// / deg(d), rows < R'):
+//
+//     dW_l1 = g^T h         dW_r1 = dy^T h         db1 = sum dy
+//     dh    = dy W_r1 + g W_l1              (rows < R'; the narrow form)
+//     dz0   = dh * [h > 0] * 1/(1-p)        (ReLU + dropout backward)
+//     dW_l0 = dz0^T agg0    dW_r0 = dz0^T x        db0 = sum dz0
+//
+// -- dW_l1 needs no rebuilt neighbour aggregate of h, and dh never leaves the
+// chip.  Launches:
+//   k_lowdim_scatter (ngnn_sage_bwd.hip)  g, float atomics (no image blocks);
+//   k_bwd2  per 32-row chunk of rows < R' and 64 hidden columns: X = [dy | g]
+//           and h / x / agg0 rows staged in LDS as two bf16 parts each;
+//           dh = X [W_r1; W_l1] on MFMA, masked, split, exchanged between
+//           the two row-tile waves; then dW_r0 / dW_l0 (A = dz0^T) and
+//           [dW_r1; dW_l1] (A = X^T, B = h) on MFMA with transposed LDS reads
+//           (ds_read_b64_tr_b16).  Partials per row slice -> slabs;
+//   k_bwd2_reduce  fixed-order slab sums into the six gradients; clears g.
+//
+// Arithmetic: fp32 operands as two bf16 parts v = v1 + v2 (+ r, |r| <= 2^-17
+// |v|); products a1 b1 + a1 b2 + a2 b1 on bf16 MFMAs (each exact in fp32,
+// fp32 accumulation), dropped terms <= ~3 2^-17 relative per product: the
+// weight-gradient bars (1e-4) with room; bf16 keeps fp32's exponent range,
+// so no scaling is needed anywhere (the forward's fp16 H2 split needs it).
+#include <algorithm>
+
+#include "ngnn_device.h"
+
+namespace ngnn {
+
+// the narrow scatter (ngnn_sage_bwd.hip): g[col[e]] += dy[d] (/ deg(d)) over
+// target rows d < *r_ptr, C4 floats per g row, no weight-image blocks
+int lowdim_scatter_launch(const float *dy, int64_t ldy, const int32_t *rowptr, const int32_t *col, int n_rows,
+                          const int32_t *r_ptr, int Fo, int C4, float *g, int mean, hipStream_t st);
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+constexpr int B2_ROWS = 32;            // rows per chunk: one 16x16x32 MFMA k-step
+constexpr int B2_NC = 64;              // hidden columns per workgroup
+constexpr int B2_NCH = 256 / B2_NC;    // workgroups per row slice
+constexpr int B2_THREADS = 512;
+// LDS row strides (bf16 elements): 56 / 40 / 72 dwords -- odd multiples of 8
+// dwords, so a transposed read's 8 rows x 32 B land on disjoint banks
+constexpr int XS = 112, HS = 80, KS = 144;
+constexpr int IMG_X = 2 * B2_ROWS * XS;  // bf16 per image buffer (2 parts)
+constexpr int IMG_H = 2 * B2_ROWS * HS;
+constexpr int IMG_K = 2 * B2_ROWS * KS;
+constexpr int SA = 4 * 2 * 64 * 8;       // dz0 A fragments: [n-tile 4][part 2][lane 64][8]
+constexpr int BUF = IMG_X + IMG_H + 2 * IMG_K + SA;  // bf16 per pipeline buffer
+
+struct B2Args {
+    const float *dy;  // [*, ldy] rows < R
+    int64_t ldy;
+    int F1;
+    const float *g;  // [n_rows][C4] rows < R' (zero past F1)
+    int C4;
+    const float *wr1, *wl1;  // [F1, 256]
+    int64_t ldw1;
+    const float *h;  // [*, ldh] rows < R'
+    int64_t ldh;
+    float yscale;
+    const float *x;
+    const float *const *x_dev;
+    const int64_t *xrow;
+    const int64_t *const *xrow_dev;
+    int64_t x_rows;
+    int64_t ldx;
+    int K0;
+    const float *agg;  // [*, ld_agg] rows < R'
+    int64_t ld_agg;
+    const int32_t *rowptr;
+    int n_rows;
+    const int32_t *r_ptr, *rn_ptr;
+    float *slab;  // [S][slab floats]
+    int S;
+};
+
+__host__ __device__ inline int64_t b2_slab_floats(int K0, int F1) {
+    return 512LL * K0 + 256 + 512LL * F1 + F1;
+}
+
+__device__ __forceinline__ void split2(float v, __bf16 &p1, __bf16 &p2) {
+    p1 = static_cast<__bf16>(v);
+    p2 = static_cast<__bf16>(v - static_cast<float>(p1));
+}
+
+__device__ __forceinline__ v4f mfma3(bf8 a1, bf8 a2, bf8 b1, bf8 b2, v4f acc) {  // smallest terms first
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+}
+
+// transposed read: the 16-lane group q takes the 4 x 16 block at rows
+// r0 + 4q .. + 3, columns c0 .. + 15 of a [rows][stride] bf16 image; lane i of
+// the group receives column c0 + i of those rows (cdna_hip_programming.md T10)
+__device__ __forceinline__ s4 tr_read(const __bf16 *img, int stride, int r0, int c0, int ln) {
+    const int q = ln >> 4, i = ln & 15;
+    const __bf16 *p = img + (r0 + 4 * q + (i >> 2)) * stride + c0 + 4 * (i & 3);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s4 *)(const_cast<__bf16 *>(p)));
+}
+
+// the MFMA operand over rows {4q .. 4q+3, 16+4q .. 16+4q+3} (the dz0
+// fragments' k order) of columns c0 + (lane & 15)
+__device__ __forceinline__ bf8 tr_frag(const __bf16 *img, int stride, int c0, int ln) {
+    const s4 a = tr_read(img, stride, 0, c0, ln), b = tr_read(img, stride, 16, c0, ln);
+    typedef short s8 __attribute__((ext_vector_type(8)));
+    const s8 v{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf8, v);
+}
+
+__device__ __forceinline__ float sum_xor16(float v) {
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __int_as_float(static_cast<int>(r[0])) + __int_as_float(static_cast<int>(r[1]));
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __int_as_float(static_cast<int>(r[0])) + __int_as_float(static_cast<int>(r[1]));
+}
+
+// Workgroup = (row slice s, hidden chunk nc): 8 waves.  Stage B (dh): wave
+// (rt = w >> 2, nt = w & 3) -> dh rows 16 rt .. + 15, columns 16 nt .. + 15 of
+// the chunk.  Stage C0: wave (mat = w >> 2, nt) -> dW_r0 (mat 0, B = x) or
+// dW_l0 (mat 1, B = agg0) rows n of tile nt, all K0 columns.  Stage C1: wave
+// w -> 3 of the 24 [dW_r1; dW_l1] tiles (6 f-tiles x 4 n-tiles).
+template <bool XR>
+__global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
+    float *sred = reinterpret_cast<float *>(lb + 2 * BUF);  // [2][256] reductions at the end
+
+    const int t = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int ln = t & 63, q = ln >> 4, l16 = ln & 15;
+    // block -> (slice, chunk): the 4 chunks of a slice on one XCD (blocks b,
+    // b + 8 share one), so they share the slice's X / x / agg0 rows in L2
+    const int bx = blockIdx.x;
+    const int nc = (bx >> 3) & (B2_NCH - 1);
+    const int s = (bx >> 5) * 8 + (bx & 7);
+    const int n0 = nc * B2_NC;
+    const int R = min(a.n_rows, *a.r_ptr);
+    const int Rn = max(R, min(a.n_rows, *a.rn_ptr));
+    const int S = a.S;
+    const int C = (Rn + B2_ROWS - 1) / B2_ROWS;  // chunks below Rn
+    const int cb = static_cast<int>(static_cast<int64_t>(s) * C / S);
+    const int ce = static_cast<int>(static_cast<int64_t>(s + 1) * C / S);
+    const int K0 = a.K0, F1 = a.F1;
+    const int KT0 = (K0 + 15) >> 4;
+
+    // ---- stage-B operand: [W_r1; W_l1] rows k = 32 kc + 8 q + j (W_r1 rows
+    // 0..47, W_l1 rows 48..95, zero past F1), column n0 + 16 nt + l16
+    const int rt = wv >> 2, nt = wv & 3;
+    bf8 wb[3][2];
+    {
+        const int n = n0 + 16 * nt + l16;
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 32 * kc + 8 * q + j;
+                const int f = k < 48 ? k : k - 48;
+                const float *w = k < 48 ? a.wr1 : a.wl1;
+                const float v = f < F1 ? w[static_cast<int64_t>(f) * a.ldw1 + n] : 0.0f;
+                __bf16 p1, p2;
+                split2(v, p1, p2);
+                wb[kc][0][j] = p1;
+                wb[kc][1][j] = p2;
+            }
+        }
+    }
+    const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
+    const int64_t *xrow = !XR ? nullptr : a.xrow_dev ? gload(a.xrow_dev, 0) : a.xrow;
+
+    // ---- per-thread staging map (512 threads, one 32-row chunk)
+    //   dy: column fd = t % 48, rows t / 48 + 10 u (t < 480, u < 4)
+    //   g:  row t / 12, float4 t % 12 (t < 384);  h: row t / 16, float4 t % 16
+    //   x / agg0: rows t / 32 + 16 u (u < 2), float4 t % 32
+    const int fd = t % 48, rd = t / 48;
+    const int rg = t / 12, cg = t % 12;
+    const int rh = t >> 4, ch = t & 15;
+    const int rx = t >> 5, cx = t & 31;
+    struct Pre {
+        float dyv[4];
+        v4f gv, hv, xv[2], av[2];
+    };
+    auto load = [&](int c, Pre &p) __attribute__((always_inline)) {
+        const int r0 = c * B2_ROWS;
+        const bool live = c < ce;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int lr = rd + 10 * u, r = r0 + lr;
+            p.dyv[u] = (live && t < 480 && lr < B2_ROWS && r < R && fd < F1) ? a.dy[static_cast<int64_t>(r) * a.ldy + fd] : 0.0f;
+        }
+        {
+            const int r = r0 + rg;
+            p.gv = (live && t < 384 && r < Rn && 4 * cg < a.C4)
+                       ? *reinterpret_cast<const v4f *>(a.g + static_cast<int64_t>(r) * a.C4 + 4 * cg)
+                       : v4f{0.f, 0.f, 0.f, 0.f};
+        }
+        {
+            const int r = r0 + rh;
+            p.hv = (live && r < Rn) ? *reinterpret_cast<const v4f *>(a.h + static_cast<int64_t>(r) * a.ldh + n0 + 4 * ch)
+                                    : v4f{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int r = r0 + rx + 16 * u;
+            const bool ok = live && r < Rn && 4 * cx < K0;
+            int64_t xr = r;
+            if (XR && xrow) xr = ok ? gload(xrow, r) : 0;
+            p.xv[u] = ok ? *reinterpret_cast<const v4f *>(xb + xr * a.ldx + 4 * cx) : v4f{0.f, 0.f, 0.f, 0.f};
+            // (an edgeless row's aggregate reads 0: its row may never be written)
+            const bool deg = ok && gload(a.rowptr, r + 1) > gload(a.rowptr, r);
+            p.av[u] = deg ? *reinterpret_cast<const v4f *>(a.agg + static_cast<int64_t>(r) * a.ld_agg + 4 * cx)
+                          : v4f{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    // two bf16 parts of 4 floats -> part images at (row, col), 8 B each
+    auto put4 = [&](__bf16 *img, int part_stride, int off, v4f v) __attribute__((always_inline)) {
+        bf4 p1, p2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __bf16 a1, a2;
+            split2(v[i], a1, a2);
+            p1[i] = a1;
+            p2[i] = a2;
+        }
+        *reinterpret_cast<bf4 *>(img + off) = p1;
+        *reinterpret_cast<bf4 *>(img + part_stride + off) = p2;
+    };
+    float d1acc = 0.0f;  // db1 partial: column fd, rows of this thread
+    auto stage_images = [&](const Pre &p, __bf16 *buf) __attribute__((always_inline)) {
+        __bf16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
+        if (t < 480) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int lr = rd + 10 * u;
+                if (lr < B2_ROWS) {
+                    __bf16 a1, a2;
+                    split2(p.dyv[u], a1, a2);
+                    ix[lr * XS + fd] = a1;
+                    ix[B2_ROWS * XS + lr * XS + fd] = a2;
+                    d1acc += p.dyv[u];
+                }
+            }
+        }
+        if (t < 384) put4(ix, B2_ROWS * XS, rg * XS + 48 + 4 * cg, p.gv);
+        put4(ih, B2_ROWS * HS, rh * HS + 4 * ch, p.hv);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            put4(ik, B2_ROWS * KS, (rx + 16 * u) * KS + 4 * cx, p.xv[u]);
+            put4(ia, B2_ROWS * KS, (rx + 16 * u) * KS + 4 * cx, p.av[u]);
+        }
+    };
+
+    // ---- stage B: dh tile (rt, nt) -> masked dz0 parts into sA
+    float d0acc = 0.0f;  // db0 partial: column 16 nt + l16, rows 16 rt + 4 q + i
+    auto stage_b = [&](const __bf16 *buf) __attribute__((always_inline)) {
+        const __bf16 *ix = buf, *ih = ix + IMG_X;
+        __bf16 *sa = const_cast<__bf16 *>(ih + IMG_H + 2 * IMG_K);
+        v4f acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc) {
+            const int off = (16 * rt + l16) * XS + 32 * kc + 8 * q;
+            const bf8 a1 = *reinterpret_cast<const bf8 *>(ix + off);
+            const bf8 a2 = *reinterpret_cast<const bf8 *>(ix + B2_ROWS * XS + off);
+            acc = mfma3(a1, a2, wb[kc][0], wb[kc][1], acc);
+        }
+        // mask: the sign of h's first part (bf16 keeps sign and zero)
+        const s4 hm = tr_read(ih, HS, 16 * rt, 16 * nt, ln);
+        v4f dz;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dz[i] = hm[i] > 0 ? acc[i] * a.yscale : 0.0f;
+            d0acc += dz[i];
+        }
+        bf4 p1, p2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __bf16 a1, a2;
+            split2(dz[i], a1, a2);
+            p1[i] = a1;
+            p2[i] = a2;
+        }
+        __bf16 *d = sa + ((nt * 2) * 64 + ln) * 8 + 4 * rt;
+        *reinterpret_cast<bf4 *>(d) = p1;
+        *reinterpret_cast<bf4 *>(d + 64 * 8) = p2;
+    };
+
+    // ---- stage C: the weight-gradient products of one staged chunk
+    v4f acc0[8], acc1[3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc0[i] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
+    const int mat = wv >> 2;
+    auto stage_c = [&](const __bf16 *buf) __attribute__((always_inline)) {
+        const __bf16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
+        const __bf16 *sa = ia + IMG_K;
+        // C0: A = dz0^T of n-tile nt (both row tiles), B = x / agg0 tiles
+        const bf8 a1 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2) * 64 + ln) * 8);
+        const bf8 a2 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2 + 1) * 64 + ln) * 8);
+        const __bf16 *img = mat ? ia : ik;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+            if (kt < KT0) {
+                const bf8 b1 = tr_frag(img, KS, 16 * kt, ln);
+                const bf8 b2 = tr_frag(img + B2_ROWS * KS, KS, 16 * kt, ln);
+                acc0[kt] = mfma3(a1, a2, b1, b2, acc0[kt]);
+            }
+        }
+        // C1: tiles 3 wv + u of [dW_r1; dW_l1] (f-tile mf, n-tile nn): A =
+        // X^T, B = h
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int tt = 3 * wv + u, mf = tt >> 2, nn = tt & 3;
+            const bf8 x1 = tr_frag(ix, XS, 16 * mf, ln);
+            const bf8 x2 = tr_frag(ix + B2_ROWS * XS, XS, 16 * mf, ln);
+            const bf8 h1 = tr_frag(ih, HS, 16 * nn, ln);
+            const bf8 h2 = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
+            acc1[u] = mfma3(x1, x2, h1, h2, acc1[u]);
+        }
+    };
+
+    // ---- pipeline over the slice's chunks (two LDS buffers):
+    //   phase 1: stage C(c - 1) on buffer (c-1)&1; images of chunk c into
+    //            buffer c&1 (from registers); loads of chunk c + 1 issued
+    //   barrier
+    //   phase 2: stage B(c) on buffer c&1 -> its dz0 fragments
+    //   barrier
+    Pre pre;
+    if (cb < ce) load(cb, pre);
+    for (int c = cb; c < ce; ++c) {
+        __bf16 *cur = lb + (c & 1) * BUF;
+        if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF);
+        stage_images(pre, cur);
+        load(c + 1, pre);
+        __syncthreads();
+        stage_b(cur);
+        __syncthreads();
+    }
+    if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF);
+
+    // ---- this workgroup's part of slab s (zeros for an empty slice)
+    float *slab = a.slab + static_cast<int64_t>(s) * b2_slab_floats(K0, F1);
+    {
+        // dW_r0 / dW_l0 rows n = n0 + 16 nt + 4 q + i, columns 16 kt + l16
+        float *d = slab + (mat ? 256LL * K0 : 0);
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+            const int k = 16 * kt + l16;
+            if (kt < KT0 && k < K0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) d[static_cast<int64_t>(n0 + 16 * nt + 4 * q + i) * K0 + k] = acc0[kt][i];
+            }
+        }
+        // dW_r1 / dW_l1 rows f = 16 mf + 4 q + i (< 48: W_r1, else W_l1),
+        // columns n0 + 16 nn + l16
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int tt = 3 * wv + u, mf = tt >> 2, nn = tt & 3;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int f = 16 * mf + 4 * q + i;
+                const int fr = f < 48 ? f : f - 48;
+                if (fr < F1) {
+                    float *d1 = slab + 512LL * K0 + 256 + (f < 48 ? 0 : 256LL * F1);
+                    d1[static_cast<int64_t>(fr) * 256 + n0 + 16 * nn + l16] = acc1[u][i];
+                }
+            }
+        }
+    }
+    // db0: lanes (q) then the two row-tile waves; db1: the 10 threads of a column
+    float v0 = sum_xor32(sum_xor16(d0acc));
+    __syncthreads();
+    if (q == 0) sred[rt * 64 + nt * 16 + l16] = v0;
+    if (t < 480) sred[128 + t] = d1acc;
+    __syncthreads();
+    if (t < 64) slab[512LL * K0 + n0 + t] = sred[t] + sred[64 + t];
+    if (nc == 0 && t < F1) {
+        float v = 0.0f;
+        for (int r = 0; r < 10; ++r) v += sred[128 + r * 48 + t];
+        slab[512LL * K0 + 256 + 512LL * F1 + t] = v;
+    }
+}
+
+// out = sum over slabs in slab order; then g rows < R' back to zero
+__global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ slab, int S, int K0, int F1,
+                                                      float *dwr0, float *dwl0, float *db0, float *dwr1,
+                                                      float *dwl1, float *db1, float *g, int C4, int n_rows,
+                                                      const int32_t *r_ptr, const int32_t *rn_ptr, int n_red) {
+    const int64_t total = b2_slab_floats(K0, F1);
+    if (static_cast<int>(blockIdx.x) >= n_red) {  // g clearing blocks
+        const int R = min(n_rows, *r_ptr);
+        const int Rn = max(R, min(n_rows, *rn_ptr));
+        const int64_t n4 = static_cast<int64_t>(Rn) * C4 / 4;
+        for (int64_t i = (static_cast<int64_t>(blockIdx.x) - n_red) * 256 + threadIdx.x; i < n4;
+             i += static_cast<int64_t>(gridDim.x - n_red) * 256)
+            reinterpret_cast<v4f *>(g)[i] = v4f{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= total) return;
+    float v = 0.0f;
+    int sl = 0;
+    for (; sl + 8 <= S; sl += 8) {
+        float w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = slab[static_cast<int64_t>(sl + u) * total + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += w[u];
+    }
+    for (; sl < S; ++sl) v += slab[static_cast<int64_t>(sl) * total + i];
+    const int64_t A = 256LL * K0, Bf = 256LL * F1;
+    if (i < A) dwr0[i] = v;
+    else if (i < 2 * A) dwl0[i - A] = v;
+    else if (i < 2 * A + 256) db0[i - 2 * A] = v;
+    else if (i < 2 * A + 256 + Bf) dwr1[i - 2 * A - 256] = v;
+    else if (i < 2 * A + 256 + 2 * Bf) dwl1[i - 2 * A - 256 - Bf] = v;
+    else db1[i - 2 * A - 256 - 2 * Bf] = v;
+}
+
+constexpr int B2_S = 64;  // row slices (x 4 hidden chunks = 256 workgroups)
+
+struct Ws3 {
+    size_t g, slab, total;
+};
+// slabs first, then g: g's offset does not depend on n_rows, so a zeroed
+// workspace grown for more rows keeps every g row it ever held at zero
+Ws3 ws3_layout(int64_t n_rows, int64_t K0, int64_t F1) {
+    Ws3 w;
+    const int64_t C4 = (F1 + 3) & ~int64_t{3};
+    w.slab = 0;
+    const size_t sb = static_cast<size_t>(B2_S) * b2_slab_floats(static_cast<int>(K0), static_cast<int>(F1)) * 4;
+    w.g = (sb + 255) & ~size_t{255};
+    w.total = w.g + static_cast<size_t>(std::max<int64_t>(n_rows, 1)) * C4 * 4;
+    return w;
+}
+
+}  // namespace
+}  // namespace ngnn
+
+using namespace ngnn;
+
+extern "C" size_t ngnn_sage2_bwd_workspace_bytes(int64_t n_rows, int64_t K0, int64_t F1) {
+    if (n_rows < 0 || K0 <= 0 || F1 <= 0) return 0;
+    return ws3_layout(n_rows, K0, F1).total;
+}
+
+extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, const float *wr1,
+                              int64_t ldw1, const float *h, int64_t ldh, float yscale, const float *x,
+                              const float *const *x_dev, const int64_t *xrow, const int64_t *const *xrow_dev,
+                              int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
+                              const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
+                              const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
+                              float *dwl0, float *dbl0, float *dwr0, void *ws, size_t ws_bytes, void *stream) {
+    NGNN_RETURN_IF(reduce != NGNN_REDUCE_MEAN && reduce != NGNN_REDUCE_SUM, NGNN_E_ARG);
+    NGNN_RETURN_IF(F1 <= 0 || F1 > 48 || K0 <= 0 || K0 > 128 || K0 % 4 != 0, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(n_rows < 0 || !fits_i32(n_rows), NGNN_E_RANGE);
+    NGNN_RETURN_IF(!dy || !wl1 || !wr1 || !h || (!x && !x_dev) || !agg0 || !rowptr || !col || !r_ptr || !rnext_ptr ||
+                       !dwl1 || !dbl1 || !dwr1 || !dwl0 || !dbl0 || !dwr0 || !ws,
+                   NGNN_E_ARG);
+    NGNN_RETURN_IF(ldy < F1 || ldw1 < 256 || ldh < 256 || ldh % 4 != 0 || ldx < K0 || ldx % 4 != 0 ||
+                       ld_agg < K0 || ld_agg % 4 != 0,
+                   NGNN_E_SHAPE);
+    NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(agg0, 16) || !aligned(ws, 256), NGNN_E_ALIGN);
+    const bool indexed = xrow || xrow_dev;
+    NGNN_RETURN_IF(indexed && x_rows <= 0, NGNN_E_ARG);
+    const Ws3 L = ws3_layout(n_rows, K0, F1);
+    NGNN_RETURN_IF(ws_bytes < L.total, NGNN_E_WORKSPACE);
+    hipStream_t st = as_stream(stream);
+    char *wsb = static_cast<char *>(ws);
+    float *g = reinterpret_cast<float *>(wsb + L.g);
+    float *slab = reinterpret_cast<float *>(wsb + L.slab);
+    const int C4 = static_cast<int>((F1 + 3) & ~int64_t{3});
+    if (n_rows > 0) {
+        const int rc = lowdim_scatter_launch(dy, ldy, rowptr, col, static_cast<int>(n_rows), r_ptr,
+                                             static_cast<int>(F1), C4, g, reduce == NGNN_REDUCE_MEAN, st);
+        if (rc) return rc;
+    }
+    B2Args b;
+    b.dy = dy;
+    b.ldy = ldy;
+    b.F1 = static_cast<int>(F1);
+    b.g = g;
+    b.C4 = C4;
+    b.wr1 = wr1;
+    b.wl1 = wl1;
+    b.ldw1 = ldw1;
+    b.h = h;
+    b.ldh = ldh;
+    b.yscale = yscale;
+    b.x = x;
+    b.x_dev = x_dev;
+    b.xrow = xrow;
+    b.xrow_dev = xrow_dev;
+    b.x_rows = x_rows;
+    b.ldx = ldx;
+    b.K0 = static_cast<int>(K0);
+    b.agg = agg0;
+    b.ld_agg = ld_agg;
+    b.rowptr = rowptr;
+    b.n_rows = static_cast<int>(n_rows);
+    b.r_ptr = r_ptr;
+    b.rn_ptr = rnext_ptr;
+    b.slab = slab;
+    b.S = B2_S;
+    const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4;
+    auto go = [&](auto xr_c) {
+        auto fn = k_bwd2<decltype(xr_c)::value>;
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+            attr = true;
+        }
+        hipLaunchKernelGGL(fn, dim3(B2_S * B2_NCH), dim3(B2_THREADS), lds, st, b);
+        return launch_status();
+    };
+    int rc = indexed ? go(std::true_type{}) : go(std::false_type{});
+    if (rc) return rc;
+    const int64_t total = b2_slab_floats(static_cast<int>(K0), static_cast<int>(F1));
+    const int n_red = static_cast<int>(ceil_div(total, 256));
+    const int n_clr = 64;
+    hipLaunchKernelGGL(k_bwd2_reduce, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S, static_cast<int>(K0),
+                       static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4, static_cast<int>(n_rows),
+                       r_ptr, rnext_ptr, n_red);
+    return launch_status();
+}

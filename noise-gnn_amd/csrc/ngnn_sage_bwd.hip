@@ -1149,6 +1149,24 @@ extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *
     return launch_status();
 }
 
+// the narrow scatter alone (ngnn_sage2_bwd, ngnn_bwd2.hip): g[col[e]] +=
+// dy[d] (/ deg(d)) over target rows d < *r_ptr, no weight-image blocks
+namespace ngnn {
+int lowdim_scatter_launch(const float *dy, int64_t ldy, const int32_t *rowptr, const int32_t *col, int n_rows,
+                          const int32_t *r_ptr, int Fo, int C4, float *g, int mean, hipStream_t st) {
+    const int gs = static_cast<int>(std::min<int64_t>(ceil_div(n_rows, 4), 2048));
+    if (gs <= 0) return NGNN_OK;
+    auto go = [&](auto mean_c) {
+        hipLaunchKernelGGL((k_lowdim_scatter<decltype(mean_c)::value, false>), dim3(gs), dim3(256), 0, st, dy, ldy,
+                           (const float *)nullptr, Fo, 1.0f, rowptr, col, n_rows, r_ptr, Fo, C4, g, gs,
+                           (const float *)nullptr, (const float *)nullptr, int64_t{0}, 0, 0, (float *)nullptr);
+    };
+    if (mean) go(std::true_type{});
+    else go(std::false_type{});
+    return launch_status();
+}
+}  // namespace ngnn
+
 // ---- low-dimensional input gradient: C ABI
 static int lowdim_ntw(int64_t K) {
     const int64_t half = ceil_div(ceil_div(K, 16), 2);

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -73,6 +73,10 @@ SIGNATURES = {
                                  _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
+    "ngnn_sage2_bwd_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "ngnn_sage2_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64,
+                              _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p,
+                              _sz, _p]),
     "ngnn_sage2_supported": (_int, [_i64, _i64, _i64, _int]),
     "ngnn_sage2_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_fwd": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int,

@@ -477,6 +477,49 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     return h, out, agg0, h_rows_dev is not None
 
 
+_use_bwd2 = True  # (tests flip it to compare with the per-layer backward)
+
+
+def reserve_sage2_bwd(dev, n_rows: int, K0: int, F1: int) -> torch.Tensor:
+    """ngnn_sage2_bwd's workspace (zero-filled when first made or grown; the
+    backward leaves its g part zero).  A graph slot reserves it before its
+    capture: a zero fill inside the captured step would replay every step."""
+    lib = _lib.load()
+    return _workspace(dev, ("sage2_bwd", K0, F1), lib.ngnn_sage2_bwd_workspace_bytes(n_rows, K0, F1),
+                      zero=True)
+
+
+def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: float, r_ptr: int,
+                   rn_ptr: int, views):
+    """Every weight gradient of the two-layer stack (include/ngnn.h
+    ngnn_sage2_bwd): [dW_l0, db0, dW_r0, dW_l1, db1, dW_r1] from dy (rows <
+    *r_ptr) with the forward's h (rows < *rn_ptr) and layer-0 aggregate.
+    views: the data-parallel bucket's gradient views (or Nones)."""
+    lib = _lib.load()
+    x, h = acts[0], acts[1]
+    wl0, bl0, wr0, wl1, bl1, wr1 = params
+    dev = dy.device
+    N, K0 = x.shape[0], wl0.shape[1]
+    F1 = wl1.shape[0]
+    w1l, w1r = wl1.detach(), wr1.detach()
+    if w1l.stride(1) != 1 or w1r.stride(0) != w1l.stride(0) or w1r.stride(1) != 1:
+        w1l, w1r = w1l.contiguous(), w1r.contiguous()
+    grads = [(g.view(q.shape) if g is not None else torch.empty_like(q))
+             for g, q in zip(views, (wl0, bl0, wr0, wl1, bl1, wr1))]
+    nrows = block.n_dst
+    ws = reserve_sage2_bwd(dev, nrows, K0, F1)
+    yscale = dropout_scale(p_drop) if p_drop > 0.0 else 1.0
+    with _timing.span("sage2_bwd", 0, 0):
+        rc = lib.ngnn_sage2_bwd(
+            _lib.ptr(dy), dy.stride(0), F1, _lib.ptr(w1l), _lib.ptr(w1r), w1l.stride(0), _lib.ptr(h),
+            h.stride(0), yscale, _lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev),
+            block.x_rows, x.stride(0), K0, _lib.ptr(agg0), agg0.stride(0), _lib.ptr(block.rowptr),
+            _lib.ptr(block.col), nrows, r_ptr, rn_ptr, _lib.REDUCE[reduce], *(_lib.ptr(g) for g in grads[3:]),
+            *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
+    _lib.check(rc, "ngnn_sage2_bwd")
+    return grads
+
+
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
@@ -485,7 +528,9 @@ class _SAGEStack(torch.autograd.Function):
         acts, aggs = [x], []
         h = x
         ctx.h_partial = False
+        ctx.sage2 = False
         if L == 2 and sage2_ok(x, block, reduce, params, w_bf16):
+            ctx.sage2 = True
             h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, params, p_drop, seed, seed_dev)
             acts += [h1, h]
             aggs += [agg0, None]
@@ -574,6 +619,10 @@ class _SAGEStack(torch.autograd.Function):
         if pre_top:
             bp[L - 1] = block.r_next[0].data_ptr()
         bptr = lambda j: bp[j]  # noqa: E731
+        if (ctx.sage2 and pre_top and not need_dx and _use_bwd2
+                and not torch.are_deterministic_algorithms_enabled()):
+            return (None, None, None, None, None, None, None, None,
+                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views))
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")

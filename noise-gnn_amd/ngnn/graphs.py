@@ -238,8 +238,13 @@ class GraphedTrainStep:
         # the backward's constant row-bound array: created now, not inside the capture
         convs = getattr(self.model, "convs", None)
         if convs is not None:
-            from .fused import const_bounds
+            from .fused import const_bounds, reserve_sage2_bwd
             const_bounds(self.x.device, len(convs), self.B)
+            if len(convs) == 2 and hasattr(convs[0], "lin_l") and hasattr(convs[1], "lin_l"):
+                # (the warm-up ran before the slot's bound hint existed, so it
+                # took the per-layer backward: reserve the two-layer one's now)
+                reserve_sage2_bwd(self.x.device, self.n_cap, convs[0].lin_l.weight.shape[1],
+                                  convs[1].lin_l.weight.shape[0])
         # data parallel: the bucket pack is the tail of the first graph and the
         # unpack (/ world) the head of the second, so between the replays the
         # host issues only the one all-reduce
