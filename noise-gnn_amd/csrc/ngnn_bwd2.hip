@@ -121,6 +121,10 @@ __device__ __forceinline__ bf8 tr_frag(const __bf16 *img, int stride, int c0, in
     return __builtin_bit_cast(bf8, v);
 }
 
+// an LDS-only workgroup barrier (ngnn_fwd2.hip): vector-memory loads in
+// flight stay in flight -- __syncthreads() would drain vmcnt
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float sum_xor16(float v) {
     const int x = __float_as_int(v);
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
@@ -137,7 +141,8 @@ __device__ __forceinline__ float sum_xor32(float v) {
 // the chunk.  Stage C0: wave (mat = w >> 2, nt) -> dW_r0 (mat 0, B = x) or
 // dW_l0 (mat 1, B = agg0) rows n of tile nt, all K0 columns.  Stage C1: wave
 // w -> 3 of the 24 [dW_r1; dW_l1] tiles (6 f-tiles x 4 n-tiles).
-template <bool XR>
+// KT: 16-column tiles of K0 computed (past K0 the images hold zeros)
+template <bool XR, int KT>
 __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
     float *sred = reinterpret_cast<float *>(lb + 2 * BUF);  // [2][256] reductions at the end
@@ -158,7 +163,6 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     const int cb = static_cast<int>(static_cast<int64_t>(s) * C / S);
     const int ce = static_cast<int>(static_cast<int64_t>(s + 1) * C / S);
     const int K0 = a.K0, F1 = a.F1;
-    const int KT0 = (K0 + 15) >> 4;
 
     // ---- stage-B operand: [W_r1; W_l1] rows k = 32 kc + 8 q + j (W_r1 rows
     // 0..47, W_l1 rows 48..95, zero past F1), column n0 + 16 nt + l16
@@ -187,14 +191,15 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     // ---- per-thread staging map (512 threads, one 32-row chunk)
     //   dy: column fd = t % 48, rows t / 48 + 10 u (t < 480, u < 4)
     //   g:  row t / 12, float4 t % 12 (t < 384);  h: row t / 16, float4 t % 16
-    //   x / agg0: rows t / 32 + 16 u (u < 2), float4 t % 32
+    //   x / agg0: row t / 16, columns 8 (t % 16) .. + 7 (two float4)
     const int fd = t % 48, rd = t / 48;
     const int rg = t / 12, cg = t % 12;
     const int rh = t >> 4, ch = t & 15;
-    const int rx = t >> 5, cx = t & 31;
+    const int rx = t >> 4, cx = t & 15;
     struct Pre {
         float dyv[4];
         v4f gv, hv, xv[2], av[2];
+        int d0, d1;  // rowptr of the agg row (edgeless rows masked at staging)
     };
     auto load = [&](int c, Pre &p) __attribute__((always_inline)) {
         const int r0 = c * B2_ROWS;
@@ -215,18 +220,37 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             p.hv = (live && r < Rn) ? *reinterpret_cast<const v4f *>(a.h + static_cast<int64_t>(r) * a.ldh + n0 + 4 * ch)
                                     : v4f{0.f, 0.f, 0.f, 0.f};
         }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int r = r0 + rx + 16 * u;
-            const bool ok = live && r < Rn && 4 * cx < K0;
+        {
+            const int r = r0 + rx;
+            const bool okr = live && r < Rn;
             int64_t xr = r;
-            if (XR && xrow) xr = ok ? gload(xrow, r) : 0;
-            p.xv[u] = ok ? *reinterpret_cast<const v4f *>(xb + xr * a.ldx + 4 * cx) : v4f{0.f, 0.f, 0.f, 0.f};
-            // (an edgeless row's aggregate reads 0: its row may never be written)
-            const bool deg = ok && gload(a.rowptr, r + 1) > gload(a.rowptr, r);
-            p.av[u] = deg ? *reinterpret_cast<const v4f *>(a.agg + static_cast<int64_t>(r) * a.ld_agg + 4 * cx)
-                          : v4f{0.f, 0.f, 0.f, 0.f};
+            if (XR && xrow) xr = okr ? gload(xrow, r) : 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int k = 8 * cx + 4 * u;
+                const bool ok = okr && k < K0;
+                p.xv[u] = ok ? *reinterpret_cast<const v4f *>(xb + xr * a.ldx + k) : v4f{0.f, 0.f, 0.f, 0.f};
+                p.av[u] = ok ? *reinterpret_cast<const v4f *>(a.agg + static_cast<int64_t>(r) * a.ld_agg + k)
+                             : v4f{0.f, 0.f, 0.f, 0.f};
+            }
+            // (an edgeless row's aggregate counts as 0: its row may never be
+            // written -- tested at staging, so no load waits on these)
+            p.d0 = okr ? gload(a.rowptr, r) : 0;
+            p.d1 = okr ? gload(a.rowptr, r + 1) : 0;
         }
+    };
+    // two bf16 parts of 8 floats -> part images at (row, col), 16 B each
+    auto put8 = [&](__bf16 *img, int part_stride, int off, v4f v0, v4f v1) __attribute__((always_inline)) {
+        bf8 p1, p2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            __bf16 a1, a2;
+            split2(i < 4 ? v0[i] : v1[i - 4], a1, a2);
+            p1[i] = a1;
+            p2[i] = a2;
+        }
+        *reinterpret_cast<bf8 *>(img + off) = p1;
+        *reinterpret_cast<bf8 *>(img + part_stride + off) = p2;
     };
     // two bf16 parts of 4 floats -> part images at (row, col), 8 B each
     auto put4 = [&](__bf16 *img, int part_stride, int off, v4f v) __attribute__((always_inline)) {
@@ -259,11 +283,10 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         }
         if (t < 384) put4(ix, B2_ROWS * XS, rg * XS + 48 + 4 * cg, p.gv);
         put4(ih, B2_ROWS * HS, rh * HS + 4 * ch, p.hv);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            put4(ik, B2_ROWS * KS, (rx + 16 * u) * KS + 4 * cx, p.xv[u]);
-            put4(ia, B2_ROWS * KS, (rx + 16 * u) * KS + 4 * cx, p.av[u]);
-        }
+        put8(ik, B2_ROWS * KS, rx * KS + 8 * cx, p.xv[0], p.xv[1]);
+        const bool deg = p.d1 > p.d0;
+        const v4f z4{0.f, 0.f, 0.f, 0.f};
+        put8(ia, B2_ROWS * KS, rx * KS + 8 * cx, deg ? p.av[0] : z4, deg ? p.av[1] : z4);
     };
 
     // ---- stage B: dh tile (rt, nt) -> masked dz0 parts into sA
@@ -301,9 +324,9 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     };
 
     // ---- stage C: the weight-gradient products of one staged chunk
-    v4f acc0[8], acc1[3];
+    v4f acc0[KT], acc1[3];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc0[i] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < KT; ++i) acc0[i] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
     const int mat = wv >> 2;
@@ -314,25 +337,28 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         const bf8 a1 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2) * 64 + ln) * 8);
         const bf8 a2 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2 + 1) * 64 + ln) * 8);
         const __bf16 *img = mat ? ia : ik;
+        // every fragment read of the stage issued before its first MFMA (the
+        // reads' latency once per chunk, not once per tile)
+        bf8 b1[KT], b2[KT], x1[3], x2[3], h1[3], h2[3];
 #pragma unroll
-        for (int kt = 0; kt < 8; ++kt) {
-            if (kt < KT0) {
-                const bf8 b1 = tr_frag(img, KS, 16 * kt, ln);
-                const bf8 b2 = tr_frag(img + B2_ROWS * KS, KS, 16 * kt, ln);
-                acc0[kt] = mfma3(a1, a2, b1, b2, acc0[kt]);
-            }
+        for (int kt = 0; kt < KT; ++kt) {
+            b1[kt] = tr_frag(img, KS, 16 * kt, ln);
+            b2[kt] = tr_frag(img + B2_ROWS * KS, KS, 16 * kt, ln);
         }
         // C1: tiles 3 wv + u of [dW_r1; dW_l1] (f-tile mf, n-tile nn): A =
         // X^T, B = h
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int tt = 3 * wv + u, mf = tt >> 2, nn = tt & 3;
-            const bf8 x1 = tr_frag(ix, XS, 16 * mf, ln);
-            const bf8 x2 = tr_frag(ix + B2_ROWS * XS, XS, 16 * mf, ln);
-            const bf8 h1 = tr_frag(ih, HS, 16 * nn, ln);
-            const bf8 h2 = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
-            acc1[u] = mfma3(x1, x2, h1, h2, acc1[u]);
+            x1[u] = tr_frag(ix, XS, 16 * mf, ln);
+            x2[u] = tr_frag(ix + B2_ROWS * XS, XS, 16 * mf, ln);
+            h1[u] = tr_frag(ih, HS, 16 * nn, ln);
+            h2[u] = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
         }
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) acc0[kt] = mfma3(a1, a2, b1[kt], b2[kt], acc0[kt]);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) acc1[u] = mfma3(x1[u], x2[u], h1[u], h2[u], acc1[u]);
     };
 
     // ---- pipeline over the slice's chunks (two LDS buffers):
@@ -348,9 +374,9 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF);
         stage_images(pre, cur);
         load(c + 1, pre);
-        __syncthreads();
+        lds_barrier();  // (LDS only: the next chunk's loads stay in flight)
         stage_b(cur);
-        __syncthreads();
+        lds_barrier();
     }
     if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF);
 
@@ -360,9 +386,9 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         // dW_r0 / dW_l0 rows n = n0 + 16 nt + 4 q + i, columns 16 kt + l16
         float *d = slab + (mat ? 256LL * K0 : 0);
 #pragma unroll
-        for (int kt = 0; kt < 8; ++kt) {
+        for (int kt = 0; kt < KT; ++kt) {
             const int k = 16 * kt + l16;
-            if (kt < KT0 && k < K0) {
+            if (k < K0) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) d[static_cast<int64_t>(n0 + 16 * nt + 4 * q + i) * K0 + k] = acc0[kt][i];
             }
@@ -519,8 +545,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.slab = slab;
     b.S = B2_S;
     const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4;
-    auto go = [&](auto xr_c) {
-        auto fn = k_bwd2<decltype(xr_c)::value>;
+    auto go = [&](auto xr_c, auto kt_c) {
+        auto fn = k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value>;
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -530,7 +556,12 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
         hipLaunchKernelGGL(fn, dim3(B2_S * B2_NCH), dim3(B2_THREADS), lds, st, b);
         return launch_status();
     };
-    int rc = indexed ? go(std::true_type{}) : go(std::false_type{});
+    auto by_kt = [&](auto xr_c) {
+        if (K0 <= 64) return go(xr_c, std::integral_constant<int, 4>{});
+        if (K0 <= 112) return go(xr_c, std::integral_constant<int, 7>{});
+        return go(xr_c, std::integral_constant<int, 8>{});
+    };
+    int rc = indexed ? by_kt(std::true_type{}) : by_kt(std::false_type{});
     if (rc) return rc;
     const int64_t total = b2_slab_floats(static_cast<int>(K0), static_cast<int>(F1));
     const int n_red = static_cast<int>(ceil_div(total, 256));
