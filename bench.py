@@ -69,7 +69,7 @@ def parse():
                          "rows (graph replay) -- no copy in the loader, +6 us L0 forward and "
                          "+5 us L0 weight gradient in the step (scattered 400-B row reads)")
     ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg,"
-                                       "sage2_prep,sage2_edge,sage2_fwd,sage2_narrow",
+                                       "sage2_edge,sage2_fwd,sage2_narrow",
                     help="comma list of kernel spans timed with HIP events in the timed region "
                          "('all', or 'none' for profiler runs)")
     return ap.parse_args()

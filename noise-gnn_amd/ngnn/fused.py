@@ -461,7 +461,6 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     h_rows = N  # (upper bound: under the slot's bound fewer rows are written)
     f16 = 16 * MFMA_F32_TFS * 1e12  # fp16 MFMA peak; three products per fp32-equivalent product
     stages = [
-        ("sage2_prep", _lib.SAGE2_PREP, 4 * 3 * H * K0 + 8 * 2 * H * F1, 0, 0.0),
         ("sage2_edge", _lib.SAGE2_EDGE,
          4 * (block.E * (K0 + 1) + n_e * (K0 + 1) + n_e * K0 + n_e * H),
          2 * n_e * K0 * H, 3 * 2 * n_e * C0p * H / f16),

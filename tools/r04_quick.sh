@@ -18,6 +18,7 @@ fi
 for c in ${BENCHES:-}; do
   case $c in
     headline) A="" ;;
+    fused) A="--gather fused" ;;
     computers) A="--dataset computers --fanout 10,5 --batch-size 300 --hidden 512 --aggr max" ;;
     arxiv) A="--dataset ogbn-arxiv" ;;
     p3_f32) A="--fanout 20,15,10 --steps 20 --warmup 5" ;;
