@@ -561,6 +561,13 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * model's fp32 logits handed back in bf16 (Tensor.to(torch.bfloat16), the
  * `SAGE.forward` return dtype of a bf16 model).  src 16-B, dst 8-B aligned. */
 int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream);
+/* n <= 16 tensors cast in one launch: to_bf16 = 0: dst[k][i] = float(src[k]
+ * [i]) (bf16 -> fp32, exact); 1: dst[k][i] = bf16(src[k][i]) (round to
+ * nearest even, NaN kept), i < numels[k] -- a bf16 model's parameters widened
+ * for the fused kernels and their fp32 gradients narrowed back (Tensor.float()
+ * and its autograd backward, one ATen copy kernel per tensor). */
+int ngnn_cast_tensors(int n, const void *const *src, void *const *dst, const int64_t *numels,
+                      int to_bf16, void *stream);
 /* dst[r, :F] = float(src[r, :F]) (bf16 -> fp32, exact) for rows r <
  * min(n_rows, *n_rows_dev) (n_rows_dev nullable): the rows of a bf16 model's
  * activations a backward kernel reads as an fp32 mask. */

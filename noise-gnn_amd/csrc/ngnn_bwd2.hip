@@ -46,6 +46,8 @@ namespace {
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef short s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) __bf16 L16;  // an LDS bf16 (32-bit addresses)
+constexpr int kOOB = static_cast<int>(0xF0000000u);  // past every buffer range (< 3.75 GiB)
 
 constexpr int B2_ROWS = 32;            // rows per chunk: one 16x16x32 MFMA k-step
 constexpr int B2_NC = 64;              // hidden columns per workgroup
@@ -105,16 +107,15 @@ __device__ __forceinline__ v4f mfma3(bf8 a1, bf8 a2, bf8 b1, bf8 b2, v4f acc) { 
 // transposed read: the 16-lane group q takes the 4 x 16 block at rows
 // r0 + 4q .. + 3, columns c0 .. + 15 of a [rows][stride] bf16 image; lane i of
 // the group receives column c0 + i of those rows (cdna_hip_programming.md T10)
-__device__ __forceinline__ s4 tr_read(const __bf16 *img, int stride, int r0, int c0, int ln) {
+__device__ __forceinline__ s4 tr_read(const L16 *img, int stride, int r0, int c0, int ln) {
     const int q = ln >> 4, i = ln & 15;
-    const __bf16 *p = img + (r0 + 4 * q + (i >> 2)) * stride + c0 + 4 * (i & 3);
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s4 *)(const_cast<__bf16 *>(p)));
+    const L16 *p = img + (r0 + 4 * q + (i >> 2)) * stride + c0 + 4 * (i & 3);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4 *)(p));
 }
 
 // the MFMA operand over rows {4q .. 4q+3, 16+4q .. 16+4q+3} (the dz0
 // fragments' k order) of columns c0 + (lane & 15)
-__device__ __forceinline__ bf8 tr_frag(const __bf16 *img, int stride, int c0, int ln) {
+__device__ __forceinline__ bf8 tr_frag(const L16 *img, int stride, int c0, int ln) {
     const s4 a = tr_read(img, stride, 0, c0, ln), b = tr_read(img, stride, 16, c0, ln);
     typedef short s8 __attribute__((ext_vector_type(8)));
     const s8 v{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
@@ -144,8 +145,9 @@ __device__ __forceinline__ float sum_xor32(float v) {
 // KT: 16-column tiles of K0 computed (past K0 the images hold zeros)
 template <bool XR, int KT>
 __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
-    extern __shared__ __attribute__((aligned(16))) __bf16 lb[];
-    float *sred = reinterpret_cast<float *>(lb + 2 * BUF);  // [2][256] reductions at the end
+    extern __shared__ __attribute__((aligned(16))) __bf16 lb_[];
+    L16 *lb = (L16 *)(lb_);  // (an address-space cast: the shared array IS in LDS)
+    float *sred = reinterpret_cast<float *>(lb_ + 2 * BUF);  // [2][256] reductions at the end
 
     const int t = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -169,21 +171,29 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     const int rt = wv >> 2, nt = wv & 3;
     bf8 wb[3][2];
     {
+        // (buffer loads over the F1 weight rows: all 24 in flight, no branches)
+        const i32x4 wrr = make_rsrc(a.wr1, static_cast<uint32_t>(F1 * a.ldw1 * 4));
+        const i32x4 wlr = make_rsrc(a.wl1, static_cast<uint32_t>(F1 * a.ldw1 * 4));
         const int n = n0 + 16 * nt + l16;
+        float v[3][8];
 #pragma unroll
-        for (int kc = 0; kc < 3; ++kc) {
+        for (int kc = 0; kc < 3; ++kc)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int k = 32 * kc + 8 * q + j;
                 const int f = k < 48 ? k : k - 48;
-                const float *w = k < 48 ? a.wr1 : a.wl1;
-                const float v = f < F1 ? w[static_cast<int64_t>(f) * a.ldw1 + n] : 0.0f;
+                const int o = f < F1 ? (f * static_cast<int>(a.ldw1) + n) * 4 : kOOB;
+                v[kc][j] = k < 48 ? buf_load1(wrr, o, 0, 0) : buf_load1(wlr, o, 0, 0);
+            }
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
                 __bf16 p1, p2;
-                split2(v, p1, p2);
+                split2(v[kc][j], p1, p2);
                 wb[kc][0][j] = p1;
                 wb[kc][1][j] = p2;
             }
-        }
     }
     const float *xb = a.x_dev ? gload(a.x_dev, 0) : a.x;
     const int64_t *xrow = !XR ? nullptr : a.xrow_dev ? gload(a.xrow_dev, 0) : a.xrow;
@@ -200,6 +210,25 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         float dyv[4];
         v4f gv, hv, xv[2], av[2];
         int d0, d1;  // rowptr of the agg row (edgeless rows masked at staging)
+        int xi;      // XR: n_id of the x row of the NEXT chunk (one chunk ahead)
+    };
+    // every operand through a buffer resource over its live rows: 32-bit
+    // offsets = a per-thread base + the chunk's row offset, no 64-bit
+    // address arithmetic per load; rows past the range read 0
+    const i32x4 dyr = make_rsrc(a.dy, static_cast<uint32_t>(static_cast<int64_t>(R) * a.ldy * 4));
+    const i32x4 gr = make_rsrc(a.g, static_cast<uint32_t>(static_cast<int64_t>(Rn) * a.C4 * 4));
+    const i32x4 hr = make_rsrc(a.h, static_cast<uint32_t>(static_cast<int64_t>(Rn) * a.ldh * 4));
+    const i32x4 ar = make_rsrc(a.agg, static_cast<uint32_t>(static_cast<int64_t>(Rn) * a.ld_agg * 4));
+    const i32x4 rpr = make_rsrc(a.rowptr, static_cast<uint32_t>(static_cast<int64_t>(Rn + 1) * 4));
+    const int64_t xrows = xrow ? a.x_rows : static_cast<int64_t>(Rn);
+    const i32x4 xrr = make_rsrc_u(xb, static_cast<uint32_t>(xrows * a.ldx * 4));
+    const i32x4 ir = make_rsrc_u(xrow, static_cast<uint32_t>(xrow ? static_cast<int64_t>(Rn) * 8 : 0));
+    const uint32_t ldy4 = static_cast<uint32_t>(a.ldy) * 4u, ldh4 = static_cast<uint32_t>(a.ldh) * 4u;
+    const uint32_t lda4 = static_cast<uint32_t>(a.ld_agg) * 4u, ldx4 = static_cast<uint32_t>(a.ldx) * 4u;
+    const uint32_t C44 = static_cast<uint32_t>(a.C4) * 4u;
+    auto iload = [&](int c) __attribute__((always_inline)) -> int {  // low word of n_id
+        const int r = c * B2_ROWS + rx;
+        return buf_load1i(ir, (c < ce && r < Rn) ? 8 * r : kOOB, 0, 0);
     };
     auto load = [&](int c, Pre &p) __attribute__((always_inline)) {
         const int r0 = c * B2_ROWS;
@@ -207,40 +236,40 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int lr = rd + 10 * u, r = r0 + lr;
-            p.dyv[u] = (live && t < 480 && lr < B2_ROWS && r < R && fd < F1) ? a.dy[static_cast<int64_t>(r) * a.ldy + fd] : 0.0f;
+            const bool ok = live && t < 480 && lr < B2_ROWS && r < R && fd < F1;
+            p.dyv[u] = buf_load1(dyr, ok ? static_cast<int>(static_cast<uint32_t>(r) * ldy4) + 4 * fd : kOOB, 0, 0);
         }
         {
             const int r = r0 + rg;
-            p.gv = (live && t < 384 && r < Rn && 4 * cg < a.C4)
-                       ? *reinterpret_cast<const v4f *>(a.g + static_cast<int64_t>(r) * a.C4 + 4 * cg)
-                       : v4f{0.f, 0.f, 0.f, 0.f};
+            const bool ok = live && t < 384 && r < Rn && 4 * cg < a.C4;
+            p.gv = buf_load4(gr, ok ? static_cast<int>(static_cast<uint32_t>(r) * C44) + 16 * cg : kOOB, 0, 0);
         }
         {
             const int r = r0 + rh;
-            p.hv = (live && r < Rn) ? *reinterpret_cast<const v4f *>(a.h + static_cast<int64_t>(r) * a.ldh + n0 + 4 * ch)
-                                    : v4f{0.f, 0.f, 0.f, 0.f};
+            p.hv = buf_load4(hr, (live && r < Rn) ? static_cast<int>(static_cast<uint32_t>(r) * ldh4) + 4 * (n0 + 4 * ch) : kOOB,
+                             0, 0);
         }
         {
             const int r = r0 + rx;
             const bool okr = live && r < Rn;
-            int64_t xr = r;
-            if (XR && xrow) xr = okr ? gload(xrow, r) : 0;
+            // (XR: this chunk's n_id word arrived a chunk ago)
+            const uint32_t xr = (XR && xrow) ? static_cast<uint32_t>(p.xi) : static_cast<uint32_t>(r);
+            if (XR) p.xi = iload(c + 1);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int k = 8 * cx + 4 * u;
                 const bool ok = okr && k < K0;
-                p.xv[u] = ok ? *reinterpret_cast<const v4f *>(xb + xr * a.ldx + k) : v4f{0.f, 0.f, 0.f, 0.f};
-                p.av[u] = ok ? *reinterpret_cast<const v4f *>(a.agg + static_cast<int64_t>(r) * a.ld_agg + k)
-                             : v4f{0.f, 0.f, 0.f, 0.f};
+                p.xv[u] = buf_load4(xrr, ok ? static_cast<int>(xr * ldx4) + 4 * k : kOOB, 0, 0);
+                p.av[u] = buf_load4(ar, ok ? static_cast<int>(static_cast<uint32_t>(r) * lda4) + 4 * k : kOOB, 0, 0);
             }
             // (an edgeless row's aggregate counts as 0: its row may never be
             // written -- tested at staging, so no load waits on these)
-            p.d0 = okr ? gload(a.rowptr, r) : 0;
-            p.d1 = okr ? gload(a.rowptr, r + 1) : 0;
+            p.d0 = buf_load1i(rpr, okr ? 4 * r : kOOB, 0, 0);
+            p.d1 = buf_load1i(rpr, okr ? 4 * r + 4 : kOOB, 0, 0);
         }
     };
     // two bf16 parts of 8 floats -> part images at (row, col), 16 B each
-    auto put8 = [&](__bf16 *img, int part_stride, int off, v4f v0, v4f v1) __attribute__((always_inline)) {
+    auto put8 = [&](L16 *img, int part_stride, int off, v4f v0, v4f v1) __attribute__((always_inline)) {
         bf8 p1, p2;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -249,11 +278,11 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             p1[i] = a1;
             p2[i] = a2;
         }
-        *reinterpret_cast<bf8 *>(img + off) = p1;
-        *reinterpret_cast<bf8 *>(img + part_stride + off) = p2;
+        *reinterpret_cast<__attribute__((address_space(3))) bf8 *>(img + off) = p1;
+        *reinterpret_cast<__attribute__((address_space(3))) bf8 *>(img + part_stride + off) = p2;
     };
     // two bf16 parts of 4 floats -> part images at (row, col), 8 B each
-    auto put4 = [&](__bf16 *img, int part_stride, int off, v4f v) __attribute__((always_inline)) {
+    auto put4 = [&](L16 *img, int part_stride, int off, v4f v) __attribute__((always_inline)) {
         bf4 p1, p2;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -262,12 +291,12 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             p1[i] = a1;
             p2[i] = a2;
         }
-        *reinterpret_cast<bf4 *>(img + off) = p1;
-        *reinterpret_cast<bf4 *>(img + part_stride + off) = p2;
+        *reinterpret_cast<__attribute__((address_space(3))) bf4 *>(img + off) = p1;
+        *reinterpret_cast<__attribute__((address_space(3))) bf4 *>(img + part_stride + off) = p2;
     };
     float d1acc = 0.0f;  // db1 partial: column fd, rows of this thread
-    auto stage_images = [&](const Pre &p, __bf16 *buf) __attribute__((always_inline)) {
-        __bf16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
+    auto stage_images = [&](const Pre &p, L16 *buf) __attribute__((always_inline)) {
+        L16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
         if (t < 480) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -291,15 +320,15 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
 
     // ---- stage B: dh tile (rt, nt) -> masked dz0 parts into sA
     float d0acc = 0.0f;  // db0 partial: column 16 nt + l16, rows 16 rt + 4 q + i
-    auto stage_b = [&](const __bf16 *buf) __attribute__((always_inline)) {
-        const __bf16 *ix = buf, *ih = ix + IMG_X;
-        __bf16 *sa = const_cast<__bf16 *>(ih + IMG_H + 2 * IMG_K);
+    auto stage_b = [&](L16 *buf) __attribute__((always_inline)) {
+        const L16 *ix = buf, *ih = ix + IMG_X;
+        L16 *sa = buf + IMG_X + IMG_H + 2 * IMG_K;
         v4f acc{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc) {
             const int off = (16 * rt + l16) * XS + 32 * kc + 8 * q;
-            const bf8 a1 = *reinterpret_cast<const bf8 *>(ix + off);
-            const bf8 a2 = *reinterpret_cast<const bf8 *>(ix + B2_ROWS * XS + off);
+            const bf8 a1 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(ix + off);
+            const bf8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(ix + B2_ROWS * XS + off);
             acc = mfma3(a1, a2, wb[kc][0], wb[kc][1], acc);
         }
         // mask: the sign of h's first part (bf16 keeps sign and zero)
@@ -318,9 +347,9 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             p1[i] = a1;
             p2[i] = a2;
         }
-        __bf16 *d = sa + ((nt * 2) * 64 + ln) * 8 + 4 * rt;
-        *reinterpret_cast<bf4 *>(d) = p1;
-        *reinterpret_cast<bf4 *>(d + 64 * 8) = p2;
+        L16 *d = sa + ((nt * 2) * 64 + ln) * 8 + 4 * rt;
+        *reinterpret_cast<__attribute__((address_space(3))) bf4 *>(d) = p1;
+        *reinterpret_cast<__attribute__((address_space(3))) bf4 *>(d + 64 * 8) = p2;
     };
 
     // ---- stage C: the weight-gradient products of one staged chunk
@@ -330,13 +359,13 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
     const int mat = wv >> 2;
-    auto stage_c = [&](const __bf16 *buf) __attribute__((always_inline)) {
-        const __bf16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
-        const __bf16 *sa = ia + IMG_K;
+    auto stage_c = [&](const L16 *buf) __attribute__((always_inline)) {
+        const L16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
+        const L16 *sa = ia + IMG_K;
         // C0: A = dz0^T of n-tile nt (both row tiles), B = x / agg0 tiles
-        const bf8 a1 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2) * 64 + ln) * 8);
-        const bf8 a2 = *reinterpret_cast<const bf8 *>(sa + ((nt * 2 + 1) * 64 + ln) * 8);
-        const __bf16 *img = mat ? ia : ik;
+        const bf8 a1 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(sa + ((nt * 2) * 64 + ln) * 8);
+        const bf8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(sa + ((nt * 2 + 1) * 64 + ln) * 8);
+        const L16 *img = mat ? ia : ik;
         // every fragment read of the stage issued before its first MFMA (the
         // reads' latency once per chunk, not once per tile)
         bf8 b1[KT], b2[KT], x1[3], x2[3], h1[3], h2[3];
@@ -368,9 +397,11 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     //   phase 2: stage B(c) on buffer c&1 -> its dz0 fragments
     //   barrier
     Pre pre;
+    pre.xi = XR ? iload(cb) : 0;
+    if (XR) asm volatile("" : "+v"(pre.xi));  // (the first chunk's n_id: waited here once)
     if (cb < ce) load(cb, pre);
     for (int c = cb; c < ce; ++c) {
-        __bf16 *cur = lb + (c & 1) * BUF;
+        L16 *cur = lb + (c & 1) * BUF;
         if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF);
         stage_images(pre, cur);
         load(c + 1, pre);
@@ -383,15 +414,15 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     // ---- this workgroup's part of slab s (zeros for an empty slice)
     float *slab = a.slab + static_cast<int64_t>(s) * b2_slab_floats(K0, F1);
     {
+        const i32x4 sr = make_rsrc(slab, static_cast<uint32_t>(b2_slab_floats(K0, F1) * 4));
         // dW_r0 / dW_l0 rows n = n0 + 16 nt + 4 q + i, columns 16 kt + l16
-        float *d = slab + (mat ? 256LL * K0 : 0);
+        const int base0 = mat ? 256 * K0 : 0;
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
             const int k = 16 * kt + l16;
-            if (k < K0) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) d[static_cast<int64_t>(n0 + 16 * nt + 4 * q + i) * K0 + k] = acc0[kt][i];
-            }
+            for (int i = 0; i < 4; ++i)
+                buf_store1(acc0[kt][i], sr, k < K0 ? 4 * (base0 + (n0 + 16 * nt + 4 * q + i) * K0 + k) : kOOB, 0, 0);
         }
         // dW_r1 / dW_l1 rows f = 16 mf + 4 q + i (< 48: W_r1, else W_l1),
         // columns n0 + 16 nn + l16
@@ -402,10 +433,8 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             for (int i = 0; i < 4; ++i) {
                 const int f = 16 * mf + 4 * q + i;
                 const int fr = f < 48 ? f : f - 48;
-                if (fr < F1) {
-                    float *d1 = slab + 512LL * K0 + 256 + (f < 48 ? 0 : 256LL * F1);
-                    d1[static_cast<int64_t>(fr) * 256 + n0 + 16 * nn + l16] = acc1[u][i];
-                }
+                const int o = 512 * K0 + 256 + (f < 48 ? 0 : 256 * F1) + fr * 256 + n0 + 16 * nn + l16;
+                buf_store1(acc1[u][i], sr, fr < F1 ? 4 * o : kOOB, 0, 0);
             }
         }
     }

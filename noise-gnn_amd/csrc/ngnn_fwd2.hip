@@ -225,20 +225,26 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     const int srow = 2 * wv + (ln >> 5), sslot = ln & 31;
     const bool scol = 4 * sslot < a.K0 && sslot < 8 * C0;
     auto tile_row = [&](int j, int rr) { return (b + j * G) * F2_ROWS + rr; };
+    // index words through buffer resources (no branches, 32-bit offsets;
+    // out-of-range slots read 0 and are masked by the degree at use)
+    const i32x4 rpr = make_rsrc(a.rowptr, static_cast<uint32_t>(static_cast<int64_t>(n_rows + 1) * 4));
+    const i32x4 cr = make_rsrc(colg, 0xF0000000u);
     auto rowptr_of = [&](int j, int &beg, int &end) __attribute__((always_inline)) {
         const int r = tile_row(j, srow);
         const bool ok = j < ntj && r < n_rows;
-        beg = ok ? gload(a.rowptr, r) : 0;
-        end = ok ? gload(a.rowptr, r + 1) : 0;
+        beg = buf_load1i(rpr, ok ? 4 * r : kOOB2, 0, 0);
+        end = buf_load1i(rpr, ok ? 4 * r + 4 : kOOB2, 0, 0);
     };
     auto ids_of = [&](int beg, int end, int e0, int (&cw)[G2_NB]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int e = 0; e < G2_NB; ++e) cw[e] = beg + e0 + e < end ? gload(colg, beg + e0 + e) : -1;
+        for (int e = 0; e < G2_NB; ++e) cw[e] = buf_load1i(cr, beg + e0 + e < end ? 4 * (beg + e0 + e) : kOOB2, 0, 0);
     };
-    auto rows_of = [&](const int (&cw)[G2_NB], v4f (&v)[G2_NB]) __attribute__((always_inline)) {
+    // (row offsets as 24-bit products: every row of a table under the 32-bit
+    // offset limit has an index < 2^24, and ld4 < 2^24)
+    auto rows_of = [&](int beg, int end, int e0, const int (&cw)[G2_NB], v4f (&v)[G2_NB]) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < G2_NB; ++e)
-            v[e] = buf_load4(xr, (cw[e] >= 0 && scol) ? static_cast<int>(static_cast<uint32_t>(cw[e]) * ld4 + 16u * sslot) : kOOB2,
+            v[e] = buf_load4(xr, (beg + e0 + e < end && scol) ? static_cast<int>(__umul24(static_cast<uint32_t>(cw[e]), ld4) + 16u * sslot) : kOOB2,
                              0, 0);
     };
 
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     for (int j = 0; j < ntj; ++j) {
         const int B = j & 1;
         v4f v[G2_NB];
-        rows_of(cw, v);
+        rows_of(begc, endc, 0, cw, v);
         // the next tile's ids, the row pointers of the one after
         int cwn[G2_NB];
         ids_of(begn, endn, 0, cwn);
@@ -269,7 +275,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
         for (int e0 = G2_NB; e0 < dmax; e0 += G2_NB) {
             int ce[G2_NB];
             ids_of(begc, endc, e0, ce);
-            rows_of(ce, v);
+            rows_of(begc, endc, e0, ce, v);
 #pragma unroll
             for (int e = 0; e < G2_NB; ++e) acc += v[e];
         }

@@ -191,34 +191,50 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
 // Tensor.to(torch.bfloat16) on the [N, C] logits.
 namespace ngnn {
 namespace {
+// W8: 8 elements per thread step (two 16-B loads, one 16-B store: wide
+// stores move the logits of a 1.5 M-row block at twice the 8-B stores' rate);
+// else 4 (8-B stores, dst only 8-B aligned)
+template <bool W8>
 __global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src,
                                                     uint16_t *__restrict__ dst, int64_t n) {
-    auto rne = [](float f) -> uint16_t {
+    auto rne = [](float f) -> uint32_t {
         const uint32_t u = __float_as_uint(f);
-        if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>(0x7fc0u);
-        return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+        return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
     };
-    const int64_t n4 = n >> 2;
+    auto pack = [&](float4 v) { return uint2{rne(v.x) | (rne(v.y) << 16), rne(v.z) | (rne(v.w) << 16)}; };
+    constexpr int E = W8 ? 8 : 4;
+    const int64_t nv = n / E;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    auto put = [&](int64_t i, float4 v) {
-        const uint2 o{static_cast<uint32_t>(rne(v.x)) | (static_cast<uint32_t>(rne(v.y)) << 16),
-                      static_cast<uint32_t>(rne(v.z)) | (static_cast<uint32_t>(rne(v.w)) << 16)};
-        reinterpret_cast<uint2 *>(dst)[i] = o;
-    };
     int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
-    // four 16-B loads in flight per thread before the first store
-    constexpr int U = 4;
-    for (; i + (U - 1) * stride < n4; i += U * stride) {
-        float4 v[U];
+    // U steps' loads in flight per thread before the first store
+    constexpr int U = W8 ? 2 : 4;
+    auto step_load = [&](int64_t k, float4 (&v)[2]) {
+        v[0] = reinterpret_cast<const float4 *>(src)[k * (E / 4)];
+        if (W8) v[1] = reinterpret_cast<const float4 *>(src)[k * 2 + 1];
+    };
+    auto step_store = [&](int64_t k, const float4 (&v)[2]) {
+        if (W8) {
+            const uint2 a = pack(v[0]), b = pack(v[1]);
+            reinterpret_cast<uint4 *>(dst)[k] = uint4{a.x, a.y, b.x, b.y};
+        } else {
+            reinterpret_cast<uint2 *>(dst)[k] = pack(v[0]);
+        }
+    };
+    for (; i + (U - 1) * stride < nv; i += U * stride) {
+        float4 v[U][2];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = reinterpret_cast<const float4 *>(src)[i + u * stride];
+        for (int u = 0; u < U; ++u) step_load(i + u * stride, v[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) put(i + u * stride, v[u]);
+        for (int u = 0; u < U; ++u) step_store(i + u * stride, v[u]);
     }
-    for (; i < n4; i += stride) put(i, reinterpret_cast<const float4 *>(src)[i]);
-    for (int64_t i = 4 * n4 + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-         i += stride)
-        dst[i] = rne(src[i]);
+    for (; i < nv; i += stride) {
+        float4 v[2];
+        step_load(i, v);
+        step_store(i, v);
+    }
+    for (int64_t k = E * nv + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; k < n; k += stride)
+        dst[k] = static_cast<uint16_t>(rne(src[k]));
 }
 }  // namespace
 }  // namespace ngnn
@@ -228,9 +244,65 @@ extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *
     NGNN_RETURN_IF(n < 0 || (n > 0 && (!src || !dst)), NGNN_E_ARG);
     NGNN_RETURN_IF(!aligned(src, 16) || !aligned(dst, 8), NGNN_E_SHAPE);
     if (n == 0) return NGNN_OK;
-    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 4), 256), 2048));
-    hipLaunchKernelGGL(k_cast_bf16, dim3(grid), dim3(256), 0, as_stream(stream), src,
-                       static_cast<uint16_t *>(dst), n);
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 8), 256), 2048));
+    if (aligned(dst, 16))
+        hipLaunchKernelGGL(k_cast_bf16<true>, dim3(grid), dim3(256), 0, as_stream(stream), src,
+                           static_cast<uint16_t *>(dst), n);
+    else
+        hipLaunchKernelGGL(k_cast_bf16<false>, dim3(grid), dim3(256), 0, as_stream(stream), src,
+                           static_cast<uint16_t *>(dst), n);
+    return launch_status();
+}
+
+// ---- n tensors cast in ONE launch: bf16 -> fp32 (exact) or fp32 -> bf16
+// (round to nearest even, NaN kept): a bf16 model's parameters widened for
+// the fused kernels and their fp32 gradients narrowed back (each was an ATen
+// copy kernel per tensor)
+namespace ngnn {
+namespace {
+struct CastTensors {
+    const void *src[kMaxT];
+    void *dst[kMaxT];
+    int64_t off[kMaxT + 1];  // prefix sums of numel
+    int n;
+};
+template <bool TO_BF16>
+__global__ __launch_bounds__(256) void k_cast_tensors(CastTensors T) {
+    const int64_t total = T.off[T.n];
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total; i += stride) {
+        int k = 0;
+        while (i >= T.off[k + 1]) ++k;  // (<= 16 tensors)
+        const int64_t j = i - T.off[k];
+        if (TO_BF16) {
+            const float v = static_cast<const float *>(T.src[k])[j];
+            static_cast<__bf16 *>(T.dst[k])[j] = static_cast<__bf16>(v);
+        } else {
+            const uint16_t b = static_cast<const uint16_t *>(T.src[k])[j];
+            static_cast<float *>(T.dst[k])[j] = __uint_as_float(static_cast<uint32_t>(b) << 16);
+        }
+    }
+}
+}  // namespace
+}  // namespace ngnn
+
+extern "C" int ngnn_cast_tensors(int n, const void *const *src, void *const *dst, const int64_t *numels,
+                                 int to_bf16, void *stream) {
+    using namespace ngnn;
+    NGNN_RETURN_IF(n < 0 || n > kMaxT || (n > 0 && (!src || !dst || !numels)), NGNN_E_ARG);
+    CastTensors T;
+    T.n = n;
+    T.off[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        NGNN_RETURN_IF(numels[k] < 0 || (numels[k] > 0 && (!src[k] || !dst[k])), NGNN_E_ARG);
+        T.src[k] = src[k];
+        T.dst[k] = dst[k];
+        T.off[k + 1] = T.off[k] + numels[k];
+    }
+    if (n == 0 || T.off[n] == 0) return NGNN_OK;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(T.off[n], 256), 1024));
+    if (to_bf16) hipLaunchKernelGGL(k_cast_tensors<true>, dim3(grid), dim3(256), 0, as_stream(stream), T);
+    else hipLaunchKernelGGL(k_cast_tensors<false>, dim3(grid), dim3(256), 0, as_stream(stream), T);
     return launch_status();
 }
 

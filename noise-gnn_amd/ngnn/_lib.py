@@ -73,6 +73,7 @@ SIGNATURES = {
                                  _i64, _p, _i64,
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
+    "ngnn_cast_tensors": (_int, [_int, _p, _p, _p, _int, _p]),
     "ngnn_sage2_bwd_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64,
                               _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p,

@@ -606,8 +606,10 @@ class _SAGEStack(torch.autograd.Function):
         written = rows_hint is None or any(
             not (pre_top and i == L - 1) for i in range(L - 1, -1 if need_dx else 0, -1))
         if written:
-            bnd = torch.full((L + 1,), int(rows_hint) if rows_hint is not None else 0,
-                             dtype=torch.int32, device=dev)
+            # a fresh copy of the cached constant (a device-to-device memcpy:
+            # no fill kernel in the step)
+            bnd = torch.empty(L + 1, dtype=torch.int32, device=dev)
+            bnd.copy_(const_bounds(dev, L, int(rows_hint) if rows_hint is not None else 0))
         else:  # read-only: a cached constant (no fill launch per step)
             bnd = const_bounds(dev, L, int(rows_hint))
         bp = [bnd.data_ptr() + 4 * j for j in range(L + 1)]
@@ -924,7 +926,7 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
         if not (keep_bf16_x and x.dtype == torch.bfloat16 and not x.requires_grad
                 and bf16_rows_ok(x)):
             x = x.float()
-        params = [None if q is None else q.float() for q in params]
+        params = widen_params(params)
     else:
         gouts = _claim_grad_views(params)
     p = model.dropout if model.training else 0.0
@@ -937,6 +939,59 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
         return _StackOutBF16.apply(out)
     from .losses import cast_keep_rows
     return cast_keep_rows(out, out_dtype)
+
+
+def _cast_tensors(src, dst, to_bf16: bool) -> None:
+    import ctypes
+    n = len(src)
+    for i in range(0, n, 16):  # (16 tensors per launch)
+        a, b = src[i:i + 16], dst[i:i + 16]
+        k = len(a)
+        S = (ctypes.c_void_p * k)(*[t.data_ptr() for t in a])
+        D = (ctypes.c_void_p * k)(*[t.data_ptr() for t in b])
+        N = (ctypes.c_int64 * k)(*[t.numel() for t in a])
+        _lib.check(_lib.load().ngnn_cast_tensors(k, S, D, N, int(to_bf16), _lib.stream_handle(a[0].device)),
+                   "ngnn_cast_tensors")
+
+
+class _WidenParams(torch.autograd.Function):
+    """A bf16 model's parameters as fp32 tensors for the fused kernels:
+    ONE ngnn_cast_tensors launch forward (bf16 -> fp32, exact) and one
+    backward (the fp32 gradients rounded to the parameters' bf16) --
+    Tensor.float() and its autograd backward were an ATen copy kernel per
+    tensor and direction (~18 per step of the products 3-layer bf16 model)."""
+
+    @staticmethod
+    def forward(ctx, *params):
+        outs = [torch.empty(q.shape, dtype=torch.float32, device=q.device) for q in params]
+        _cast_tensors([q.contiguous() for q in params], outs, to_bf16=False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        live = [i for i, g in enumerate(grads) if g is not None]
+        outs = [None] * len(grads)
+        if live:
+            src = [grads[i].contiguous() for i in live]
+            dst = [torch.empty(g.shape, dtype=torch.bfloat16, device=g.device) for g in src]
+            _cast_tensors(src, dst, to_bf16=True)
+            for i, d in zip(live, dst):
+                outs[i] = d
+        return tuple(outs)
+
+
+def widen_params(params):
+    """fp32 views of the stack's parameters: bf16 ones through _WidenParams
+    (one launch each way), fp32 ones as they are, None kept."""
+    idx = [i for i, q in enumerate(params) if q is not None and q.dtype == torch.bfloat16]
+    out = [None if (q is None or q.dtype == torch.bfloat16) else q.float() for q in params]
+    if idx:
+        wide = _WidenParams.apply(*[params[i] for i in idx])
+        if not isinstance(wide, tuple):
+            wide = (wide,)
+        for i, w in zip(idx, wide):
+            out[i] = w
+    return out
 
 
 _out_grads: dict = {}
@@ -968,6 +1023,12 @@ class _StackOutBF16(torch.autograd.Function):
             buf = torch.empty(g.shape, dtype=torch.float32, device=g.device)
             _out_grads[key] = buf
         R = min(int(rows), g.size(0))
-        buf[:R].copy_(g[:R])
+        if g.dtype == torch.bfloat16 and g.dim() == 2 and g.stride(1) == 1:
+            _lib.check(_lib.load().ngnn_widen_bf16_rows(_lib.ptr(g), g.stride(0), g.size(1), R, None,
+                                                        _lib.ptr(buf), buf.stride(0),
+                                                        _lib.stream_handle(g.device)),
+                       "ngnn_widen_bf16_rows")
+        else:
+            buf[:R].copy_(g[:R])
         buf._ngnn_nonzero_rows = R  # rows >= R are stale: the stack never reads them
         return buf

@@ -159,9 +159,15 @@ class _SeedXentBF16(torch.autograd.Function):
     def forward(ctx, logits, y, batch_size: int, ignore_index: int):
         B = int(batch_size)
         ctx.n_full = logits.size(0)
-        # the fp32 node's forward on the widened seed rows (it fills ctx for
+        # the seed rows widened by the library (exact; an ATen copy kernel
+        # otherwise), then the fp32 node's forward on them (it fills ctx for
         # its backward: saved rows, ws, B, n = B)
-        return _SeedXent.forward(ctx, logits[:B].float(), y, B, ignore_index)
+        lw = logits if logits.stride(1) == 1 else logits.contiguous()
+        wide = torch.empty(B, lw.size(1), dtype=torch.float32, device=lw.device)
+        _lib.check(_lib.load().ngnn_widen_bf16_rows(_lib.ptr(lw), lw.stride(0), lw.size(1), B, None,
+                                                    _lib.ptr(wide), wide.stride(0),
+                                                    _lib.stream_handle(lw.device)), "ngnn_widen_bf16_rows")
+        return _SeedXent.forward(ctx, wide, y, B, ignore_index)
 
     @staticmethod
     def backward(ctx, g):
@@ -173,7 +179,9 @@ class _SeedXentBF16(torch.autograd.Function):
             buf = torch.zeros(max(n, 1), C, dtype=torch.bfloat16, device=dx.device)
             _bf16_rows[key] = buf
         out = buf[:n]
-        out[:B].copy_(dx[:B])
+        d = dx[:B] if dx[:B].is_contiguous() else dx[:B].contiguous()
+        _lib.check(_lib.load().ngnn_cast_f32_bf16(_lib.ptr(d), _lib.ptr(out), B * C,
+                                                  _lib.stream_handle(d.device)), "ngnn_cast_f32_bf16")
         out._ngnn_nonzero_rows = B
         return out, None, None, None
 
