@@ -80,7 +80,7 @@ int dispatch_rt(int ntw, const RtArgs &a, int reduce, bool wl_lds, bool x3, int 
 // rounding).  16 lanes per row (float4 columns), 4 rows per wave, 8
 // neighbour rows in flight per lane; per column edge order from 0, then
 // / deg for mean.
-constexpr int NA_UNR = 8;
+constexpr int NA_UNR = 16;
 template <bool MEAN>
 __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z, int64_t ldz, int Fo,
                                                     const int32_t *__restrict__ rowptr,
@@ -93,18 +93,27 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
     if (n_edge_dev) nr = min(nr, *n_edge_dev);
     const int sub = threadIdx.x & 15;
     const int F4 = (Fo + 3) >> 2;
+    // index words through buffer resources (masked slots read 0, no
+    // branches): a row's first 16 neighbour ids in ONE round trip, then its
+    // 16 z rows in one more (a fanout of <= 16 needs exactly two)
+    const i32x4 cr = make_rsrc(col, 0xF0000000u);
+    const uint32_t ldz4 = static_cast<uint32_t>(ldz) * 4u;
+    constexpr int OOB = static_cast<int>(0xF0000000u);
     for (int d = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; d < nr; d += (gridDim.x * blockDim.x) >> 4) {
         const int beg = rowptr[d], end = rowptr[d + 1];
         if (beg == end) continue;
         for (int c4 = sub; c4 < F4; c4 += 16) {
             v4f acc{0.f, 0.f, 0.f, 0.f};
             for (int e = beg; e < end; e += NA_UNR) {
+                int id[NA_UNR];
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
+                const i32x4 zr = make_rsrc(z, 0xF0000000u);
                 v4f v[NA_UNR];
 #pragma unroll
-                for (int u = 0; u < NA_UNR; ++u) {
-                    const int ee = min(e + u, end - 1);  // a short batch re-reads its last row
-                    v[u] = *reinterpret_cast<const v4f *>(z + static_cast<int64_t>(col[ee]) * ldz + 4 * c4);
-                }
+                for (int u = 0; u < NA_UNR; ++u)
+                    v[u] = buf_load4(zr, e + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(id[u]), ldz4)) + 16 * c4 : OOB,
+                                     0, 0);
 #pragma unroll
                 for (int u = 0; u < NA_UNR; ++u)
                     if (e + u < end) acc += v[u];
@@ -184,6 +193,8 @@ int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *ro
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
                       const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st) {
     const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
+    // (32-bit buffer offsets into z: a 24-bit row index times the row bytes)
+    NGNN_RETURN_IF(n_rows * ldz * 4 >= 0xF0000000ll || n_rows >= (1 << 24) || ldz * 4 >= (1 << 24), NGNN_E_RANGE);
     const unsigned grid = static_cast<unsigned>(
         std::max<int64_t>(1, std::min<int64_t>(4 * num_cus(), ceil_div(rows, 16))));
     if (reduce == NGNN_REDUCE_MEAN)
