@@ -482,10 +482,16 @@ def main():
             "avg_us_eager_pass": None if eager_us is None else round(eager_us, 2),
             "alg_bytes_per_launch": int(nbytes / n), "alg_flops_per_launch": int(flops / n),
             "hbm_frac": round(f_hbm, 4), "mfma_frac": round(f_mfma, 4),
-            "mfma_peak_note": "f32-equivalent peak of the instruction mix: root term 6 bf16 "
-                              "products per f32 product (16x the 157.3 TF f32 MFMA rate), "
-                              "neighbour term f32 MFMA; a layer on the 64-row fallback kernel "
-                              "(exact f32 MFMA throughout) is priced at the 157.3 TF f32 peak",
+            "mfma_peak_note": (
+                "f32-equivalent peak of the instruction mix: every fp32 product as three fp16 "
+                "MFMA products of two-part (hi/lo) fp16 splits, priced at the dense fp16 rate "
+                "(16x the 157.3 TF f32 MFMA rate) / 3; both layers' products (k_fwd2: root + "
+                "neighbour of layer 0 on the edge-row complement, both layer-1 products)"
+                if name == "sage2_fwd" else
+                "f32-equivalent peak of the instruction mix: root term 6 bf16 "
+                "products per f32 product (16x the 157.3 TF f32 MFMA rate), "
+                "neighbour term f32 MFMA; a layer on the 64-row fallback kernel "
+                "(exact f32 MFMA throughout) is priced at the 157.3 TF f32 peak"),
             "all_kernels": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
                                 "GBps": round(v[2] / (v[1] * 1e-3) / 1e9, 1),
                                 "TFps": round(v[3] / (v[1] * 1e-3) / 1e12, 2),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 14
+#define NGNN_ABI_VERSION 15
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -348,7 +348,40 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  * the rows with in-edges, MAIN every row's layer 0 + layer-1 products,
  * NARROW the z aggregate into out; PREP is accepted and does nothing (the
  * kernels load their weight slices themselves).
+ * head (nullable, ABI 15): the seed-row cross entropy of the training step
+ * (pipeline.py:158, F.cross_entropy(out[:B], y[:B]) -- ngnn_seed_xent_fwd_grad's
+ * contract) computed by the NARROW launch from the logits it finishes, plus
+ * the first step of the backward (see ngnn_xent_head).
  * ws: ngnn_sage2_workspace_bytes(K0, F1, n_rows), 256-B aligned. */
+/* The loss head of ngnn_sage2_fwd (ABI 15).  For the logit rows d < B:
+ *   loss   = sum_{d < B, y[d] != ignore_index} (lse(out[d]) - out[d][y[d]]) / count
+ *   count  = #{d < B : y[d] != ignore_index}   (an out-of-range label: NaN loss)
+ *   dy[d]  = (softmax(out[d]) - onehot(y[d])) / count   (0 for an ignored row)
+ *            -- d loss / d out at unit scale, rows >= B not written;
+ *   g[s]  += dy[d] (/ deg(d) for MEAN) for every edge s -> d, d < B (float
+ *            atomics; exact zeros skipped): the narrow scatter ngnn_sage2_bwd
+ *            runs first, already done -- pass g as its g_pre.  g [>= R' rows,
+ *            C4 = ceil4(F1) floats]: its rows < min(g_rows, *g_rows_dev) are
+ *            zeroed by the EDGE launch of the same call (so a head whose
+ *            backward never runs leaves nothing behind); nullable (no scatter).
+ * ws: ngnn_xent_head_workspace_bytes(B) bytes, 16-B aligned, zero-filled
+ * before its first use (it is zero again on return).  The loss sum is in a
+ * fixed order (deterministic); needs the EDGE and NARROW stages in one call
+ * or in order, F1 <= 64. */
+typedef struct ngnn_xent_head {
+    const int64_t *y;
+    int64_t B;
+    int64_t ignore_index;
+    float *loss, *count;
+    float *dy;
+    int64_t ldd;
+    float *g;
+    int64_t g_rows;
+    const int32_t *g_rows_dev;
+    void *ws;
+    size_t ws_bytes;
+} ngnn_xent_head;
+size_t ngnn_xent_head_workspace_bytes(int64_t B);
 #define NGNN_SAGE2_PREP 1
 #define NGNN_SAGE2_EDGE 2
 #define NGNN_SAGE2_MAIN 4
@@ -365,7 +398,8 @@ int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xro
                    const float *wr1, int64_t ldw1, int64_t F1, float p_drop, uint64_t seed,
                    const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
                    const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
-                   int64_t ldo, int stages, void *ws, size_t ws_bytes, void *stream);
+                   int64_t ldo, const ngnn_xent_head *head, int stages, void *ws, size_t ws_bytes,
+                   void *stream);
 
 /* Every weight gradient of the two-layer stack above in three launches
  * (ngnn_bwd2.hip): the backward of sage.py:33-39 under
@@ -387,7 +421,8 @@ int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xro
  * return; its offset depends on K0 and F1 only, so a zeroed workspace may be
  * grown for more rows).  Float atomics
  * build g: not bitwise reproducible run to run (as the reference's CUDA
- * index_add_). */
+ * index_add_).  g_pre (nullable, ABI 15): g already built (ngnn_sage2_fwd's
+ * loss head, [>= R' rows, ceil4(F1)]): no scatter launch, g read from it. */
 size_t ngnn_sage2_bwd_workspace_bytes(int64_t n_rows, int64_t K0, int64_t F1);
 int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, const float *wr1,
                    int64_t ldw1, const float *h, int64_t ldh, float yscale, const float *x,
@@ -395,7 +430,8 @@ int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, c
                    int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
                    const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
                    const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
-                   float *dwl0, float *dbl0, float *dwr0, void *ws, size_t ws_bytes, void *stream);
+                   float *dwl0, float *dbl0, float *dwr0, const float *g_pre, void *ws, size_t ws_bytes,
+                   void *stream);
 
 /* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
  * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The

@@ -521,7 +521,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
                               int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
                               const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
                               const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
-                              float *dwl0, float *dbl0, float *dwr0, void *ws, size_t ws_bytes, void *stream) {
+                              float *dwl0, float *dbl0, float *dwr0, const float *g_pre, void *ws, size_t ws_bytes,
+                              void *stream) {
     NGNN_RETURN_IF(reduce != NGNN_REDUCE_MEAN && reduce != NGNN_REDUCE_SUM, NGNN_E_ARG);
     NGNN_RETURN_IF(F1 <= 0 || F1 > 48 || K0 <= 0 || K0 > 128 || K0 % 4 != 0, NGNN_E_SHAPE);
     NGNN_RETURN_IF(n_rows < 0 || !fits_i32(n_rows), NGNN_E_RANGE);
@@ -531,7 +532,9 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     NGNN_RETURN_IF(ldy < F1 || ldw1 < 256 || ldh < 256 || ldh % 4 != 0 || ldx < K0 || ldx % 4 != 0 ||
                        ld_agg < K0 || ld_agg % 4 != 0,
                    NGNN_E_SHAPE);
-    NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(agg0, 16) || !aligned(ws, 256), NGNN_E_ALIGN);
+    NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(agg0, 16) || !aligned(ws, 256) ||
+                       (g_pre && !aligned(g_pre, 16)),
+                   NGNN_E_ALIGN);
     const bool indexed = xrow || xrow_dev;
     NGNN_RETURN_IF(indexed && x_rows <= 0, NGNN_E_ARG);
     const Ws3 L = ws3_layout(n_rows, K0, F1);
@@ -541,7 +544,9 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     float *g = reinterpret_cast<float *>(wsb + L.g);
     float *slab = reinterpret_cast<float *>(wsb + L.slab);
     const int C4 = static_cast<int>((F1 + 3) & ~int64_t{3});
-    if (n_rows > 0) {
+    // (g_pre: the forward's loss head scattered it already -- the workspace's
+    // g stays zero, and its clearing blocks below have nothing to do)
+    if (n_rows > 0 && !g_pre) {
         const int rc = lowdim_scatter_launch(dy, ldy, rowptr, col, static_cast<int>(n_rows), r_ptr,
                                              static_cast<int>(F1), C4, g, reduce == NGNN_REDUCE_MEAN, st);
         if (rc) return rc;
@@ -550,7 +555,7 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.dy = dy;
     b.ldy = ldy;
     b.F1 = static_cast<int>(F1);
-    b.g = g;
+    b.g = g_pre ? g_pre : g;
     b.C4 = C4;
     b.wr1 = wr1;
     b.wl1 = wl1;
@@ -594,7 +599,7 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     if (rc) return rc;
     const int64_t total = b2_slab_floats(static_cast<int>(K0), static_cast<int>(F1));
     const int n_red = static_cast<int>(ceil_div(total, 256));
-    const int n_clr = 64;
+    const int n_clr = g_pre ? 0 : 64;
     hipLaunchKernelGGL(k_bwd2_reduce, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S, static_cast<int>(K0),
                        static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4, static_cast<int>(n_rows),
                        r_ptr, rnext_ptr, n_red);

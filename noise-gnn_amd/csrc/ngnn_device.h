@@ -63,6 +63,23 @@ __device__ __forceinline__ v4f bf16x4_to_f32(i32x2 w) {
     return o;
 }
 
+// The training step's seed-row cross entropy computed by the narrow output
+// launch (include/ngnn.h ngnn_xent_head; ngnn_sage_rt.hip k_narrow_agg)
+struct NarrowHead {
+    const int64_t *y;
+    int B;
+    int64_t ignore;
+    float *loss, *count;
+    float *dy;
+    int64_t ldd;
+    float *g;  // nullable: no scatter
+    int ldg;
+    float *part;       // per-workgroup loss partials
+    uint32_t *ticket;  // zero between calls
+    const float *cnt_in;  // the valid-label count, written by an earlier launch (nullable: count here)
+    int dbg;              // (profiling builds only: time-attribution variants; 0)
+};
+
 // byte offset that is always outside a resource of < 2 GiB
 constexpr int kBufOOB = 0x7fffffff;
 

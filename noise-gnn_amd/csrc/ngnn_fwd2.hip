@@ -182,6 +182,18 @@ struct G2Args {
     int64_t ld_agg;
     float *nb;   // [>= rows of the edge tiles, 256]
     int64_t cap_rows;  // rows of agg / nb
+    // the loss head's g (nullable): rows < min(gz_rows, *gz_rows_dev) of
+    // gz_ld floats (a multiple of 4) are zeroed here, before its scatter
+    float *gz;
+    int gz_ld;
+    int gz_rows;
+    const int32_t *gz_rows_dev;
+    // ... and its valid-label count: #{i < cnt_B : cnt_y[i] != cnt_ignore}
+    // into *cnt_out (nullable), by the last workgroup
+    const int64_t *cnt_y;
+    int cnt_B;
+    int64_t cnt_ignore;
+    float *cnt_out;
 };
 
 constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip for fanouts <= 16)
@@ -189,18 +201,30 @@ constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip 
 // The rows with in-edges, 16-row tiles, one workgroup (8 waves) per CU
 // walking its tiles.  Per tile: every wave gathers TWO rows (32 lanes x 4
 // columns per row: the x split layout of k_fwd2), all of a row's neighbours
-// in one round trip (their ids were fetched during the previous tile, the
-// row pointers two tiles ahead), sums them in edge order from +0.0 and
-// divides by max(deg, 1) for mean -- the fp32 sequence of ngnn_seg_agg_fwd
-// (the saved aggregate is bit-identical to it); stores the aggregate, splits
-// it into fp16 parts in LDS; after one barrier every wave multiplies the tile
-// by ITS 32 columns of W_l0 (slice in registers) and stores nb, unscaled.
-template <int C0>
+// in one round trip, sums them in edge order from +0.0 and divides by
+// max(deg, 1) for mean -- the fp32 sequence of ngnn_seg_agg_fwd (the saved
+// aggregate is bit-identical to it); stores the aggregate, splits it into
+// fp16 parts in LDS; after one barrier every wave multiplies the tile by ITS
+// 32 columns of W_l0 (slice in registers) and stores nb, unscaled.
+//
+// Two tiles' gathers in flight: the rows of tile j+1 are requested BEFORE
+// tile j is consumed (they land during its sum, split, barrier and MFMAs),
+// the neighbour ids two tiles ahead, the row pointers three.  vmcnt retires
+// in issue order, so every index word a request needs was issued before the
+// rows still in flight (per step: rowptr(j+3), ids(j+2), rows(j+1), then
+// tile j) and waiting on it never drains them.  A row's ids are spread over
+// its 32 lanes (lane s holds neighbour s: one word per lane per tile) and
+// broadcast with bpermute at the request.  The first tile's rows are
+// requested before the weight slices load (the two latencies overlap).
+// DBG (profiling builds only, NGNN_EDGE_DBG): bit 0 skips the row gathers
+// (out-of-range requests), 1 the MFMAs and nb stores, 2 the aggregate stores
+template <int C0, int DBG = 0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     constexpr int PSTR = 32 * C0 + 16;  // 72 dwords = 8 mod 64 banks: conflict-free fragment reads
     constexpr int XPB = 2 * F2_ROWS * PSTR;
     __shared__ __attribute__((aligned(16))) _Float16 sxp[2 * XPB];
     __shared__ int serow[2 * F2_ROWS];
+    __shared__ __attribute__((aligned(16))) int sid[64 * F2_WAVES];
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63, q = ln >> 4, rl = ln & 15;
     int n_rows = a.n_rows;
@@ -210,6 +234,27 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     n_rows = __builtin_amdgcn_readfirstlane(n_rows);
     const int n_tiles = __builtin_amdgcn_readfirstlane((max(ne, 0) + F2_ROWS - 1) / F2_ROWS);
     const int G = gridDim.x, b = blockIdx.x;
+    if (a.gz) {  // the loss head's g rows, spread over the whole grid
+        int gr = a.gz_rows;
+        if (a.gz_rows_dev) gr = min(gr, *a.gz_rows_dev);
+        const int n4 = max(gr, 0) * (a.gz_ld >> 2);
+        for (int i = b * (F2_WAVES * 64) + static_cast<int>(threadIdx.x); i < n4; i += G * F2_WAVES * 64)
+            reinterpret_cast<v4f *>(a.gz)[i] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+    if (a.cnt_out && b == G - 1) {  // (the last workgroup: the fewest tiles)
+        __shared__ float s_cnt[F2_WAVES];
+        float c = 0.0f;
+        for (int i = threadIdx.x; i < a.cnt_B; i += F2_WAVES * 64) c += (a.cnt_y[i] != a.cnt_ignore) ? 1.0f : 0.0f;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if (ln == 0) s_cnt[wv] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t = 0.0f;
+            for (int w = 0; w < F2_WAVES; ++w) t += s_cnt[w];
+            *a.cnt_out = t;
+        }
+    }
     const int ntj = n_tiles > b ? (n_tiles - 1 - b) / G + 1 : 0;
     if (ntj == 0) return;  // (uniform over the workgroup)
 
@@ -226,7 +271,8 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     const bool scol = 4 * sslot < a.K0 && sslot < 8 * C0;
     auto tile_row = [&](int j, int rr) { return (b + j * G) * F2_ROWS + rr; };
     // index words through buffer resources (no branches, 32-bit offsets;
-    // out-of-range slots read 0 and are masked by the degree at use)
+    // out-of-range slots read 0 and are masked by the degree at use; a tile
+    // past the last reads beg = end = 0: no rows)
     const i32x4 rpr = make_rsrc(a.rowptr, static_cast<uint32_t>(static_cast<int64_t>(n_rows + 1) * 4));
     const i32x4 cr = make_rsrc(colg, 0xF0000000u);
     auto rowptr_of = [&](int j, int &beg, int &end) __attribute__((always_inline)) {
@@ -235,47 +281,45 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
         beg = buf_load1i(rpr, ok ? 4 * r : kOOB2, 0, 0);
         end = buf_load1i(rpr, ok ? 4 * r + 4 : kOOB2, 0, 0);
     };
-    auto ids_of = [&](int beg, int end, int e0, int (&cw)[G2_NB]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < G2_NB; ++e) cw[e] = buf_load1i(cr, beg + e0 + e < end ? 4 * (beg + e0 + e) : kOOB2, 0, 0);
+    // lane sslot of the row's 32 holds neighbour e0 + sslot's id
+    auto ids_of = [&](int beg, int end, int e0) __attribute__((always_inline)) {
+        return buf_load1i(cr, beg + e0 + sslot < end ? 4 * (beg + e0 + sslot) : kOOB2, 0, 0);
     };
     // (row offsets as 24-bit products: every row of a table under the 32-bit
     // offset limit has an index < 2^24, and ld4 < 2^24)
-    auto rows_of = [&](int beg, int end, int e0, const int (&cw)[G2_NB], v4f (&v)[G2_NB]) __attribute__((always_inline)) {
+    // (the row's ids pass through LDS: one word written per lane, the 16 in
+    // use read back as four broadcast 16-B reads -- a wave's own LDS accesses
+    // stay in order, no barrier)
+    int *const sidr = sid + 64 * wv + (ln & 32);
+    auto rows_of = [&](int beg, int end, int e0, int idl, v4f (&v)[G2_NB]) __attribute__((always_inline)) {
+        sidr[sslot] = idl;
+        int id[G2_NB];
+#pragma unroll
+        for (int k = 0; k < G2_NB / 4; ++k) {
+            const i32x4 w = *reinterpret_cast<const i32x4 *>(sidr + ((e0 & 31) + 4 * k));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) id[4 * k + i] = w[i];
+        }
 #pragma unroll
         for (int e = 0; e < G2_NB; ++e)
-            v[e] = buf_load4(xr, (beg + e0 + e < end && scol) ? static_cast<int>(__umul24(static_cast<uint32_t>(cw[e]), ld4) + 16u * sslot) : kOOB2,
+            v[e] = buf_load4(xr, (beg + e0 + e < end && scol && !(DBG & 1)) ? static_cast<int>(__umul24(static_cast<uint32_t>(id[e]), ld4) + 16u * sslot) : kOOB2,
                              0, 0);
     };
 
-    // index loads of the first tiles, then this wave's W_l0 slice
-    int begc, endc, begn, endn;
-    int cw[G2_NB];
-    rowptr_of(0, begc, endc);
-    ids_of(begc, endc, 0, cw);
-    rowptr_of(1, begn, endn);
-    half8 wl[2][C0][2];
-    const int eW = load_w0_slice<C0>(a.wl0, a.ldw0, a.K0, wv, ln, wl);
-
-    for (int j = 0; j < ntj; ++j) {
+    // tile j (its rows requested in v): sum, aggregate store, split, nb
+    auto consume = [&](int j, int beg, int end, int idl, v4f (&v)[G2_NB]) __attribute__((always_inline)) {
         const int B = j & 1;
-        v4f v[G2_NB];
-        rows_of(begc, endc, 0, cw, v);
-        // the next tile's ids, the row pointers of the one after
-        int cwn[G2_NB];
-        ids_of(begn, endn, 0, cwn);
-        int begm, endm;
-        rowptr_of(j + 2, begm, endm);
         v4f acc{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < G2_NB; ++e) acc += v[e];
-        const int deg = endc - begc;
-        // (rare: rows with more than G2_NB neighbours -- one round trip each)
+        const int deg = end - beg;
+        // (rare: rows with more than G2_NB neighbours -- one round trip per
+        // 16 more; ids past 32 read here)
         const int dmax = __builtin_amdgcn_readfirstlane(__float_as_int(wave_max(__int_as_float(deg))));
         for (int e0 = G2_NB; e0 < dmax; e0 += G2_NB) {
-            int ce[G2_NB];
-            ids_of(begc, endc, e0, ce);
-            rows_of(begc, endc, e0, ce, v);
+            const int il = (e0 & 31) == 0 ? ids_of(beg, end, e0) : idl;
+            idl = il;
+            rows_of(beg, end, e0, il, v);
 #pragma unroll
             for (int e = 0; e < G2_NB; ++e) acc += v[e];
         }
@@ -285,7 +329,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
             for (int i = 0; i < 4; ++i) acc[i] = acc[i] / dv;
         }
         const int r = tile_row(j, srow);
-        buf_store4(acc, ar, (r < n_rows && scol) ? r * static_cast<int>(a.ld_agg) * 4 + 16 * sslot : kOOB2, 0, 0);
+        buf_store4(acc, ar, (r < n_rows && scol && !(DBG & 4)) ? r * static_cast<int>(a.ld_agg) * 4 + 16 * sslot : kOOB2, 0, 0);
         {  // parts of the tile row (max over the row's 32 lanes)
             const int e = h2_exp(max_xor16(max_row16(amax4(acc))));
             const v4f vs = ldexp4(acc, e);
@@ -303,8 +347,10 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
             }
             if (sslot == 0) serow[B * F2_ROWS + srow] = e;
         }
-        lds_barrier();
-        // nb of the tile, this wave's 32 columns
+    };
+    auto multiply = [&](int j, const half8 (&wl)[2][C0][2], int eW) __attribute__((always_inline)) {
+        if (DBG & 2) return;
+        const int B = j & 1;
         v4f o[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
         const _Float16 *xp = sxp + B * XPB + rl * PSTR + 8 * q;
 #pragma unroll
@@ -319,13 +365,44 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
         const int no = r2 < a.cap_rows ? r2 * F2_HID * 4 + (32 * wv + 4 * q) * 4 : kOOB2;
         buf_store4(ldexp4(o[0], un), nr, no, 0, 0);
         buf_store4(ldexp4(o[1], un), nr, no == kOOB2 ? kOOB2 : no + 64, 0, 0);
-#pragma unroll
-        for (int e = 0; e < G2_NB; ++e) cw[e] = cwn[e];
-        begc = begn;
-        endc = endn;
-        begn = begm;
-        endn = endm;
+    };
+
+    // prologue: row pointers of tiles 0..2, ids of 0..1, rows of tile 0 --
+    // then this wave's W_l0 slice while they are in flight
+    int b0, e0, b1, e1, b2, e2;
+    rowptr_of(0, b0, e0);
+    rowptr_of(1, b1, e1);
+    int i0 = ids_of(b0, e0, 0);
+    rowptr_of(2, b2, e2);
+    int i1 = ids_of(b1, e1, 0);
+    v4f va[G2_NB], vb[G2_NB];
+    rows_of(b0, e0, 0, i0, va);
+    half8 wl[2][C0][2];
+    const int eW = load_w0_slice<C0>(a.wl0, a.ldw0, a.K0, wv, ln, wl);
+
+    // one step: request rowptr(j+3), ids(j+2), rows(j+1) into vn; consume
+    // tile j from vc
+    auto step = [&](int j, v4f (&vc)[G2_NB], v4f (&vn)[G2_NB]) __attribute__((always_inline)) {
+        int b3, e3;
+        rowptr_of(j + 3, b3, e3);
+        const int i2 = ids_of(b2, e2, 0);
+        rows_of(b1, e1, 0, i1, vn);
+        consume(j, b0, e0, i0, vc);
+        lds_barrier();
+        multiply(j, wl, eW);
+        b0 = b1; e0 = e1; i0 = i1;
+        b1 = b2; e1 = e2; i1 = i2;
+        b2 = b3; e2 = e3;
+    };
+    // (pairs of steps with ONE exit: at the back edge the tile in flight is
+    // in va on every path, so the wait counters stay exact there; an odd
+    // tail runs after the loop.  Requests past the last tile read nothing.)
+    const int npair = ntj >> 1;
+    for (int jj = 0; jj < npair; ++jj) {
+        step(2 * jj, va, vb);
+        step(2 * jj + 1, vb, va);
     }
+    if (ntj & 1) step(ntj - 1, va, vb);
 }
 
 // ---------------------------------------------------------------- k_fwd2
@@ -777,9 +854,9 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     return launch_status();
 }
 
-template <int C0>
+template <int C0, int DBG = 0>
 int launch_edge_nb(const G2Args &a, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_edge_nb<C0>, dim3(grid), dim3(F2_WAVES * 64), 0, st, a);
+    hipLaunchKernelGGL((k_edge_nb<C0, DBG>), dim3(grid), dim3(F2_WAVES * 64), 0, st, a);
     return launch_status();
 }
 
@@ -809,7 +886,8 @@ Ws2 ws2_layout(int64_t K0, int64_t F1, int64_t n_rows) {
 // narrow-mode neighbour term (ngnn_sage_rt.hip)
 int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *rowptr, const int32_t *col,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
-                      const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st);
+                      const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st,
+                      const NarrowHead *head);
 
 }  // namespace ngnn
 
@@ -820,6 +898,13 @@ extern "C" int ngnn_sage2_supported(int64_t K0, int64_t H, int64_t F1, int reduc
             (reduce == NGNN_REDUCE_MEAN || reduce == NGNN_REDUCE_SUM))
                ? 1
                : 0;
+}
+
+extern "C" size_t ngnn_xent_head_workspace_bytes(int64_t B) {
+    // the top ticket and the label count, 32 group tickets (from byte 64),
+    // then 32 group sums and one partial per workgroup holding seed rows (at
+    // most B of them) from byte 256
+    return B > 0 ? 256 + 4 * (32 + static_cast<size_t>(B)) : 0;
 }
 
 extern "C" size_t ngnn_sage2_workspace_bytes(int64_t K0, int64_t F1, int64_t n_rows) {
@@ -835,7 +920,8 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
                               const float *wr1, int64_t ldw1, int64_t F1, float p_drop, uint64_t seed,
                               const uint64_t *seed_dev, float *h, int64_t ldh, int64_t h_rows,
                               const int32_t *h_rows_dev, float *agg0, int64_t ld_agg, float *out,
-                              int64_t ldo, int stages, void *ws, size_t ws_bytes, void *stream) {
+                              int64_t ldo, const ngnn_xent_head *head, int stages, void *ws, size_t ws_bytes,
+                              void *stream) {
     NGNN_RETURN_IF(!ngnn_sage2_supported(K0, H, F1, reduce), NGNN_E_SHAPE);
     NGNN_RETURN_IF(n_rows < 0 || n_edge_rows < 0 || h_rows < 0, NGNN_E_ARG);
     NGNN_RETURN_IF(p_drop < 0.0f || !(p_drop <= 1.0f), NGNN_E_ARG);
@@ -861,6 +947,15 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
                    NGNN_E_RANGE);
     const Ws2 L = ws2_layout(K0, F1, n_rows);
     NGNN_RETURN_IF(ws_bytes < L.total, NGNN_E_WORKSPACE);
+    const int64_t C4 = (F1 + 3) & ~int64_t{3};
+    if (head) {
+        NGNN_RETURN_IF(!head->y || !head->loss || !head->count || !head->dy || !head->ws, NGNN_E_ARG);
+        NGNN_RETURN_IF(head->B <= 0 || head->B > n_rows || head->ldd < F1, NGNN_E_ARG);
+        NGNN_RETURN_IF(head->g && (head->g_rows < 0 || head->g_rows > n_rows), NGNN_E_ARG);
+        NGNN_RETURN_IF(head->ws_bytes < ngnn_xent_head_workspace_bytes(head->B), NGNN_E_WORKSPACE);
+        NGNN_RETURN_IF(!aligned(head->ws, 16) || (head->g && !aligned(head->g, 16)), NGNN_E_ALIGN);
+        NGNN_RETURN_IF(head->g && head->g_rows * C4 * 4 > lim, NGNN_E_RANGE);
+    }
     hipStream_t st = as_stream(stream);
     char *wsb = static_cast<char *>(ws);
     const int C0 = static_cast<int>(ceil_div(K0, 32)), NT1 = static_cast<int>(ceil_div(F1, 16));
@@ -894,11 +989,36 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         g.ld_agg = ld_agg;
         g.nb = nb;
         g.cap_rows = n_rows;  // (agg0 has n_rows rows; nb has cap_rows >= n_rows)
+        g.gz = head ? head->g : nullptr;
+        g.gz_ld = static_cast<int>(C4);
+        g.gz_rows = head ? static_cast<int>(head->g_rows) : 0;
+        g.gz_rows_dev = head ? head->g_rows_dev : nullptr;
+        g.cnt_y = head ? head->y : nullptr;
+        g.cnt_B = head ? static_cast<int>(head->B) : 0;
+        g.cnt_ignore = head ? head->ignore_index : 0;
+        g.cnt_out = head ? reinterpret_cast<float *>(static_cast<char *>(head->ws) + 4) : nullptr;
         const int tiles = static_cast<int>(ceil_div(g.n_edge, 16));
         const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, tiles)));
         int rc = NGNN_E_SHAPE;
+#ifdef NGNN_FWD2_DBG_BUILD
+        if (const char *d = getenv("NGNN_EDGE_DBG")) {
+            switch (C0 == 4 ? atoi(d) : 0) {
+                case 1: return launch_edge_nb<4, 1>(g, grid, st);
+                case 2: return launch_edge_nb<4, 2>(g, grid, st);
+                case 3: return launch_edge_nb<4, 3>(g, grid, st);
+                case 4: return launch_edge_nb<4, 4>(g, grid, st);
+                case 6: return launch_edge_nb<4, 6>(g, grid, st);
+                case 7: return launch_edge_nb<4, 7>(g, grid, st);
+                default: break;
+            }
+        }
+#endif
         if (C0 == 4) rc = launch_edge_nb<4>(g, grid, st);
         if (rc) return rc;
+    } else if ((stages & NGNN_SAGE2_EDGE) && head && head->g && head->g_rows > 0) {
+        // (no edge launch to zero the head's g: every row up to its static bound)
+        const hipError_t e = hipMemsetAsync(head->g, 0, static_cast<size_t>(head->g_rows * C4 * 4), st);
+        if (e != hipSuccess) return static_cast<int>(e);
     }
     if (stages & NGNN_SAGE2_MAIN) {
         F2Args f;
@@ -964,6 +1084,30 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         if (rc) return rc;
     }
     if (!(stages & NGNN_SAGE2_NARROW)) return NGNN_OK;
+    NarrowHead nh{};
+    if (head) {
+        nh.y = head->y;
+        nh.B = static_cast<int>(head->B);
+        nh.ignore = head->ignore_index;
+        nh.loss = head->loss;
+        nh.count = head->count;
+        nh.dy = head->dy;
+        nh.ldd = head->ldd;
+        nh.g = head->g;
+        nh.ldg = static_cast<int>(C4);
+        nh.ticket = static_cast<uint32_t *>(head->ws);
+        nh.part = reinterpret_cast<float *>(static_cast<char *>(head->ws) + 256);
+        // the count from this call's edge launch (ws + 4), else counted there
+        nh.cnt_in = ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0)
+                        ? reinterpret_cast<const float *>(static_cast<char *>(head->ws) + 4)
+                        : nullptr;
+#ifdef NGNN_FWD2_DBG_BUILD
+        if (const char *d = getenv("NGNN_HEAD_DBG")) {
+            nh.dbg = atoi(d);
+            if (nh.dbg & 16) nh.cnt_in = reinterpret_cast<const float *>(static_cast<char *>(head->ws) + 4);
+        }
+#endif
+    }
     return narrow_agg_launch(z, ldz, F1, rowptr, col, n_rows, n_rows_dev, n_edge_rows, n_edge_rows_dev, reduce,
-                             out, ldo, st);
+                             out, ldo, st, head ? &nh : nullptr);
 }

@@ -81,13 +81,43 @@ int dispatch_rt(int ntw, const RtArgs &a, int reduce, bool wl_lds, bool x3, int 
 // neighbour rows in flight per lane; per column edge order from 0, then
 // / deg for mean.
 constexpr int NA_UNR = 16;
-template <bool MEAN>
+
+// max / sum over the 16 lanes of a row group (a DPP row: lanes 16 k ..
+// 16 k + 15, all active together) on VALU only: quad_perm [1,0,3,2] and
+// [2,3,0,1] combine a quad, row_half_mirror the two quads of a half,
+// row_mirror the two halves -- every lane ends with the row's value
+__device__ __forceinline__ float max16(float v) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+    return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+}
+__device__ __forceinline__ float sum16(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+}
+
+// HEAD (the loss head, ngnn_xent_head): the rows d < B are visited with or
+// without in-edges; once a row's logits are final the group takes its cross
+// entropy -- max, sum of exp and the label's logit over the group, the
+// gradient row (softmax - onehot) / count as ngnn_seed_xent_fwd_grad writes
+// it -- and scatters the gradient row onto its sources (g[col[e]] += dy[d] /
+// deg(d), as the backward's narrow scatter).  count: every workgroup that
+// holds seed rows counts the valid labels itself (B label reads from L2, no
+// count pass).  The loss: per-group sums in row order, per workgroup in
+// group order, and the last workgroup to finish (a device ticket) adds the
+// workgroup partials in a fixed order -- deterministic; the hand-off is
+// k_xent_fused's (ngnn_loss.hip: agent-scope partial stores drained before
+// one ticket atomic, agent-scope loads by the last adder).
+template <bool MEAN, bool HEAD>
 __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z, int64_t ldz, int Fo,
                                                     const int32_t *__restrict__ rowptr,
                                                     const int32_t *__restrict__ col, int n_rows,
                                                     const int32_t *__restrict__ n_rows_dev,
                                                     const int32_t *__restrict__ n_edge_dev,
-                                                    float *__restrict__ out, int64_t ldo) {
+                                                    float *__restrict__ out, int64_t ldo, NarrowHead hd) {
     int nr = n_rows;
     if (n_rows_dev) nr = min(nr, *n_rows_dev);
     if (n_edge_dev) nr = min(nr, *n_edge_dev);
@@ -99,30 +129,218 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
     const i32x4 cr = make_rsrc(col, 0xF0000000u);
     const uint32_t ldz4 = static_cast<uint32_t>(ldz) * 4u;
     constexpr int OOB = static_cast<int>(0xF0000000u);
-    for (int d = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; d < nr; d += (gridDim.x * blockDim.x) >> 4) {
-        const int beg = rowptr[d], end = rowptr[d + 1];
-        if (beg == end) continue;
-        for (int c4 = sub; c4 < F4; c4 += 16) {
-            v4f acc{0.f, 0.f, 0.f, 0.f};
-            for (int e = beg; e < end; e += NA_UNR) {
-                int id[NA_UNR];
+    // the neighbour mean / sum of z of row d, columns 4 c4 .. 4 c4 + 3
+    auto gather = [&](int beg, int end, int c4) __attribute__((always_inline)) {
+        v4f acc{0.f, 0.f, 0.f, 0.f};
+        for (int e = beg; e < end; e += NA_UNR) {
+            int id[NA_UNR];
 #pragma unroll
-                for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
-                const i32x4 zr = make_rsrc(z, 0xF0000000u);
+            for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
+            const i32x4 zr = make_rsrc(z, 0xF0000000u);
+            v4f v[NA_UNR];
+#pragma unroll
+            for (int u = 0; u < NA_UNR; ++u)
+                v[u] = buf_load4(zr, e + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(id[u]), ldz4)) + 16 * c4 : OOB,
+                                 0, 0);
+#pragma unroll
+            for (int u = 0; u < NA_UNR; ++u)
+                if (e + u < end) acc += v[u];
+        }
+        if (MEAN && end > beg) acc = acc / static_cast<float>(end - beg);
+        return acc;
+    };
+    const int stride = (gridDim.x * blockDim.x) >> 4;
+    if constexpr (!HEAD) {
+        for (int d = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; d < nr; d += stride) {
+            const int beg = rowptr[d], end = rowptr[d + 1];
+            if (beg == end) continue;
+            for (int c4 = sub; c4 < F4; c4 += 16) {
+                const v4f acc = gather(beg, end, c4);
+                float *o = out + static_cast<int64_t>(d) * ldo + 4 * c4;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * c4 + j < Fo) o[j] += acc[j];
+            }
+        }
+    } else {
+        // (host: F4 <= 16, one column quad per lane; B <= n_rows)
+        __shared__ float s_red[256];
+        __shared__ float s_grp[16];
+        // rows to workgroups as the plain kernel's (16 consecutive rows per
+        // workgroup and pass): the seed rows sit in the first ceil(B / 16)
+        // workgroups.  (Measured alternatives, tools/fwd2_micro.py --head:
+        // seed rows one per workgroup over all of them spread the scatter
+        // atomics but cost the rest of the launch its row locality, 36 us
+        // against 18; 4 per workgroup on wave 0 of ceil(B / 4) workgroups, 25.)
+        const int B = hd.B, G = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
+        const int nh = min(G, (B + 15) >> 4);  // workgroups holding seed rows
+        const bool hwg = bx < nh;              // (uniform)
+        float cnt = 0.0f;
+        if (hd.cnt_in) {
+            cnt = *hd.cnt_in;
+        } else if (hwg) {
+            float c = 0.0f;
+            for (int i = threadIdx.x; i < B; i += 256) c += (hd.y[i] != hd.ignore) ? 1.0f : 0.0f;
+            s_red[threadIdx.x] = c;
+            __syncthreads();
+            for (int h = 128; h > 0; h >>= 1) {
+                if (threadIdx.x < h) s_red[threadIdx.x] += s_red[threadIdx.x + h];
+                __syncthreads();
+            }
+            cnt = s_red[0];
+        }
+        float lsum = 0.0f;
+        const int c4 = sub;
+        const i32x4 zr = make_rsrc(z, 0xF0000000u);
+        const int dl = max(nr, B);
+        for (int d = (bx * 256 + static_cast<int>(threadIdx.x)) >> 4; d < dl; d += 16 * G) {
+            const bool hrow = d < B;
+            const int beg = rowptr[d], end = (d < nr) ? rowptr[d + 1] : beg;
+            if (beg == end && !hrow) continue;
+            // the label, the root logits and the first 16 neighbour ids in
+            // one round trip; the ids stay in registers for the scatter
+            const int64_t t = hrow ? hd.y[d] : 0;
+            float *o = out + static_cast<int64_t>(d) * ldo + 4 * c4;
+            v4f ov{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo) ov[j] = o[j];
+            int id[NA_UNR];
+#pragma unroll
+            for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, beg + u < end ? 4 * (beg + u) : OOB, 0, 0);
+            v4f acc{0.f, 0.f, 0.f, 0.f};
+            if (c4 < F4 && end > beg) {
                 v4f v[NA_UNR];
 #pragma unroll
                 for (int u = 0; u < NA_UNR; ++u)
-                    v[u] = buf_load4(zr, e + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(id[u]), ldz4)) + 16 * c4 : OOB,
+                    v[u] = buf_load4(zr, beg + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(id[u]), ldz4)) + 16 * c4 : OOB,
                                      0, 0);
 #pragma unroll
                 for (int u = 0; u < NA_UNR; ++u)
-                    if (e + u < end) acc += v[u];
+                    if (beg + u < end) acc += v[u];
+                // (rare: more than 16 neighbours -- the rest in further round trips,
+                // edge order kept: the sum continues from the first 16)
+                for (int e = beg + NA_UNR; e < end; e += NA_UNR) {
+                    int ie[NA_UNR];
+#pragma unroll
+                    for (int u = 0; u < NA_UNR; ++u) ie[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < NA_UNR; ++u)
+                        v[u] = buf_load4(zr, e + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(ie[u]), ldz4)) + 16 * c4 : OOB,
+                                         0, 0);
+#pragma unroll
+                    for (int u = 0; u < NA_UNR; ++u)
+                        if (e + u < end) acc += v[u];
+                }
+                if (MEAN) acc = acc / static_cast<float>(end - beg);
             }
-            if (MEAN) acc = acc / static_cast<float>(end - beg);
-            float *o = out + static_cast<int64_t>(d) * ldo + 4 * c4;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (4 * c4 + j < Fo) o[j] += acc[j];
+                if (4 * c4 + j < Fo && end > beg) {
+                    ov[j] = ov[j] + acc[j];
+                    o[j] = ov[j];  // (edgeless rows keep their bits, -0.0 included)
+                }
+            if (!hrow) continue;
+            if (hd.dbg & 4) continue;  // (profiling: no cross entropy)
+            // the row's cross entropy (torch's log_softmax order: max, then
+            // the sum of exp(x - max))
+            float m = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo) m = fmaxf(m, ov[j]);
+            m = max16(m);
+            float s = 0.0f, ot = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo) {
+                    s += expf(ov[j] - m);
+                    if (4 * c4 + j == t) ot = ov[j];
+                }
+            s = sum16(s);
+            ot = sum16(ot);  // (the label's logit: one lane holds it, the others add 0)
+            const float lse = m + logf(s);
+            const bool ign = t == hd.ignore;
+            const float l = ign ? 0.0f : ((t >= 0 && t < Fo) ? lse - ot : NAN);  // out-of-range label: NaN
+            v4f dv{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo && !ign) dv[j] = (expf(ov[j] - lse) - (4 * c4 + j == t ? 1.0f : 0.0f)) / cnt;
+            float *dr = hd.dy + static_cast<int64_t>(d) * hd.ldd + 4 * c4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * c4 + j < Fo) dr[j] = dv[j];
+            if (hd.g && !ign && end > beg && !(hd.dbg & 1)) {
+                if (MEAN) dv = dv * (1.0f / static_cast<float>(end - beg));
+                // the row's sources from the registers (no load between the
+                // atomics); past 16 neighbours, reloaded 16 at a time
+#pragma unroll
+                for (int u = 0; u < NA_UNR; ++u)
+                    if (beg + u < end) {
+                        float *gr = hd.g + static_cast<int64_t>(id[u]) * hd.ldg + 4 * c4;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (4 * c4 + j < Fo && dv[j] != 0.0f) atomicAdd(gr + j, dv[j]);  // exact 0 adds nothing
+                    }
+                for (int e = beg + NA_UNR; e < end; e += NA_UNR) {
+                    int ie[NA_UNR];
+#pragma unroll
+                    for (int u = 0; u < NA_UNR; ++u) ie[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < NA_UNR; ++u)
+                        if (e + u < end) {
+                            float *gr = hd.g + static_cast<int64_t>(ie[u]) * hd.ldg + 4 * c4;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (4 * c4 + j < Fo && dv[j] != 0.0f) atomicAdd(gr + j, dv[j]);
+                        }
+                }
+            }
+            lsum += l;
+        }
+        if (hwg && !(hd.dbg & 2)) {
+            // the loss: the workgroup's rows in group order, then a two-level
+            // hand-off by one lane behind an LDS-only barrier (the waves'
+            // scatter atomics and stores stay in flight) -- groups of 32
+            // workgroups count on their own ticket, the last of a group adds
+            // the group's partials in order and counts on the top ticket,
+            // whose last adds the group sums in order (same-address atomics
+            // serialise at the memory side: 32 per address instead of one per
+            // workgroup)
+            if (sub == 0) s_grp[threadIdx.x >> 4] = lsum;
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            float p = 0.0f;
+            for (int i = 0; i < 16; ++i) p += s_grp[i];
+            if (threadIdx.x == 0) {
+                float *gpart = hd.part;            // [32] group sums
+                float *wpart = hd.part + 32;       // [nh] workgroup partials
+                uint32_t *tick1 = hd.ticket + 16;  // [32] group tickets
+                __hip_atomic_store(wpart + bx, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int gi = bx >> 5, g0 = gi << 5, gs = min(32, nh - g0), ngr = (nh + 31) >> 5;
+                if (atomicAdd(tick1 + gi, 1u) == static_cast<uint32_t>(gs - 1)) {
+                    float v[32];
+#pragma unroll
+                    for (int i = 0; i < 32; ++i)
+                        v[i] = i < gs ? __hip_atomic_load(wpart + g0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+                    float a = 0.0f;
+#pragma unroll
+                    for (int i = 0; i < 32; ++i) a += v[i];
+                    tick1[gi] = 0u;  // (every member has counted: ready for the next call)
+                    __hip_atomic_store(gpart + gi, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (atomicAdd(hd.ticket, 1u) == static_cast<uint32_t>(ngr - 1)) {
+#pragma unroll
+                        for (int i = 0; i < 32; ++i)
+                            v[i] = i < ngr ? __hip_atomic_load(gpart + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+                        float t = 0.0f;
+#pragma unroll
+                        for (int i = 0; i < 32; ++i) t += v[i];
+                        *hd.loss = t / cnt;  // 0/0 = NaN when every row is ignored, as torch
+                        *hd.count = cnt;
+                        *hd.ticket = 0u;
+                    }
+                }
+            }
         }
     }
 }
@@ -188,21 +406,34 @@ __global__ __launch_bounds__(256) void k_gcn_agg(const float *__restrict__ z, in
 }  // namespace
 
 // out[d, :Fo] += mean / sum_{e into d} z[col[e], :Fo] for the rows with
-// in-edges (the narrow output layer's neighbour term; also ngnn_fwd2.hip)
+// in-edges (the narrow output layer's neighbour term; also ngnn_fwd2.hip);
+// head (nullable): the loss head over rows < head->B (ngnn_fwd2.hip)
 int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *rowptr, const int32_t *col,
                       int64_t n_rows, const int32_t *n_rows_dev, int64_t n_edge_rows,
-                      const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st) {
+                      const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st,
+                      const NarrowHead *head) {
     const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
     // (32-bit buffer offsets into z: a 24-bit row index times the row bytes)
     NGNN_RETURN_IF(n_rows * ldz * 4 >= 0xF0000000ll || n_rows >= (1 << 24) || ldz * 4 >= (1 << 24), NGNN_E_RANGE);
+    NGNN_RETURN_IF(head && (Fo > 64 || head->B <= 0 || head->B > n_rows), NGNN_E_ARG);
     const unsigned grid = static_cast<unsigned>(
-        std::max<int64_t>(1, std::min<int64_t>(4 * num_cus(), ceil_div(rows, 16))));
-    if (reduce == NGNN_REDUCE_MEAN)
-        hipLaunchKernelGGL(k_narrow_agg<true>, dim3(grid), dim3(256), 0, st, z, ldz, static_cast<int>(Fo),
-                           rowptr, col, static_cast<int>(n_rows), n_rows_dev, n_edge_rows_dev, out, ldo);
-    else
-        hipLaunchKernelGGL(k_narrow_agg<false>, dim3(grid), dim3(256), 0, st, z, ldz, static_cast<int>(Fo),
-                           rowptr, col, static_cast<int>(n_rows), n_rows_dev, n_edge_rows_dev, out, ldo);
+        std::max<int64_t>(1, std::min<int64_t>(head ? std::min(4 * num_cus(), 1024) : 4 * num_cus(),
+                                               ceil_div(std::max<int64_t>(rows, head ? head->B : 0), 16))));
+    // (the head's hand-off: at most 32 groups of 32 workgroups)
+    const NarrowHead hd = head ? *head : NarrowHead{};
+    auto go = [&](auto mean_c, auto head_c) {
+        hipLaunchKernelGGL((k_narrow_agg<decltype(mean_c)::value, decltype(head_c)::value>), dim3(grid), dim3(256), 0,
+                           st, z, ldz, static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
+                           n_edge_rows_dev, out, ldo, hd);
+    };
+    const bool mean = reduce == NGNN_REDUCE_MEAN;
+    if (head) {
+        if (mean) go(std::true_type{}, std::true_type{});
+        else go(std::false_type{}, std::true_type{});
+    } else {
+        if (mean) go(std::true_type{}, std::false_type{});
+        else go(std::false_type{}, std::false_type{});
+    }
     return launch_status();
 }
 
@@ -482,7 +713,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
                              w_bf16, false, false, false, n_edge_rows, n_edge_rows_dev, img_ws)) {
             if (rc) return rc;
             return narrow_agg_launch(z, ldz, Fo, rowptr, col, n_rows, n_rows_dev, n_edge_rows,
-                                     n_edge_rows_dev, reduce, out, ldo, st);
+                                     n_edge_rows_dev, reduce, out, ldo, st, nullptr);
         }
     }
     // wide layers (the row-tile kernel's weight image too large for its LDS,

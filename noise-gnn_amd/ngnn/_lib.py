@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 OK = 0
 E_ARG, E_DTYPE, E_SHAPE, E_ALIGN, E_RANGE, E_WORKSPACE = -1, -2, -3, -4, -5, -6
@@ -76,14 +76,15 @@ SIGNATURES = {
     "ngnn_cast_tensors": (_int, [_int, _p, _p, _p, _int, _p]),
     "ngnn_sage2_bwd_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64,
-                              _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p,
+                              _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p, _p,
                               _sz, _p]),
     "ngnn_sage2_supported": (_int, [_i64, _i64, _i64, _int]),
     "ngnn_sage2_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_fwd": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int,
                               _p, _p, _p, _i64,
                               _i64, _p, _p, _p, _i64, _i64, ctypes.c_float, ctypes.c_uint64, _p, _p,
-                              _i64, _i64, _p, _p, _i64, _p, _i64, _int, _p, _sz, _p]),
+                              _i64, _i64, _p, _p, _i64, _p, _i64, _p, _int, _p, _sz, _p]),
+    "ngnn_xent_head_workspace_bytes": (_sz, [_i64]),
     "ngnn_gcn_agg_fwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _p, _int, ctypes.c_float,
                                 ctypes.c_uint64, _p, _p, _i64, _p]),
     "ngnn_row_extent": (_int, [_p, _i64, _i64, _i64, _p, _p]),
@@ -142,6 +143,13 @@ def check(rc: int, what: str = "") -> None:
     if rc != OK:
         msg = load().ngnn_strerror(rc).decode()
         raise NGNNError(f"{what}: {msg} (rc={rc})" if what else f"{msg} (rc={rc})")
+
+
+class XentHead(ctypes.Structure):
+    """include/ngnn.h ngnn_xent_head (ngnn_sage2_fwd's loss head, ABI 15)."""
+    _fields_ = [("y", _p), ("B", _i64), ("ignore_index", _i64), ("loss", _p), ("count", _p),
+                ("dy", _p), ("ldd", _i64), ("g", _p), ("g_rows", _i64), ("g_rows_dev", _p),
+                ("ws", _p), ("ws_bytes", _sz)]
 
 
 def ptr(t) -> int:

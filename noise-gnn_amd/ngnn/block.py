@@ -116,6 +116,9 @@ class Block:
         self.col_x = None  # int32 col mapped through n_id (the slot load writes it)
         # (W_l parameter, ngnn_pack_weight(W_l) kept current by a producer) or None
         self.wl_prepacked = None
+        # the producer's loss head (ngnn.fused.LossHead: the step's
+        # seed_cross_entropy taken by the two-layer forward), or None
+        self.loss_head = None
 
     @property
     def rowptr(self):
@@ -164,6 +167,7 @@ class _BlockCache:
             if hint[9] is not None:
                 blk.xrow_dev, blk.x_rows, blk.col_x = hint[9]
             blk.wl_prepacked = hint[10]
+            blk.loss_head = hint[11]
         else:
             blk = Block(edge_index, num_nodes)
         with self._lock:
@@ -191,7 +195,7 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
                     csr: CSR | None = None, seed_dev: torch.Tensor | None = None,
                     x_dev: torch.Tensor | None = None, r_next=None,
                     n_edge_rows_dev: torch.Tensor | None = None, xrow=None,
-                    wl_prepacked=None) -> None:
+                    wl_prepacked=None, loss_head=None) -> None:
     """n_active: number of leading target rows that can have in-edges (all
     later rows have none) -- only used for roofline accounting.  n_rows_dev:
     device int32 scalar bounding the real rows of a padded slot.  csr: a
@@ -208,12 +212,15 @@ def hint_edge_index(edge_index: torch.Tensor, *, dst_sorted: bool, src_sorted: b
     (fused x[n_id] gather), 0 otherwise, and keeps col_x = n_id[col] (int32).
     wl_prepacked: (W_l parameter, buffer[, state]) -- the producer keeps the
     buffer = ngnn_pack_weight(W_l) current (the slot load's pack job); state
-    (ngnn.graphs.PackState): the pack is current only while state.armed."""
+    (ngnn.graphs.PackState): the pack is current only while state.armed.
+    loss_head: ngnn.fused.LossHead -- the producer's loss is
+    seed_cross_entropy(out, loss_head.y, loss_head.B) of this block's logits,
+    which a two-layer forward may take itself (include/ngnn.h ngnn_xent_head)."""
     ref = weakref.ref(edge_index, lambda _r, k=id(edge_index): _drop_hint(k))
     with _hints_lock:
         _hints[id(edge_index)] = (ref, edge_index._version, dst_sorted, src_sorted, n_active,
                                   n_rows_dev, csr, seed_dev, x_dev, r_next, n_edge_rows_dev, xrow,
-                                  wl_prepacked)
+                                  wl_prepacked, loss_head)
 
 
 def _drop_hint(key):
@@ -226,7 +233,7 @@ def _hint_for(edge_index):
         h = _hints.get(id(edge_index))
     if h is None or h[0]() is not edge_index or h[1] != edge_index._version:
         return None
-    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]
+    return h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13]
 
 
 def get_block(edge_index, num_nodes: int) -> Block:

@@ -30,6 +30,7 @@ graph's up to fp32 summation order; nothing is read back to the host.
 """
 from __future__ import annotations
 
+import ctypes
 import weakref
 
 import torch
@@ -414,13 +415,13 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
 
 
 def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev,
-                  stages: int | None = None, bufs=None):
+                  stages: int | None = None, bufs=None, head: "HeadResult | None" = None):
     """(h, logits, layer-0 aggregate, h partial?) of a two-layer stack in one
     call (include/ngnn.h ngnn_sage2_fwd).  h holds the rows the bounded
     backward reads: every row, or rows < R' when the graph slot vouches that
     the loss reads rows < its B (block.r_next[2]).  stages / bufs (bench.py's
     per-launch timing): a subset of the launches, on the (h, out, agg0) of an
-    earlier call."""
+    earlier call.  head: this forward's loss head (LossHead.start), or None."""
     wl0, bl0, wr0, wl1, bl1, wr1 = (q.detach() for q in params)
     if wl0.stride(1) != 1 or wr0.stride(0) != wl0.stride(0) or wr0.stride(1) != 1:
         wl0, wr0 = wl0.contiguous(), wr0.contiguous()
@@ -450,8 +451,9 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
             seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(h), h.stride(0), N,
             _lib.ptr(h_rows_dev), _lib.ptr(agg0), agg0.stride(0), _lib.ptr(out), out.stride(0)]
     tail = [_lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)]
+    hp = None if head is None else ctypes.byref(head.struct)
     if stages is not None or not _timing.timing():
-        _lib.check(lib.ngnn_sage2_fwd(*args, _lib.SAGE2_ALL if stages is None else stages, *tail),
+        _lib.check(lib.ngnn_sage2_fwd(*args, hp, _lib.SAGE2_ALL if stages is None else stages, *tail),
                    "ngnn_sage2_fwd")
         return h, out, agg0, h_rows_dev is not None
     # timed: one span per launch.  Algorithmic bytes / flops per launch
@@ -471,9 +473,62 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     ]
     for name, st, nbytes, flops, mfma_s in stages:
         with _timing.span(name, nbytes, flops, mfma_s):
-            rc = lib.ngnn_sage2_fwd(*args, st, *tail)
+            rc = lib.ngnn_sage2_fwd(*args, hp, st, *tail)
         _lib.check(rc, "ngnn_sage2_fwd")
     return h, out, agg0, h_rows_dev is not None
+
+
+class LossHead:
+    """A graph slot's seed-row cross entropy, seed_cross_entropy(out, y, B),
+    taken by the two-layer forward's narrow launch from the logits it
+    finishes (include/ngnn.h ngnn_xent_head): the loss, the unit-scale
+    gradient rows and their scatter onto the source rows -- the loss launch
+    and the backward's scatter launch of the step disappear.  Persistent
+    buffers made before the capture (nothing allocated or filled inside it):
+    dy [n_rows, F1] (rows >= B stay zero), g [n_rows, ceil4(F1)] (rows < R'
+    zeroed by the forward's edge launch every step), the hand-off workspace.
+    One pending head per slot (the step's one forward)."""
+
+    def __init__(self, y: torch.Tensor, B: int, n_rows: int, F1: int, r_word: torch.Tensor,
+                 ignore_index: int = -100):
+        dev = y.device
+        self.y, self.B, self.ignore, self.n_rows, self.F1 = y, int(B), int(ignore_index), int(n_rows), int(F1)
+        self.dy = torch.zeros(self.n_rows, self.F1, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(self.n_rows, (self.F1 + 3) & ~3, dtype=torch.float32, device=dev)
+        self.ws = torch.zeros(max(_lib.load().ngnn_xent_head_workspace_bytes(self.B), 16), dtype=torch.uint8,
+                              device=dev)
+        self.r_word = r_word  # the slot's R' word (its low int32 half)
+
+    def start(self) -> "HeadResult":
+        """The outputs of one forward's head (fresh loss / count scalars)."""
+        return HeadResult(self)
+
+
+class HeadResult:
+    __slots__ = ("head", "loss", "count", "struct", "used")
+
+    def __init__(self, head: LossHead):
+        dev = head.y.device
+        self.head = head
+        self.loss = torch.empty((), dtype=torch.float32, device=dev)
+        self.count = torch.empty((), dtype=torch.float32, device=dev)
+        self.used = False
+        self.struct = _lib.XentHead(
+            _lib.ptr(head.y), head.B, head.ignore, _lib.ptr(self.loss), _lib.ptr(self.count),
+            _lib.ptr(head.dy), head.dy.stride(0), _lib.ptr(head.g), head.n_rows, _lib.ptr(head.r_word),
+            _lib.ptr(head.ws), head.ws.numel())
+
+
+def head_ok(block: Block, x, params) -> bool:
+    """May this forward take the slot's loss head?  (grad mode on -- the
+    loss head is a training-step device; the atomics of its scatter are
+    not deterministic)."""
+    hd = block.loss_head
+    if (hd is None or len(params) != 6 or not torch.is_grad_enabled()
+            or torch.are_deterministic_algorithms_enabled()):
+        return False
+    return (x.size(0) == hd.n_rows and params[3].shape[0] == hd.F1 and hd.B <= x.size(0)
+            and any(q.requires_grad for q in params))
 
 
 _use_bwd2 = True  # (tests flip it to compare with the per-layer backward)
@@ -489,11 +544,12 @@ def reserve_sage2_bwd(dev, n_rows: int, K0: int, F1: int) -> torch.Tensor:
 
 
 def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: float, r_ptr: int,
-                   rn_ptr: int, views):
+                   rn_ptr: int, views, g_pre=None):
     """Every weight gradient of the two-layer stack (include/ngnn.h
     ngnn_sage2_bwd): [dW_l0, db0, dW_r0, dW_l1, db1, dW_r1] from dy (rows <
     *r_ptr) with the forward's h (rows < *rn_ptr) and layer-0 aggregate.
-    views: the data-parallel bucket's gradient views (or Nones)."""
+    views: the data-parallel bucket's gradient views (or Nones).  g_pre: the
+    scatter of dy onto the source rows, already built (LossHead), or None."""
     lib = _lib.load()
     x, h = acts[0], acts[1]
     wl0, bl0, wr0, wl1, bl1, wr1 = params
@@ -514,7 +570,8 @@ def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: fl
             h.stride(0), yscale, _lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev),
             block.x_rows, x.stride(0), K0, _lib.ptr(agg0), agg0.stride(0), _lib.ptr(block.rowptr),
             _lib.ptr(block.col), nrows, r_ptr, rn_ptr, _lib.REDUCE[reduce], *(_lib.ptr(g) for g in grads[3:]),
-            *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
+            *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(g_pre), _lib.ptr(ws), ws.numel(),
+            _lib.stream_handle(dev))
     _lib.check(rc, "ngnn_sage2_bwd")
     return grads
 
@@ -522,7 +579,7 @@ def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: fl
 class _SAGEStack(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block: Block, reduce: str, p_drop: float, seed: int, seed_dev, gouts,
-                w_bf16: bool, *params):
+                w_bf16: bool, head, *params):
         L = len(params) // 3
         acts, aggs = [x], []
         h = x
@@ -530,7 +587,10 @@ class _SAGEStack(torch.autograd.Function):
         ctx.sage2 = False
         if L == 2 and sage2_ok(x, block, reduce, params, w_bf16):
             ctx.sage2 = True
-            h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, params, p_drop, seed, seed_dev)
+            h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, params, p_drop, seed, seed_dev,
+                                                       head=head)
+            if head is not None:
+                h._ngnn_head = head  # (seed_cross_entropy takes the loss from it)
             acts += [h1, h]
             aggs += [agg0, None]
             L = 0  # (the per-layer loop below is skipped)
@@ -622,8 +682,10 @@ class _SAGEStack(torch.autograd.Function):
         bptr = lambda j: bp[j]  # noqa: E731
         if (ctx.sage2 and pre_top and not need_dx and _use_bwd2
                 and not torch.are_deterministic_algorithms_enabled()):
-            return (None, None, None, None, None, None, None, None,
-                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views))
+            # (a loss head's gradient arrives with its scatter done: g_pre)
+            return (None, None, None, None, None, None, None, None, None,
+                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views,
+                                    g_pre=getattr(dout, "_ngnn_g_pre", None)))
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")
@@ -758,7 +820,7 @@ class _SAGEStack(torch.autograd.Function):
                 _lib.check(rc, "ngnn_sage_dgrad_scatter")
             dy = dh
         dx = dy if (need_dx and L > 0) else None
-        return (dx, None, None, None, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, None, None, None, *grads)
 
 
 _IO_DTYPES = (torch.float32, torch.bfloat16)
@@ -931,7 +993,8 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
         gouts = _claim_grad_views(params)
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
-    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16,
+    head = block.loss_head.start() if (out_dtype == torch.float32 and head_ok(block, xc, params)) else None
+    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16, head,
                            *params)
     if out_dtype == torch.float32:
         return out

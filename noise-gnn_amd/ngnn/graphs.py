@@ -85,6 +85,7 @@ class GraphedTrainStep:
         # (layer-0 W_l, its packed image): the slot load packs the weight's
         # current values, the captured forward reads them prepacked
         self._pack = None
+        self._head = None  # fused.LossHead (made at capture)
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -226,12 +227,21 @@ class GraphedTrainStep:
         if self.x_rows:
             self.col_x = torch.zeros(self.e_cap, dtype=torch.int32, device=self.x.device)
         self._pack = _prepack_target(self.model)
+        # the step's loss taken by a two-layer forward (fused.LossHead): its
+        # persistent buffers made here, outside the capture
+        self._head = None
+        convs = getattr(self.model, "convs", None)
+        if (self.loss_fn is seed_cross_entropy and convs is not None and len(convs) == 2
+                and self.x.dtype == torch.float32
+                and all(hasattr(c, "lin_l") and c.lin_l.weight.dtype == torch.float32 for c in convs)):
+            from .fused import LossHead
+            self._head = LossHead(self.y, self.B, self.n_cap, convs[1].lin_l.weight.shape[0], self.r_next)
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
                         x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B, self.loss_fn is seed_cross_entropy),
                         n_edge_rows_dev=self.n_edge_rows,
                         xrow=(self.xrow_dev, self.x_rows, self.col_x) if self.x_rows else None,
-                        wl_prepacked=self._pack)
+                        wl_prepacked=self._pack, loss_head=self._head)
         if self._pack is not None:  # the capture's own forward reads it: pack it now
             self.load(x, edge_index, y)
         self.opt.zero_grad(set_to_none=True)

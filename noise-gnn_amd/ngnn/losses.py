@@ -209,11 +209,54 @@ def cast_keep_rows(x: torch.Tensor, dtype) -> torch.Tensor:
     return x if x.dtype == dtype else _CastKeepRows.apply(x, dtype)
 
 
+class _HeadXent(torch.autograd.Function):
+    """The loss a graph slot's two-layer forward already took (ngnn.fused.
+    LossHead, include/ngnn.h ngnn_xent_head): forward hands its loss over;
+    backward, for the training step's unit gradient, hands over the gradient
+    rows that forward wrote -- marked with their scatter onto the source rows
+    (_ngnn_g_pre), which the stack's backward then skips.  Any other incoming
+    gradient: the scaled rows recomputed from the logits (ngnn_seed_xent_bwd)."""
+
+    @staticmethod
+    def forward(ctx, logits, res):
+        ctx.res = res
+        ctx.n = logits.size(0)
+        ctx.save_for_backward(logits)
+        return res.loss
+
+    @staticmethod
+    def backward(ctx, g):
+        res = ctx.res
+        hd = res.head
+        if getattr(g, "_ngnn_unit", False):
+            dy = hd.dy[:ctx.n]
+            dy._ngnn_nonzero_rows = hd.B
+            dy._ngnn_g_pre = hd.g
+            return dy, None
+        (x,) = ctx.saved_tensors
+        dx = _grad_buffer(x.device, ctx.n, x.size(1), hd.B)
+        yy = hd.y[:hd.B]
+        g = g.contiguous()
+        _lib.check(_lib.load().ngnn_seed_xent_bwd(
+            _lib.ptr(x), x.stride(0), hd.B, x.size(1), _lib.ptr(yy), hd.ignore, _lib.ptr(hd.ws),
+            _lib.ptr(g), _lib.ptr(res.count), _lib.ptr(dx), dx.stride(0), _lib.stream_handle(x.device)),
+            "ngnn_seed_xent_bwd")
+        dx._ngnn_nonzero_rows = hd.B
+        return dx, None
+
+
 def seed_cross_entropy(logits: torch.Tensor, y: torch.Tensor, batch_size: int,
                        ignore_index: int = -100) -> torch.Tensor:
     """Mean cross entropy of ``logits[:batch_size]`` against ``y[:batch_size]``."""
     if not logits.is_cuda:
         raise RuntimeError("ngnn.losses.seed_cross_entropy: GPU only (no CPU fallback)")
+    res = getattr(logits, "_ngnn_head", None)
+    if (res is not None and not res.used and logits.dtype == torch.float32 and logits.requires_grad
+            and y.data_ptr() == res.head.y.data_ptr() and y.numel() >= batch_size
+            and int(batch_size) == res.head.B and int(ignore_index) == res.head.ignore):
+        # the slot's forward took this loss already (ngnn.fused.LossHead)
+        res.used = True
+        return _HeadXent.apply(logits, res)
     if logits.dtype == torch.bfloat16:  # bf16 models: the loss is taken in fp32
         if logits.dim() == 2 and 0 < batch_size <= logits.size(0) and y.numel() >= batch_size:
             return _SeedXentBF16.apply(logits, y, batch_size, ignore_index)

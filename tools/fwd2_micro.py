@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--stages", default="edge,main,narrow")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--dbg", default="", help="comma list of NGNN_FWD2_DBG values to time 'main' under")
+    ap.add_argument("--edge-dbg", default="", help="comma list of NGNN_EDGE_DBG values to time 'edge' under")
+    ap.add_argument("--head", action="store_true", help="the narrow stage with the loss head (fused.LossHead)")
+    ap.add_argument("--head-dbg", default="", help="comma list of NGNN_HEAD_DBG values to time 'narrow' under")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
@@ -41,28 +44,47 @@ def main():
     params = [c0.lin_l.weight, c0.lin_l.bias, c0.lin_r.weight, c1.lin_l.weight, c1.lin_l.bias, c1.lin_r.weight]
     assert fused.sage2_ok(b.x, blk, "mean", params, False), "not the sage2 shape"
     seed = 12345
-    bufs = fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None)[:3]
+    head = None
+    if args.head:
+        y = torch.randint(0, 47, (1024,), device=dev)
+        n_e0 = int(blk.n_active or 0)
+        lh = fused.LossHead(y, 1024, b.num_nodes, 47, torch.tensor([n_e0], dtype=torch.int32, device=dev))
+        head = lh.start()
+    bufs = fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, head=head)[:3]
     torch.cuda.synchronize()
     st = {"edge": _lib.SAGE2_EDGE, "main": _lib.SAGE2_MAIN, "narrow": _lib.SAGE2_NARROW}
     n_e = int(blk.n_active or 0)
     print(f"block: N={b.num_nodes} E={b.edge_index.size(1)} n_edge_rows={n_e} "
           f"dbg={os.environ.get('NGNN_FWD2_DBG', '-')}")
-    runs = [(n, None) for n in args.stages.split(",")]
-    runs += [("main", v) for v in args.dbg.split(",") if v]
-    for name, dbg in runs:
+    runs = [(n, None, None) for n in args.stages.split(",")]
+    runs += [("main", "NGNN_FWD2_DBG", v) for v in args.dbg.split(",") if v]
+    runs += [("edge", "NGNN_EDGE_DBG", v) for v in args.edge_dbg.split(",") if v]
+    runs += [("narrow", "NGNN_HEAD_DBG", v) for v in args.head_dbg.split(",") if v]
+    for name, env, dbg in runs:
+        os.environ.pop("NGNN_FWD2_DBG", None)
+        os.environ.pop("NGNN_EDGE_DBG", None)
+        os.environ.pop("NGNN_HEAD_DBG", None)
         if dbg is not None:
-            os.environ["NGNN_FWD2_DBG"] = dbg
+            os.environ[env] = dbg
         for _ in range(5):
-            fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, stages=st[name], bufs=bufs)
+            fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, stages=st[name], bufs=bufs,
+                                    head=head if name == "narrow" else None)
+        torch.cuda.synchronize()
+        # the REPS launches as one graph (no host issue between them)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(args.reps):
+                fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, stages=st[name], bufs=bufs,
+                                    head=head if name == "narrow" else None)
+        g.replay()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
-        for _ in range(args.reps):
-            fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, stages=st[name], bufs=bufs)
+        g.replay()
         e1.record()
         torch.cuda.synchronize()
-        tag = name if dbg is None else f"main/dbg{dbg}"
-        print(f"{tag:12s} {e0.elapsed_time(e1) * 1e3 / args.reps:8.1f} us/launch (incl. host issue)", flush=True)
+        tag = name if dbg is None else f"{name}/dbg{dbg}"
+        print(f"{tag:12s} {e0.elapsed_time(e1) * 1e3 / args.reps:8.1f} us/launch (graph of back-to-back launches)", flush=True)
 
 
 if __name__ == "__main__":
