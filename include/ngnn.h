@@ -422,7 +422,18 @@ int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xro
  * grown for more rows).  Float atomics
  * build g: not bitwise reproducible run to run (as the reference's CUDA
  * index_add_).  g_pre (nullable, ABI 15): g already built (ngnn_sage2_fwd's
- * loss head, [>= R' rows, ceil4(F1)]): no scatter launch, g read from it. */
+ * loss head, [n_rows, ceil4(F1)]): no scatter launch, g read from it.
+ * adam (nullable, ABI 15): the optimizer step folded into the reduction --
+ * every parameter updated from its gradient as ngnn_adam_step would (same
+ * arithmetic, the same device step count advanced once); the gradients are
+ * still written.  For a training step whose gradients need no exchange
+ * (one rank) and whose optimizer holds exactly these six tensors. */
+typedef struct ngnn_adam_fold {
+    /* in the order dW_l1, db1, dW_r1, dW_l0, db0, dW_r0 (the gradient order) */
+    float *param[6], *exp_avg[6], *exp_avg_sq[6];
+    float *step; /* the device step count (advanced once, then read) */
+    float lr, beta1, beta2, eps, weight_decay;
+} ngnn_adam_fold;
 size_t ngnn_sage2_bwd_workspace_bytes(int64_t n_rows, int64_t K0, int64_t F1);
 int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, const float *wr1,
                    int64_t ldw1, const float *h, int64_t ldh, float yscale, const float *x,
@@ -430,8 +441,8 @@ int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, c
                    int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
                    const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
                    const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
-                   float *dwl0, float *dbl0, float *dwr0, const float *g_pre, void *ws, size_t ws_bytes,
-                   void *stream);
+                   float *dwl0, float *dbl0, float *dwr0, const float *g_pre, const ngnn_adam_fold *adam,
+                   void *ws, size_t ws_bytes, void *stream);
 
 /* GCNConv(normalize=False) layer (convolution.py:19-35; PyG GCNConv [ext]):
  * out = act(A (x W^T) + b), A the target-grouped sum over in-edges.  The

@@ -87,6 +87,7 @@ struct B2Args {
     const int32_t *r_ptr, *rn_ptr;
     float *slab;  // [S][slab floats]
     int S;
+    float *step_inc;  // nullable: the folded Adam step's count, advanced once here
 };
 
 __host__ __device__ inline int64_t b2_slab_floats(int K0, int F1) {
@@ -150,6 +151,9 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     float *sred = reinterpret_cast<float *>(lb_ + 2 * BUF);  // [2][256] reductions at the end
 
     const int t = threadIdx.x;
+    // (the folded Adam step: k_bwd2_reduce, the next launch, reads the
+    // advanced count -- stream order, no ticket)
+    if (a.step_inc && blockIdx.x == 0 && t == 0) *a.step_inc = *a.step_inc + 1.0f;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int ln = t & 63, q = ln >> 4, l16 = ln & 15;
     // block -> (slice, chunk): the 4 chunks of a slice on one XCD (blocks b,
@@ -452,11 +456,23 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     }
 }
 
-// out = sum over slabs in slab order; then g rows < R' back to zero
+// Adam over the six gradients as they are summed (ngnn_adam_fold): the
+// update of ngnn_adam_step's k_adam, element by element, same arithmetic
+struct AdamFold {
+    float *p[6], *m[6], *v[6];  // in the reduce's order: W_r0, W_l0, b0, W_r1, W_l1, b1
+    float *step;
+    float lr, b1, b2, eps, wd;
+};
+
+// out = sum over slabs in slab order; with ADAM the parameters are updated
+// from them too (k_bwd2 has advanced the step count already: t = *step);
+// then g rows < R' back to zero (blocks >= n_red)
+template <bool ADAM>
 __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ slab, int S, int K0, int F1,
                                                       float *dwr0, float *dwl0, float *db0, float *dwr1,
                                                       float *dwl1, float *db1, float *g, int C4, int n_rows,
-                                                      const int32_t *r_ptr, const int32_t *rn_ptr, int n_red) {
+                                                      const int32_t *r_ptr, const int32_t *rn_ptr, int n_red,
+                                                      AdamFold af) {
     const int64_t total = b2_slab_floats(K0, F1);
     if (static_cast<int>(blockIdx.x) >= n_red) {  // g clearing blocks
         const int R = min(n_rows, *r_ptr);
@@ -469,6 +485,8 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
     }
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (i >= total) return;
+    float t = 0.0f;
+    if (ADAM) t = *af.step;  // (issued before the slab loads)
     float v = 0.0f;
     int sl = 0;
     for (; sl + 8 <= S; sl += 8) {
@@ -480,12 +498,30 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
     }
     for (; sl < S; ++sl) v += slab[static_cast<int64_t>(sl) * total + i];
     const int64_t A = 256LL * K0, Bf = 256LL * F1;
-    if (i < A) dwr0[i] = v;
-    else if (i < 2 * A) dwl0[i - A] = v;
-    else if (i < 2 * A + 256) db0[i - 2 * A] = v;
-    else if (i < 2 * A + 256 + Bf) dwr1[i - 2 * A - 256] = v;
-    else if (i < 2 * A + 256 + 2 * Bf) dwl1[i - 2 * A - 256 - Bf] = v;
-    else db1[i - 2 * A - 256 - 2 * Bf] = v;
+    int k;
+    int64_t e;
+    if (i < A) k = 0, e = i;
+    else if (i < 2 * A) k = 1, e = i - A;
+    else if (i < 2 * A + 256) k = 2, e = i - 2 * A;
+    else if (i < 2 * A + 256 + Bf) k = 3, e = i - 2 * A - 256;
+    else if (i < 2 * A + 256 + 2 * Bf) k = 4, e = i - 2 * A - 256 - Bf;
+    else k = 5, e = i - 2 * A - 256 - 2 * Bf;
+    float *const outs[6] = {dwr0, dwl0, db0, dwr1, dwl1, db1};
+    outs[k][e] = v;
+    if (ADAM) {  // k_adam's update (ngnn_optim.hip) of element e of tensor k
+        const float bc1 = 1.0f - powf(af.b1, t);
+        const float bc2s = sqrtf(1.0f - powf(af.b2, t));
+        const float step_size = af.lr / bc1;
+        float gr = v, p = af.p[k][e], m = af.m[k][e], vv = af.v[k][e];
+        if (af.wd != 0.0f) gr = gr + af.wd * p;
+        m = m + (1.0f - af.b1) * (gr - m);
+        vv = af.b2 * vv + (1.0f - af.b2) * gr * gr;
+        const float denom = sqrtf(vv) / bc2s + af.eps;
+        p = p - step_size * (m / denom);
+        af.m[k][e] = m;
+        af.v[k][e] = vv;
+        af.p[k][e] = p;
+    }
 }
 
 constexpr int B2_S = 64;  // row slices (x 4 hidden chunks = 256 workgroups)
@@ -521,8 +557,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
                               int64_t x_rows, int64_t ldx, int64_t K0, const float *agg0, int64_t ld_agg,
                               const int32_t *rowptr, const int32_t *col, int64_t n_rows, const int32_t *r_ptr,
                               const int32_t *rnext_ptr, int reduce, float *dwl1, float *dbl1, float *dwr1,
-                              float *dwl0, float *dbl0, float *dwr0, const float *g_pre, void *ws, size_t ws_bytes,
-                              void *stream) {
+                              float *dwl0, float *dbl0, float *dwr0, const float *g_pre,
+                              const ngnn_adam_fold *adam, void *ws, size_t ws_bytes, void *stream) {
     NGNN_RETURN_IF(reduce != NGNN_REDUCE_MEAN && reduce != NGNN_REDUCE_SUM, NGNN_E_ARG);
     NGNN_RETURN_IF(F1 <= 0 || F1 > 48 || K0 <= 0 || K0 > 128 || K0 % 4 != 0, NGNN_E_SHAPE);
     NGNN_RETURN_IF(n_rows < 0 || !fits_i32(n_rows), NGNN_E_RANGE);
@@ -537,6 +573,11 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
                    NGNN_E_ALIGN);
     const bool indexed = xrow || xrow_dev;
     NGNN_RETURN_IF(indexed && x_rows <= 0, NGNN_E_ARG);
+    if (adam) {
+        NGNN_RETURN_IF(!adam->step, NGNN_E_ARG);
+        for (int k = 0; k < 6; ++k)
+            NGNN_RETURN_IF(!adam->param[k] || !adam->exp_avg[k] || !adam->exp_avg_sq[k], NGNN_E_ARG);
+    }
     const Ws3 L = ws3_layout(n_rows, K0, F1);
     NGNN_RETURN_IF(ws_bytes < L.total, NGNN_E_WORKSPACE);
     hipStream_t st = as_stream(stream);
@@ -578,6 +619,7 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.rn_ptr = rnext_ptr;
     b.slab = slab;
     b.S = B2_S;
+    b.step_inc = adam ? adam->step : nullptr;
     const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4;
     auto go = [&](auto xr_c, auto kt_c) {
         auto fn = k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value>;
@@ -600,8 +642,28 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     const int64_t total = b2_slab_floats(static_cast<int>(K0), static_cast<int>(F1));
     const int n_red = static_cast<int>(ceil_div(total, 256));
     const int n_clr = g_pre ? 0 : 64;
-    hipLaunchKernelGGL(k_bwd2_reduce, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S, static_cast<int>(K0),
-                       static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4, static_cast<int>(n_rows),
-                       r_ptr, rnext_ptr, n_red);
+    AdamFold af{};
+    if (adam) {
+        // (the header's order dW_l1, db1, dW_r1, dW_l0, db0, dW_r0 -> the reduce's)
+        static const int ord[6] = {5, 3, 4, 2, 0, 1};
+        for (int k = 0; k < 6; ++k) {
+            af.p[k] = adam->param[ord[k]];
+            af.m[k] = adam->exp_avg[ord[k]];
+            af.v[k] = adam->exp_avg_sq[ord[k]];
+        }
+        af.step = adam->step;
+        af.lr = adam->lr;
+        af.b1 = adam->beta1;
+        af.b2 = adam->beta2;
+        af.eps = adam->eps;
+        af.wd = adam->weight_decay;
+        hipLaunchKernelGGL(k_bwd2_reduce<true>, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S,
+                           static_cast<int>(K0), static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4,
+                           static_cast<int>(n_rows), r_ptr, rnext_ptr, n_red, af);
+    } else {
+        hipLaunchKernelGGL(k_bwd2_reduce<false>, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S,
+                           static_cast<int>(K0), static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4,
+                           static_cast<int>(n_rows), r_ptr, rnext_ptr, n_red, af);
+    }
     return launch_status();
 }

@@ -77,7 +77,7 @@ SIGNATURES = {
     "ngnn_sage2_bwd_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64,
                               _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p, _p,
-                              _sz, _p]),
+                              _p, _sz, _p]),
     "ngnn_sage2_supported": (_int, [_i64, _i64, _i64, _int]),
     "ngnn_sage2_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_fwd": (_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _int,
@@ -150,6 +150,13 @@ class XentHead(ctypes.Structure):
     _fields_ = [("y", _p), ("B", _i64), ("ignore_index", _i64), ("loss", _p), ("count", _p),
                 ("dy", _p), ("ldd", _i64), ("g", _p), ("g_rows", _i64), ("g_rows_dev", _p),
                 ("ws", _p), ("ws_bytes", _sz)]
+
+
+class AdamFold(ctypes.Structure):
+    """include/ngnn.h ngnn_adam_fold (ngnn_sage2_bwd's optimizer step, ABI 15)."""
+    _fields_ = [("param", _p * 6), ("exp_avg", _p * 6), ("exp_avg_sq", _p * 6), ("step", _p),
+                ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float)]
 
 
 def ptr(t) -> int:

@@ -543,6 +543,61 @@ def reserve_sage2_bwd(dev, n_rows: int, K0: int, F1: int) -> torch.Tensor:
                       zero=True)
 
 
+# the graph slot's Adam step folded into the two-layer backward's reduction
+# (include/ngnn.h ngnn_adam_fold): set by GraphedTrainStep around its capture
+# only -- an eager backward never updates parameters
+_adam_fold = None
+
+
+class AdamFoldSpec:
+    """ngnn.optim.Adam's step for the six tensors of a two-layer stack,
+    taken by ngnn_sage2_bwd's reduction (one launch less per step).  used:
+    set when a captured backward took it (the slot then captures no
+    optimizer launch)."""
+
+    def __init__(self, opt, params):
+        st = opt.state
+        group = opt.param_groups[0]
+        step = st[params[0]]["step"]
+        self.params = params  # [W_l0, b0, W_r0, W_l1, b1, W_r1] (the stack's order)
+        b1, b2 = group["betas"]
+        # the header's order: dW_l1, db1, dW_r1, dW_l0, db0, dW_r0
+        order = [params[3], params[4], params[5], params[0], params[1], params[2]]
+        P = (ctypes.c_void_p * 6)(*[q.data_ptr() for q in order])
+        M = (ctypes.c_void_p * 6)(*[st[q]["exp_avg"].data_ptr() for q in order])
+        V = (ctypes.c_void_p * 6)(*[st[q]["exp_avg_sq"].data_ptr() for q in order])
+        self._keep = step
+        self.struct = _lib.AdamFold(P, M, V, step.data_ptr(), float(group["lr"]),
+                                    float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]))
+        self.used = False
+
+    @staticmethod
+    def make(opt, model):
+        """The spec when `opt` is ngnn.optim.Adam over exactly the two-layer
+        stack's six fp32 parameters with its state made (after a warm-up
+        step), else None."""
+        from .optim import Adam
+        convs = getattr(model, "convs", None)
+        if not isinstance(opt, Adam) or convs is None or len(convs) != 2 or len(opt.param_groups) != 1:
+            return None
+        params = []
+        for c in convs:
+            if not (hasattr(c, "lin_l") and hasattr(c, "lin_r")) or c.lin_r is None:
+                return None
+            params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
+        group = opt.param_groups[0]["params"]
+        if len(group) != 6 or {id(q) for q in group} != {id(q) for q in params}:
+            return None
+        for q in params:
+            s = opt.state.get(q, {})
+            if (q is None or q.dtype != torch.float32 or not q.is_contiguous() or "step" not in s
+                    or s["exp_avg"].dtype != torch.float32):
+                return None
+        if len({opt.state[q]["step"].data_ptr() for q in params}) != 1:
+            return None
+        return AdamFoldSpec(opt, params)
+
+
 def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: float, r_ptr: int,
                    rn_ptr: int, views, g_pre=None):
     """Every weight gradient of the two-layer stack (include/ngnn.h
@@ -564,13 +619,20 @@ def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: fl
     nrows = block.n_dst
     ws = reserve_sage2_bwd(dev, nrows, K0, F1)
     yscale = dropout_scale(p_drop) if p_drop > 0.0 else 1.0
+    fold = _adam_fold
+    if fold is not None and not (len(params) == 6 and all(
+            a.data_ptr() == b.data_ptr() for a, b in zip(params, fold.params))):
+        fold = None
+    if fold is not None:
+        fold.used = True
     with _timing.span("sage2_bwd", 0, 0):
         rc = lib.ngnn_sage2_bwd(
             _lib.ptr(dy), dy.stride(0), F1, _lib.ptr(w1l), _lib.ptr(w1r), w1l.stride(0), _lib.ptr(h),
             h.stride(0), yscale, _lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev),
             block.x_rows, x.stride(0), K0, _lib.ptr(agg0), agg0.stride(0), _lib.ptr(block.rowptr),
             _lib.ptr(block.col), nrows, r_ptr, rn_ptr, _lib.REDUCE[reduce], *(_lib.ptr(g) for g in grads[3:]),
-            *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(g_pre), _lib.ptr(ws), ws.numel(),
+            *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(g_pre),
+            None if fold is None else ctypes.byref(fold.struct), _lib.ptr(ws), ws.numel(),
             _lib.stream_handle(dev))
     _lib.check(rc, "ngnn_sage2_bwd")
     return grads

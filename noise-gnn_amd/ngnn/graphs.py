@@ -86,6 +86,7 @@ class GraphedTrainStep:
         # current values, the captured forward reads them prepacked
         self._pack = None
         self._head = None  # fused.LossHead (made at capture)
+        self.folded = False  # the captured backward took the Adam step (fused.AdamFoldSpec)
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -261,16 +262,29 @@ class GraphedTrainStep:
         red = self.reducer if (self.reducer is not None and hasattr(self.reducer, "active")
                                and self.reducer.active()) else None
         self._split_reduce = red is not None
+        # one rank: the Adam step folds into the two-layer backward's
+        # reduction (fused.AdamFoldSpec) -- then no optimizer graph
+        from . import fused as _fused
+        exchange = red is not None or (self.reducer is not None and not (
+            hasattr(self.reducer, "active") and not self.reducer.active()))
+        fold = None if exchange else _fused.AdamFoldSpec.make(self.opt, self.model)
         self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb):
-            self.loss = self._fwd_bwd()
-            if red is not None:
-                red.pack()
-        self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
-            if red is not None:
-                red.unpack()
-            self.opt.step()
+        _fused._adam_fold = fold
+        try:
+            with torch.cuda.graph(self.g_fb):
+                self.loss = self._fwd_bwd()
+                if red is not None:
+                    red.pack()
+        finally:
+            _fused._adam_fold = None
+        self.folded = fold is not None and fold.used
+        self.g_opt = None
+        if not self.folded:
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
+                if red is not None:
+                    red.unpack()
+                self.opt.step()
         block_cache.clear()
         torch.cuda.synchronize()
         if snap is not None:
@@ -299,7 +313,8 @@ class GraphedTrainStep:
             self.reducer.allreduce()
         elif self.reducer is not None:
             self.reducer()
-        self.g_opt.replay()
+        if self.g_opt is not None:  # (None: the backward's reduction took the Adam step)
+            self.g_opt.replay()
         return self.loss
 
 

@@ -109,7 +109,7 @@ def _run(c, R, Rn, reduce, yscale, ws=None):
         yscale, _lib.ptr(x), None, _lib.ptr(xrow), None, x.size(0) if xr else 0, K0, K0,
         _lib.ptr(d["agg0"]), K0, _lib.ptr(d["rowptr"]), _lib.ptr(d["col"]), N,
         bounds.data_ptr(), bounds.data_ptr() + 4, _lib.REDUCE[reduce],
-        *(_lib.ptr(out[k]) for k in ("dWl1", "dbl1", "dWr1", "dWl0", "dbl0", "dWr0")), None,
+        *(_lib.ptr(out[k]) for k in ("dWl1", "dbl1", "dWr1", "dWl0", "dbl0", "dWr0")), None, None,
         _lib.ptr(ws), ws.numel(), _lib.stream_handle(DEV))
     assert rc == _lib.OK, rc
     torch.cuda.synchronize()

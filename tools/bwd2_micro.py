@@ -41,7 +41,7 @@ def main(reps=50):
         rc = lib.ngnn_sage2_bwd(_lib.ptr(dy), F1, F1, _lib.ptr(wl1), _lib.ptr(wr1), 256, _lib.ptr(h), 256, 2.0,
                                 _lib.ptr(x), None, None, None, 0, K0, K0, _lib.ptr(agg0), K0,
                                 _lib.ptr(rowptr), _lib.ptr(col), N, bounds.data_ptr(), bounds.data_ptr() + 4,
-                                _lib.REDUCE["mean"], *(_lib.ptr(o) for o in out), _lib.ptr(ws), ws.numel(),
+                                _lib.REDUCE["mean"], *(_lib.ptr(o) for o in out), None, None, _lib.ptr(ws), ws.numel(),
                                 _lib.stream_handle(dev))
         assert rc == _lib.OK, rc
     for _ in range(5):
