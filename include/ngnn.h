@@ -608,6 +608,11 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * model's fp32 logits handed back in bf16 (Tensor.to(torch.bfloat16), the
  * `SAGE.forward` return dtype of a bf16 model).  src 16-B, dst 8-B aligned. */
 int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream);
+/* The same over rows < min(n_rows, *n_rows_dev) of row_elems contiguous
+ * elements each (n_rows_dev nullable): a graph slot's logits, cast for the
+ * block's real rows only (ABI 15). */
+int ngnn_cast_f32_bf16_rows(const float *src, void *dst, int64_t n_rows, int64_t row_elems,
+                            const int32_t *n_rows_dev, void *stream);
 /* n <= 16 tensors cast in one launch: to_bf16 = 0: dst[k][i] = float(src[k]
  * [i]) (bf16 -> fp32, exact); 1: dst[k][i] = bf16(src[k][i]) (round to
  * nearest even, NaN kept), i < numels[k] -- a bf16 model's parameters widened

@@ -196,7 +196,11 @@ namespace {
 // else 4 (8-B stores, dst only 8-B aligned)
 template <bool W8>
 __global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src,
-                                                    uint16_t *__restrict__ dst, int64_t n) {
+                                                    uint16_t *__restrict__ dst, int64_t n,
+                                                    const int32_t *__restrict__ rows_dev, int64_t row_elems) {
+    // (rows_dev: only the block's real rows -- a graph slot's logits are
+    // sized for its capacity, 2.3x the rows of a 3-layer products block)
+    if (rows_dev) n = min(n, static_cast<int64_t>(max(*rows_dev, 0)) * row_elems);
     auto rne = [](float f) -> uint32_t {
         const uint32_t u = __float_as_uint(f);
         if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
@@ -239,7 +243,8 @@ __global__ __launch_bounds__(256) void k_cast_bf16(const float *__restrict__ src
 }  // namespace
 }  // namespace ngnn
 
-extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream) {
+static int cast_f32_bf16(const float *src, void *dst, int64_t n, const int32_t *rows_dev, int64_t row_elems,
+                         void *stream) {
     using namespace ngnn;
     NGNN_RETURN_IF(n < 0 || (n > 0 && (!src || !dst)), NGNN_E_ARG);
     NGNN_RETURN_IF(!aligned(src, 16) || !aligned(dst, 8), NGNN_E_SHAPE);
@@ -247,11 +252,21 @@ extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(ceil_div(n, 8), 256), 2048));
     if (aligned(dst, 16))
         hipLaunchKernelGGL(k_cast_bf16<true>, dim3(grid), dim3(256), 0, as_stream(stream), src,
-                           static_cast<uint16_t *>(dst), n);
+                           static_cast<uint16_t *>(dst), n, rows_dev, row_elems);
     else
         hipLaunchKernelGGL(k_cast_bf16<false>, dim3(grid), dim3(256), 0, as_stream(stream), src,
-                           static_cast<uint16_t *>(dst), n);
+                           static_cast<uint16_t *>(dst), n, rows_dev, row_elems);
     return launch_status();
+}
+
+extern "C" int ngnn_cast_f32_bf16(const float *src, void *dst, int64_t n, void *stream) {
+    return cast_f32_bf16(src, dst, n, nullptr, 0, stream);
+}
+
+extern "C" int ngnn_cast_f32_bf16_rows(const float *src, void *dst, int64_t n_rows, int64_t row_elems,
+                                       const int32_t *n_rows_dev, void *stream) {
+    NGNN_RETURN_IF(n_rows < 0 || row_elems < 0, NGNN_E_ARG);
+    return cast_f32_bf16(src, dst, n_rows * row_elems, n_rows_dev, row_elems, stream);
 }
 
 // ---- n tensors cast in ONE launch: bf16 -> fp32 (exact) or fp32 -> bf16

@@ -91,6 +91,7 @@ SIGNATURES = {
     "ngnn_block_prefix_stats": (_int, [_p, _p, _p, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad_workspace_bytes": (_sz, [_i64, _i64]),
     "ngnn_cast_f32_bf16": (_int, [_p, _p, _i64, _p]),
+    "ngnn_cast_f32_bf16_rows": (_int, [_p, _p, _i64, _i64, _p, _p]),
     "ngnn_widen_bf16_rows": (_int, [_p, _i64, _i64, _i64, _p, _p, _i64, _p]),
     "ngnn_sage_wgrad": (_int, [_p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _int, _i64, _p,
                                _i64, _p, _i64,

@@ -1060,8 +1060,8 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                            *params)
     if out_dtype == torch.float32:
         return out
-    if out_dtype == torch.bfloat16 and out.is_contiguous():
-        return _StackOutBF16.apply(out)
+    if out_dtype == torch.bfloat16 and out.is_contiguous() and out.dim() == 2:
+        return _StackOutBF16.apply(out, block.n_rows_dev)
     from .losses import cast_keep_rows
     return cast_keep_rows(out, out_dtype)
 
@@ -1130,18 +1130,20 @@ class _StackOutBF16(torch.autograd.Function):
     into a cached buffer, and the hint travels on."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, rows_dev=None):
+        # (rows_dev: a graph slot's device row count -- only the block's real
+        # rows are cast; the slot's padding rows of y are left unwritten)
         y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-        _lib.check(_lib.load().ngnn_cast_f32_bf16(_lib.ptr(x), _lib.ptr(y), x.numel(),
-                                                  _lib.stream_handle(x.device)),
-                   "ngnn_cast_f32_bf16")
+        _lib.check(_lib.load().ngnn_cast_f32_bf16_rows(_lib.ptr(x), _lib.ptr(y), x.size(0), x[0].numel(),
+                                                       _lib.ptr(rows_dev), _lib.stream_handle(x.device)),
+                   "ngnn_cast_f32_bf16_rows")
         return y
 
     @staticmethod
     def backward(ctx, g):
         rows = getattr(g, "_ngnn_nonzero_rows", None)
         if rows is None:
-            return g.float()
+            return g.float(), None
         key = (g.device, tuple(g.shape))
         buf = _out_grads.get(key)
         if buf is None:
@@ -1156,4 +1158,4 @@ class _StackOutBF16(torch.autograd.Function):
         else:
             buf[:R].copy_(g[:R])
         buf._ngnn_nonzero_rows = R  # rows >= R are stale: the stack never reads them
-        return buf
+        return buf, None
