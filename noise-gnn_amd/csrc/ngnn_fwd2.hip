@@ -135,29 +135,50 @@ __device__ __forceinline__ float wave_max(float v) { return max_xor32(max_xor16(
 
 // layer 0's slice of wave wv: rows 32 wv + 16 mt + m of w ([256, K0], row
 // stride ldw), k = 32 c + 8 q .. + 7; returns the wave's exponent
+// (in two halves, so a caller can issue other loads between the slice's
+// loads and their use: w0_slice_issue, then w0_slice_finish)
+// (buffer loads, as the callers' other loads: the compiler counts them in
+// issue order with the rest -- mixed with global loads it waited for the
+// whole slice before the first index word)
 template <int C0>
-__device__ __forceinline__ int load_w0_slice(const float *w, int64_t ldw, int K0, int wv, int ln,
-                                             half8 (&frag)[2][C0][2]) {
+__device__ __forceinline__ void w0_slice_issue(const float *w, int64_t ldw, int K0, int wv, int ln,
+                                               v4f (&t)[2][C0][2]) {
     const int q = ln >> 4, m = ln & 15;
-    v4f t[2][C0][2];
-    float mx = 0.0f;
+    const i32x4 wr = make_rsrc(w, static_cast<uint32_t>(static_cast<int64_t>(F2_HID) * ldw * 4));
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-        const float *row = w + static_cast<int64_t>(32 * wv + 16 * mt + m) * ldw;
+        const int rb = (32 * wv + 16 * mt + m) * static_cast<int>(ldw) * 4;
 #pragma unroll
         for (int c = 0; c < C0; ++c)
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                t[mt][c][p] = wload4(row, 32 * c + 8 * q + 4 * p, K0, true);
-                mx = fmaxf(mx, amax4(t[mt][c][p]));
+                const int k = 32 * c + 8 * q + 4 * p;
+                t[mt][c][p] = buf_load4(wr, k < K0 ? rb + 4 * k : kOOB2, 0, 0);
             }
     }
+}
+template <int C0>
+__device__ __forceinline__ int w0_slice_finish(const v4f (&t)[2][C0][2], half8 (&frag)[2][C0][2]) {
+    float mx = 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int c = 0; c < C0; ++c)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) mx = fmaxf(mx, amax4(t[mt][c][p]));
     const int e = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int c = 0; c < C0; ++c) h2_split(ldexp4(t[mt][c][0], e), ldexp4(t[mt][c][1], e), frag[mt][c][0], frag[mt][c][1]);
     return e;
+}
+template <int C0>
+__device__ __forceinline__ int load_w0_slice(const float *w, int64_t ldw, int K0, int wv, int ln,
+                                             half8 (&frag)[2][C0][2]) {
+    v4f t[2][C0][2];
+    w0_slice_issue<C0>(w, ldw, K0, wv, ln, t);
+    return w0_slice_finish<C0>(t, frag);
 }
 
 // ---------------------------------------------------------------- k_edge_nb
@@ -369,16 +390,35 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
 
     // prologue: row pointers of tiles 0..2, ids of 0..1, rows of tile 0 --
     // then this wave's W_l0 slice while they are in flight
+    // (issue order: the index words, the weight slice, then tile 0's rows --
+    // so the slice is split while the rows are in flight, and waiting for
+    // tile 0's ids does not wait for the slice)
     int b0, e0, b1, e1, b2, e2;
     rowptr_of(0, b0, e0);
     rowptr_of(1, b1, e1);
     int i0 = ids_of(b0, e0, 0);
     rowptr_of(2, b2, e2);
     int i1 = ids_of(b1, e1, 0);
+    v4f wt[2][C0][2];
+    __builtin_amdgcn_sched_barrier(0);  // (keep the issue order: the scheduler hoists loads)
+    if (!(DBG & 16)) w0_slice_issue<C0>(a.wl0, a.ldw0, a.K0, wv, ln, wt);
+    __builtin_amdgcn_sched_barrier(0);
     v4f va[G2_NB], vb[G2_NB];
     rows_of(b0, e0, 0, i0, va);
     half8 wl[2][C0][2];
-    const int eW = load_w0_slice<C0>(a.wl0, a.ldw0, a.K0, wv, ln, wl);
+    int eW = 0;
+    if (DBG & 16) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int c = 0; c < C0; ++c) wl[mt][c][0] = wl[mt][c][1] = half8{};
+    } else {
+        eW = w0_slice_finish<C0>(wt, wl);
+    }
+    if (DBG & 8) {  // (profiling: the prologue alone)
+        if (va[0][0] == 1.2345f && wl[0][0][0][0] == static_cast<_Float16>(1.0f)) a.nb[0] = 0.0f;
+        return;
+    }
 
     // one step: request rowptr(j+3), ids(j+2), rows(j+1) into vn; consume
     // tile j from vc
@@ -473,17 +513,22 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     {
         // layer 1: output rows 16 m1' + m of W_r1 (m1 < NT1) / W_l1 (the rest),
         // K rows 32 wv + (4 q + j, 16 + 4 q + j): the order of the lane's h
+        // (buffer loads, counted in order with the kernel's other loads)
         v4f t[MT1][2];
         float mx = 0.0f;
+        const i32x4 r1r = make_rsrc(a.wr1, static_cast<uint32_t>(a.F1 * a.ldw1 * 4));
+        const i32x4 l1r = make_rsrc(a.wl1, static_cast<uint32_t>(a.F1 * a.ldw1 * 4));
 #pragma unroll
         for (int m1 = 0; m1 < MT1; ++m1) {
             const int zt = m1 >= NT1;
             const int o = 16 * (m1 - zt * NT1) + rl;
-            const float *row = (zt ? a.wl1 : a.wr1) + static_cast<int64_t>(min(o, a.F1 - 1)) * a.ldw1;
-            t[m1][0] = wload4(row, 32 * wv + 4 * q, F2_HID, o < a.F1);
-            t[m1][1] = wload4(row, 32 * wv + 16 + 4 * q, F2_HID, o < a.F1);
-            mx = fmaxf(mx, fmaxf(amax4(t[m1][0]), amax4(t[m1][1])));
+            const int rb = o < a.F1 ? o * static_cast<int>(a.ldw1) * 4 : kOOB2;
+            const int c0 = (32 * wv + 4 * q) * 4, c1 = (32 * wv + 16 + 4 * q) * 4;
+            t[m1][0] = buf_load4(zt ? l1r : r1r, rb == kOOB2 ? kOOB2 : rb + c0, 0, 0);
+            t[m1][1] = buf_load4(zt ? l1r : r1r, rb == kOOB2 ? kOOB2 : rb + c1, 0, 0);
         }
+#pragma unroll
+        for (int m1 = 0; m1 < MT1; ++m1) mx = fmaxf(mx, fmaxf(amax4(t[m1][0]), amax4(t[m1][1])));
         eW1 = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
         for (int m1 = 0; m1 < MT1; ++m1) h2_split(ldexp4(t[m1][0], eW1), ldexp4(t[m1][1], eW1), w1[m1][0], w1[m1][1]);
@@ -1009,6 +1054,10 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
                 case 4: return launch_edge_nb<4, 4>(g, grid, st);
                 case 6: return launch_edge_nb<4, 6>(g, grid, st);
                 case 7: return launch_edge_nb<4, 7>(g, grid, st);
+                case 8: return launch_edge_nb<4, 8>(g, grid, st);
+                case 16: return launch_edge_nb<4, 16>(g, grid, st);
+                case 23: return launch_edge_nb<4, 23>(g, grid, st);
+                case 24: return launch_edge_nb<4, 24>(g, grid, st);
                 default: break;
             }
         }
