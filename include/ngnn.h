@@ -360,7 +360,7 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  *            -- d loss / d out at unit scale, rows >= B not written;
  *   g[s]  += dy[d] (/ deg(d) for MEAN) for every edge s -> d, d < B (float
  *            atomics; exact zeros skipped): the narrow scatter ngnn_sage2_bwd
- *            runs first, already done -- pass g as its g_pre.  g [>= R' rows,
+ *            runs first, already done -- pass g as its g_pre.  g [n_rows rows,
  *            C4 = ceil4(F1) floats]: its rows < min(g_rows, *g_rows_dev) are
  *            zeroed by the EDGE launch of the same call (so a head whose
  *            backward never runs leaves nothing behind); nullable (no scatter).
