@@ -166,14 +166,19 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
         // (host: F4 <= 16, one column quad per lane; B <= n_rows)
         __shared__ float s_red[256];
         __shared__ float s_grp[16];
-        // rows to workgroups as the plain kernel's (16 consecutive rows per
-        // workgroup and pass): the seed rows sit in the first ceil(B / 16)
-        // workgroups.  (Measured alternatives, tools/fwd2_micro.py --head:
-        // seed rows one per workgroup over all of them spread the scatter
-        // atomics but cost the rest of the launch its row locality, 36 us
-        // against 18; 4 per workgroup on wave 0 of ceil(B / 4) workgroups, 25.)
+        // rows to workgroups as the plain kernel's (16 consecutive row slots
+        // per workgroup and pass), except that the first 2 B8 slots (B8 =
+        // ceil8(B)) interleave: a workgroup's groups 0-7 take 8 consecutive
+        // seed rows, groups 8-15 the 8 rows B8 + the same offset -- the seed
+        // rows, and their scatter atomics, spread over twice the workgroups
+        // with the row locality kept.  (Measured alternatives,
+        // tools/fwd2_micro.py --head: seed rows one per workgroup over all
+        // of them spread the atomics but cost the rest of the launch its row
+        // locality, 36 us against 18; 4 per workgroup on wave 0 of ceil(B /
+        // 4) workgroups, 25.)
         const int B = hd.B, G = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
-        const int nh = min(G, (B + 15) >> 4);  // workgroups holding seed rows
+        const int B8 = (B + 7) & ~7;
+        const int nh = min(G, B8 >> 3);  // workgroups holding seed rows
         const bool hwg = bx < nh;              // (uniform)
         float cnt = 0.0f;
         if (hd.cnt_in) {
@@ -193,7 +198,11 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
         const int c4 = sub;
         const i32x4 zr = make_rsrc(z, 0xF0000000u);
         const int dl = max(nr, B);
-        for (int d = (bx * 256 + static_cast<int>(threadIdx.x)) >> 4; d < dl; d += 16 * G) {
+        const int vl = max(dl, 2 * B8);
+        for (int v = (bx * 256 + static_cast<int>(threadIdx.x)) >> 4; v < vl; v += 16 * G) {
+            const int vg = v & 15;
+            const int d = v < 2 * B8 ? ((v >> 4) << 3) + (vg & 7) + (vg >= 8 ? B8 : 0) : v;
+            if (d >= dl) continue;
             const bool hrow = d < B;
             const int beg = rowptr[d], end = (d < nr) ? rowptr[d + 1] : beg;
             if (beg == end && !hrow) continue;
@@ -418,7 +427,7 @@ int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *ro
     NGNN_RETURN_IF(head && (Fo > 64 || head->B <= 0 || head->B > n_rows), NGNN_E_ARG);
     const unsigned grid = static_cast<unsigned>(
         std::max<int64_t>(1, std::min<int64_t>(head ? std::min(4 * num_cus(), 1024) : 4 * num_cus(),
-                                               ceil_div(std::max<int64_t>(rows, head ? head->B : 0), 16))));
+                                               ceil_div(std::max<int64_t>(rows, head ? 2 * ((head->B + 7) & ~int64_t{7}) : 0), 16))));
     // (the head's hand-off: at most 32 groups of 32 workgroups)
     const NarrowHead hd = head ? *head : NarrowHead{};
     auto go = [&](auto mean_c, auto head_c) {
