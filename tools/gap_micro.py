@@ -17,21 +17,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "noise-gnn_amd"))
 
 
+def _short(name):
+    import re
+    m = re.search(r"(k_\w+)", name)
+    return m.group(1) if m else name[:28]
+
+
 def report(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    phase, gaps = None, {}
-    prev = None
-    for r in rows:
-        name = r["Kernel_Name"]
-        if "fill" in name.lower() and "ngnn" not in name:
-            phase = {None: "A", "A": "B", "B": "C", "C": "end"}[phase]
-            prev = None
-            continue
-        if phase in ("A", "B", "C") and prev is not None:
+    # the last four non-ngnn kernels are the phase marks (fills)
+    marks = [i for i, r in enumerate(rows) if "ngnn" not in r["Kernel_Name"]][-4:]
+    gaps = {}
+    for ph, (i0, i1) in zip("ABC", zip(marks, marks[1:])):
+        for k in range(i0 + 2, i1):
+            prev, r = rows[k - 1], rows[k]
             g = (int(r["Start_Timestamp"]) - int(prev["End_Timestamp"])) / 1e3
-            key = (phase, prev["Kernel_Name"].split("(")[0][-28:], name.split("(")[0][-28:])
+            key = (ph, _short(prev["Kernel_Name"]), _short(r["Kernel_Name"]))
             gaps.setdefault(key, []).append(g)
-        prev = r
     for (ph, a, b), v in sorted(gaps.items()):
         v.sort()
         print(f"{ph}  {a:28s} -> {b:28s} n={len(v):4d} median gap {v[len(v) // 2]:7.2f} us")
