@@ -535,6 +535,21 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 #pragma unroll 1  // one neighbour pair in flight: keep the register budget
         for (int e4 = 0; 4 * e4 < ne; ++e4) {
             const int srcl = rl + 16 * e4;
+            // bf16 rows: all four neighbours' 8-B pieces issued before the
+            // first sum (half the registers of fp32 fragments; summed in
+            // edge order below, so the result is unchanged)
+            i32x2 rb[XB ? 4 : 1][RT_KC];
+            if (XB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = e0 + 4 * e4 + j;
+                    const int o = lt_mask(e, deg)
+                                      ? static_cast<int>(static_cast<uint32_t>(__shfl(cb[j], srcl)) * ld4 + kofs)
+                                      : kOOB;
+#pragma unroll
+                    for (int g = 0; g < RT_KC; ++g) rb[XB ? j : 0][g] = buf_load2i(xr, o + 32 * g, 0, 0);
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 4; j += 2) {
                 const int e = e0 + 4 * e4 + j;
@@ -550,8 +565,8 @@ __device__ __forceinline__ void gather_chunk(v4f (&ag)[RT_KC], const RtArgs &a, 
 #pragma unroll
                 for (int g = 0; g < RT_KC; ++g) {
                     if (XB) {  // 4 bf16 per lane and k-group: one 8-B load, widened exactly
-                        v0[g] = bf16x4_to_f32(buf_load2i(xr, o0 + 32 * g, 0, 0));
-                        v1[g] = bf16x4_to_f32(buf_load2i(xr, o1 + 32 * g, 0, 0));
+                        v0[g] = bf16x4_to_f32(rb[XB ? j : 0][g]);
+                        v1[g] = bf16x4_to_f32(rb[XB ? j + 1 : 0][g]);
                     } else {
                         v0[g] = buf_load4(xr, o0 + 64 * g, 0, 0);
                         v1[g] = buf_load4(xr, o1 + 64 * g, 0, 0);
