@@ -1,7 +1,7 @@
 """Headline benchmark: aggregated edges/s (+ epoch time) of GraphSAGE training
 on ogbn-products-shaped mini-batches, fanout [15,10], batch 1024 (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts N ranks itself)
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Workload (config.workload = "products-[15,10]-bs1024"): synthetic graph with
@@ -312,8 +312,78 @@ def _allreduce_name(world: int) -> str:
     return "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without torchrun's env: start the N ranks
+    here, one child process per GPU with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set (what torchrun would set), and return the first non-zero
+    exit code.  This process never touches the GPU (no exec after a HIP
+    call: children only)."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"[bench] rank exit codes {rcs}", file=sys.stderr)
+    return bad[0] if bad else 0
+
+
+def check_world(gpus: int, world: int) -> None:
+    """The run must have exactly --gpus ranks, one per GPU (a mismatch would
+    print a line whose n_gpus is not what was asked for)."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the process group has {world} rank(s) "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}); launch with "
+                         f"torchrun --nproc-per-node {gpus} or without torchrun's env")
+    rehearsal = os.environ.get("NGNN_DIST_BACKEND") == "gloo"
+    if world > 1 and not rehearsal and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: --gpus {world} needs {world} visible GPUs, found "
+                         f"{torch.cuda.device_count()} (NGNN_DIST_BACKEND=gloo rehearses "
+                         f"several ranks on fewer GPUs)")
+
+
+def allreduce_us(reducer, world: int, reps: int = 50):
+    """Host-timed gradient all-reduce of the step's bucket (the one
+    collective of a DP step), averaged over `reps` calls between syncs."""
+    if world <= 1 or not reducer.active():
+        return None
+    import torch.distributed as dist
+    saved = reducer.bucket.clone()
+    for _ in range(5):
+        reducer.allreduce()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        reducer.allreduce()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    reducer.bucket.copy_(saved)
+    t = torch.tensor([dt], dtype=torch.float64, device=reducer.bucket.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"us": round(1e6 * float(t), 2), "bytes": reducer.bucket.numel() * 4, "reps": reps,
+            "note": "host-timed all_reduce(SUM) of the flat fp32 gradient bucket, max over ranks"}
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch.distributed as dist
 
     import ngnn
@@ -322,6 +392,7 @@ def main():
     from ngnn.loader import NeighborLoader, sample_block, synthetic_graph
 
     rank, world, local = init()
+    check_world(args.gpus, world)
     # (one GPU per rank; modulo only matters when rehearsing N ranks on fewer GPUs)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
@@ -404,6 +475,7 @@ def main():
             for i in range(args.steps):
                 train_step(model, opt, reducer, batches[(args.warmup + i) % nb])
         barrier()
+    ar = allreduce_us(reducer, world)
     t = torch.tensor([dt, float(edges)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
@@ -539,6 +611,7 @@ def main():
                                and graph and gstep.x_rows else "loader copies x[n_id]"),
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
             "epoch_batches_per_rank": len(loader),
+            "allreduce": ar,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

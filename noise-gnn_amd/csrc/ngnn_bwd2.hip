@@ -18,19 +18,29 @@
 // chip.  Launches:
 //   k_lowdim_scatter (ngnn_sage_bwd.hip)  g, float atomics (no image blocks);
 //   k_bwd2  per 32-row chunk of rows < R' and 64 hidden columns: X = [dy | g]
-//           and h / x / agg0 rows staged in LDS as two bf16 parts each;
+//           and h / x / agg0 rows staged in LDS as two fp16 parts each;
 //           dh = X [W_r1; W_l1] on MFMA, masked, split, exchanged between
 //           the two row-tile waves; then dW_r0 / dW_l0 (A = dz0^T) and
 //           [dW_r1; dW_l1] (A = X^T, B = h) on MFMA with transposed LDS reads
 //           (ds_read_b64_tr_b16).  Partials per row slice -> slabs;
 //   k_bwd2_reduce  fixed-order slab sums into the six gradients; clears g.
 //
-// Arithmetic: fp32 operands as two bf16 parts v = v1 + v2 (+ r, |r| <= 2^-17
-// |v|); products a1 b1 + a1 b2 + a2 b1 on bf16 MFMAs (each exact in fp32,
-// fp32 accumulation), dropped terms <= ~3 2^-17 relative per product: the
-// weight-gradient bars (1e-4) with room; bf16 keeps fp32's exponent range,
-// so no scaling is needed anywhere (the forward's fp16 H2 split needs it).
+// Arithmetic (H2, as the forward; round 5): every operand is scaled by a power
+// of two that puts its block's max |v| in [2^14, 2^15) and split into two fp16
+// parts, v 2^e = v1 + v2 (+ r, |r| <= 2^-22 |v 2^e|); products a1 b1 + a1 b2 +
+// a2 b1 on fp16 MFMAs (each exact in fp32, fp32 accumulation): ~3 2^-22
+// relative per product, fp32-class (tests/gradbar.py: max|g - g_ref| <= 1e-5
+// max|g_ref|; the round-4 two-part bf16 split, 2^-17, measured up to 1.1e-5).
+// The weight-gradient products sum over ROWS, so a scale must be uniform over
+// the rows of an MFMA: one scale per operand per 32-row chunk (its max over
+// the chunk, found while the chunk's loads land: each wave's maxima go
+// through LDS at the barrier that ends the previous chunk -- no barrier of
+// its own); each chunk's products start from zero and are unscaled (v_ldexp,
+// exact) into the fp32 accumulators.  dh = X W1 sums over F1, so its scales
+// are X's chunk scale and the wave's W1 slice scale; dz0 is scaled by the
+// bound 96 2^30 yscale of |dh| in those units (a constant shift, e_dz).
 #include <algorithm>
+#include <cmath>
 
 #include "ngnn_device.h"
 
@@ -43,10 +53,10 @@ int lowdim_scatter_launch(const float *dy, int64_t ldy, const int32_t *rowptr, c
 
 namespace {
 
-typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef _Float16 bf8 __attribute__((ext_vector_type(8)));  // (fp16 parts; the names kept from the bf16 split)
+typedef _Float16 bf4 __attribute__((ext_vector_type(4)));
 typedef short s4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) __bf16 L16;  // an LDS bf16 (32-bit addresses)
+typedef __attribute__((address_space(3))) _Float16 L16;  // an LDS fp16 (32-bit addresses)
 constexpr int kOOB = static_cast<int>(0xF0000000u);  // past every buffer range (< 3.75 GiB)
 
 constexpr int B2_ROWS = 32;            // rows per chunk: one 16x16x32 MFMA k-step
@@ -73,6 +83,7 @@ struct B2Args {
     const float *h;  // [*, ldh] rows < R'
     int64_t ldh;
     float yscale;
+    int e_dz;  // dz0's fp16 scale: |dh| 2^(eX + eW) <= 96 2^30, times yscale, shifted by 2^-e_dz
     const float *x;
     const float *const *x_dev;
     const int64_t *xrow;
@@ -94,15 +105,16 @@ __host__ __device__ inline int64_t b2_slab_floats(int K0, int F1) {
     return 512LL * K0 + 256 + 512LL * F1 + F1;
 }
 
-__device__ __forceinline__ void split2(float v, __bf16 &p1, __bf16 &p2) {
-    p1 = static_cast<__bf16>(v);
-    p2 = static_cast<__bf16>(v - static_cast<float>(p1));
+// two fp16 parts (round to nearest even) of a scaled value
+__device__ __forceinline__ void split2(float v, _Float16 &p1, _Float16 &p2) {
+    p1 = static_cast<_Float16>(v);
+    p2 = static_cast<_Float16>(v - static_cast<float>(p1));
 }
 
 __device__ __forceinline__ v4f mfma3(bf8 a1, bf8 a2, bf8 b1, bf8 b2, v4f acc) {  // smallest terms first
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b2, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b1, acc, 0, 0, 0);
 }
 
 // transposed read: the 16-lane group q takes the 4 x 16 block at rows
@@ -174,6 +186,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     // 0..47, W_l1 rows 48..95, zero past F1), column n0 + 16 nt + l16
     const int rt = wv >> 2, nt = wv & 3;
     bf8 wb[3][2];
+    int eW;  // the slice's scale
     {
         // (buffer loads over the F1 weight rows: all 24 in flight, no branches)
         const i32x4 wrr = make_rsrc(a.wr1, static_cast<uint32_t>(F1 * a.ldw1 * 4));
@@ -189,12 +202,20 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
                 const int o = f < F1 ? (f * static_cast<int>(a.ldw1) + n) * 4 : kOOB;
                 v[kc][j] = k < 48 ? buf_load1(wrr, o, 0, 0) : buf_load1(wlr, o, 0, 0);
             }
+        // the wave's scale: its slice is n-tile nt of [W_r1; W_l1] (the same
+        // for both row-tile waves of nt and for stage C0's wave of nt)
+        float mx = 0.0f;
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[kc][j]));
+        eW = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
         for (int kc = 0; kc < 3; ++kc)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                __bf16 p1, p2;
-                split2(v[kc][j], p1, p2);
+                _Float16 p1, p2;
+                split2(__builtin_amdgcn_ldexpf(v[kc][j], eW), p1, p2);
                 wb[kc][0][j] = p1;
                 wb[kc][1][j] = p2;
             }
@@ -272,26 +293,59 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             p.d1 = buf_load1i(rpr, okr ? 4 * r + 4 : kOOB, 0, 0);
         }
     };
-    // two bf16 parts of 8 floats -> part images at (row, col), 16 B each
-    auto put8 = [&](L16 *img, int part_stride, int off, v4f v0, v4f v1) __attribute__((always_inline)) {
+    // per-chunk scales: X = [dy | g], h, x, agg0 (powers of two, uniform)
+    struct Exps {
+        int X, H, x, a;
+    };
+    // the chunk's maxima over the values staging writes (loads past a range
+    // read 0; edgeless rows' aggregate counts as 0), wave-reduced, into LDS
+    // slot sl (8 waves x 4); every thread reads them back after a barrier
+    float4 *smax = reinterpret_cast<float4 *>(sred + 2 * 256 + 480);  // [2][8]
+    auto publish_max = [&](const auto &p, int sl) __attribute__((always_inline)) {
+        float mX = fmaxf(amax4(p.gv), fmaxf(fmaxf(fabsf(p.dyv[0]), fabsf(p.dyv[1])),
+                                          fmaxf(fabsf(p.dyv[2]), fabsf(p.dyv[3]))));
+        float mH = amax4(p.hv);
+        float mx = fmaxf(amax4(p.xv[0]), amax4(p.xv[1]));
+        float ma = p.d1 > p.d0 ? fmaxf(amax4(p.av[0]), amax4(p.av[1])) : 0.0f;
+        mX = wave_max(mX);
+        mH = wave_max(mH);
+        mx = wave_max(mx);
+        ma = wave_max(ma);
+        if (ln == 0) smax[sl * 8 + wv] = float4{mX, mH, mx, ma};
+    };
+    auto read_exps = [&](int sl) __attribute__((always_inline)) -> Exps {
+        float4 m = smax[sl * 8];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) {
+            const float4 o = smax[sl * 8 + w];
+            m.x = fmaxf(m.x, o.x);
+            m.y = fmaxf(m.y, o.y);
+            m.z = fmaxf(m.z, o.z);
+            m.w = fmaxf(m.w, o.w);
+        }
+        return Exps{__builtin_amdgcn_readfirstlane(h2_exp(m.x)), __builtin_amdgcn_readfirstlane(h2_exp(m.y)),
+                    __builtin_amdgcn_readfirstlane(h2_exp(m.z)), __builtin_amdgcn_readfirstlane(h2_exp(m.w))};
+    };
+    // two fp16 parts of 8 floats (scaled by 2^e) -> part images at (row, col), 16 B each
+    auto put8 = [&](L16 *img, int part_stride, int off, v4f v0, v4f v1, int e) __attribute__((always_inline)) {
         bf8 p1, p2;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            __bf16 a1, a2;
-            split2(i < 4 ? v0[i] : v1[i - 4], a1, a2);
+            _Float16 a1, a2;
+            split2(__builtin_amdgcn_ldexpf(i < 4 ? v0[i] : v1[i - 4], e), a1, a2);
             p1[i] = a1;
             p2[i] = a2;
         }
         *reinterpret_cast<__attribute__((address_space(3))) bf8 *>(img + off) = p1;
         *reinterpret_cast<__attribute__((address_space(3))) bf8 *>(img + part_stride + off) = p2;
     };
-    // two bf16 parts of 4 floats -> part images at (row, col), 8 B each
-    auto put4 = [&](L16 *img, int part_stride, int off, v4f v) __attribute__((always_inline)) {
+    // two fp16 parts of 4 floats (scaled by 2^e) -> part images at (row, col), 8 B each
+    auto put4 = [&](L16 *img, int part_stride, int off, v4f v, int e) __attribute__((always_inline)) {
         bf4 p1, p2;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            __bf16 a1, a2;
-            split2(v[i], a1, a2);
+            _Float16 a1, a2;
+            split2(__builtin_amdgcn_ldexpf(v[i], e), a1, a2);
             p1[i] = a1;
             p2[i] = a2;
         }
@@ -299,32 +353,32 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         *reinterpret_cast<__attribute__((address_space(3))) bf4 *>(img + part_stride + off) = p2;
     };
     float d1acc = 0.0f;  // db1 partial: column fd, rows of this thread
-    auto stage_images = [&](const Pre &p, L16 *buf) __attribute__((always_inline)) {
+    auto stage_images = [&](const Pre &p, L16 *buf, const Exps &e) __attribute__((always_inline)) {
         L16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
         if (t < 480) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int lr = rd + 10 * u;
                 if (lr < B2_ROWS) {
-                    __bf16 a1, a2;
-                    split2(p.dyv[u], a1, a2);
+                    _Float16 a1, a2;
+                    split2(__builtin_amdgcn_ldexpf(p.dyv[u], e.X), a1, a2);
                     ix[lr * XS + fd] = a1;
                     ix[B2_ROWS * XS + lr * XS + fd] = a2;
                     d1acc += p.dyv[u];
                 }
             }
         }
-        if (t < 384) put4(ix, B2_ROWS * XS, rg * XS + 48 + 4 * cg, p.gv);
-        put4(ih, B2_ROWS * HS, rh * HS + 4 * ch, p.hv);
-        put8(ik, B2_ROWS * KS, rx * KS + 8 * cx, p.xv[0], p.xv[1]);
+        if (t < 384) put4(ix, B2_ROWS * XS, rg * XS + 48 + 4 * cg, p.gv, e.X);
+        put4(ih, B2_ROWS * HS, rh * HS + 4 * ch, p.hv, e.H);
+        put8(ik, B2_ROWS * KS, rx * KS + 8 * cx, p.xv[0], p.xv[1], e.x);
         const bool deg = p.d1 > p.d0;
         const v4f z4{0.f, 0.f, 0.f, 0.f};
-        put8(ia, B2_ROWS * KS, rx * KS + 8 * cx, deg ? p.av[0] : z4, deg ? p.av[1] : z4);
+        put8(ia, B2_ROWS * KS, rx * KS + 8 * cx, deg ? p.av[0] : z4, deg ? p.av[1] : z4, e.a);
     };
 
     // ---- stage B: dh tile (rt, nt) -> masked dz0 parts into sA
     float d0acc = 0.0f;  // db0 partial: column 16 nt + l16, rows 16 rt + 4 q + i
-    auto stage_b = [&](L16 *buf) __attribute__((always_inline)) {
+    auto stage_b = [&](L16 *buf, const Exps &e) __attribute__((always_inline)) {
         const L16 *ix = buf, *ih = ix + IMG_X;
         L16 *sa = buf + IMG_X + IMG_H + 2 * IMG_K;
         v4f acc{0.f, 0.f, 0.f, 0.f};
@@ -335,19 +389,22 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             const bf8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(ix + B2_ROWS * XS + off);
             acc = mfma3(a1, a2, wb[kc][0], wb[kc][1], acc);
         }
-        // mask: the sign of h's first part (bf16 keeps sign and zero)
+        // mask: the sign of h's first part (a positive h below 2^-39 of its
+        // chunk's max rounds to +0 -- a pre-activation that far inside fp32's
+        // noise of the ReLU kink)
         const s4 hm = tr_read(ih, HS, 16 * rt, 16 * nt, ln);
         v4f dz;
+        const int eu = -(e.X + eW);  // acc -> dh
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             dz[i] = hm[i] > 0 ? acc[i] * a.yscale : 0.0f;
-            d0acc += dz[i];
+            d0acc += __builtin_amdgcn_ldexpf(dz[i], eu);
         }
         bf4 p1, p2;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            __bf16 a1, a2;
-            split2(dz[i], a1, a2);
+            _Float16 a1, a2;
+            split2(__builtin_amdgcn_ldexpf(dz[i], -a.e_dz), a1, a2);
             p1[i] = a1;
             p2[i] = a2;
         }
@@ -363,7 +420,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
     const int mat = wv >> 2;
-    auto stage_c = [&](const L16 *buf) __attribute__((always_inline)) {
+    auto stage_c = [&](const L16 *buf, const Exps &e) __attribute__((always_inline)) {
         const L16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
         const L16 *sa = ia + IMG_K;
         // C0: A = dz0^T of n-tile nt (both row tiles), B = x / agg0 tiles
@@ -388,10 +445,15 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             h1[u] = tr_frag(ih, HS, 16 * nn, ln);
             h2[u] = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
         }
+        // this chunk's products from zero, unscaled into the accumulators:
+        // dz0 carries 2^(eX + eW - e_dz), x / agg0 2^(ex | ea); X 2^eX, h 2^eH
+        const v4f z{0.f, 0.f, 0.f, 0.f};
+        const int e0 = a.e_dz - e.X - eW - (mat ? e.a : e.x);
+        const int e1 = -(e.X + e.H);
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) acc0[kt] = mfma3(a1, a2, b1[kt], b2[kt], acc0[kt]);
+        for (int kt = 0; kt < KT; ++kt) acc0[kt] += ldexp4(mfma3(a1, a2, b1[kt], b2[kt], z), e0);
 #pragma unroll
-        for (int u = 0; u < 3; ++u) acc1[u] = mfma3(x1[u], x2[u], h1[u], h2[u], acc1[u]);
+        for (int u = 0; u < 3; ++u) acc1[u] += ldexp4(mfma3(x1[u], x2[u], h1[u], h2[u], z), e1);
     };
 
     // ---- pipeline over the slice's chunks (two LDS buffers):
@@ -400,20 +462,30 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     //   barrier
     //   phase 2: stage B(c) on buffer c&1 -> its dz0 fragments
     //   barrier
+    //   (and, before the second barrier, chunk c + 1's maxima: its loads have
+    //   landed by then -- published to the next iteration's staging)
     Pre pre;
     pre.xi = XR ? iload(cb) : 0;
     if (XR) asm volatile("" : "+v"(pre.xi));  // (the first chunk's n_id: waited here once)
-    if (cb < ce) load(cb, pre);
+    Exps ep{0, 0, 0, 0};
+    if (cb < ce) {
+        load(cb, pre);
+        publish_max(pre, cb & 1);
+    }
+    lds_barrier();
     for (int c = cb; c < ce; ++c) {
         L16 *cur = lb + (c & 1) * BUF;
-        if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF);
-        stage_images(pre, cur);
+        if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF, ep);
+        const Exps ec = read_exps(c & 1);
+        stage_images(pre, cur, ec);
         load(c + 1, pre);
         lds_barrier();  // (LDS only: the next chunk's loads stay in flight)
-        stage_b(cur);
+        stage_b(cur, ec);
+        publish_max(pre, (c + 1) & 1);
         lds_barrier();
+        ep = ec;
     }
-    if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF);
+    if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF, ep);
 
     // ---- this workgroup's part of slab s (zeros for an empty slice)
     float *slab = a.slab + static_cast<int64_t>(s) * b2_slab_floats(K0, F1);
@@ -604,6 +676,13 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.h = h;
     b.ldh = ldh;
     b.yscale = yscale;
+    // |dh| in the scaled units <= 96 2^30 (two operands of max < 2^15, 96
+    // terms); dz0 = dh yscale must stay below fp16's 2^16 after 2^-e_dz
+    {
+        int e = 0;
+        (void)std::frexp(std::max(yscale, 1.0f), &e);  // yscale <= 2^e
+        b.e_dz = 21 + e;
+    }
     b.x = x;
     b.x_dev = x_dev;
     b.xrow = xrow;
@@ -620,7 +699,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.slab = slab;
     b.S = B2_S;
     b.step_inc = adam ? adam->step : nullptr;
-    const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4;
+    // (+ the chunk maxima: [2][8] float4)
+    const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4 + 2 * 8 * 16;
     auto go = [&](auto xr_c, auto kt_c) {
         auto fn = k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value>;
         static bool attr = false;

@@ -63,6 +63,48 @@ __device__ __forceinline__ v4f bf16x4_to_f32(i32x2 w) {
     return o;
 }
 
+// ---- H2 scaling (two-layer forward and backward): powers of two that put a
+// block's max |v| in [2^14, 2^15) before an fp16 split, and the cross-lane
+// maxima that find it
+// e with max|v| 2^e in [2^14, 2^15) (0 -> 15; inf / NaN rows stay inf / NaN)
+__device__ __forceinline__ int h2_exp(float amax) { return 15 - __builtin_amdgcn_frexp_expf(amax); }
+
+__device__ __forceinline__ v4f ldexp4(v4f v, int e) {
+    v4f o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_ldexpf(v[i], e);
+    return o;
+}
+
+__device__ __forceinline__ float amax4(v4f v) {
+    return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+
+// cross-lane max of non-negative floats (their bit patterns order as ints),
+// on VALU only (no LDS round trip): DPP inside a 16-lane row, the gfx950
+// permlane swaps across rows
+__device__ __forceinline__ float max_xor16(float v) {  // lanes l and l ^ 16
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
+}
+__device__ __forceinline__ float max_xor32(float v) {  // lanes l and l ^ 32
+    const int x = __float_as_int(v);
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
+}
+__device__ __forceinline__ float max_row16(float v) {  // all 16 lanes of the row
+    int x = __float_as_int(v);
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));  // row_mirror
+    return __int_as_float(x);
+}
+
+// max of a non-negative float over the wave
+__device__ __forceinline__ float wave_max(float v) { return max_xor32(max_xor16(max_row16(v))); }
+
 // The training step's seed-row cross entropy computed by the narrow output
 // launch (include/ngnn.h ngnn_xent_head; ngnn_sage_rt.hip k_narrow_agg)
 struct NarrowHead {

@@ -57,9 +57,6 @@ constexpr int F2_HID = 256;    // hidden width of the fused shape
 constexpr int F2_ROWS = 16;    // rows per tile (one MFMA n-block)
 constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
 
-// e with max|v| 2^e in [2^14, 2^15) (0 -> 15; inf / NaN rows stay inf / NaN)
-__device__ __forceinline__ int h2_exp(float amax) { return 15 - __builtin_amdgcn_frexp_expf(amax); }
-
 // two fp16 parts (round to nearest even) of 8 scaled values
 __device__ __forceinline__ void h2_split(v4f a, v4f b, half8 &p1, half8 &p2) {
 #pragma unroll
@@ -69,39 +66,6 @@ __device__ __forceinline__ void h2_split(v4f a, v4f b, half8 &p1, half8 &p2) {
         p1[j] = h;
         p2[j] = static_cast<_Float16>(v - static_cast<float>(h));
     }
-}
-
-__device__ __forceinline__ v4f ldexp4(v4f v, int e) {
-    v4f o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_ldexpf(v[i], e);
-    return o;
-}
-
-__device__ __forceinline__ float amax4(v4f v) {
-    return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-}
-
-// cross-lane max of non-negative floats (their bit patterns order as ints),
-// on VALU only (no LDS round trip): DPP inside a 16-lane row, the gfx950
-// permlane swaps across rows
-__device__ __forceinline__ float max_xor16(float v) {  // lanes l and l ^ 16
-    const int x = __float_as_int(v);
-    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
-}
-__device__ __forceinline__ float max_xor32(float v) {  // lanes l and l ^ 32
-    const int x = __float_as_int(v);
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return __int_as_float(max(static_cast<int>(r[0]), static_cast<int>(r[1])));
-}
-__device__ __forceinline__ float max_row16(float v) {  // all 16 lanes of the row
-    int x = __float_as_int(v);
-    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));  // row_half_mirror
-    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));  // row_mirror
-    return __int_as_float(x);
 }
 
 // three-product H2 MFMA: acc += (a1 + a2)(b1 + b2) - a2 b2, smallest first
@@ -126,12 +90,6 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // two fp16 parts.  Per-wave scales are exact to undo: every product is
 // unscaled per wave before any cross-wave sum -- so there is no weight-prep
 // launch and no cross-workgroup hand-off (a round-3 design had both).
-__device__ __forceinline__ v4f wload4(const float *row, int k, int kmax, bool ok) {
-    return (ok && k < kmax) ? *reinterpret_cast<const v4f *>(row + k) : v4f{0.f, 0.f, 0.f, 0.f};
-}
-
-// max of a non-negative float over the wave
-__device__ __forceinline__ float wave_max(float v) { return max_xor32(max_xor16(max_row16(v))); }
 
 // layer 0's slice of wave wv: rows 32 wv + 16 mt + m of w ([256, K0], row
 // stride ldw), k = 32 c + 8 q .. + 7; returns the wave's exponent

@@ -54,6 +54,10 @@ def _pad16(n: int) -> int:
 # debug hook (None in normal use): a list receives (layer, d output, saved
 # aggregate) from every fused-stack backward
 _debug_grads = None
+# test hook: when a list, every stack forward appends fp32 clones of its hidden
+# activations (inside a capture the clones replay with the step) -- the oracle
+# tests take the GPU's ReLU decision where a pre-activation sits at the kink
+_debug_acts = None
 
 
 def dropout_scale(p: float) -> float:
@@ -692,6 +696,8 @@ class _SAGEStack(torch.autograd.Function):
                                              and wr is not None), **xrow)
             acts.append(h)
             aggs.append(agg)
+        if _debug_acts is not None:
+            _debug_acts.append([a.detach().float().clone() for a in acts[1:-1]])
         ctx.block, ctx.reduce, ctx.p_drop, ctx.L = block, reduce, p_drop, len(params) // 3
         ctx.gouts = gouts  # _GradViews (buffers the weight gradients go into) or None
         ctx.save_for_backward(*acts, *aggs, *params)

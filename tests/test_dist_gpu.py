@@ -91,3 +91,115 @@ def test_graph_step_data_parallel_two_ranks():
         assert same, f"rank {rank}: parameters differ across ranks"
         # graph vs eager: same batches and rule; float-atomic input gradients -> tolerance
         assert diff < 1e-4, diff
+
+
+def _worker_headline(rank, world, port, q):
+    """the config #4 path -- SAGE(100, 256, 47) (k_fwd2 +
+    loss head + k_bwd2 writing the bucket views), products-shaped graph,
+    [15, 10] bs 1024 -- through GraphedTrainStep with the split reduce (pack
+    in the first graph, one all-reduce, unpack + Adam in the second)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    try:
+        import torch.nn.functional as F
+
+        import ngnn
+        from ngnn import fused
+        from ngnn.distributed import GradAllReduce, init
+        from ngnn.graphs import GraphedTrainStep, slot_size
+        from ngnn.loader import NeighborLoader, synthetic_graph
+        from ngnn.optim import Adam
+        from test_gpu_configs import _gpu_hidden, _hooked_capture, _slot_masks
+        from test_gpu_fused import _MaskedSAGE
+        init(backend="gloo")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        graph = synthetic_graph("ogbn-products", dev, seed=0, scale=0.01)
+        loader = NeighborLoader(graph, graph.train_idx, [15, 10], 1024, shuffle=True, seed=3,
+                                rank=rank, world_size=world)
+        it = iter(loader)
+        warm, b = next(it), next(it)
+        torch.manual_seed(1234)
+        model = ngnn.SAGE(100, 256, 47, 2, dropout=0.5).to(dev).train()
+        init_sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        opt = Adam(model.parameters(), lr=1e-3)
+        red = GradAllReduce(model.parameters())
+        n_cap, e_cap = slot_size(1024, [15, 10])
+        step = GraphedTrainStep(model, opt, 1024, n_cap, e_cap, 100, dev, reducer=red)
+        calls = []
+        orig = fused.sage2_backward
+
+        def spy(*a, **k):
+            calls.append(1)
+            return orig(*a, **k)
+
+        fused.sage2_backward = spy
+        try:
+            _hooked_capture(step, warm.x, warm.edge_index, warm.y)
+        finally:
+            fused.sage2_backward = orig
+        assert calls, "the captured backward did not take ngnn_sage2_bwd"
+        assert step._split_reduce and not step.folded
+        step(b.x, b.edge_index, b.y, b.batch_size)
+        torch.cuda.synchronize()
+        params = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+        grads = {k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()}
+        # this rank's own gradient, by the oracle on its block with the replay's masks
+        seed_state = int(step.seed_state.item()) & (2**64 - 1)
+        N = b.num_nodes
+        hid, rn = _gpu_hidden(step)
+        ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 256, 0.5, 2),
+                          gpu_hidden=hid, kink_rows=rn)
+        ref.load_state_dict(init_sd)
+        out_r = ref(b.x.cpu(), b.edge_index.cpu())
+        F.cross_entropy(out_r[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
+        mine_local = torch.cat([q.grad.reshape(-1) for q in ref.parameters()])
+        gathered = [torch.empty_like(mine_local) for _ in range(world)]
+        dist.all_gather(gathered, mine_local)
+        avg = torch.stack(gathered).mean(0)
+        pg = [torch.empty_like(params) for _ in range(world)]
+        dist.all_gather(pg, params)
+        same_ranks = all(torch.equal(pg[0], t) for t in pg)
+        # the single-process step on the rank-averaged oracle gradients
+        off, worst, upd = 0, 0.0, 0.0
+        for (k, q) in ref.named_parameters():
+            n = q.numel()
+            want = avg[off:off + n].view(q.shape)
+            err = float((grads[k] - want).abs().max()) / max(float(want.abs().max()), 1e-30)
+            worst = max(worst, err)
+            q.grad = want.clone()
+            off += n
+        o_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
+        o_ref.step()
+        named = dict(model.named_parameters())
+        for k, q in ref.named_parameters():
+            p = named[k].detach().cpu()
+            sure = q.grad.abs() > 1e-2 * q.grad.abs().max()
+            upd = max(upd, float((p[sure] - q.detach()[sure]).abs().max()))
+        q.put((rank, same_ranks, worst, upd, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, False, float("inf"), float("inf"), traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_headline_model_data_parallel_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_headline, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=280) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, same, worst, upd, err in out:
+        assert err is None, err
+        assert same, f"rank {rank}: parameters differ across ranks"
+        # the all-reduced .grad = the mean of the ranks' oracle gradients
+        assert worst <= 1e-5, worst
+        # and the parameters = torch's Adam step on that mean (step 1: |dp| ~ lr)
+        assert upd <= 2e-6, upd

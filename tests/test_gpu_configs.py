@@ -22,7 +22,8 @@ counts), and checks it against the CPU oracle (oracle/pyg_ref.py: the PyG
 * config #1's widths, a CitationFull-Cora SAGE(8710,512,70) [10,5] bs 512.
 
 Tolerances as tests/test_gpu_fused.py: outputs 1e-5, input gradients
-rtol 1e-4 / atol 1e-5, weight gradients 1e-4; bf16 2e-2.
+rtol 1e-4 / atol 1e-5, weight gradients max|g - g_ref| <= 1e-5 max|g_ref|
+(tests/gradbar.py); bf16 2e-2.
 """
 import pytest
 import torch
@@ -31,7 +32,8 @@ import torch.nn.functional as F
 import ngnn
 from oracle import pyg_ref
 
-from test_gpu_fused import GRAD, OUT, WGRAD, _MaskedSAGE, dropout_keep, dropout_scale
+from test_gpu_fused import GRAD, OUT, _MaskedSAGE, dropout_keep, dropout_scale
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -40,6 +42,24 @@ DEV = torch.device("cuda:0")
 def _graph(name, seed=0, **kw):
     from ngnn.loader import synthetic_graph
     return synthetic_graph(name, DEV, seed=seed, **kw)
+
+
+def _hooked_capture(step, x, ei, y):
+    """step.capture with fused._debug_acts on: the captured forward's hidden
+    activations (rewritten by every replay) kept as step._test_acts."""
+    from ngnn import fused
+    fused._debug_acts = []
+    try:
+        step.capture(x, ei, y)
+        step._test_acts = fused._debug_acts[-1]
+    finally:
+        fused._debug_acts = None
+
+
+def _gpu_hidden(step):
+    """(the last replay's hidden activations on the host, the rows it wrote:
+    the slot's R')."""
+    return [a.cpu() for a in step._test_acts], int(step.r_next.item()) & 0xFFFFFFFF
 
 
 def _eager_vs_oracle(b, mine, hidden, train, aggr, seed=99, out_tol=OUT, check_dx=False):
@@ -70,7 +90,7 @@ def _eager_vs_oracle(b, mine, hidden, train, aggr, seed=99, out_tol=OUT, check_d
     if check_dx:
         torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
-        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+        assert_wgrad(p.grad.cpu(), q.grad, msg=k)
 
 
 @pytest.mark.timeout(300)
@@ -92,7 +112,7 @@ def test_headline_graph_step_full_products_block():
     opt = Adam(mine.parameters(), lr=1e-3)
     n_cap, e_cap = slot_size(1024, [15, 10])
     step = GraphedTrainStep(mine, opt, 1024, n_cap, e_cap, 100, DEV)
-    step.capture(b2.x, b2.edge_index, b2.y)  # warm-up on another block; state restored
+    _hooked_capture(step, b2.x, b2.edge_index, b2.y)  # warm-up on another block; state restored
     loss = step(b.x, b.edge_index, b.y)
     torch.cuda.synchronize()
     assert step.zero_copy
@@ -100,7 +120,8 @@ def test_headline_graph_step_full_products_block():
     grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
     seed_state = int(step.seed_state.item()) & (2**64 - 1)
     masks = [dropout_keep((7919 * i) ^ seed_state, N, 256, 0.5).float() for i in range(1)]
-    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5, masks=masks)
+    hid, rn = _gpu_hidden(step)
+    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5, masks=masks, gpu_hidden=hid, kink_rows=rn)
     ref.load_state_dict(init)
     out_r = ref(b.x.cpu(), b.edge_index.cpu())
     loss_r = F.cross_entropy(out_r[:1024], b.y[:1024].cpu())
@@ -108,7 +129,7 @@ def test_headline_graph_step_full_products_block():
     torch.testing.assert_close(out, out_r.detach(), **OUT)
     assert abs(float(loss) - float(loss_r)) < 1e-5
     for k, q in ref.named_parameters():
-        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+        assert_wgrad(grads[k], q.grad, msg=k)
     # post-step parameters: torch's Adam on the oracle's gradients.  At step 1
     # the update is lr * g / (|g| + eps): compare where |g| is well away from 0
     # (elsewhere a 1e-7 gradient difference may flip the sign of a 1e-3 step)
@@ -119,6 +140,9 @@ def test_headline_graph_step_full_products_block():
         sure = q.grad.abs() > 1e-4
         torch.testing.assert_close(p[sure], q.detach()[sure], rtol=0, atol=2e-6, msg=k)
         assert (p - init[k]).abs().max() <= 1e-3 + 1e-6, k
+    _check_step1_state(step, mine, ref)
+    b3 = sample_block(g, g.train_idx[2048:3072], [15, 10], seed=9)
+    _check_second_step(step, mine, b3, 100, 256, 47, 2, 1024)
 
 
 @pytest.mark.timeout(300)
@@ -141,14 +165,15 @@ def test_headline_graph_step_fused_row_gather_vs_oracle():
     opt = Adam(mine.parameters(), lr=1e-3)
     n_cap, e_cap = slot_size(1024, [15, 10])
     step = GraphedTrainStep(mine, opt, 1024, n_cap, e_cap, 100, DEV)
-    step.capture(IndexedRows(g.x, b2.n_id), b2.edge_index, b2.y)
+    _hooked_capture(step, IndexedRows(g.x, b2.n_id), b2.edge_index, b2.y)
     assert step.zero_copy and step.x_rows == g.num_nodes
     loss = step(IndexedRows(g.x, b.n_id), b.edge_index, b.y)
     torch.cuda.synchronize()
     out = step.out[:N].cpu()
     grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
     seed_state = int(step.seed_state.item()) & (2**64 - 1)
-    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5,
+    hid, rn = _gpu_hidden(step)
+    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5, gpu_hidden=hid, kink_rows=rn,
                       masks=[dropout_keep(seed_state, N, 256, 0.5).float()])
     ref.load_state_dict(init)
     xm = g.x[b.n_id].cpu()  # the materialized rows
@@ -159,13 +184,14 @@ def test_headline_graph_step_fused_row_gather_vs_oracle():
     torch.testing.assert_close(out, out_r.detach(), **OUT)
     assert abs(float(loss) - float(loss_r)) < 1e-5
     for k, q in ref.named_parameters():
-        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+        assert_wgrad(grads[k], q.grad, msg=k)
     o_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
     o_ref.step()
     for k, q in ref.named_parameters():
         p = dict(mine.named_parameters())[k].detach().cpu()
         sure = q.grad.abs() > 1e-4
         torch.testing.assert_close(p[sure], q.detach()[sure], rtol=0, atol=2e-6, msg=k)
+    _check_step1_state(step, mine, ref)
 
 
 def _graph_step(model, b, warm, fanout, bs, in_dim, lr=1e-3):
@@ -178,7 +204,7 @@ def _graph_step(model, b, warm, fanout, bs, in_dim, lr=1e-3):
     opt = Adam(model.parameters(), lr=lr)
     n_cap, e_cap = slot_size(bs, fanout)
     step = GraphedTrainStep(model, opt, bs, n_cap, e_cap, in_dim, DEV)
-    step.capture(warm.x, warm.edge_index, warm.y)
+    _hooked_capture(step, warm.x, warm.edge_index, warm.y)
     loss = step(b.x, b.edge_index, b.y)
     torch.cuda.synchronize()
     return step, loss, int(step.seed_state.item()) & (2**64 - 1)
@@ -188,6 +214,60 @@ def _slot_masks(seed_state, N, hidden, p, L):
     """The dropout keep masks of a graph replay (layer i keyed by the slot
     seed: (7919 i) ^ seed_state)."""
     return [dropout_keep((7919 * i) ^ seed_state, N, hidden, p).float() for i in range(L - 1)]
+
+
+def _check_second_step(step, mine, b2, in_dim, hidden, C, L, bs, lr=1e-3, aggr="mean"):
+    """Adam step 2, where the update depends on |g| (at step
+    1 it is ~lr * sign(g)).  The step-1 Adam state the GPU kept (exp_avg =
+    0.1 g1, exp_avg_sq = 0.001 g1^2) is checked against the oracle's step-1
+    gradients (caller: q.grad) by the gradient bar; then a second replay on
+    block b2, and the oracle -- started from the GPU's step-1 parameters and
+    Adam state, so both sides see identical inputs -- takes the same step:
+    its gradients at the bar, the loss at 1e-5, the parameters after torch's
+    Adam step 2 at 2e-6 where |g1|, |g2| >= 1e-2 of their tensor's max."""
+    named = dict(mine.named_parameters())
+    p1 = {k: p.detach().cpu().clone() for k, p in named.items()}
+    st1 = {k: (step.opt.state[p]["exp_avg"].detach().cpu().clone(),
+               step.opt.state[p]["exp_avg_sq"].detach().cpu().clone()) for k, p in named.items()}
+    loss2 = step(b2.x, b2.edge_index, b2.y)
+    torch.cuda.synchronize()
+    seed2 = int(step.seed_state.item()) & (2**64 - 1)
+    grads2 = {k: p.grad.detach().cpu().clone() for k, p in named.items()}
+    N2 = b2.num_nodes
+    hid, rn = _gpu_hidden(step)
+    ref2 = _MaskedSAGE(in_dim, hidden, C, L, dropout=0.5, aggr=aggr,
+                       masks=_slot_masks(seed2, N2, hidden, 0.5, L), gpu_hidden=hid, kink_rows=rn)
+    ref2.load_state_dict(p1)
+    out2 = ref2(b2.x.cpu(), b2.edge_index.cpu())
+    loss_r2 = F.cross_entropy(out2[:bs], b2.y[:bs].cpu())
+    loss_r2.backward()
+    assert abs(float(loss2) - float(loss_r2)) < 1e-5
+    for k, q in ref2.named_parameters():
+        assert_wgrad(grads2[k], q.grad, msg=f"step2:{k}")
+    o2 = torch.optim.Adam(ref2.parameters(), lr=lr)
+    for k, q in ref2.named_parameters():
+        o2.state[q] = dict(step=torch.tensor(1.0), exp_avg=st1[k][0].clone(), exp_avg_sq=st1[k][1].clone())
+    o2.step()
+    for k, q in ref2.named_parameters():
+        p = named[k].detach().cpu()
+        g1 = st1[k][0] / 0.1
+        sure = (g1.abs() >= 1e-2 * g1.abs().max()) & (q.grad.abs() >= 1e-2 * q.grad.abs().max())
+        assert int(sure.sum()) > 0, k
+        torch.testing.assert_close(p[sure], q.detach()[sure], rtol=0, atol=2e-6, msg=f"step2:{k}")
+
+
+def _check_step1_state(step, mine, ref):
+    """The step-1 Adam moments the GPU kept are (1 - beta1) g and (1 - beta2)
+    g^2 of ITS gradients (the factors as fp32 computes them: 1 - 0.999f is
+    0.0010000467): against the oracle's gradients at the bar."""
+    one = torch.tensor(1.0, dtype=torch.float32)
+    c1 = float(one - torch.tensor(0.9, dtype=torch.float32))
+    c2 = float(one - torch.tensor(0.999, dtype=torch.float32))
+    for k, q in ref.named_parameters():
+        p = dict(mine.named_parameters())[k]
+        assert_wgrad(step.opt.state[p]["exp_avg"].cpu().double() / c1, q.grad, msg=f"exp_avg:{k}")
+        v = step.opt.state[p]["exp_avg_sq"].cpu().double() / c2
+        assert_wgrad(v.sqrt(), q.grad.double().abs(), msg=f"exp_avg_sq:{k}")
 
 
 def _check_adam_step(mine, ref, init, lr=1e-3, bf16=False):
@@ -229,7 +309,9 @@ def test_config_arxiv_graph_step():
     N = b.num_nodes
     out = step.out[:N].cpu()
     grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
-    ref = _MaskedSAGE(128, 256, 40, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 256, 0.5, 2))
+    hid, rn = _gpu_hidden(step)
+    ref = _MaskedSAGE(128, 256, 40, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 256, 0.5, 2),
+                      gpu_hidden=hid, kink_rows=rn)
     ref.load_state_dict(init)
     out_r = ref(b.x.cpu(), b.edge_index.cpu())
     loss_r = F.cross_entropy(out_r[:1024], b.y[:1024].cpu())
@@ -237,8 +319,11 @@ def test_config_arxiv_graph_step():
     torch.testing.assert_close(out, out_r.detach(), **OUT)
     assert abs(float(loss) - float(loss_r)) < 1e-5
     for k, q in ref.named_parameters():
-        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+        assert_wgrad(grads[k], q.grad, msg=k)
     _check_adam_step(mine, ref, init)
+    _check_step1_state(step, mine, ref)
+    _check_second_step(step, mine, sample_block(g, g.train_idx[2048:3072], [15, 10], seed=5),
+                       128, 256, 40, 2, 1024)
 
 
 @pytest.mark.timeout(300)
@@ -294,12 +379,12 @@ def test_config_computers_max_graph_step():
     assert not h1.grad[rn:].any()
     torch.testing.assert_close(dbg[0][0][:rn], h1.grad[:rn], **GRAD)
     for n, q in ref.convs[1].named_parameters():
-        torch.testing.assert_close(grads[f"convs.1.{n}"], q.grad, **WGRAD, msg=n)
+        assert_wgrad(grads[f"convs.1.{n}"], q.grad, msg=n)
     # layer 0 (relu + dropout) under the GPU's output gradient
     h0 = ref.convs[0](x, ei).relu() * mask * dropout_scale(0.5)
     h0.backward(torch.cat([dbg[0][0][:rn], torch.zeros(N - rn, 512)]))
     for n, q in ref.convs[0].named_parameters():
-        torch.testing.assert_close(grads[f"convs.0.{n}"], q.grad, **WGRAD, msg=n)
+        assert_wgrad(grads[f"convs.0.{n}"], q.grad, msg=n)
     _check_adam_step(mine, ref, init)
 
 
@@ -320,7 +405,9 @@ def test_config_cora_width_graph_step():
     N = b.num_nodes
     out = step.out[:N].cpu()
     grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
-    ref = _MaskedSAGE(8710, 512, 70, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 512, 0.5, 2))
+    hid, rn = _gpu_hidden(step)
+    ref = _MaskedSAGE(8710, 512, 70, 2, dropout=0.5, masks=_slot_masks(seed_state, N, 512, 0.5, 2),
+                      gpu_hidden=hid, kink_rows=rn)
     ref.load_state_dict(init)
     out_r = ref(b.x.cpu(), b.edge_index.cpu())
     loss_r = F.cross_entropy(out_r[:512], b.y[:512].cpu())
@@ -328,8 +415,11 @@ def test_config_cora_width_graph_step():
     torch.testing.assert_close(out, out_r.detach(), **OUT)
     assert abs(float(loss) - float(loss_r)) < 1e-5
     for k, q in ref.named_parameters():
-        torch.testing.assert_close(grads[k], q.grad, **WGRAD, msg=k)
+        assert_wgrad(grads[k], q.grad, msg=k)
     _check_adam_step(mine, ref, init)
+    _check_step1_state(step, mine, ref)
+    _check_second_step(step, mine, sample_block(g, g.train_idx[:512], [10, 5], seed=11),
+                       8710, 512, 70, 2, 512)
 
 
 def _receptive_rows(ei, rows, hops):

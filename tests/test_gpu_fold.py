@@ -18,7 +18,7 @@ import torch
 import ngnn
 from ngnn import fused
 
-from test_gpu_fused import WGRAD
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -70,8 +70,8 @@ def test_adam_fold_matches_the_optimizer_launch():
     for x, y in zip(a["losses"], b["losses"]):
         assert abs(x - y) <= 1e-5 * max(1.0, abs(y))
     for k in b["params"]:
-        torch.testing.assert_close(a["grads"][k], b["grads"][k], **WGRAD, msg=k)
-        torch.testing.assert_close(a["m"][k], b["m"][k], **WGRAD, msg=k)
+        assert_wgrad(a["grads"][k], b["grads"][k], msg=k)
+        assert_wgrad(a["m"][k], b["m"][k], msg=k)
         torch.testing.assert_close(a["v"][k], b["v"][k], rtol=1e-3, atol=1e-12, msg=k)
         # the update is lr m / (sqrt(v) + eps): compared where |m| is away from 0
         sure = b["m"][k].abs() > 1e-5

@@ -2,7 +2,7 @@
 
 Tolerances (fp32): outputs rtol = atol = 1e-5 (north star); gradients, one
 more GEMM deep, rtol = 1e-4 / atol = 1e-5; weight gradients (sums over up to
-~1e4 rows) atol = 1e-4.  Dropout in the fused path uses a counter-based hash
+~1e4 rows) max|g - g_ref| <= 1e-5 max|g_ref| per tensor (tests/gradbar.py).  Dropout in the fused path uses a counter-based hash
 RNG; ``dropout_keep`` below replicates it on the host so train-mode results are
 checked element for element against the oracle with the same mask.
 """
@@ -15,12 +15,12 @@ import ngnn
 from ngnn.block import Block
 from ngnn.fused import sage_layer_fwd
 from oracle import c_agg, pyg_ref
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 OUT = dict(rtol=1e-5, atol=1e-5)
 GRAD = dict(rtol=1e-4, atol=1e-5)
-WGRAD = dict(rtol=1e-4, atol=1e-4)
 
 M32 = np.uint64(0xFFFFFFFF)
 
@@ -223,19 +223,48 @@ def test_wide_layer_matches_oracle(K, Fo, reduce):
     torch.testing.assert_close(got2[:900], want2, **OUT)
 
 
-class _MaskedSAGE(pyg_ref.SAGE):
-    """Oracle SAGE whose dropout uses given keep masks (one per hidden layer)."""
+KINK_TOL = 1e-5
 
-    def __init__(self, *a, masks=None, **k):
+
+class _MaskedSAGE(pyg_ref.SAGE):
+    """Oracle SAGE whose dropout uses given keep masks (one per hidden layer;
+    None: no dropout).
+
+    gpu_hidden (optional, one [N, H] tensor per hidden layer: the GPU's own
+    post-ReLU/dropout activations, fused._debug_acts): ReLU's kink.  Where a
+    pre-activation lies within KINK_TOL of its row's largest magnitude, fp32
+    summation order alone (GPU vs CPU) decides its sign, and with it whether
+    the whole gradient of that element passes -- one flipped element moved a
+    hidden unit's weight-gradient row by ~5e-3 of its max (round 5).  There
+    the oracle takes the GPU's decision (h > 0), everywhere else its own:
+    backward pinned on identical ReLU masks, as the max tests pin ties.
+    kink_rows: only rows below it (the rows the GPU wrote: its R')."""
+
+    def __init__(self, *a, masks=None, gpu_hidden=None, kink_rows=None, **k):
         super().__init__(*a, **k)
         self.masks = masks
+        self.gpu_hidden = gpu_hidden
+        self.kink_rows = kink_rows
+        self.kinks = []  # ambiguous elements overridden, per hidden layer
 
     def forward(self, x, edge_index):
+        self.kinks = []
         for i, conv in enumerate(self.convs):
             x = conv(x, edge_index)
             if i != self.num_layers - 1:
-                x = x.relu()
-                x = x * self.masks[i] * dropout_scale(self.dropout)
+                gh = None if self.gpu_hidden is None else self.gpu_hidden[i]
+                if gh is None:
+                    x = x.relu()
+                else:
+                    pre = x.detach()
+                    amb = pre.abs() <= KINK_TOL * pre.abs().amax(1, keepdim=True)
+                    if self.kink_rows is not None:
+                        amb[self.kink_rows:] = False
+                    gate = torch.where(amb, gh[:pre.size(0)].cpu() > 0, pre > 0)
+                    self.kinks.append(int((amb & (gate != (pre > 0))).sum()))
+                    x = x * gate
+                if self.masks is not None:
+                    x = x * self.masks[i] * dropout_scale(self.dropout)
         return x
 
 
@@ -277,7 +306,7 @@ def test_stack_fwd_bwd_matches_oracle(layers, aggr, train):
     torch.testing.assert_close(out.detach().cpu(), out_r.detach(), **OUT)
     torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
-        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+        assert_wgrad(p.grad.cpu(), q.grad, msg=k)
 
 
 @pytest.mark.parametrize("aggr", ["mean", "max"])
@@ -310,7 +339,7 @@ def test_stack_deterministic_mode(aggr):
     F.cross_entropy(ref(xr, b.edge_index.cpu())[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
     torch.testing.assert_close(runs[0][0].cpu(), xr.grad, **GRAD)
     for g, (k, q) in zip(runs[0][1:], ref.named_parameters()):
-        torch.testing.assert_close(g.cpu(), q.grad, **WGRAD, msg=k)
+        assert_wgrad(g.cpu(), q.grad, msg=k)
 
 
 def test_stack_full_output_gradient():
@@ -329,7 +358,7 @@ def test_stack_full_output_gradient():
     (ref(xr, ei) * G).sum().backward()
     torch.testing.assert_close(xd.grad.cpu(), xr.grad, **GRAD)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
-        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+        assert_wgrad(p.grad.cpu(), q.grad, msg=k)
 
 
 def test_zero_gradient_and_no_grad_paths():
@@ -489,7 +518,7 @@ def test_gcn_stack_fwd_bwd_matches_oracle(dims, layers, train):
                                atol=OUT["atol"] * scale)
     torch.testing.assert_close(x.grad.cpu(), xr.grad, **GRAD)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
-        torch.testing.assert_close(p.grad.cpu(), q.grad, **WGRAD, msg=k)
+        assert_wgrad(p.grad.cpu(), q.grad, msg=k)
 
 
 @pytest.mark.parametrize("hidden", [64, 160])

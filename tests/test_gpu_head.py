@@ -14,7 +14,8 @@ scatter onto the source rows (the first step of the backward).
   loss, logits, every gradient and the post-step parameters; a non-unit
   loss gradient (eager, on the slot's block) falls back to the scaled rows.
 Bars: the loss and dy at 1e-6 relative (the head reduces in another order
-than torch's log_softmax), g at WGRAD, gradients at WGRAD.
+than torch's log_softmax), g and gradients at
+tests/gradbar.py's bar (1e-5 of each tensor's max).
 """
 import pytest
 import torch
@@ -24,7 +25,7 @@ import ngnn
 from ngnn import fused, losses
 from ngnn.block import Block
 
-from test_gpu_fused import WGRAD
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -99,7 +100,7 @@ def test_head_matches_torch(reduce, K0, F1, B):
     assert float(res.count) == float((y != -100).sum())
     torch.testing.assert_close(lh.dy[:B].double(), dy_r, rtol=1e-5, atol=1e-7)
     assert int(lh.dy[B:].count_nonzero()) == 0
-    torch.testing.assert_close(lh.g[:Rn, :F1].double(), g_r, **WGRAD)
+    assert_wgrad(lh.g[:Rn, :F1].double(), g_r)
     assert int(lh.g[:Rn, F1:].count_nonzero()) == 0
     assert bool((lh.g[Rn:] == 7.0).all())  # rows past R' untouched
     # the hand-off ticket is zero again: a second call repeats the loss bitwise
@@ -177,8 +178,8 @@ def test_graph_step_takes_the_head_and_matches():
     assert abs(with_head["loss"] - without["loss"]) <= 1e-6 * max(1.0, abs(without["loss"]))
     torch.testing.assert_close(with_head["out"], without["out"], rtol=0, atol=0)
     for k in without["grads"]:
-        torch.testing.assert_close(with_head["grads"][k], without["grads"][k], **WGRAD, msg=k)
-        torch.testing.assert_close(with_head["grads3"][k], without["grads3"][k], **WGRAD, msg=k)
+        assert_wgrad(with_head["grads"][k], without["grads"][k], msg=k)
+        assert_wgrad(with_head["grads3"][k], without["grads3"][k], msg=k)
         # post-step parameters: at step 1 Adam's update is lr g / (|g| + eps),
         # compared where |g| is well away from 0 (as the headline test)
         sure = without["grads"][k].abs() > 1e-4

@@ -16,6 +16,7 @@ from ngnn.block import Block, build_csr
 from oracle import c_agg, pyg_ref
 
 from test_oracle import MODEL_CASES, _load, load_params
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -182,8 +183,7 @@ def test_models_match_reference_golden(golden_dir, name):
     torch.testing.assert_close(out.detach().cpu(), torch.from_numpy(rec["out"]), **OUT_TOL)
     torch.testing.assert_close(x.grad.cpu(), torch.from_numpy(rec["grad_x"]), **GRAD_TOL)
     for k, p in m.named_parameters():
-        torch.testing.assert_close(p.grad.cpu(), torch.from_numpy(rec["grad/" + k]),
-                                   rtol=1e-4, atol=1e-4, msg=f"{name}:{k}")
+        assert_wgrad(p.grad.cpu(), torch.from_numpy(rec["grad/" + k]), msg=f"{name}:{k}")
 
 
 def test_inference_matches_reference_golden(golden_dir):

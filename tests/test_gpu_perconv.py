@@ -15,7 +15,8 @@ import torch.nn.functional as F
 import ngnn
 from oracle import pyg_ref
 
-from test_gpu_fused import GRAD, OUT, WGRAD
+from test_gpu_fused import GRAD, OUT
+from gradbar import assert_wgrad
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -95,7 +96,7 @@ def _tie_sync(mine, ref):
     return seen, hooks, [c.register_forward_hook(sync) for c in ref.convs]
 
 
-def _compare(mine, ref, b, dtype=torch.float32, tol_out=OUT, tol_g=GRAD, tol_w=WGRAD):
+def _compare(mine, ref, b, dtype=torch.float32, tol_out=OUT, tol_g=GRAD, tol_w=None):
     x = b.x.to(dtype).clone().requires_grad_(True)
     patches = _no_gemm()
     _, mh, rh = _tie_sync(mine, ref)
@@ -121,6 +122,9 @@ def _compare(mine, ref, b, dtype=torch.float32, tol_out=OUT, tol_g=GRAD, tol_w=W
     torch.testing.assert_close(out.detach().float().cpu(), out_r.detach(), **tol_out)
     torch.testing.assert_close(x.grad.float().cpu(), xr.grad, **tol_g)
     for (k, p), (_, q) in zip(mine.named_parameters(), ref.named_parameters()):
+        if tol_w is None:
+            assert_wgrad(p.grad.float().cpu(), q.grad, msg=k)
+            continue
         d = (p.grad.float().cpu() - q.grad).abs()
         torch.testing.assert_close(p.grad.float().cpu(), q.grad, **tol_w,
                                    msg=f"{k}: max |diff| {d.max():.3g} (|ref| max {q.grad.abs().max():.3g})")
