@@ -41,6 +41,7 @@
 // bound 96 2^30 yscale of |dh| in those units (a constant shift, e_dz).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "ngnn_device.h"
 
@@ -156,7 +157,10 @@ __device__ __forceinline__ float sum_xor32(float v) {
 // dW_l0 (mat 1, B = agg0) rows n of tile nt, all K0 columns.  Stage C1: wave
 // w -> 3 of the 24 [dW_r1; dW_l1] tiles (6 f-tiles x 4 n-tiles).
 // KT: 16-column tiles of K0 computed (past K0 the images hold zeros)
-template <bool XR, int KT>
+// LAG: a chunk's maxima published at the barrier that ends the previous chunk
+// (its loads waited for right after stage B) -- else after stage C, at a
+// barrier of their own (the loads keep stage C to land)
+template <bool XR, int KT, bool LAG>
 __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     extern __shared__ __attribute__((aligned(16))) __bf16 lb_[];
     L16 *lb = (L16 *)(lb_);  // (an address-space cast: the shared array IS in LDS)
@@ -313,7 +317,10 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         ma = wave_max(ma);
         if (ln == 0) smax[sl * 8 + wv] = float4{mX, mH, mx, ma};
     };
-    auto read_exps = [&](int sl) __attribute__((always_inline)) -> Exps {
+    // (a scale may grow by at most 2^20 from one chunk to the next, so the
+    // accumulators, rescaled in place by the change, never overflow; a chunk
+    // held below its own scale has values 2^20 under the previous one's)
+    auto read_exps = [&](int sl, const Exps &pe, bool first) __attribute__((always_inline)) -> Exps {
         float4 m = smax[sl * 8];
 #pragma unroll
         for (int w = 1; w < 8; ++w) {
@@ -323,8 +330,15 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             m.z = fmaxf(m.z, o.z);
             m.w = fmaxf(m.w, o.w);
         }
-        return Exps{__builtin_amdgcn_readfirstlane(h2_exp(m.x)), __builtin_amdgcn_readfirstlane(h2_exp(m.y)),
-                    __builtin_amdgcn_readfirstlane(h2_exp(m.z)), __builtin_amdgcn_readfirstlane(h2_exp(m.w))};
+        Exps e{__builtin_amdgcn_readfirstlane(h2_exp(m.x)), __builtin_amdgcn_readfirstlane(h2_exp(m.y)),
+               __builtin_amdgcn_readfirstlane(h2_exp(m.z)), __builtin_amdgcn_readfirstlane(h2_exp(m.w))};
+        if (!first) {
+            e.X = min(e.X, pe.X + 20);
+            e.H = min(e.H, pe.H + 20);
+            e.x = min(e.x, pe.x + 20);
+            e.a = min(e.a, pe.a + 20);
+        }
+        return e;
     };
     // two fp16 parts of 8 floats (scaled by 2^e) -> part images at (row, col), 16 B each
     auto put8 = [&](L16 *img, int part_stride, int off, v4f v0, v4f v1, int e) __attribute__((always_inline)) {
@@ -420,6 +434,12 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
     const int mat = wv >> 2;
+    // the accumulators hold sums in the units of the last chunk added:
+    // 2^E0 (dz0 2^(eX + eW - e_dz) times x / agg0 2^(ex | ea)), 2^E1 (X 2^eX
+    // times h 2^eH); each chunk rescales them by the change (v_ldexp, exact
+    // unless a sum falls below fp32's range) and its MFMAs accumulate on top
+    int E0 = 0, E1 = 0;
+    bool acc_empty = true;
     auto stage_c = [&](const L16 *buf, const Exps &e) __attribute__((always_inline)) {
         const L16 *ix = buf, *ih = ix + IMG_X, *ik = ih + IMG_H, *ia = ik + IMG_K;
         const L16 *sa = ia + IMG_K;
@@ -445,15 +465,21 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             h1[u] = tr_frag(ih, HS, 16 * nn, ln);
             h2[u] = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
         }
-        // this chunk's products from zero, unscaled into the accumulators:
-        // dz0 carries 2^(eX + eW - e_dz), x / agg0 2^(ex | ea); X 2^eX, h 2^eH
-        const v4f z{0.f, 0.f, 0.f, 0.f};
-        const int e0 = a.e_dz - e.X - eW - (mat ? e.a : e.x);
-        const int e1 = -(e.X + e.H);
+        const int e0 = e.X + eW - a.e_dz + (mat ? e.a : e.x);
+        const int e1 = e.X + e.H;
+        if (!acc_empty) {
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) acc0[kt] += ldexp4(mfma3(a1, a2, b1[kt], b2[kt], z), e0);
+            for (int kt = 0; kt < KT; ++kt) acc0[kt] = ldexp4(acc0[kt], e0 - E0);
 #pragma unroll
-        for (int u = 0; u < 3; ++u) acc1[u] += ldexp4(mfma3(x1[u], x2[u], h1[u], h2[u], z), e1);
+            for (int u = 0; u < 3; ++u) acc1[u] = ldexp4(acc1[u], e1 - E1);
+        }
+        E0 = e0;
+        E1 = e1;
+        acc_empty = false;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) acc0[kt] = mfma3(a1, a2, b1[kt], b2[kt], acc0[kt]);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) acc1[u] = mfma3(x1[u], x2[u], h1[u], h2[u], acc1[u]);
     };
 
     // ---- pipeline over the slice's chunks (two LDS buffers):
@@ -470,22 +496,31 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     Exps ep{0, 0, 0, 0};
     if (cb < ce) {
         load(cb, pre);
-        publish_max(pre, cb & 1);
+        if (LAG) publish_max(pre, cb & 1);
     }
-    lds_barrier();
+    if (LAG) lds_barrier();
     for (int c = cb; c < ce; ++c) {
         L16 *cur = lb + (c & 1) * BUF;
         if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF, ep);
-        const Exps ec = read_exps(c & 1);
+        if (!LAG) {
+            publish_max(pre, c & 1);
+            lds_barrier();
+        }
+        const Exps ec = read_exps(c & 1, ep, c == cb);
         stage_images(pre, cur, ec);
         load(c + 1, pre);
         lds_barrier();  // (LDS only: the next chunk's loads stay in flight)
         stage_b(cur, ec);
-        publish_max(pre, (c + 1) & 1);
+        if (LAG) publish_max(pre, (c + 1) & 1);
         lds_barrier();
         ep = ec;
     }
     if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF, ep);
+    // back to true units
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) acc0[kt] = ldexp4(acc0[kt], -E0);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc1[u] = ldexp4(acc1[u], -E1);
 
     // ---- this workgroup's part of slab s (zeros for an empty slice)
     float *slab = a.slab + static_cast<int64_t>(s) * b2_slab_floats(K0, F1);
@@ -701,8 +736,13 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.step_inc = adam ? adam->step : nullptr;
     // (+ the chunk maxima: [2][8] float4)
     const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4 + 2 * 8 * 16;
+    static const bool lag = [] {
+        const char *v = std::getenv("NGNN_B2_LAG");  // (A/B switch, read once; default lagged: measured
+        return !(v && v[0] == '0');                  // 43.8 vs 44.6 us per call, tools/bwd2_micro.py)
+    }();
     auto go = [&](auto xr_c, auto kt_c) {
-        auto fn = k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value>;
+        auto fn = lag ? k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value, true>
+                      : k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value, false>;
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,

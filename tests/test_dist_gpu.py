@@ -109,12 +109,18 @@ def _worker_headline(rank, world, port, q):
         from ngnn.graphs import GraphedTrainStep, slot_size
         from ngnn.loader import NeighborLoader, synthetic_graph
         from ngnn.optim import Adam
+        import datetime
+        import sys
         from test_gpu_configs import _gpu_hidden, _hooked_capture, _slot_masks
         from test_gpu_fused import _MaskedSAGE
-        init(backend="gloo")
+        # a short collective timeout: a rank that fails leaves its peer in a
+        # collective, which then raises instead of waiting out the test
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=90))
+        print(f"[rank {rank}] up", file=sys.stderr, flush=True)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        graph = synthetic_graph("ogbn-products", dev, seed=0, scale=0.01)
+        graph = synthetic_graph("ogbn-products", dev, seed=0, scale=0.03)  # ~2.9 k seeds per rank
         loader = NeighborLoader(graph, graph.train_idx, [15, 10], 1024, shuffle=True, seed=3,
                                 rank=rank, world_size=world)
         it = iter(loader)
@@ -140,8 +146,10 @@ def _worker_headline(rank, world, port, q):
             fused.sage2_backward = orig
         assert calls, "the captured backward did not take ngnn_sage2_bwd"
         assert step._split_reduce and not step.folded
+        print(f"[rank {rank}] captured", file=sys.stderr, flush=True)
         step(b.x, b.edge_index, b.y, b.batch_size)
         torch.cuda.synchronize()
+        print(f"[rank {rank}] stepped", file=sys.stderr, flush=True)
         params = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
         grads = {k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()}
         # this rank's own gradient, by the oracle on its block with the replay's masks
@@ -162,20 +170,20 @@ def _worker_headline(rank, world, port, q):
         same_ranks = all(torch.equal(pg[0], t) for t in pg)
         # the single-process step on the rank-averaged oracle gradients
         off, worst, upd = 0, 0.0, 0.0
-        for (k, q) in ref.named_parameters():
-            n = q.numel()
-            want = avg[off:off + n].view(q.shape)
+        for (k, rp) in ref.named_parameters():
+            n = rp.numel()
+            want = avg[off:off + n].view(rp.shape)
             err = float((grads[k] - want).abs().max()) / max(float(want.abs().max()), 1e-30)
             worst = max(worst, err)
-            q.grad = want.clone()
+            rp.grad = want.clone()
             off += n
         o_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
         o_ref.step()
         named = dict(model.named_parameters())
-        for k, q in ref.named_parameters():
+        for k, rp in ref.named_parameters():
             p = named[k].detach().cpu()
-            sure = q.grad.abs() > 1e-2 * q.grad.abs().max()
-            upd = max(upd, float((p[sure] - q.detach()[sure]).abs().max()))
+            sure = rp.grad.abs() > 1e-2 * rp.grad.abs().max()
+            upd = max(upd, float((p[sure] - rp.detach()[sure]).abs().max()))
         q.put((rank, same_ranks, worst, upd, None))
         dist.barrier()
         dist.destroy_process_group()
@@ -193,7 +201,7 @@ def test_headline_model_data_parallel_two_ranks():
     procs = [ctx.Process(target=_worker_headline, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=280) for _ in range(world)]
+    out = [q.get(timeout=150) for _ in range(world)]
     for p in procs:
         p.join(timeout=30)
     for rank, same, worst, upd, err in out:
