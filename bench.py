@@ -58,6 +58,8 @@ def parse():
                     help="model / feature storage dtype (bf16: bf16 feature rows and one-part bf16 weight images, fp32 accumulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
+    ap.add_argument("--no-eager-ref", action="store_true",
+                    help="skip the eager reference-loop timing (eager_drop_in)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python instead of replaying the captured "
@@ -178,6 +180,50 @@ def cpu_baseline(batches, args, layers):
                       f"(avg E={E:.0f}) at {threads} threads, then {n1} at 1 thread; "
                       f"torch {torch.__version__} CPU; PyG 2.5.1 op sequence restated in "
                       f"oracle/pyg_ref.py"}
+
+
+def eager_reference_loop(batches, args, F_in, C, layers, dev, steps, verbatim=False):
+    """The reference's training loop (pipeline.py:152-169) run verbatim on
+    ngnn's modules after the INTEGRATION.md Option-B swap -- no graph capture,
+    no loss head, no Adam fold: out = model(x, edge_index)[:batch_size];
+    F.cross_entropy; optimizer.zero_grad(); loss.backward(); and the
+    reference optimiser, torch.optim.Adam (model.py:66-69).  verbatim: also
+    the loop's per-step host reads (total_loss += float(loss), the
+    accuracy count).  Returns ms per step over `steps` batches."""
+    import torch.nn.functional as F
+
+    import ngnn
+    torch.manual_seed(1234)
+    if args.module == "gcn":
+        model = ngnn.SimpleGCN(F_in, args.hidden, C, layers, dropout=0.5).to(dev)
+    else:
+        model = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
+    if args.dtype == "bf16":
+        model = model.to(torch.bfloat16)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    model.train()
+    total_loss, total_correct = 0.0, 0
+
+    def one(b):
+        nonlocal total_loss, total_correct
+        out = model(_rows(b.x), b.edge_index)[:b.batch_size]
+        y = b.y[:b.batch_size].squeeze()
+        loss = F.cross_entropy(out, y)
+        if verbatim:
+            total_loss += float(loss)
+            total_correct += int(out.argmax(dim=-1).eq(y).sum())
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    for i in range(3):
+        one(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    return 1e3 * (time.perf_counter() - t0) / steps
 
 
 def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512, dom: str = "sage_fwd_l0"):
@@ -571,6 +617,24 @@ def main():
                                 "mfma_frac": round(v[4] / (v[1] * 1e-3), 4)}
                             for k, v in summ.items()}})
 
+    # the reference loop verbatim on the eager path (INTEGRATION Option B):
+    # what a user gets without GraphedTrainStep / ngnn.optim.Adam
+    eager_ref = None
+    if rank == 0 and world == 1 and not args.no_eager_ref:
+        timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
+        ms_core = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps)
+        ms_verb = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps, verbatim=True)
+        graph_ms = 1e3 * dt / args.steps
+        eager_ref = {
+            "ms_per_step": round(ms_core, 4),
+            "value": round(sum(layers * b.edge_index.shape[1] for b in timed) / args.steps / (ms_core * 1e-3), 1),
+            "unit": "edges/s", "vs_graph_step": round(ms_core / graph_ms, 3),
+            "ms_per_step_with_host_reads": round(ms_verb, 4),
+            "note": "pipeline.py:152-169 after the INTEGRATION.md Option-B swap: model(x, edge_index)"
+                    "[:batch_size], F.cross_entropy, zero_grad, backward, torch.optim.Adam; no capture, "
+                    "no loss head, no Adam fold (with_host_reads: + the loop's float(loss) and accuracy "
+                    "count per step)"}
+
     # full epoch incl. GPU sampling (this rank's shard)
     epoch_s = None
     if not args.no_epoch:
@@ -612,6 +676,7 @@ def main():
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
             "epoch_batches_per_rank": len(loader),
             "allreduce": ar,
+            "eager_drop_in": eager_ref,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

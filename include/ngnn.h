@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 15
+#define NGNN_ABI_VERSION 16
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -656,8 +656,16 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * current values of a weight the captured step's forward then reads with
  * NGNN_WL_PREPACKED (no pack launch inside the step; read at load time, so
  * parameters changed between steps are picked up).
+ * err (nullable; may be host memory the device can write, e.g. pinned):
+ * bits OR-ed in (never cleared here) when the block breaks the slot's
+ * contract -- NGNN_SLOT_UNSORTED: a target smaller than the one before it;
+ * NGNN_SLOT_RANGE: a source or target outside [0, N).  The CSR of such a
+ * block is wrong (never written out of bounds); the caller checks the word
+ * without a device sync (ABI 16: replaces a host read-back of the targets).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
+#define NGNN_SLOT_UNSORTED 1
+#define NGNN_SLOT_RANGE 2
 int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int64_t *edge_index,
                    int64_t ld_ei, int64_t E, const int64_t *y, int64_t B, float *slot_x,
                    int64_t ld_slot, int64_t n_cap, int64_t *slot_ei, int64_t e_cap,
@@ -665,7 +673,7 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
                    int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
                    int32_t *slot_colx, const float *pack_w, int64_t pack_ldw, int64_t pack_fo,
-                   int64_t pack_k, float *pack_dst, void *stream);
+                   int64_t pack_k, float *pack_dst, int32_t *err, void *stream);
 
 #ifdef __cplusplus
 }

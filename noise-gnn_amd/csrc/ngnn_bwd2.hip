@@ -680,6 +680,14 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
                    NGNN_E_ALIGN);
     const bool indexed = xrow || xrow_dev;
     NGNN_RETURN_IF(indexed && x_rows <= 0, NGNN_E_ARG);
+    {
+        // 32-bit buffer offsets: every operand's live rows under 3.75 GiB (as
+        // ngnn_sage2_fwd checks; past it the resources would truncate)
+        const int64_t lim = 0xF0000000ll - 4096, C4 = (F1 + 3) & ~int64_t{3};
+        NGNN_RETURN_IF(n_rows * ldh * 4 > lim || n_rows * ld_agg * 4 > lim || n_rows * ldy * 4 > lim ||
+                           std::max(n_rows, indexed ? x_rows : 0) * ldx * 4 > lim || n_rows * C4 * 4 > lim,
+                       NGNN_E_RANGE);
+    }
     if (adam) {
         NGNN_RETURN_IF(!adam->step, NGNN_E_ARG);
         for (int k = 0; k < 6; ++k)

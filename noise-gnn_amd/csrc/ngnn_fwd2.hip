@@ -441,13 +441,18 @@ struct F2Args {
 
 // DM: dropout mode (0 none, 1 byte, 2 bit: Dropout in ngnn_device.h).  XR:
 // the fused x[n_id] gather (rows through n_id, whose loads run four tiles
-// ahead of the row loads that use them).
+// ahead of the row loads that use them).  T16: K0 <= 32 C0 - 16 -- the last
+// 32-deep chunk of layer 0 runs as a 16-deep one on v_mfma_f32_16x16x16_f16
+// (K0 = 100: 3 x 32 + 16 instead of 4 x 32 -- an eighth of the launch's
+// MFMA work and 8 weight registers).
 // DBG (profiling builds only, NGNN_FWD2_DBG): bit 0 skips the reduce, 1 the
 // layer-1 products, 2 layer 0's products, 3 the x split, 4 the out / z
 // stores (offsets out of range) -- time attribution
-template <int C0, int NT1, int DM, bool XR, int DBG = 0>
+template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     constexpr int MT1 = 2 * NT1;
+    constexpr int CF = T16 ? C0 - 1 : C0;    // full 32-deep chunks of layer 0
+    constexpr int KC = 32 * CF + (T16 ? 16 : 0);  // K0 padded to the chunks
     constexpr int PSTR = 32 * C0 + 16;       // halves per parts row: 72 dwords = 8 mod 64 banks (conflict-free fragment reads)
     constexpr int XPB = 2 * F2_ROWS * PSTR;  // halves per x-parts buffer (2 parts)
     constexpr int NIT = MT1 * 8;             // reduce items per wave (MT1 x 64 over 8 waves)
@@ -465,8 +470,43 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     if (threadIdx.x < F2_HID) sb0[threadIdx.x] = a.b0[threadIdx.x];
     if (threadIdx.x < 16 * NT1) sb1[threadIdx.x] = static_cast<int>(threadIdx.x) < a.F1 ? a.b1[threadIdx.x] : 0.0f;
     // ---- this wave's weight slices, for the whole launch
-    half8 wr[2][C0][2], w1[MT1][2];
-    const int eW0 = load_w0_slice<C0>(a.wr0, a.ldw0, a.K0, wv, ln, wr);
+    half8 wr[2][CF][2], w1[MT1][2];
+    half4 wt[2][2];  // T16: the tail chunk, k = 32 CF + 4 q .. + 3
+    int eW0;
+    {
+        v4f t[2][CF][2], tt[2];
+        w0_slice_issue<CF>(a.wr0, a.ldw0, a.K0, wv, ln, t);
+        if (T16) {
+            const i32x4 wrs = make_rsrc(a.wr0, static_cast<uint32_t>(static_cast<int64_t>(F2_HID) * a.ldw0 * 4));
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int k = 32 * CF + 4 * q;
+                tt[mt] = buf_load4(wrs, k < a.K0 ? (32 * wv + 16 * mt + rl) * static_cast<int>(a.ldw0) * 4 + 4 * k : kOOB2, 0, 0);
+            }
+        }
+        float mx = 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+            for (int c = 0; c < CF; ++c) mx = fmaxf(mx, fmaxf(amax4(t[mt][c][0]), amax4(t[mt][c][1])));
+            if (T16) mx = fmaxf(mx, amax4(tt[mt]));
+        }
+        eW0 = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+            for (int c = 0; c < CF; ++c) h2_split(ldexp4(t[mt][c][0], eW0), ldexp4(t[mt][c][1], eW0), wr[mt][c][0], wr[mt][c][1]);
+            if (T16) {
+                const v4f v = ldexp4(tt[mt], eW0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const _Float16 hh = static_cast<_Float16>(v[i]);
+                    wt[mt][0][i] = hh;
+                    wt[mt][1][i] = static_cast<_Float16>(v[i] - static_cast<float>(hh));
+                }
+            }
+        }
+    }
     int eW1;
     {
         // layer 1: output rows 16 m1' + m of W_r1 (m1 < NT1) / W_l1 (the rest),
@@ -538,7 +578,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
 
     // ---- x split lanes: row srow of the tile, columns 4 sslot .. + 3
     const int srow = 2 * wv + (ln >> 5), sslot = ln & 31;
-    const bool scol = 4 * sslot < a.K0 && sslot < 8 * C0;
+    const bool scol = 4 * sslot < a.K0 && 4 * sslot < KC;
     auto tile_of = [&](int j) { return b + j * G; };
     // XR: the split row's feature-table index (low word of n_id; rows past
     // the block read 0 and are masked at use)
@@ -572,7 +612,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
             p1[i] = hh;
             p2[i] = static_cast<_Float16>(vs[i] - static_cast<float>(hh));
         }
-        if (sslot < 8 * C0) {
+        if (4 * sslot < KC) {
             _Float16 *d = sxp + buf * XPB + srow * PSTR + 4 * sslot;
             *reinterpret_cast<half4 *>(d) = p1;
             *reinterpret_cast<half4 *>(d + F2_ROWS * PSTR) = p2;
@@ -586,17 +626,30 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         acc[0] = v4f{0.f, 0.f, 0.f, 0.f};
         acc[1] = v4f{0.f, 0.f, 0.f, 0.f};
         const _Float16 *xp = sxp + buf * XPB + rl * PSTR + 8 * q;
-        half8 xf[C0][2];  // every fragment read issued before the first MFMA
+        half8 xf[CF][2];  // every fragment read issued before the first MFMA
+        half4 xt[2];
 #pragma unroll
-        for (int c = 0; c < C0; ++c) {
+        for (int c = 0; c < CF; ++c) {
             xf[c][0] = *reinterpret_cast<const half8 *>(xp + 32 * c);
             xf[c][1] = *reinterpret_cast<const half8 *>(xp + F2_ROWS * PSTR + 32 * c);
         }
+        if (T16) {  // (16x16x16: lane (q, rl) holds k = 4 q .. + 3 of row rl)
+            xt[0] = *reinterpret_cast<const half4 *>(xp - 4 * q + 32 * CF);
+            xt[1] = *reinterpret_cast<const half4 *>(xp - 4 * q + 32 * CF + F2_ROWS * PSTR);
+        }
         s0 = __builtin_amdgcn_ldexpf(1.0f, -(eW0 + serow[buf * F2_ROWS + rl]));
 #pragma unroll
-        for (int c = 0; c < C0; ++c)
+        for (int c = 0; c < CF; ++c)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) acc[mt] = mfma_h2(wr[mt][c][0], wr[mt][c][1], xf[c][0], xf[c][1], acc[mt]);
+        if (T16) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x16f16(wt[mt][1], xt[0], acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x16f16(wt[mt][0], xt[1], acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x16f16(wt[mt][0], xt[0], acc[mt], 0, 0, 0);
+            }
+        }
     };
     // one tile after layer 0: epilogue, h rows, layer-1 partial into spart[buf]
     auto finish = [&](int j, int buf, const v4f (&acc)[2], float s0, const v4f (&nbv)[2], auto nb_c)
@@ -607,7 +660,9 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         // row, global column) exactly as every other forward kernel.  The
         // unscale rides the fma (acc s0 is exact: a power of two)
         const uint32_t rk = DM ? drop.row_key(static_cast<uint32_t>(r)) : 0u;
-        const uint32_t hw = DM == 2 ? lowbias32(rk + static_cast<uint32_t>(wv)) : 0u;  // columns 32 wv .. + 31
+        // columns 32 wv .. + 31; the lane's bits 16 mt + 4 q + i, shifted by 4 q
+        // once so the per-value shifts are immediates
+        const uint32_t hw = DM == 2 ? lowbias32(rk + static_cast<uint32_t>(wv)) >> (4 * q) : 0u;
         v4f hv[2], b0v[2];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) b0v[mt] = *reinterpret_cast<const v4f *>(sb0 + 32 * wv + 16 * mt + 4 * q);
@@ -619,7 +674,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
                 float y = __builtin_fmaf(acc[mt][i], s0, b0v[mt][i]);
                 if (NB) y += nbv[mt][i];
                 bool zero = y < 0.0f;
-                if (DM == 2) zero = zero || !((hw >> (16 * mt + 4 * q + i)) & 1u);
+                if (DM == 2) zero = zero || !((hw >> (16 * mt + i)) & 1u);
                 if (DM == 1) zero = zero || ((hq >> (8 * i)) & 0xffu) < drop.thresh;
                 hv[mt][i] = zero ? 0.0f : (DM ? y * drop.scale : y);
             }
@@ -634,16 +689,18 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         const int eh = h2_exp(m);
         half8 h1, h2;
         h2_split(ldexp4(hv[0], eh), ldexp4(hv[1], eh), h1, h2);
-        const int un1 = -(eW1 + eh);
+        // (the unscale as a packed multiply by 2^un1: exact, a subnormal
+        // factor only for partials far below fp32's range anyway)
+        const float f1 = __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eh));
         v4f *pp = spart + (buf * F2_WAVES + wv) * MT1 * 64 + ln;
         if (DBG & 2) {
-            asm volatile("" : "+v"(h1), "+v"(h2) : "v"(un1));
+            asm volatile("" : "+v"(h1), "+v"(h2) : "v"(f1));
             return;
         }
 #pragma unroll
         for (int m1 = 0; m1 < MT1; ++m1) {
             const v4f o = mfma_h2(w1[m1][0], w1[m1][1], h1, h2, v4f{0.f, 0.f, 0.f, 0.f});
-            pp[m1 * 64] = ldexp4(o, un1);
+            pp[m1 * 64] = o * f1;
         }
     };
     // the 8 partials of this lane's item, summed in wave order (+ b1), stored
@@ -841,9 +898,9 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     else pipeline(std::false_type{});
 }
 
-template <int C0, int NT1, int DM, bool XR, int DBG = 0>
+template <int C0, int NT1, int DM, bool XR, int DBG = 0, bool T16 = false>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
-    auto fn = k_fwd2<C0, NT1, DM, XR, DBG>;
+    auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
                        (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4;
@@ -1081,8 +1138,18 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
             }
         }
 #endif
+        // (K0 <= 112: the 16-deep tail chunk; NGNN_FWD2_T16=0 forces 4 x 32 -- A/B)
+        static const bool t16_ok = [] {
+            const char *v = std::getenv("NGNN_FWD2_T16");
+            return !(v && v[0] == '0');
+        }();
+        const bool t16 = t16_ok && K0 <= 112;
         auto go = [&](auto xr_c) {
             constexpr bool XRv = decltype(xr_c)::value;
+            if (t16)
+                return dm == 2   ? launch_fwd2<4, 3, 2, XRv, 0, true>(f, grid, st)
+                       : dm == 1 ? launch_fwd2<4, 3, 1, XRv, 0, true>(f, grid, st)
+                                 : launch_fwd2<4, 3, 0, XRv, 0, true>(f, grid, st);
             return dm == 2   ? launch_fwd2<4, 3, 2, XRv>(f, grid, st)
                    : dm == 1 ? launch_fwd2<4, 3, 1, XRv>(f, grid, st)
                              : launch_fwd2<4, 3, 0, XRv>(f, grid, st);

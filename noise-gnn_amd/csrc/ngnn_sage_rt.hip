@@ -111,7 +111,10 @@ __device__ __forceinline__ float sum16(float v) {
 // workgroup partials in a fixed order -- deterministic; the hand-off is
 // k_xent_fused's (ngnn_loss.hip: agent-scope partial stores drained before
 // one ticket atomic, agent-scope loads by the last adder).
-template <bool MEAN, bool HEAD>
+// WIDE: z row offsets by a full 32-bit multiply (n_rows or the row bytes past
+// 24 bits); else v_mul_u32_u24.  Edge offsets are unsigned 32-bit: col reads
+// are exact below 2^30 edges (the resource's 3.75 GiB range).
+template <bool MEAN, bool HEAD, bool WIDE = false>
 __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z, int64_t ldz, int Fo,
                                                     const int32_t *__restrict__ rowptr,
                                                     const int32_t *__restrict__ col, int n_rows,
@@ -135,12 +138,15 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
         for (int e = beg; e < end; e += NA_UNR) {
             int id[NA_UNR];
 #pragma unroll
-            for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, e + u < end ? 4 * (e + u) : OOB, 0, 0);
+            for (int u = 0; u < NA_UNR; ++u)
+                id[u] = buf_load1i(cr, e + u < end ? static_cast<int>(4u * static_cast<uint32_t>(e + u)) : OOB, 0, 0);
             const i32x4 zr = make_rsrc(z, 0xF0000000u);
             v4f v[NA_UNR];
 #pragma unroll
             for (int u = 0; u < NA_UNR; ++u)
-                v[u] = buf_load4(zr, e + u < end ? static_cast<int>(__umul24(static_cast<uint32_t>(id[u]), ldz4)) + 16 * c4 : OOB,
+                v[u] = buf_load4(zr, e + u < end ? static_cast<int>((WIDE ? static_cast<uint32_t>(id[u]) * ldz4
+                                                               : __umul24(static_cast<uint32_t>(id[u]), ldz4))) + 16 * c4
+                                                  : OOB,
                                  0, 0);
 #pragma unroll
             for (int u = 0; u < NA_UNR; ++u)
@@ -422,18 +428,26 @@ int narrow_agg_launch(const float *z, int64_t ldz, int64_t Fo, const int32_t *ro
                       const int32_t *n_edge_rows_dev, int reduce, float *out, int64_t ldo, hipStream_t st,
                       const NarrowHead *head) {
     const int64_t rows = std::max<int64_t>(1, std::min(n_edge_rows, n_rows));
-    // (32-bit buffer offsets into z: a 24-bit row index times the row bytes)
-    NGNN_RETURN_IF(n_rows * ldz * 4 >= 0xF0000000ll || n_rows >= (1 << 24) || ldz * 4 >= (1 << 24), NGNN_E_RANGE);
+    // (32-bit buffer offsets into z; past 24-bit rows or row bytes the z
+    // offsets take the full multiply: k_narrow_agg<..., WIDE>)
+    NGNN_RETURN_IF(n_rows * ldz * 4 >= 0xF0000000ll, NGNN_E_RANGE);
+    const bool wide = n_rows >= (1 << 24) || ldz * 4 >= (1 << 24);
     NGNN_RETURN_IF(head && (Fo > 64 || head->B <= 0 || head->B > n_rows), NGNN_E_ARG);
+    NGNN_RETURN_IF(head && n_rows >= (1 << 24), NGNN_E_RANGE);
     const unsigned grid = static_cast<unsigned>(
         std::max<int64_t>(1, std::min<int64_t>(head ? std::min(4 * num_cus(), 1024) : 4 * num_cus(),
                                                ceil_div(std::max<int64_t>(rows, head ? 2 * ((head->B + 7) & ~int64_t{7}) : 0), 16))));
     // (the head's hand-off: at most 32 groups of 32 workgroups)
     const NarrowHead hd = head ? *head : NarrowHead{};
     auto go = [&](auto mean_c, auto head_c) {
-        hipLaunchKernelGGL((k_narrow_agg<decltype(mean_c)::value, decltype(head_c)::value>), dim3(grid), dim3(256), 0,
-                           st, z, ldz, static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
-                           n_edge_rows_dev, out, ldo, hd);
+        if (wide && !decltype(head_c)::value)  // (the loss head's blocks are NeighborLoader-sized)
+            hipLaunchKernelGGL((k_narrow_agg<decltype(mean_c)::value, false, true>), dim3(grid), dim3(256), 0,
+                               st, z, ldz, static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
+                               n_edge_rows_dev, out, ldo, hd);
+        else
+            hipLaunchKernelGGL((k_narrow_agg<decltype(mean_c)::value, decltype(head_c)::value>), dim3(grid), dim3(256),
+                               0, st, z, ldz, static_cast<int>(Fo), rowptr, col, static_cast<int>(n_rows), n_rows_dev,
+                               n_edge_rows_dev, out, ldo, hd);
     };
     const bool mean = reduce == NGNN_REDUCE_MEAN;
     if (head) {

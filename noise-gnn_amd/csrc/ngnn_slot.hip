@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
     uint32_t gen, int32_t *__restrict__ n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
     int32_t *__restrict__ colx, int vec, const float *__restrict__ pk_w, int64_t pk_ldw, int pk_fo,
-    int pk_k, float *__restrict__ pk_dst) {
+    int pk_k, float *__restrict__ pk_dst, int32_t *err) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     if (x_dev) {  // zero-copy: the captured kernels read x where it is
@@ -55,11 +55,14 @@ __global__ __launch_bounds__(256) void k_slot_load(
         }
     }
     const int64_t n_pad = e_cap - E, span = n_cap - N;
+    int bad = 0;  // the block's contract: targets non-decreasing, ids in [0, N)
     for (int64_t e = tid; e < e_cap; e += nthr) {
         int64_t s, d;
         if (e < E) {
             s = ei[e];
             d = ei[ld_ei + e];
+            if (s < 0 || s >= N || d < 0 || d >= N) bad |= NGNN_SLOT_RANGE;
+            if (e > 0 && d < ei[ld_ei + e - 1]) bad |= NGNN_SLOT_UNSORTED;
         } else {
             d = N + ((e - E) * span) / n_pad;
             s = d;
@@ -69,20 +72,23 @@ __global__ __launch_bounds__(256) void k_slot_load(
             sei[e_cap + e] = d;
         }
     }
+    if (bad && err) atomicOr(err, bad);
     for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
     if (rowptr) {
         // rowptr[r] = first padded edge with target >= r.  Padding: closed
         // form (target of padding edge j is N + floor(j span / n_pad)); rows
         // past the last real target (NeighborLoader: every row that received
         // no edges, ~90% of a products block): E.
-        const int64_t last_dst = E > 0 ? ei[ld_ei + E - 1] : -1;
+        // (a block breaking the contract gets a wrong CSR, but every write
+        // stays inside rowptr: targets clamped to [-1, n_cap])
+        const int64_t last_dst = E > 0 ? min(max(ei[ld_ei + E - 1], int64_t{-1}), n_cap) : -1;
         // rows up to the last target: edge e writes rowptr[r] = e for every
         // r in (dst[e-1], dst[e]] -- the lower bound of r over the sorted
         // targets, each row written once, two independent loads per edge
         // (a per-row binary search was a chain of ~17 dependent loads)
         for (int64_t e = tid; e < E; e += nthr) {
-            const int64_t d = ei[ld_ei + e];
-            const int64_t p = e > 0 ? ei[ld_ei + e - 1] : -1;
+            const int64_t d = min(ei[ld_ei + e], n_cap);
+            const int64_t p = e > 0 ? max(ei[ld_ei + e - 1], int64_t{-1}) : -1;
             for (int64_t r = p + 1; r <= d; ++r) rowptr[r] = static_cast<int32_t>(e);
         }
         for (int64_t r = last_dst + 1 + tid; r <= n_cap; r += nthr) {
@@ -103,7 +109,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
         // layer 0's gather columns: the sources' rows in the feature table
         // (padding edges feed skipped rows only: 0)
         for (int64_t e = tid; e < e_cap; e += nthr)
-            colx[e] = static_cast<int32_t>(e < E ? (xrow ? xrow[ei[e]] : ei[e]) : 0);
+            colx[e] = static_cast<int32_t>((e < E && ei[e] >= 0 && ei[e] < N) ? (xrow ? xrow[ei[e]] : ei[e]) : 0);
     }
     if (r_next) {
         // max(B, 1 + max source over the edges into rows < B), as a 64-bit
@@ -144,7 +150,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
     if (tid == 0) {
         *n_valid = static_cast<int32_t>(N);
         if (n_edge_rows)  // rows past the last target have no in-edges
-            *n_edge_rows = E > 0 ? static_cast<int32_t>(ei[ld_ei + E - 1] + 1) : 0;
+            *n_edge_rows = E > 0 ? static_cast<int32_t>(min(max(ei[ld_ei + E - 1] + 1, int64_t{0}), N)) : 0;
         if (seed_state) {  // splitmix64 step: state <- mix(state + golden gamma)
             uint64_t z = *seed_state + 0x9e3779b97f4a7c15ULL;
             z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -167,7 +173,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               const float **x_dev, int64_t *r_next, uint32_t gen,
                               int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
                               int32_t *slot_colx, const float *pack_w, int64_t pack_ldw,
-                              int64_t pack_fo, int64_t pack_k, float *pack_dst, void *stream) {
+                              int64_t pack_fo, int64_t pack_k, float *pack_dst, int32_t *err, void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
@@ -190,6 +196,6 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
                        n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
                        xrow, xrow_dev, slot_colx, vec, pack_w, pack_ldw, static_cast<int>(pack_fo),
-                       static_cast<int>(pack_k), pack_dst);
+                       static_cast<int>(pack_k), pack_dst, err);
     return launch_status();
 }

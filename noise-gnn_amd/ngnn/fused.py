@@ -95,13 +95,24 @@ class exact_f32:
         return False
 
 
+# superseded workspaces, kept alive: a captured HIP graph holds the raw
+# address of the buffer it was captured with, so a later, larger eager call
+# must never free it (the replays would write into memory the caching
+# allocator has handed on -- ADVICE r4).  Growth is rare (sizes follow the
+# largest block seen); the list only ever holds the smaller generations.
+_ws_retired: list = []
+
+
 def _workspace(dev: torch.device, name: str, nbytes: int, zero: bool = False) -> torch.Tensor:
     """Per-device scratch buffers, grown on demand and reused across calls
-    (stream-ordered).  zero: zero-filled when (re)allocated."""
+    (stream-ordered).  zero: zero-filled when (re)allocated.  A grown
+    buffer's predecessor is retired, not freed (graph captures may hold it)."""
     key = (dev, name)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         alloc = torch.zeros if zero else torch.empty
+        if buf is not None:
+            _ws_retired.append(buf)
         buf = alloc(max(nbytes, 256), dtype=torch.uint8, device=dev)
         _ws[key] = buf
     return buf
@@ -591,6 +602,10 @@ class AdamFoldSpec:
             params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
         group = opt.param_groups[0]["params"]
         if len(group) != 6 or {id(q) for q in group} != {id(q) for q in params}:
+            return None
+        # (ngnn.optim.Adam skips a parameter with no gradient -- a frozen one;
+        # the folded reduction would update all six: no fold then)
+        if not all(q.requires_grad for q in params):
             return None
         for q in params:
             s = opt.state.get(q, {})
@@ -1140,7 +1155,7 @@ class _StackOutBF16(torch.autograd.Function):
         # (rows_dev: a graph slot's device row count -- only the block's real
         # rows are cast; the slot's padding rows of y are left unwritten)
         y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-        _lib.check(_lib.load().ngnn_cast_f32_bf16_rows(_lib.ptr(x), _lib.ptr(y), x.size(0), x[0].numel(),
+        _lib.check(_lib.load().ngnn_cast_f32_bf16_rows(_lib.ptr(x), _lib.ptr(y), x.size(0), x.size(1),
                                                        _lib.ptr(rows_dev), _lib.stream_handle(x.device)),
                    "ngnn_cast_f32_bf16_rows")
         return y

@@ -34,7 +34,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .block import CSR, _hint_for, block_cache, hint_edge_index
+from .block import CSR, block_cache, hint_edge_index
 from .loader import IndexedRows
 from .losses import seed_cross_entropy
 
@@ -87,6 +87,11 @@ class GraphedTrainStep:
         self._pack = None
         self._head = None  # fused.LossHead (made at capture)
         self.folded = False  # the captured backward took the Adam step (fused.AdamFoldSpec)
+        # the slot kernel's contract check (include/ngnn.h NGNN_SLOT_*): a word
+        # in pinned host memory the device ORs into -- read by the host with
+        # no device sync (load() raises on a word set by an earlier batch;
+        # check_inputs() syncs and raises for the batches so far)
+        self._err = torch.zeros(1, dtype=torch.int32).pin_memory()
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -126,14 +131,11 @@ class GraphedTrainStep:
             x = x.clone(memory_format=torch.contiguous_format)
         # a step captured for indexed rows: the word gets n_id's address or 0
         xrow_word = self.xrow_dev if (zero_copy and self.x_rows) else None
-        # the slot kernel's CSR assumes non-decreasing targets; a producer hint
-        # (ngnn.loader's sampler) vouches for that, anything else is checked
-        # here (one host read-back) instead of yielding a corrupt rowptr
-        hint = _hint_for(edge_index)
-        if (hint is None or not hint[0]) and E > 1 and not bool(
-                (edge_index[1, 1:] >= edge_index[1, :-1]).all()):
-            raise ValueError("GraphedTrainStep needs target-sorted edges (NeighborLoader's "
-                             "order); sort edge_index by edge_index[1] (stable) first")
+        # the slot kernel's CSR assumes non-decreasing targets and ids in
+        # [0, N): the kernel checks every edge and sets the pinned error word
+        # (no host read-back of the targets per step); a word set by an
+        # earlier batch raises here
+        self._raise_if_bad()
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
         y = y[:bs].contiguous()
@@ -158,10 +160,29 @@ class GraphedTrainStep:
             *((_lib.ptr(self._pack[0]), self._pack[0].stride(0), self._pack[0].shape[0],
                self._pack[0].shape[1], _lib.ptr(self._pack[1])) if self._pack is not None
               else (None, 0, 0, 0, None)),
-            _lib.stream_handle(self.x.device)), "ngnn_slot_load")
+            self._err.data_ptr(), _lib.stream_handle(self.x.device)), "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
         if self._pack is not None:  # this load packed the current W_l: one forward may use it
             self._pack[2].armed = True
+
+    def _raise_if_bad(self) -> None:
+        bad = int(self._err[0])
+        if bad:
+            self._err.zero_()
+            what = []
+            if bad & _lib.SLOT_UNSORTED:
+                what.append("targets not sorted (NeighborLoader's order: sort edge_index by "
+                            "edge_index[1], stable)")
+            if bad & _lib.SLOT_RANGE:
+                what.append("node ids outside [0, N)")
+            raise ValueError("GraphedTrainStep: a batch loaded into the slot broke its contract -- "
+                             + "; ".join(what) + " -- and was trained on a wrong CSR")
+
+    def check_inputs(self) -> None:
+        """Synchronize and raise if any batch loaded so far broke the slot's
+        contract (load() reports such a batch at the next load without a sync)."""
+        torch.cuda.synchronize(self.x.device)
+        self._raise_if_bad()
 
     def _next_gen(self) -> int:
         self._gen += 1

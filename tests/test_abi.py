@@ -93,6 +93,12 @@ def test_argument_errors_return_before_launch():
     assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, None, 1, ws, 1, None) == -1
     assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1023, 0, 1, 100, 1, ws, 1, 1, None, None,
                                         None, 0, 0, None, 0, None) == -3
+    # two-layer backward: operands past the 32-bit buffer range are refused
+    # before any launch: n_rows x ldh x 4 B > 3.75 GiB
+    big = 1 << 22
+    assert lib.ngnn_sage2_bwd(16, 47, 47, 16, 16, 256, 16, 1024, 1.0, 16, None, None, None, 0, 100, 100,
+                              16, 100, 16, 16, big, 16, 16, 0, 16, 16, 16, 16, 16, 16, None, None,
+                              256, 1 << 40, None) == -5
     # zero-size work is a no-op success
     assert lib.ngnn_seg_agg_fwd(None, 4, 4, 1, None, 0, 1, 0, None, 4, None) == 0
 

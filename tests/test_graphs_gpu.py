@@ -320,7 +320,7 @@ def test_slot_load_csr_equals_lower_bound(case):
         _lib.ptr(x), x.stride(0), N, F, _lib.ptr(ei) if E else None, max(E, 0), E, _lib.ptr(y), 8,
         _lib.ptr(sx), sx.stride(0), n_cap, _lib.ptr(sei), e_cap, _lib.ptr(sy), _lib.ptr(nv),
         _lib.ptr(rowptr), _lib.ptr(col), None, None, None, 0, None, None, None, None,
-        None, 0, 0, 0, None, _lib.stream_handle(DEV)), "ngnn_slot_load")
+        None, 0, 0, 0, None, None, _lib.stream_handle(DEV)), "ngnn_slot_load")
     torch.cuda.synchronize()
     n_pad, span = e_cap - E, n_cap - N
     pad = N + (torch.arange(n_pad) * span) // max(n_pad, 1) if n_pad else torch.zeros(0, dtype=torch.int64)
@@ -333,9 +333,10 @@ def test_slot_load_csr_equals_lower_bound(case):
 
 
 def test_slot_rejects_unsorted_targets():
-    """The slot load writes the CSR for non-decreasing targets only: edges the
-    sampler did not vouch for are checked, and unsorted ones are refused
-    (instead of a rowptr with rows never written)."""
+    """The slot load writes the CSR for non-decreasing targets only: the slot
+    kernel checks every batch itself (ABI 16, no host read-back), and an
+    unsorted one is reported -- by check_inputs() after a sync, and by the
+    next load() without one."""
     from ngnn.graphs import GraphedTrainStep, slot_size
     m, batches = _setup(0.0)
     b = batches[0]
@@ -344,9 +345,17 @@ def test_slot_rejects_unsorted_targets():
     step = GraphedTrainStep(m, opt, 256, n_cap, e_cap, b.x.size(1), DEV)
     step.load(b.x, b.edge_index, b.y)            # sampler output (hinted): accepted
     step.load(b.x, b.edge_index.clone(), b.y)    # unhinted but sorted: accepted
+    step.check_inputs()
     perm = torch.randperm(b.edge_index.size(1), device=DEV)
-    with pytest.raises(ValueError, match="target-sorted"):
-        step.load(b.x, b.edge_index[:, perm], b.y)
+    step.load(b.x, b.edge_index[:, perm], b.y)
+    with pytest.raises(ValueError, match="not sorted"):
+        step.check_inputs()
+    step.load(b.x, b.edge_index[:, perm], b.y)
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="not sorted"):
+        step.load(b.x, b.edge_index, b.y)  # (the previous batch's word, no sync in load)
+    step.load(b.x, b.edge_index, b.y)
+    step.check_inputs()
 
 
 @pytest.mark.parametrize("fo,k", [(256, 100), (47, 256), (5, 3), (600, 64)])
@@ -370,7 +379,7 @@ def test_slot_pack_job_equals_pack_weight(fo, k):
     _lib.check(lib.ngnn_slot_load(
         _lib.ptr(x), F, N, F, _lib.ptr(ei), 2, 2, _lib.ptr(y), 1, _lib.ptr(sx), F, n_cap,
         _lib.ptr(sei), 2, _lib.ptr(sy), _lib.ptr(nv), None, None, None, None, None, 0, None,
-        None, None, None, _lib.ptr(w), w.stride(0), fo, k, _lib.ptr(dst),
+        None, None, None, _lib.ptr(w), w.stride(0), fo, k, _lib.ptr(dst), None,
         _lib.stream_handle(DEV)), "ngnn_slot_load")
     want = pack_weight(w)
     torch.cuda.synchronize()
@@ -399,3 +408,75 @@ def test_slot_prepacked_wl_never_stale():
         got = model(step.x, step.ei)[:b.num_nodes]
         want = model(b.x.clone(), b.edge_index.clone())
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+
+
+def test_slot_contract_error_word():
+    """ABI 16: the slot kernel checks the block's contract itself (targets
+    non-decreasing, ids in [0, N)) and ORs NGNN_SLOT_* into a pinned word --
+    no host read-back of the targets per load; check_inputs() syncs and
+    raises, and a good batch afterwards trains normally."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import sample_block, synthetic_graph
+    from ngnn.optim import Adam
+    graph = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.005)
+    b = sample_block(graph, graph.train_idx[:64], [5, 3], seed=1)
+    torch.manual_seed(0)
+    model = ngnn.SAGE(100, 64, 47, 2).to(DEV)
+    n_cap, e_cap = slot_size(64, [5, 3])
+    step = GraphedTrainStep(model, Adam(model.parameters(), lr=1e-3), 64, n_cap, e_cap, 100, DEV)
+    step.capture(b.x, b.edge_index, b.y)
+    step(b.x, b.edge_index, b.y)
+    step.check_inputs()  # a NeighborLoader block: clean
+    bad = b.edge_index.flip(1).contiguous()  # targets descending
+    step(b.x, bad, b.y)
+    with pytest.raises(ValueError, match="not sorted"):
+        step.check_inputs()
+    oob = b.edge_index.clone()
+    oob[0, 0] = b.num_nodes + 5
+    step(b.x, oob, b.y)
+    with pytest.raises(ValueError, match="outside"):
+        step.check_inputs()
+    step(b.x, b.edge_index, b.y)
+    step.check_inputs()
+    assert torch.isfinite(step.loss).all()
+
+
+def test_replay_survives_workspace_growth():
+    """a captured step holds the raw addresses of the fused
+    kernels' cached workspaces; an eager call on a larger block grows them --
+    the superseded buffers must stay alive (fused._ws_retired), so the next
+    replay reads and writes valid memory and gives the same gradients."""
+    import ngnn
+    from ngnn import fused
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import sample_block, synthetic_graph
+    from ngnn.losses import seed_cross_entropy
+    from ngnn.optim import Adam
+    from gradbar import assert_wgrad
+    graph = synthetic_graph("ogbn-products", DEV, seed=4, scale=0.02)
+    small = sample_block(graph, graph.train_idx[:128], [15, 10], seed=2)
+    big = sample_block(graph, graph.train_idx[:2048], [15, 10], seed=3)
+    assert big.num_nodes > 2 * small.num_nodes
+    torch.manual_seed(0)
+    model = ngnn.SAGE(100, 256, 47, 2, dropout=0.0).to(DEV).train()
+    opt = Adam(model.parameters(), lr=0.0)  # parameters fixed: replays comparable
+    n_cap, e_cap = slot_size(128, [15, 10])
+    step = GraphedTrainStep(model, opt, 128, n_cap, e_cap, 100, DEV)
+    step.capture(small.x, small.edge_index, small.y)
+    step(small.x, small.edge_index, small.y)
+    torch.cuda.synchronize()
+    g1 = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    before = {k: v.data_ptr() for k, v in fused._ws.items()}
+    # an eager step on a block with many more rows: the workspaces grow
+    other = ngnn.SAGE(100, 256, 47, 2, dropout=0.0).to(DEV).train()
+    out = other(big.x, big.edge_index)
+    seed_cross_entropy(out, big.y, big.batch_size).backward()
+    torch.cuda.synchronize()
+    grown = [k for k, v in fused._ws.items() if k in before and v.data_ptr() != before[k]]
+    assert grown, "the larger block did not grow any workspace"
+    torch.empty(1 << 28, dtype=torch.uint8, device=DEV).fill_(0xFF)  # reuse freed memory, if any
+    step(small.x, small.edge_index, small.y)
+    torch.cuda.synchronize()
+    for k, p in model.named_parameters():
+        assert_wgrad(p.grad, g1[k], msg=k)
