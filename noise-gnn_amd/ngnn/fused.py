@@ -769,6 +769,22 @@ class _SAGEStack(torch.autograd.Function):
             return (None, None, None, None, None, None, None, None, None,
                     *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views,
                                     g_pre=getattr(dout, "_ngnn_g_pre", None)))
+        if (ctx.sage2 and not ctx.h_partial and not need_dx and _use_bwd2
+                and not torch.are_deterministic_algorithms_enabled()):
+            # an eager step (the reference loop after the Option-B swap: no
+            # graph slot, F.cross_entropy on out[:batch_size]): the same
+            # two-layer backward, its row bounds from dout on the device --
+            # R = the rows of dout that can be nonzero, R' their sources'
+            # bound -- instead of the per-layer kernels (which rebuilt layer
+            # 1's aggregate over every row without a loss hint)
+            if rows_hint is None:
+                _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
+                                               stream), "ngnn_row_extent")
+            _lib.check(lib.ngnn_block_prefix_stats(_lib.ptr(block.rowptr), _lib.ptr(block.col),
+                                                   bptr(L), None, bptr(L - 1), block.E, stream),
+                       "ngnn_block_prefix_stats")
+            return (None, None, None, None, None, None, None, None, None,
+                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views))
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")

@@ -203,3 +203,49 @@ def test_stack_backward_routes_through_bwd2():
         grads.append({k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()})
     for k in grads[0]:
         assert_wgrad(grads[0][k], grads[1][k], msg=k)
+
+
+def test_eager_reference_loop_routes_through_bwd2():
+    """The reference loop on ngnn's modules without a graph slot (INTEGRATION
+    Option B: out = model(x, ei)[:bs], F.cross_entropy, backward; x needs no
+    gradient) takes ngnn_sage2_bwd with row bounds from dout on the device;
+    its gradients match the per-layer backward's and the oracle's."""
+    import torch.nn.functional as F
+
+    import ngnn
+    from ngnn import fused
+    from ngnn.loader import sample_block, synthetic_graph
+    from test_gpu_fused import _MaskedSAGE, dropout_keep
+    graph = synthetic_graph("ogbn-products", DEV, seed=6, scale=0.02)
+    b = sample_block(graph, graph.train_idx[:512], [15, 10], seed=3)
+    grads, calls, hid = [], [], None
+    orig = fused.sage2_backward
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    for use in (True, False):
+        torch.manual_seed(0)
+        model = ngnn.SAGE(100, 256, 47, 2, dropout=0.5).to(DEV).train()
+        init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        torch.manual_seed(42)
+        seed = int(torch.randint(0, 2**62, (1,)).item())
+        torch.manual_seed(42)
+        fused.sage2_backward, fused._use_bwd2, fused._debug_acts = spy, use, []
+        try:
+            out = model(b.x, b.edge_index)[:b.batch_size]
+            F.cross_entropy(out, b.y[:b.batch_size]).backward()
+            hid = [a.cpu() for a in fused._debug_acts[-1]]
+        finally:
+            fused.sage2_backward, fused._use_bwd2, fused._debug_acts = orig, True, None
+        assert bool(calls) == use
+        calls.clear()
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()})
+    ref = _MaskedSAGE(100, 256, 47, 2, dropout=0.5, gpu_hidden=hid,
+                      masks=[dropout_keep(seed, b.num_nodes, 256, 0.5).float()])
+    ref.load_state_dict(init)
+    F.cross_entropy(ref(b.x.cpu(), b.edge_index.cpu())[:b.batch_size], b.y[:b.batch_size].cpu()).backward()
+    for k, q in ref.named_parameters():
+        assert_wgrad(grads[0][k], q.grad, msg=f"bwd2:{k}")
+        assert_wgrad(grads[1][k], q.grad, msg=f"per-layer:{k}")

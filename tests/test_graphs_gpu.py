@@ -454,6 +454,10 @@ def test_replay_survives_workspace_growth():
     from ngnn.losses import seed_cross_entropy
     from ngnn.optim import Adam
     from gradbar import assert_wgrad
+    # (a fresh workspace cache, sized by this test's small slot; the older
+    # buffers retired, as a growth would)
+    fused._ws_retired.extend(fused._ws.values())
+    fused._ws.clear()
     graph = synthetic_graph("ogbn-products", DEV, seed=4, scale=0.02)
     small = sample_block(graph, graph.train_idx[:128], [15, 10], seed=2)
     big = sample_block(graph, graph.train_idx[:2048], [15, 10], seed=3)
