@@ -463,11 +463,18 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     float *sb0 = reinterpret_cast<float *>(serow + 2 * F2_ROWS);        // [256] b0
     float *sb1 = sb0 + F2_HID;                                          // [16 NT1] b1 (0 past F1)
     float *sout = sb1 + 16 * NT1;                                       // [2][16 F1] out tiles, packed rows
+    float *sf1 = sout + 2 * F2_ROWS * 16 * NT1;                         // [2][16][8] partial unscales (row, wave)
+    float *strash = sf1 + 2 * F2_ROWS * F2_WAVES;                       // [64] sink of the lanes with nothing to write
+    static_assert(PSTR >= 128, "the split's lanes 4 sslot + 3 < 128 write inside a parts row");
 
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63, q = ln >> 4, rl = ln & 15;
-    // the biases in LDS (read per tile: registers are the scarce resource here)
-    if (threadIdx.x < F2_HID) sb0[threadIdx.x] = a.b0[threadIdx.x];
+    // the biases in LDS (read per tile: registers are the scarce resource here).
+    // Bit-mode dropout (DM 2) keeps with the exact scale 2: b0, the unscale
+    // and nb carry that factor (2 (acc s + b0) + 2 nb rounds as acc 2s + 2 b0
+    // + 2 nb: scaling by two commutes with rounding), so the epilogue has no
+    // multiply
+    if (threadIdx.x < F2_HID) sb0[threadIdx.x] = DM == 2 ? 2.0f * a.b0[threadIdx.x] : a.b0[threadIdx.x];
     if (threadIdx.x < 16 * NT1) sb1[threadIdx.x] = static_cast<int>(threadIdx.x) < a.F1 ? a.b1[threadIdx.x] : 0.0f;
     // ---- this wave's weight slices, for the whole launch
     half8 wr[2][CF][2], w1[MT1][2];
@@ -612,12 +619,13 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
             p1[i] = hh;
             p2[i] = static_cast<_Float16>(vs[i] - static_cast<float>(hh));
         }
-        if (4 * sslot < KC) {
-            _Float16 *d = sxp + buf * XPB + srow * PSTR + 4 * sslot;
-            *reinterpret_cast<half4 *>(d) = p1;
-            *reinterpret_cast<half4 *>(d + F2_ROWS * PSTR) = p2;
-        }
-        if (sslot == 0) serow[buf * F2_ROWS + srow] = e;
+        // (no branches in a step: the lanes past KC write zeros into the row's
+        // padding, the row's other 31 lanes their exponent into the sink)
+        _Float16 *d = sxp + buf * XPB + srow * PSTR + 4 * sslot;
+        *reinterpret_cast<half4 *>(d) = p1;
+        *reinterpret_cast<half4 *>(d + F2_ROWS * PSTR) = p2;
+        int *ed = sslot == 0 ? serow + buf * F2_ROWS + srow : reinterpret_cast<int *>(strash) + ln;
+        *ed = e;
     };
     // layer 0's products of one tile (its parts buffer), this wave's 32
     // columns; s0 = the lane row's unscale 2^-(eW0 + e_row) (read here: the
@@ -637,7 +645,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
             xt[0] = *reinterpret_cast<const half4 *>(xp - 4 * q + 32 * CF);
             xt[1] = *reinterpret_cast<const half4 *>(xp - 4 * q + 32 * CF + F2_ROWS * PSTR);
         }
-        s0 = __builtin_amdgcn_ldexpf(1.0f, -(eW0 + serow[buf * F2_ROWS + rl]));
+        s0 = __builtin_amdgcn_ldexpf(1.0f, (DM == 2 ? 1 : 0) - (eW0 + serow[buf * F2_ROWS + rl]));
 #pragma unroll
         for (int c = 0; c < CF; ++c)
 #pragma unroll
@@ -672,11 +680,18 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float y = __builtin_fmaf(acc[mt][i], s0, b0v[mt][i]);
-                if (NB) y += nbv[mt][i];
-                bool zero = y < 0.0f;
-                if (DM == 2) zero = zero || !((hw >> (16 * mt + i)) & 1u);
-                if (DM == 1) zero = zero || ((hq >> (8 * i)) & 0xffu) < drop.thresh;
-                hv[mt][i] = zero ? 0.0f : (DM ? y * drop.scale : y);
+                if (NB) y = DM == 2 ? __builtin_fmaf(nbv[mt][i], 2.0f, y) : y + nbv[mt][i];
+                if (DM == 1) {
+                    const bool zero = y < 0.0f || ((hq >> (8 * i)) & 0xffu) < drop.thresh;
+                    hv[mt][i] = zero ? 0.0f : y * drop.scale;
+                } else {
+                    // ReLU and the keep bit as bit masks (three VALU ops):
+                    // y & ~sign(y) & keep -- +NaN passes, -NaN and -0 give +0
+                    const int yb = __float_as_int(y);
+                    int m = ~(yb >> 31);
+                    if (DM == 2) m &= __builtin_amdgcn_sbfe(static_cast<int>(hw), 16 * mt + i, 1);
+                    hv[mt][i] = __int_as_float(yb & m);
+                }
             }
         }
         // h rows the backward reads (past the bound: dropped by the range)
@@ -684,53 +699,84 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, 0);
         buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, 0);
         // layer 1: this wave's 32 rows of K -- the B fragment is the lane's own
-        // 8 values of h (k order 4q + i, 16 + 4q + i: the slice matches)
-        const float m = max_xor32(max_xor16(fmaxf(amax4(hv[0]), amax4(hv[1]))));  // lanes rl + 16 q
+        // 8 values of h (k order 4q + i, 16 + 4q + i: the slice matches).
+        // h >= +0 (or +NaN): its bit patterns order as ints
+        int mb = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mb = max(mb, __float_as_int(i < 4 ? hv[0][i] : hv[1][i - 4]));
+        const float m = max_xor32(max_xor16(__int_as_float(mb)));  // lanes rl + 16 q
         const int eh = h2_exp(m);
         half8 h1, h2;
         h2_split(ldexp4(hv[0], eh), ldexp4(hv[1], eh), h1, h2);
-        // (the unscale as a packed multiply by 2^un1: exact, a subnormal
-        // factor only for partials far below fp32's range anyway)
-        const float f1 = __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eh));
+        // the partials leave scaled: their unscale 2^-(eW1 + eh) (exact) goes
+        // to the reduce, which takes it in its fma
+        {
+            float *fd = q == 0 ? sf1 + (buf * F2_ROWS + rl) * F2_WAVES + wv : strash + ln;
+            *fd = __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eh));
+        }
         v4f *pp = spart + (buf * F2_WAVES + wv) * MT1 * 64 + ln;
         if (DBG & 2) {
-            asm volatile("" : "+v"(h1), "+v"(h2) : "v"(f1));
+            asm volatile("" : "+v"(h1), "+v"(h2));
             return;
         }
 #pragma unroll
         for (int m1 = 0; m1 < MT1; ++m1) {
-            const v4f o = mfma_h2(w1[m1][0], w1[m1][1], h1, h2, v4f{0.f, 0.f, 0.f, 0.f});
-            pp[m1 * 64] = o * f1;
+            v4f o = mfma_h2(w1[m1][0], w1[m1][1], h1, h2, v4f{0.f, 0.f, 0.f, 0.f});
+            // (a 16-state pad before the partial's LDS store: measured
+            // 82.7 vs 84.7 us per launch without it -- the pad spaces the
+            // SIMD partners' stores; not needed for correctness)
+            asm volatile("s_nop 7\n\ts_nop 7" : "+v"(o));
+            pp[m1 * 64] = o;
         }
     };
     // the 8 partials of this lane's item, summed in wave order (+ b1), stored
     // (jj < 0: the step before the first tile -- nothing live)
     // reduce(jj): the summed partials of tile jj -- out waves stage them in
     // sout[jj & 1] (+ b1), z waves keep them for their store
-    auto reduce = [&](int jj, int buf) __attribute__((always_inline)) -> v4f {
+    // (RZ: a z wave -- waves 4-7, the LAG half; compile-time inside the
+    // pipeline, so a step has no branches).  The partials are unscaled here,
+    // in the fma that sums them (wave order, as a sum of the exact products)
+    auto reduce = [&](int jj, int buf, auto z_c) __attribute__((always_inline)) -> v4f {
+        constexpr bool RZ = decltype(z_c)::value;
         const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + rmt * 64 + rln;
-        v4f s = pp[0];
+        const float *fp = sf1 + (buf * F2_ROWS + (rln & 15)) * F2_WAVES;
+        const v4f fa = *reinterpret_cast<const v4f *>(fp), fb = *reinterpret_cast<const v4f *>(fp + 4);
+        v4f s = pp[0] * fa[0];
 #pragma unroll
-        for (int w = 1; w < F2_WAVES; ++w) s += pp[w * MT1 * 64];
-        if (!rzt) s += *reinterpret_cast<const v4f *>(sb1 + rcol);
-        float *d = sout + (jj & 1) * F2_ROWS * F1 + (rln & 15) * F1 + rcol;
+        for (int w = 1; w < F2_WAVES; ++w) {
+            const v4f o = pp[w * MT1 * 64];
+            const float f = w < 4 ? fa[w] : fb[w - 4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (!rzt && ln < NIT && rcol + i < F1) d[i] = s[i];
+            for (int i = 0; i < 4; ++i) s[i] = __builtin_fmaf(o[i], f, s[i]);
+        }
+        if (!RZ) {
+            s += *reinterpret_cast<const v4f *>(sb1 + rcol);
+            // (columns past F1 and lanes >= NIT -- a repeat of lane 0's item --
+            // into the sink: with two lanes of one ds_write on the same dword,
+            // other lanes' stores sporadically did not land)
+            float *d = sout + (jj & 1) * F2_ROWS * F1 + (rln & 15) * F1 + rcol;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) *(ln < NIT && rcol + i < F1 ? d + i : strash + ln) = s[i];
+        }
         return s;
     };
     // ONE 16-B store per wave: z waves the z item of tile jz (sum s), out
     // waves piece p = threadIdx.x of the staged out tile jo (sout[jo & 1]:
     // tile jo's 16 rows are 4 F1 contiguous 16-B pieces of out)
-    auto store = [&](int jz, v4f s, int jo) __attribute__((always_inline)) {
-        const int p = static_cast<int>(threadIdx.x);  // (out waves: < 256)
-        const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
-        const int zrow = tile_of(jz) * F2_ROWS + (rln & 15);
-        const int zo = (jz >= 0 && ln < NIT && zrow < n_rows)
-                           ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
-                           : kOOB2;
-        const int oo = (jo >= 0 && p < 4 * F1) ? tile_of(jo) * F2_ROWS * F1 * 4 + 16 * p : kOOB2;
-        buf_store4(rzt ? s : v, rzt ? zrs : ors, (DBG & 16) ? kOOB2 : rzt ? zo : oo, 0, 0);
+    auto store = [&](int jz, v4f s, int jo, auto z_c) __attribute__((always_inline)) {
+        constexpr bool RZ = decltype(z_c)::value;
+        if (RZ) {
+            const int zrow = tile_of(jz) * F2_ROWS + (rln & 15);
+            const int zo = (jz >= 0 && ln < NIT && zrow < n_rows)
+                               ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
+                               : kOOB2;
+            buf_store4(s, zrs, (DBG & 16) ? kOOB2 : zo, 0, 0);
+        } else {
+            const int p = static_cast<int>(threadIdx.x);  // (out waves: < 256)
+            const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
+            const int oo = (jo >= 0 && p < 4 * F1) ? tile_of(jo) * F2_ROWS * F1 * 4 + 16 * p : kOOB2;
+            buf_store4(v, ors, (DBG & 16) ? kOOB2 : oo, 0, 0);
+        }
     };
     // the workgroup's last tile jo, which may end inside a piece (n_rows not
     // a multiple of 16): element stores for that piece
@@ -820,8 +866,8 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
                 if (!(DBG & 1)) {
                     // z of tile j - 1 / out of tile j - 2 (staged in step j - 1;
                     // the buffers differ from this step's staging writes)
-                    const v4f rs = reduce(j - 1, B ^ 1);
-                    store(j - 1, rs, j - 2);
+                    const v4f rs = reduce(j - 1, B ^ 1, lag_c);
+                    store(j - 1, rs, j - 2, lag_c);
                 }
             };
             // back: the VALU-heavy epilogue + layer-1 products, the split, the loads
@@ -841,11 +887,15 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
             // (the halves are independent within a step; SIMD partners -- waves
             // w and w + 4 -- run them in opposite orders, so one's MFMAs meet the
             // other's VALU instead of both stalling on the same phase)
+            // The halves stay apart (sched_barrier): left to interleave them,
+            // the scheduler's order measured 84.3 vs 82.7 us per launch
             if (!LAG) {
                 front();
+                __builtin_amdgcn_sched_barrier(0);
                 back();
             } else {
                 back();
+                __builtin_amdgcn_sched_barrier(0);
                 front();
             }
             lds_barrier();
@@ -888,8 +938,8 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
         if (!(DBG & 1)) {
             // z of the last tile, out of tile ntj - 2 (staged before the last
             // barrier); then the last tile's out: staged, one more barrier
-            const v4f rs = reduce(ntj - 1, (ntj - 1) & 1);
-            store(ntj - 1, rs, ntj - 2);
+            const v4f rs = reduce(ntj - 1, (ntj - 1) & 1, lag_c);
+            store(ntj - 1, rs, ntj - 2, lag_c);
             lds_barrier();
             out_store_last(ntj - 1);
         }
@@ -903,7 +953,7 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
-                       (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4;
+                       (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
     static bool attr_set = false;  // benign race: idempotent
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,

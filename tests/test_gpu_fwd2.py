@@ -110,6 +110,27 @@ def test_fwd2_ragged_blocks(N, n_act):
     torch.testing.assert_close(out, out_r, **OUT)
 
 
+@pytest.mark.parametrize("p", [0.0, 0.5, 0.25])
+def test_fwd2_many_tiles_per_workgroup(p):
+    """~12 tiles per workgroup (the blocks above give each workgroup one):
+    every step of the software pipeline -- both parts-buffer parities, the
+    edge phase and the plain phase, the reduce of the previous tile -- against
+    the oracle, and two launches bit-identical (a cross-wave race or a missed
+    register hazard shows up as scattered wrong rows that move between runs)."""
+    N, n_act, K0, H, F1 = 48_000 + 13, 9_000, 100, 256, 47
+    ei, blk = _block(31, N, n_act, deg_max=10, zero_rows=(5, 4096, 8191))
+    x = torch.randn(N, K0, generator=torch.Generator().manual_seed(32))
+    ref = _params(K0, H, F1, 4)
+    seed = 99 + int(100 * p)
+    h, out, _ = _run_fwd2(x, blk, ref, "mean", p, seed)
+    h2, out2, _ = _run_fwd2(x, blk, ref, "mean", p, seed)
+    assert torch.equal(h, h2) and torch.equal(out, out2)
+    with torch.no_grad():
+        h_r, out_r = _oracle(x, ei, ref, "mean", p, seed, N, H)
+    torch.testing.assert_close(h, h_r, **OUT)
+    torch.testing.assert_close(out, out_r, **OUT)
+
+
 @pytest.mark.parametrize("xscale,wscale", [(1e6, 1.0), (1e-8, 1.0), (1.0, 1e3), (1e4, 1e-3)])
 def test_fwd2_scaling_extremes(xscale, wscale):
     """Power-of-two scaling per row / per matrix keeps the fp16 parts in

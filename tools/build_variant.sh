@@ -1,15 +1,11 @@
 #!/bin/bash
-# Build an A/B variant of libngnn.so with extra -D flags into ablib/<name>.so:
-# the in-tree build's objects are reused, the row-tile kernel units are
-# rebuilt with the flags.  usage: tools/build_variant.sh NAME "-DFOO=1 ..."
-set -eu
+# build_variant.sh NAME "DEFINES" [SRC]: libngnn with SRC (default ngnn_fwd2.hip)
+# recompiled under DEFINES, into ablib/libngnn_NAME.so (A/B experiments)
+set -e
 cd "$(dirname "$0")/../noise-gnn_amd/csrc"
-n=$1; shift
-rm -rf build_$n && mkdir -p build_$n ../../ablib
-cp -p build/*.o build_$n/
-# (REBUILD: object stems to rebuild; default the row-tile kernel units)
-for o in ${REBUILD:-ngnn_rt_* ngnn_sage_rt.hip ngnn_root.hip}; do rm -f build_$n/$o.o; done
-make -s -j8 OBJ=build_$n OUT=../../ablib/_$n EXTRA="$*" >/dev/null
-mv ../../ablib/_$n/libngnn.so ../../ablib/$n.so && rmdir ../../ablib/_$n
-rm -rf build_$n
-echo "built ablib/$n.so"
+N=$1; D=$2; S=${3:-ngnn_fwd2.hip}
+mkdir -p /tmp/abobj_$N
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -I../../include -I. $D -c $S -o /tmp/abobj_$N/$S.o
+OBJS=$(ls build/*.o | grep -v "build/$S.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ablib/libngnn_$N.so $OBJS /tmp/abobj_$N/$S.o
+echo built ablib/libngnn_$N.so

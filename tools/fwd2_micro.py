@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--edge-dbg", default="", help="comma list of NGNN_EDGE_DBG values to time 'edge' under")
     ap.add_argument("--head", action="store_true", help="the narrow stage with the loss head (fused.LossHead)")
     ap.add_argument("--head-dbg", default="", help="comma list of NGNN_HEAD_DBG values to time 'narrow' under")
+    ap.add_argument("--all-h", action="store_true",
+                    help="write h for every row (default: rows < n_edge_rows, the step's R' bound)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     graph = synthetic_graph("ogbn-products", dev, seed=0, scale=args.scale)
@@ -43,6 +45,9 @@ def main():
     c0, c1 = model.convs
     params = [c0.lin_l.weight, c0.lin_l.bias, c0.lin_r.weight, c1.lin_l.weight, c1.lin_l.bias, c1.lin_r.weight]
     assert fused.sage2_ok(b.x, blk, "mean", params, False), "not the sage2 shape"
+    if not args.all_h:  # h rows as in the step: the slot's R' (rows with in-edges)
+        n_e_ = int(blk.n_active or 0)
+        blk.r_next = (torch.tensor([n_e_], dtype=torch.int32, device=dev), n_e_, True)
     seed = 12345
     head = None
     if args.head:
