@@ -418,7 +418,30 @@ __global__ __launch_bounds__(256) void k_gcn_agg(const float *__restrict__ z, in
     }
 }
 
+// W_l [Fo, K] (bf16-exact fp32 values, row stride ldw) -> the bf16 image
+// [NT][CL][64] x 8 of the row-tile kernel's bf16 neighbour term (RtArgs::wlb):
+// element j of lane (q, m) in chunk c is W_l[16 t + m][32 c + 4 q + j] (j < 4)
+// or [32 c + 16 + 4 q + j - 4] (j >= 4); zero outside Fo x K.  One thread per
+// element (RNE conversion -- exact on bf16-exact weights).
+__global__ __launch_bounds__(256) void k_pack_wl_b16(const float *__restrict__ w, int64_t ldw, int Fo, int K,
+                                                     int CL, int NT, uint16_t *__restrict__ dst) {
+    const int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+    if (idx >= static_cast<int64_t>(NT) * CL * 512) return;
+    const int j = idx & 7, lane = (idx >> 3) & 63;
+    const int64_t tc = idx >> 9;
+    const int c = static_cast<int>(tc % CL), t = static_cast<int>(tc / CL);
+    const int q = lane >> 4, n = 16 * t + (lane & 15);
+    const int k = 32 * c + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
+    const float v = (n < Fo && k < K) ? w[static_cast<int64_t>(n) * ldw + k] : 0.0f;
+    dst[idx] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+}
+
 }  // namespace
+
+// bytes of the bf16 W_l image (k_pack_wl_b16)
+size_t wl_b16_bytes(int64_t Fo, int64_t K) {
+    return static_cast<size_t>(ceil_div(Fo, 16)) * static_cast<size_t>(ceil_div(K, 32)) * 64 * 16;
+}
 
 // out[d, :Fo] += mean / sum_{e into d} z[col[e], :Fo] for the rows with
 // in-edges (the narrow output layer's neighbour term; also ngnn_fwd2.hip);
@@ -585,6 +608,28 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             }
             a.wl = static_cast<const v4f *>(wl_ws) + toff;
         }
+        // one-part (bf16-exact) W_l streamed from L2: the neighbour term on
+        // bf16 MFMA from a bf16 image behind the packed fp32 one in the
+        // workspace (the kernel's W1 streamed form has no fp32 steps)
+        a.wlb = nullptr;
+        a.CL = static_cast<int>(ceil_div(K, 32));
+        if (w1 && has_l && !wl_lds) {
+            if (!ldw || !wl_ws || wl_ws_bytes < ngnn_pack_weight_bytes(Fo, K) + wl_b16_bytes(Fo, K)) {
+                *rc = NGNN_E_WORKSPACE;
+                return 1;
+            }
+            uint16_t *img16 = reinterpret_cast<uint16_t *>(static_cast<char *>(wl_ws) + ngnn_pack_weight_bytes(Fo, K));
+            if (c0 == 0) {
+                const int NTa = static_cast<int>(ceil_div(Fo, 16));
+                const int64_t total = static_cast<int64_t>(NTa) * a.CL * 512;
+                hipLaunchKernelGGL(k_pack_wl_b16, dim3(static_cast<unsigned>(ceil_div(total, 256))), dim3(256), 0, st,
+                                   static_cast<const float *>(wl_packed), ldw, static_cast<int>(Fo),
+                                   static_cast<int>(K), a.CL, NTa, img16);
+                *rc = launch_status();
+                if (*rc) return 1;
+            }
+            a.wlb = img16 + (c0 / 16) * a.CL * 64 * 8;
+        }
         a.NT = NT;
         a.NT1 = NT1;
         // (unknown: every row may have in-edges -- no root-only phase)
@@ -670,8 +715,9 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64
     const size_t wide = (sage_wide_preferred(K, Fo, false) || sage_wide_preferred(K, Fo, true))
                             ? sage_wide_workspace_bytes(K, n_rows)
                             : 0;
-    // + the prebuilt root image at the workspace's tail (kImgWsBytes)
-    return std::max({ngnn_pack_weight_bytes(Fo, K), z, wide}) + kImgWsBytes;
+    // + the prebuilt root image at the workspace's tail (kImgWsBytes); the
+    // packed W_l is followed by its bf16 image (one-part layers)
+    return std::max({ngnn_pack_weight_bytes(Fo, K) + wl_b16_bytes(Fo, K), z, wide}) + kImgWsBytes;
 }
 
 extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *xrow,
@@ -715,7 +761,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     // the root image's region: the workspace's last kImgWsBytes (16-B aligned)
     // when the rest still holds z (narrow) / a packed W_l
     const size_t head = want_narrow ? static_cast<size_t>(n_rows) * ldz * sizeof(float)
-                                    : ngnn_pack_weight_bytes(Fo, K);
+                                    : ngnn_pack_weight_bytes(Fo, K) + wl_b16_bytes(Fo, K);
     void *img_ws = nullptr;
     // (NGNN_IMG=0, read once: every workgroup builds its image -- A/B only)
     static const bool img_on = [] {

@@ -10,6 +10,9 @@
 #ifndef NGNN_RT_WSTREAM_DEPTH
 #define NGNN_RT_WSTREAM_DEPTH 2  // (A/B build flag) W_l fragment groups in flight from L2
 #endif
+#ifndef NGNN_RT_NB_H
+#define NGNN_RT_NB_H 4  // (A/B build flag) output tiles per streamed group of the bf16 neighbour term
+#endif
 #ifndef NGNN_RT_MAXNTW
 #define NGNN_RT_MAXNTW 16  // (A/B build flag) widest output-tile slice
 #endif
@@ -132,6 +135,14 @@ struct RtArgs {
     const float *wz_raw;
     float *z;
     int64_t ldz;
+    // non-null (one-part W1 layers, W_l streamed from L2): W_l as a bf16
+    // image [NT][CL][64] x 16 B for the neighbour term on 16x16x32 bf16 MFMA
+    // (k_pack_wl_b16: lane (q, m) holds W_l[16 t + m][32 c + 4 q + j] for j <
+    // 4 and [32 c + 16 + 4 q + j - 4] for j >= 4 -- the order of the fp32
+    // aggregate fragments ag[2 c], ag[2 c + 1] the lane already holds);
+    // CL = ceil(K / 32)
+    const void *wlb;
+    int CL;
 };
 
 namespace {
@@ -461,6 +472,54 @@ __device__ __forceinline__ void mfma_chunk_rt(v4f (&acc)[NTW], const v4f (&xf)[R
                 for (int h = 0; h < H; ++h)
                     acc[p * H + h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[s % NB][h][i], xf[g][i],
                                                                           acc[p * H + h], 0, 0, 0);
+        }
+    }
+}
+
+// neighbour term of one 128-column group on bf16 MFMA (W1 layers: W_l is
+// bf16-exact, one part): per 32-deep chunk the lane's fp32 aggregate values
+// (ag[2 c], ag[2 c + 1]: columns 32 c + 4 q .. + 3 and 32 c + 16 + 4 q .. + 3
+// of its row) split into three bf16 parts (|agg - a1 - a2 - a3| <= 2^-24
+// |agg|, split3), three v_mfma_f32_16x16x32_bf16 per output tile against the
+// W_l image of the same column order, smallest product first -- the
+// fp32-exact 16x16x4 f32 steps this replaces cost 5.3x the MFMA cycles.  The
+// image streams from L2 in groups of H output tiles, one group ahead, over
+// the chunks without a restart.  Chunks past nkg (columns past K) are
+// skipped; their image slots are zero anyway.
+template <int NTW>
+__device__ __forceinline__ void nb_chunk_b16(v4f (&acc)[NTW], const v4f (&ag)[RT_KC],
+                                             const bf16x8 *__restrict__ wlb, int CL, int cc0,
+                                             int nkg, int NT, int lane) {
+    asm volatile("" : "+s"(NT));
+    asm volatile("" : "+s"(CL));
+    constexpr int H = NTW % NGNN_RT_NB_H == 0 ? NGNN_RT_NB_H : NTW % 3 == 0 ? 3 : NTW;  // tiles per streamed group
+    constexpr int NG = NTW / H;
+    constexpr int NS = (RT_KC / 2) * NG;  // steps: (32-chunk, group)
+    auto wload = [&](bf16x8 (&w)[H], int s) __attribute__((always_inline)) {
+        const int cc = min(cc0 + s / NG, CL - 1);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            const int m = min((s % NG) * H + h, NT - 1);
+            w[h] = wlb[(static_cast<int64_t>(m) * CL + cc) * 64 + lane];
+        }
+    };
+    bf16x8 wb[2][H];
+    bf16x8 x1, x2, x3;
+    wload(wb[0], 0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int c = s / NG, g = s % NG;
+        if (s + 1 < NS) wload(wb[(s + 1) & 1], s + 1);
+        if (g == 0) split3<false>(ag[2 * c], ag[2 * c + 1], x1, x2, x3);
+        if (2 * c < nkg) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const int m = g * H + h;
+                v4f t = acc[m];
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[s & 1][h], x3, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[s & 1][h], x2, t, 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[s & 1][h], x1, t, 0, 0, 0);
+            }
         }
     }
 }
@@ -1202,10 +1261,13 @@ __global__ __launch_bounds__(RT_WAVES * 64) void k_sage_rt(RtArgs a) {
                         if (g < nkg) buf_store4(ag[g], ar, ((aoff + 64 * g) & mk) | (kOOB & ~mk), 0, 0);
                     }
                 }
-                if constexpr (WL_LDS)
+                if constexpr (WL_LDS) {
                     mfma_chunk_rt<NTW, true>(acc, ag, swl, a.KG, c * RT_KC, nkg, a.NT, lane);
-                else
+                } else if constexpr (W1) {  // (the host always provides the bf16 image here)
+                    nb_chunk_b16<NTW>(acc, ag, static_cast<const bf16x8 *>(a.wlb), a.CL, 4 * c, nkg, a.NT, lane);
+                } else {
                     mfma_chunk_rt<NTW, false>(acc, ag, a.wl, a.KG, c * RT_KC, nkg, a.NT, lane);
+                }
             }
         }
 

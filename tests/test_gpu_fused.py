@@ -623,9 +623,14 @@ def test_bf16_features_stack_matches_widened(layers):
 def test_bf16_weights_one_part_image_bitwise(K, Fo, narrow, reduce, xdt):
     """NGNN_W_BF16 (a bf16 model's weights, widened): the one-part split
     image skips the products with the weights' second and third parts, which
-    are exact zeros, so the layer is BITWISE the three-part layer -- with
-    fp32 and bf16 rows, across column slices (256 -> 256 takes 3 slices with
-    the three-part image and 1 with one part), and in narrow mode."""
+    are exact zeros -- the root term is BITWISE the three-part layer's (narrow
+    mode: the whole layer), with fp32 and bf16 rows, across column slices
+    (256 -> 256 takes 3 slices with the three-part image and 1 with one
+    part).  The neighbour term of a one-part layer streaming W_l runs on bf16
+    MFMA (the aggregate split in three bf16 parts against the bf16 W_l image,
+    csrc/ngnn_sage_rt_kern.h nb_chunk_b16) instead of exact fp32 steps: the two
+    layers then agree within the fp32 bars, and the saved aggregate is the
+    same bits."""
     if narrow and xdt == torch.bfloat16:
         pytest.skip("narrow mode reads fp32 rows")
     N, E = 900, 6000
@@ -644,8 +649,10 @@ def test_bf16_weights_one_part_image_bitwise(K, Fo, narrow, reduce, xdt):
         o = sage_layer_fwd(x, blk, reduce, wl, bl, wr, seed=5, agg_out=agg, narrow=narrow,
                            w_bf16=w1, **epi)
         outs.append((o.cpu(), None if agg is None else agg.cpu()))
-    assert torch.equal(outs[0][0], outs[1][0])
-    if not narrow:
+    if narrow:
+        assert torch.equal(outs[0][0], outs[1][0])
+    else:
+        torch.testing.assert_close(outs[0][0], outs[1][0], **OUT)
         assert torch.equal(outs[0][1], outs[1][1])
     with torch.no_grad():
         c2 = pyg_ref.SAGEConv(K, Fo, aggr=reduce)
