@@ -245,6 +245,7 @@ constexpr size_t kImgWsBytes = 160 * 1024;
 // the workspace) + a 2-D tiled fp32-MFMA dual GEMM.  Raw [F_out, K] weights.
 bool sage_wide_preferred(int64_t K, int64_t Fo, bool exact);
 size_t sage_wide_workspace_bytes(int64_t K, int64_t n_rows);
+size_t wide_wimg_bytes(int64_t K, int64_t Fo);  // the split-bf16 weight image (at the workspace's tail)
 int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                         const int32_t *n_rows_dev, int64_t n_edge_rows,
                         const int32_t *n_edge_rows_dev, const int32_t *rowptr, const int32_t *col,
@@ -255,6 +256,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,
                   const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
                   int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
-                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st);
+                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st,
+                  bool exact = false);
 
 }  // namespace ngnn

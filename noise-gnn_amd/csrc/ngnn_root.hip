@@ -334,6 +334,20 @@ __global__ __launch_bounds__(256) void k_x3_image(RtArgs a, v4f *dst) {
         const float *row = wrow(n);
         swt[st] = (row && k < a.K) ? row[k] : 0.0f;
     }
+    // the bf16 W_l image of the neighbour term (k_pack_wl_b16's layout), one
+    // 16-B slot per thread past the root image's slots
+    const int sb = st - a.T4 * NTW * 64;
+    if (a.wlb_src && sb >= 0 && sb < ((a.wlb_fo + 15) >> 4) * a.CL * 64) {
+        const int l = sb & 63, c = (sb >> 6) % a.CL, t = (sb >> 6) / a.CL;
+        const int q = l >> 4, n = 16 * t + (l & 15);
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * c + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4);
+            v[j] = static_cast<__bf16>((n < a.wlb_fo && k < a.K) ? a.wlb_src[static_cast<int64_t>(n) * a.ldw + k] : 0.0f);
+        }
+        reinterpret_cast<bf16x8 *>(const_cast<void *>(a.wlb))[sb] = v;
+    }
 }
 
 #if NGNN_ROOT_TRACE
@@ -349,7 +363,8 @@ size_t x3_image_bytes(int ntw, int C, int T4, bool w1) {
 }
 
 int build_image(RtArgs &a, int ntw, void *dst, hipStream_t st) {
-    const int slots = a.C * ntw * 64 + a.T4 * ntw * 64;
+    const int slots = a.C * ntw * 64 + a.T4 * ntw * 64 +
+                      (a.wlb_src ? static_cast<int>(ceil_div(a.wlb_fo, 16)) * a.CL * 64 : 0);
     const unsigned grid = static_cast<unsigned>(ceil_div(slots, 256));
     v4f *d = static_cast<v4f *>(dst);
     const bool w1 = a.w1 != 0;

@@ -153,6 +153,50 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded); MASK: 
             *reinterpret_cast<T *>(lds + r * ldl + c) = w;
         }
     }
+
+    // X3 staging (VEC only): the masked values as three bf16 parts (round to
+    // nearest: v - p1 - p2 - p3 <= 2^-24 |v|) into the images img[0..NP) of
+    // row stride ld (bf16 elements); NP == 1 for bf16 rows (exact in one
+    // part, stored as loaded)
+    template <int NP>
+    __device__ __forceinline__ void store_parts(__bf16 *img0, __bf16 *img1, __bf16 *img2, int ld,
+                                                float mscale) const {
+        static_assert(VEC, "16-B staging");
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            const int idx = static_cast<int>(threadIdx.x) + u * 512;
+            const int r = idx / CPR, c = (idx % CPR) * W;
+            if constexpr (NP == 1 && BF && !MASK && !DEG) {
+                *reinterpret_cast<i32x2 *>(img0 + r * ld + c) = raw[u];
+                continue;
+            }
+            T w;
+            if constexpr (BF) w = bf16x4_to_f32(raw[u]);
+            else w = v[u];
+            T mv;
+            if constexpr (MASK == 2) mv = bf16x4_to_f32(mraw[u]);
+            else mv = m[MASK ? u : 0];
+            typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+            b4 p1, p2, p3;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float x = w[i];
+                if (MASK) x = mv[i] > 0.f ? x * mscale : 0.f;
+                if (DEG) x = d1[u] > d0[u] ? x : 0.f;
+                const __bf16 h1 = static_cast<__bf16>(x);
+                const float r1 = x - static_cast<float>(h1);
+                const __bf16 h2 = static_cast<__bf16>(r1);
+                p1[i] = h1;
+                p2[i] = h2;
+                p3[i] = static_cast<__bf16>(r1 - static_cast<float>(h2));
+            }
+            *reinterpret_cast<b4 *>(img0 + r * ld + c) = p1;
+            if constexpr (NP > 1) {
+                *reinterpret_cast<b4 *>(img1 + r * ld + c) = p2;
+                *reinterpret_cast<b4 *>(img2 + r * ld + c) = p3;
+            }
+        }
+    }
 };
 
 // the MFMAs of one staged chunk: nks 4-row k-steps, KTN (<= KTW) live K tiles
@@ -297,6 +341,188 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_partial(
             for (int g = 0; g < 8; ++g) t += smem[g * 64 + lane];
             slab[2 * static_cast<size_t>(Fo) * K + n0 + lane] = t;
         }
+    }
+}
+
+// ---- the weight gradient on bf16 MFMA (X3), Fo >= 64 with 16-B rows: the
+// grid, slices and slab layout of k_wgrad_partial (k_wgrad_reduce unchanged).
+// Per 64-row chunk the operands are staged in LDS as bf16 parts (dz and agg:
+// three, RNE split3; h: three, or one for bf16 rows), and wave (mat = w >> 2,
+// Fo tile w & 3) multiplies over the rows with v_mfma_f32_16x16x32_bf16 --
+// A = dz^T, B = h (mat 0) / agg (mat 1), both through transposed LDS reads
+// (ds_read_b64_tr_b16) in the row order {4q .. 4q+3, 16+4q .. 16+4q+3} of
+// each 32-row step.  fp32 x fp32: the six products of the X3 forward
+// (v1w1, v1w2, v2w1, v2w2, v1w3, v3w1; the dropped ones <= 2^-26 relative,
+// each product exact in fp32), one-part bf16 h: three.  Against the exact
+// 16x16x4 f32 steps: 16 vs 256 cycles per 32 rows and product.  db (column
+// sums of dz) rides on the mat-0 waves as three more MFMAs per step against
+// a ones operand.
+constexpr int X3H = WG_KC + 16;  // LDS row strides (bf16): 72 dwords (and 40 / 72 for dz, below),
+                                 // odd multiples of 8 -- transposed reads conflict-free
+typedef __attribute__((address_space(3))) __bf16 LB16;
+typedef short s4w __attribute__((ext_vector_type(4)));
+typedef short s8w __attribute__((ext_vector_type(8)));
+typedef __bf16 b8w __attribute__((ext_vector_type(8)));
+
+// the MFMA operand of 32 rows x 16 columns c0 .. + 15 of a [rows][stride]
+// bf16 image: lane (q, i) holds column c0 + i of rows 4q .. 4q+3, 16+4q ..
+__device__ __forceinline__ b8w x3_frag(const LB16 *img, int stride, int c0, int ln) {
+    const int q = ln >> 4, i = ln & 15;
+    const LB16 *p = img + (4 * q + (i >> 2)) * stride + c0 + 4 * (i & 3);
+    const s4w a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4w *)(p));
+    const s4w b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4w *)(p + 16 * stride));
+    const s8w v{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(b8w, v);
+}
+
+// NFW: Fo tiles per wave -- a workgroup covers 64 NFW columns of Fo, so the
+// h / agg rows are read ceil(Fo / 64 NFW) times (NFW 2: half the re-reads of
+// the products layers' 256-wide Fo; bf16 h only, where the images fit in LDS)
+template <bool HB, int MASK, int NFW>
+__global__ __launch_bounds__(512, 1) void k_wgrad_x3(
+    const float *__restrict__ dy, int64_t ldy, const float *__restrict__ y, int64_t ldyy,
+    float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
+    const int64_t *h_idx_arg, const int64_t *const *h_idx_dev, int64_t h_rows,
+    const float *__restrict__ agg, int64_t ld_agg, const int32_t *__restrict__ rowptr,
+    const int32_t *__restrict__ r_ptr, int Fo, int K, float *__restrict__ ws) {
+    constexpr int NPH = HB ? 1 : 3;
+    constexpr int WNC = WG_NC * NFW;  // Fo columns per workgroup
+    constexpr int X3Z = WNC + 16;
+    extern __shared__ __attribute__((aligned(16))) __bf16 x3s[];
+    __bf16 *zi = x3s;                              // [3][64][X3Z]
+    __bf16 *hi = zi + 3 * WG_BM * X3Z;             // [NPH][64][X3H]
+    __bf16 *ai = hi + NPH * WG_BM * X3H;           // [3][64][X3H]
+    const float *__restrict__ h = h_dev ? *h_dev : h_arg;
+    const int64_t *h_idx = h_idx_dev ? *h_idx_dev : h_idx_arg;
+    const int R = *r_ptr;
+    const int S = wgrad_slices(R, gridDim.x);
+    const int s = blockIdx.x;
+    if (s >= S) return;
+    const int R4 = (R + 3) >> 2;
+    const int rb = 4 * static_cast<int>(static_cast<int64_t>(s) * R4 / S);
+    const int re = min(R, 4 * static_cast<int>(static_cast<int64_t>(s + 1) * R4 / S));
+    const int k0 = blockIdx.y * WG_KC;
+    const int n0 = blockIdx.z * WNC;
+    const int kc = min(WG_KC, K - k0);
+    const int nc = min(WNC, Fo - n0);
+    const int KT = __builtin_amdgcn_readfirstlane((kc + 15) >> 4);
+    const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int ln = threadIdx.x & 63;
+    const int mat = wv >> 2, w4 = wv & 3;
+    const bool do_bias = blockIdx.y == 0 && mat == 0;
+
+    v4f acc[NFW][8], accb[NFW];
+#pragma unroll
+    for (int f = 0; f < NFW; ++f) {
+        accb[f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[f][b] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+    b8w ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.0f);
+
+    Chunk<WNC, true, MASK, false> cz;
+    Chunk<WG_KC, true, false, false, HB> ch;
+    Chunk<WG_KC, true, false, true> ca;
+    if (rb < re) {
+        cz.load(dy, ldy, y, ldyy, nullptr, rb, re, n0, Fo);
+        ch.load(h, ldh, nullptr, 0, nullptr, rb, re, k0, K, h_idx, h_rows);
+        ca.load(agg, ld_agg, nullptr, 0, rowptr, rb, re, k0, K);
+    }
+    const LB16 *lz = (const LB16 *)(zi), *lh = (const LB16 *)(hi), *la = (const LB16 *)(ai);
+    // the chunk loop, one copy per B-operand part count (one: the bf16 h of
+    // the mat-0 waves) -- straight-line MFMA code in each (a run-time branch
+    // between the two forms inside the loop made the compiler spill ~2.6 k
+    // VGPRs)
+    auto run = [&](auto nbp_c) __attribute__((always_inline)) {
+        constexpr int NB = decltype(nbp_c)::value;
+        const LB16 *lb = mat ? la : lh;
+        for (int c0 = rb; c0 < re; c0 += WG_BM) {
+            __syncthreads();  // the previous chunk's MFMAs are done with LDS
+            cz.template store_parts<3>(zi, zi + WG_BM * X3Z, zi + 2 * WG_BM * X3Z, X3Z, yscale);
+            ch.template store_parts<NPH>(hi, hi + WG_BM * X3H, hi + 2 * WG_BM * X3H, X3H, 1.0f);
+            ca.template store_parts<3>(ai, ai + WG_BM * X3H, ai + 2 * WG_BM * X3H, X3H, 1.0f);
+            __syncthreads();
+            const int c1 = c0 + WG_BM;
+            if (c1 < re) {  // the next chunk's loads overlap this chunk's MFMAs
+                cz.load(dy, ldy, y, ldyy, nullptr, c1, re, n0, Fo);
+                ch.load(h, ldh, nullptr, 0, nullptr, c1, re, k0, K, h_idx, h_rows);
+                ca.load(agg, ld_agg, nullptr, 0, rowptr, c1, re, k0, K);
+            }
+            const int nsteps = re - c0 > 32 ? 2 : 1;  // 32-row MFMA steps holding rows (uniform)
+            for (int ks = 0; ks < nsteps; ++ks) {
+                const int ro = 32 * ks;
+                // Fo tiles NFW w4 + f of the workgroup's 4 NFW
+                b8w a1[NFW], a2[NFW], a3[NFW];
+#pragma unroll
+                for (int f = 0; f < NFW; ++f) {
+                    const int c = 16 * (NFW * w4 + f);
+                    a1[f] = x3_frag(lz + ro * X3Z, X3Z, c, ln);
+                    a2[f] = x3_frag(lz + (WG_BM + ro) * X3Z, X3Z, c, ln);
+                    a3[f] = x3_frag(lz + (2 * WG_BM + ro) * X3Z, X3Z, c, ln);
+                    if (do_bias) {
+                        accb[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[f], ones, accb[f], 0, 0, 0);
+                        accb[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[f], ones, accb[f], 0, 0, 0);
+                        accb[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[f], ones, accb[f], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int kt = 0; kt < 8; ++kt) {
+                    if (kt < KT) {
+                        const b8w b1 = x3_frag(lb + ro * X3H, X3H, 16 * kt, ln);
+                        b8w b2, b3;
+                        if constexpr (NB == 3) {
+                            b2 = x3_frag(lb + (WG_BM + ro) * X3H, X3H, 16 * kt, ln);
+                            b3 = x3_frag(lb + (2 * WG_BM + ro) * X3H, X3H, 16 * kt, ln);
+                        }
+#pragma unroll
+                        for (int f = 0; f < NFW; ++f) {
+                            v4f t = acc[f][kt];
+                            if constexpr (NB == 1) {
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[f], b1, t, 0, 0, 0);
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[f], b1, t, 0, 0, 0);
+                            } else {
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[f], b1, t, 0, 0, 0);
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[f], b3, t, 0, 0, 0);
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[f], b2, t, 0, 0, 0);
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[f], b1, t, 0, 0, 0);
+                                t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[f], b2, t, 0, 0, 0);
+                            }
+                            acc[f][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[f], b1, t, 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+    };
+    if (HB && mat == 0) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, 3>{});
+    // ---- partial slab [Pr Fo x K][Pl Fo x K][Pb Fo] (k_wgrad_partial's layout)
+    float *slab = ws + static_cast<size_t>(s) * slab_floats(Fo, K);
+    const i32x4 prs = make_rsrc(slab + static_cast<size_t>(mat) * Fo * K,
+                                static_cast<uint32_t>(Fo) * static_cast<uint32_t>(K) * 4u);
+    const int i16 = ln & 15, q = ln >> 4;
+#pragma unroll
+    for (int f = 0; f < NFW; ++f)
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) {
+            const int k = k0 + 16 * kt + i16;
+            const bool kok = k < K && kt < KT;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = n0 + 16 * (NFW * w4 + f) + 4 * q + j;
+                buf_store1(acc[f][kt][j], prs, (kok && n < n0 + nc) ? (n * K + k) * 4 : kBufOOB, 0, 0);
+            }
+        }
+    if (do_bias && i16 == 0) {
+#pragma unroll
+        for (int f = 0; f < NFW; ++f)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = 16 * (NFW * w4 + f) + 4 * q + j;
+                if (n < nc) slab[2 * static_cast<size_t>(Fo) * K + n0 + n] = accb[f][j];
+            }
     }
 }
 
@@ -994,7 +1220,49 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
     const int NT = static_cast<int>(ceil_div(std::min<int64_t>(Fo, WG_NC), 16));
 #define NGNN_WG_ARGS grid, st, vz, vh, dy, ldy, y, ldyy, y_bf16, yscale, h, h_dev, ldh, h_idx, h_idx_dev, \
                      h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf
-    if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
+    // (NGNN_WGRAD_X3=0, read once: the exact-f32 MFMA kernel for every shape -- A/B)
+    static const bool x3_on = [] {
+        const char *e = std::getenv("NGNN_WGRAD_X3");
+        return !(e && e[0] == '0');
+    }();
+    if (NT == 4 && vz && vh && x3_on) {
+        const bool hb = vh == 2;
+        // bf16 h with Fo >= 128: two Fo tiles per wave (half the h / agg re-reads)
+        // (NGNN_WGRAD_NFW=2, read once: two Fo tiles per wave -- half the
+        // h / agg re-reads, but the bf16-mask form spills: 429 vs 250 us on
+        // config #3's layer 0, A/B only)
+        static const int nfw_max = [] {
+            const char *e = std::getenv("NGNN_WGRAD_NFW");
+            return e ? std::max(1, std::min(2, std::atoi(e))) : 1;
+        }();
+        const int nfw = hb && Fo >= 128 ? nfw_max : 1;
+        const size_t lds = (static_cast<size_t>(3) * WG_BM * (WG_NC * nfw + 16) + (hb ? 1 : 3) * WG_BM * X3H +
+                            static_cast<size_t>(3) * WG_BM * X3H) * 2;
+        const dim3 grid2(S, static_cast<unsigned>(gy), static_cast<unsigned>(ceil_div(Fo, WG_NC * nfw)));
+        auto go = [&](auto hb_c, auto m_c) {
+            constexpr bool HBv = decltype(hb_c)::value;
+            auto fn = (HBv && nfw == 2) ? k_wgrad_x3<HBv, decltype(m_c)::value, 2>
+                                        : k_wgrad_x3<HBv, decltype(m_c)::value, 1>;
+            static bool attr[3] = {false, false, false};  // per NFW; benign race: idempotent
+            if (!attr[nfw]) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr[nfw] = true;
+            }
+            hipLaunchKernelGGL(fn, grid2, dim3(512), lds, st, dy, ldy, y, ldyy, yscale, h, h_dev, ldh,
+                               h_idx, h_idx_dev, h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf);
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        auto by_mask = [&](auto hb_c) {
+            if (y && y_bf16) go(hb_c, I2{});
+            else if (y) go(hb_c, I1{});
+            else go(hb_c, I0{});
+        };
+        if (hb) by_mask(std::true_type{});
+        else by_mask(std::false_type{});
+    } else if (NT == 4) launch_wgrad<1, 8, true>(NGNN_WG_ARGS);
     else if (NT == 1) launch_wgrad<1, 2, false>(NGNN_WG_ARGS);
     else if (NT == 2) launch_wgrad<2, 2, false>(NGNN_WG_ARGS);
     else launch_wgrad<3, 2, false>(NGNN_WG_ARGS);

@@ -592,7 +592,8 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         if (ldw && has_l && !wl_lds) {
             // raw W_l that must stream from L2: pack it once (all slices) into
             // the caller's workspace -- fragment-ordered 1-KiB wave loads
-            if (c0 == 0) {
+            // (one-part layers stream the bf16 image below instead: no fp32 pack)
+            if (c0 == 0 && !w1) {
                 if (!wl_ws || wl_ws_bytes < ngnn_pack_weight_bytes(Fo, K)) {
                     *rc = NGNN_E_WORKSPACE;
                     return 1;
@@ -612,14 +613,21 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         // bf16 MFMA from a bf16 image behind the packed fp32 one in the
         // workspace (the kernel's W1 streamed form has no fp32 steps)
         a.wlb = nullptr;
+        a.wlb_src = nullptr;
+        a.wlb_fo = static_cast<int>(Fo);
         a.CL = static_cast<int>(ceil_div(K, 32));
+        // (the root image's launch packs it too when that image is prebuilt)
+        const bool img_pre = x3 && !no_root && img_ws && x3_image_bytes(NTW, C, T4, w1) <= kImgWsBytes;
         if (w1 && has_l && !wl_lds) {
             if (!ldw || !wl_ws || wl_ws_bytes < ngnn_pack_weight_bytes(Fo, K) + wl_b16_bytes(Fo, K)) {
                 *rc = NGNN_E_WORKSPACE;
                 return 1;
             }
             uint16_t *img16 = reinterpret_cast<uint16_t *>(static_cast<char *>(wl_ws) + ngnn_pack_weight_bytes(Fo, K));
-            if (c0 == 0) {
+            if (c0 == 0 && img_pre) {
+                a.wlb = img16;
+                a.wlb_src = static_cast<const float *>(wl_packed);
+            } else if (c0 == 0) {
                 const int NTa = static_cast<int>(ceil_div(Fo, 16));
                 const int64_t total = static_cast<int64_t>(NTa) * a.CL * 512;
                 hipLaunchKernelGGL(k_pack_wl_b16, dim3(static_cast<unsigned>(ceil_div(total, 256))), dim3(256), 0, st,
@@ -666,10 +674,11 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         // the split-bf16 root image built once (k_x3_image) into img_ws and
         // DMA-copied by every workgroup (else each workgroup builds it)
         a.img = nullptr;
-        if (x3 && !no_root && img_ws && x3_image_bytes(NTW, C, T4, w1) <= kImgWsBytes) {
+        if (img_pre) {
             *rc = build_image(a, NTW, img_ws, st);
             if (*rc) return 1;
         }
+        a.wlb_src = nullptr;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         // the tiles past the edge-row bound on k_root (ngnn_root.hip) when an
         // instantiation covers this layer: k_sage_rt takes the tiles with
@@ -713,7 +722,7 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64
     const size_t z = static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * ceil_div(Fo, 16) * 16 *
                      sizeof(float);
     const size_t wide = (sage_wide_preferred(K, Fo, false) || sage_wide_preferred(K, Fo, true))
-                            ? sage_wide_workspace_bytes(K, n_rows)
+                            ? sage_wide_workspace_bytes(K, n_rows) + wide_wimg_bytes(K, Fo) + 256
                             : 0;
     // + the prebuilt root image at the workspace's tail (kImgWsBytes); the
     // packed W_l is followed by its bf16 image (one-part layers)
@@ -791,7 +800,7 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
         (agg_out || !wl || ws_bytes >= sage_wide_workspace_bytes(K, n_edge_rows)))
         return sage_fwd_wide(x, ldx, K, n_rows, n_rows_dev, n_edge_rows, n_edge_rows_dev, rowptr,
                              col, reduce, wl, wr, ldw, bias, Fo, out, ldo, relu, p_drop, seed,
-                             seed_dev, agg_out, ld_agg, ws, ws_bytes, st);
+                             seed_dev, agg_out, ld_agg, ws, ws_bytes, st, exact);
     // max layers with a wide input: the aggregate by its own launch (a wave per
     // row, every column in flight) into the saved-aggregate buffer, which the
     // row-tile kernel's edge tiles then read densely -- its in-kernel gather

@@ -143,6 +143,10 @@ struct RtArgs {
     // CL = ceil(K / 32)
     const void *wlb;
     int CL;
+    // non-null: k_x3_image also packs the bf16 W_l image (wlb, all wlb_fo
+    // rows) from these raw rows (row stride ldw) -- one launch for both images
+    const float *wlb_src;
+    int wlb_fo;
 };
 
 namespace {

@@ -29,6 +29,7 @@
 // 157.3 TF f32 MFMA peak; bytes x (N K 4) + gathered rows (E K 4) + agg write
 // and re-read (2 N_edge K 4) + out (N F_out 4).
 #include <algorithm>
+#include <cstdlib>
 
 #include "ngnn_device.h"
 
@@ -276,7 +277,208 @@ __global__ __launch_bounds__(256, 2) void k_wide_gemm(WideArgs a) {
     }
 }
 
+// ---- the split-bf16 (X3) form of k_wide_gemm: the same tiles, stages and
+// epilogue, the products on v_mfma_f32_16x16x32_bf16.  Each operand value v =
+// v1 + v2 + v3 (bf16, RNE; |v - v1 - v2 - v3| <= 2^-24 |v|) and the six
+// products whose magnitude reaches 2^-18 of the leading one (v1w1, v1w2,
+// v2w1, v2w2, v1w3, v3w1; each exact in fp32) -- the row-tile kernel's
+// root-term arithmetic (ngnn_sage_rt.hip), here for the
+// neighbour term too: 16 cycles per 32-deep k-step and product against 256
+// for the exact f32 steps (2.7x fewer MFMA cycles).  W_r / W_l are split ONCE
+// per launch into a global image (k_wide_wimg: [mat][part][Fo][Kp] bf16, Kp =
+// K rounded up to 32, zero padded); x / agg are split when a stage is staged.
+// LDS rows are 32 bf16 (one stage) in four 16-B chunks, chunk c of row r at
+// position c ^ ((r >> 2) & 3): the fragment reads (16 rows x one chunk per
+// 16 lanes) and the staging writes are bank-conflict free.
+constexpr int XW_STAGE = 3 * WBM * WKC + 3 * WBN * WKC;  // bf16 per stage buffer (36 KiB)
+
+__global__ __launch_bounds__(256) void k_wide_wimg(const float *__restrict__ wr, const float *__restrict__ wl,
+                                                   int64_t ldw, int Fo, int K, int Kp,
+                                                   __bf16 *__restrict__ img) {
+    const int64_t per = static_cast<int64_t>(Fo) * Kp;  // bf16 per part
+    const int64_t idx = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) * 8;
+    if (idx >= 2 * per) return;
+    const int mat = static_cast<int>(idx / per);
+    const int64_t e = idx - mat * per;
+    const int n = static_cast<int>(e / Kp), k0 = static_cast<int>(e - static_cast<int64_t>(n) * Kp);
+    const float *w = mat ? wl : wr;
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    b8 p1, p2, p3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = (w && k0 + j < K) ? w[static_cast<int64_t>(n) * ldw + k0 + j] : 0.0f;
+        const __bf16 h1 = static_cast<__bf16>(v);
+        const float r1 = v - static_cast<float>(h1);
+        const __bf16 h2 = static_cast<__bf16>(r1);
+        p1[j] = h1;
+        p2[j] = h2;
+        p3[j] = static_cast<__bf16>(r1 - static_cast<float>(h2));
+    }
+    __bf16 *o = img + static_cast<int64_t>(mat) * 3 * per + e;
+    *reinterpret_cast<b8 *>(o) = p1;
+    *reinterpret_cast<b8 *>(o + per) = p2;
+    *reinterpret_cast<b8 *>(o + 2 * per) = p3;
+}
+
+template <bool VOUT>
+__global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__restrict__ wimg, int Kp) {
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) __bf16 xlds[];  // [2][XW_STAGE]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int rows = a.n_rows;
+    if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
+    int erows = min(a.n_edge, rows);
+    if (a.n_edge_dev) erows = min(erows, *a.n_edge_dev);
+    const int nK = (a.K + WKC - 1) / WKC;
+    const int c_root = a.wr ? nK : 0;
+    const int n_live = ((rows + WBM - 1) / WBM) * a.n_ct;
+    const int64_t per = static_cast<int64_t>(a.Fo) * Kp;
+    const int wn = (wave & 1) * 64, wm = (wave >> 1) * 32;
+    const int i16 = lane & 15, q = lane >> 4;
+    Dropout drop = a.epi.drop;
+    if (a.seed_dev) drop.reseed(*a.seed_dev);
+    // staging roles: x / agg row xr_r = tid >> 2, its 8 values of chunk tid & 3;
+    // W row tid >> 1 (of 128), chunks 2 (tid & 1), + 1
+    const int xr_r = tid >> 2, xr_c = tid & 3;
+    const int w_n = tid >> 1, w_h = tid & 1;
+    float xv[8];
+    b8 wv[3][2];
+    auto sw = [](int r, int c) { return c ^ ((r >> 2) & 3); };
+
+    for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
+        const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
+        const int r0 = rt * WBM, n0 = ct * WBN;
+        const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);
+        auto load = [&](int c) {
+            const bool nb = c >= c_root;
+            const int kc = (nb ? c - c_root : c) * WKC;
+            const float *src = nb ? a.agg : a.x;
+            const int64_t ld = nb ? a.ld_agg : a.ldx;
+            const int rlim = nb ? erows : rows;
+            const int r = r0 + xr_r;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = kc + 8 * xr_c + j;
+                xv[j] = (r < rlim && k < a.K) ? src[static_cast<int64_t>(r) * ld + k] : 0.0f;
+            }
+            const int n = n0 + w_n;
+            const __bf16 *wb = wimg + (nb ? 3 * per : 0) + static_cast<int64_t>(min(n, a.Fo - 1)) * Kp + kc + 16 * w_h;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                wv[p][0] = *reinterpret_cast<const b8 *>(wb + p * per);
+                wv[p][1] = *reinterpret_cast<const b8 *>(wb + p * per + 8);
+                if (n >= a.Fo) {  // (rows past F_out: zero, never stored)
+                    wv[p][0] = b8{};
+                    wv[p][1] = b8{};
+                }
+            }
+        };
+        auto store = [&](__bf16 *s) {
+            b8 p1, p2, p3;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const __bf16 h1 = static_cast<__bf16>(xv[j]);
+                const float r1 = xv[j] - static_cast<float>(h1);
+                const __bf16 h2 = static_cast<__bf16>(r1);
+                p1[j] = h1;
+                p2[j] = h2;
+                p3[j] = static_cast<__bf16>(r1 - static_cast<float>(h2));
+            }
+            const int xo = xr_r * WKC + 8 * sw(xr_r, xr_c);
+            *reinterpret_cast<b8 *>(s + xo) = p1;
+            *reinterpret_cast<b8 *>(s + WBM * WKC + xo) = p2;
+            *reinterpret_cast<b8 *>(s + 2 * WBM * WKC + xo) = p3;
+            __bf16 *ws = s + 3 * WBM * WKC;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    *reinterpret_cast<b8 *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, 2 * w_h + h)) = wv[p][h];
+        };
+        v4f acc[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (nch > 0) {
+            load(0);
+            store(xlds);
+            __syncthreads();
+        }
+        for (int c = 0; c < nch; ++c) {
+            const bool more = c + 1 < nch;
+            if (more) load(c + 1);  // in flight during this stage's MFMAs
+            const __bf16 *s = xlds + (c & 1) * XW_STAGE;
+            const __bf16 *ws = s + 3 * WBM * WKC;
+            b8 xb[2][3];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int r = wm + 16 * nt + i16;
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    xb[nt][p] = *reinterpret_cast<const b8 *>(s + p * WBM * WKC + r * WKC + 8 * sw(r, q));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int n = wn + 16 * mt + i16;
+                b8 w[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) w[p] = *reinterpret_cast<const b8 *>(ws + p * WBN * WKC + n * WKC + 8 * sw(n, q));
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    v4f t2 = acc[mt][nt];
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], xb[nt][0], t2, 0, 0, 0);
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xb[nt][2], t2, 0, 0, 0);
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xb[nt][1], t2, 0, 0, 0);
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xb[nt][0], t2, 0, 0, 0);
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xb[nt][1], t2, 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xb[nt][0], t2, 0, 0, 0);
+                }
+            }
+            if (more) store(xlds + ((c + 1) & 1) * XW_STAGE);
+            __syncthreads();
+        }
+        // ---- epilogue (k_wide_gemm's): lane holds columns n0 + wn + 16 mt +
+        // 4 q + (0..3) of row r0 + wm + 16 nt + i16
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int r = r0 + wm + nt * 16 + i16;
+            if (r >= rows) continue;
+            const uint32_t rk = drop.row_key(static_cast<uint32_t>(r));
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int c0 = n0 + wn + mt * 16 + 4 * q;
+                if (c0 >= a.Fo) continue;
+                const uint32_t kb =
+                    drop.thresh ? drop.keep4(rk, static_cast<uint32_t>(a.epi.col_base + c0) >> 2) : 0xfu;
+                v4f v = acc[mt][nt];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float e = v[j];
+                    if (a.epi.bias && c0 + j < a.Fo) e += a.epi.bias[c0 + j];
+                    if (a.epi.relu) e = (e < 0.0f) ? 0.0f : e;  // NaN passes, like torch.relu
+                    if (drop.thresh) e = ((kb >> j) & 1u) ? e * drop.scale : 0.0f;
+                    v[j] = e;
+                }
+                float *o = a.out + static_cast<int64_t>(r) * a.ldo + c0;
+                if (VOUT && c0 + 4 <= a.Fo) {
+                    *reinterpret_cast<v4f *>(o) = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (c0 + j < a.Fo) o[j] = v[j];
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
+
+// bytes of the wide layer's split weight image (k_wide_wimg)
+size_t wide_wimg_bytes(int64_t K, int64_t Fo) {
+    return static_cast<size_t>(2 * 3) * static_cast<size_t>(Fo) * static_cast<size_t>(ceil_div(K, 32) * 32) * 2;
+}
 
 // The row-tile kernel holds the W_r image of its whole column slice in LDS
 // and re-reads x once per slice: the wide path takes a layer when F_out needs
@@ -313,7 +515,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,
                   const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
                   int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
-                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st) {
+                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st, bool exact) {
     const int64_t n_edge = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
     float *agg = nullptr;
     int64_t lda = ld_agg;
@@ -369,6 +571,38 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     // multiple of 8 (one per XCD in turn)
     const int64_t grid = std::max<int64_t>(8, std::min<int64_t>(ceil_div(tiles, 8) * 8, 2 * num_cus()));
     const bool vout = (ldo % 4 == 0) && aligned(out, 16);
+    // the split-bf16 form (not under NGNN_MATH_EXACT_F32): its weight image at
+    // the workspace's tail (NGNN_WIDE_X3=0, read once: the exact f32 form -- A/B)
+    static const bool x3_on = [] {
+        const char *e = std::getenv("NGNN_WIDE_X3");
+        return !(e && e[0] == '0');
+    }();
+    const size_t ib = wide_wimg_bytes(K, Fo);
+    const size_t head = agg == ws ? sage_wide_workspace_bytes(K, n_edge) : 0;
+    if (!exact && x3_on && ws && ws_bytes >= head + ib + 256) {
+        const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib) & ~uintptr_t(255);
+        __bf16 *img = reinterpret_cast<__bf16 *>(e);
+        const int Kp = static_cast<int>(ceil_div(K, 32) * 32);
+        const int64_t nthr = static_cast<int64_t>(2) * Fo * Kp / 8;
+        hipLaunchKernelGGL(k_wide_wimg, dim3(static_cast<unsigned>(ceil_div(nthr, 256))), dim3(256), 0, st, wr, wl,
+                           ldw, static_cast<int>(Fo), static_cast<int>(K), Kp, img);
+        int rc = launch_status();
+        if (rc) return rc;
+        const size_t lds = static_cast<size_t>(2) * XW_STAGE * 2;
+        auto go = [&](auto v_c) {
+            auto fn = k_wide_x3<decltype(v_c)::value>;
+            static bool attr = false;  // benign race: idempotent
+            if (!attr) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+                attr = true;
+            }
+            hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(256), lds, st, a, img, Kp);
+        };
+        if (vout) go(std::true_type{});
+        else go(std::false_type{});
+        return launch_status();
+    }
     if (vout)
         hipLaunchKernelGGL(k_wide_gemm<true>, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, a);
     else
