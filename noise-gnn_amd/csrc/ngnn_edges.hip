@@ -10,9 +10,13 @@
 // HBM-streaming kernels (int64 -> int32 narrowing copy + a lower_bound per
 // row).  Unsorted inputs (rewired edges, augmentation.py:82-85, are
 // source-sorted) take a stable LSD radix sort limited to ceil(log2 n_rows)
-// key bits.  Stability keeps edge order inside each row, so every per-row
-// reduction downstream runs in PyG's CPU scatter order.
-#include <hipcub/hipcub.hpp>
+// key bits: in-tree counting passes over 4-bit digits (per pass: per-block
+// digit counts, one exclusive scan of the [digit][block] counts, a stable
+// scatter in which every thread places its 16 consecutive items in order).
+// Stability keeps edge order inside each row, so every per-row reduction
+// downstream runs in PyG's CPU scatter order.
+
+#include <utility>
 
 #include "ngnn_internal.h"
 
@@ -102,6 +106,102 @@ __global__ __launch_bounds__(256) void k_permute_vals(const int64_t *__restrict_
     }
 }
 
+// ---- stable LSD radix sort of (key, value) int32 pairs, 4-bit digits
+constexpr int RS_T = 256;           // threads per block
+constexpr int RS_IPT = 16;          // consecutive items per thread
+constexpr int RS_CH = RS_T * RS_IPT;  // items per block
+constexpr int RS_D = 16;            // digits
+
+// hist[d * nb + b] = #{items of block b with digit d}
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const int32_t *__restrict__ keys, int32_t E, int shift,
+                                                  int32_t *__restrict__ hist) {
+    __shared__ int cnt[RS_D][RS_T + 1];
+    const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+#pragma unroll
+    for (int d = 0; d < RS_D; ++d) cnt[d][t] = 0;
+    const int64_t i0 = static_cast<int64_t>(b) * RS_CH + static_cast<int64_t>(t) * RS_IPT;
+    for (int i = 0; i < RS_IPT; ++i)
+        if (i0 + i < E) ++cnt[(keys[i0 + i] >> shift) & (RS_D - 1)][t];
+    __syncthreads();
+    if (t < RS_D) {
+        int s = 0;
+        for (int j = 0; j < RS_T; ++j) s += cnt[t][j];
+        hist[t * nb + b] = s;
+    }
+}
+
+// in place exclusive scan of n ints (one block of 1024 threads, chunks of 1024)
+__global__ __launch_bounds__(1024) void k_rs_scan(int32_t *__restrict__ v, int n) {
+    __shared__ int s[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + threadIdx.x;
+        const int x = i < n ? v[i] : 0;
+        s[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele
+            const int y = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+            __syncthreads();
+            s[threadIdx.x] += y;
+            __syncthreads();
+        }
+        const int base = carry;
+        if (i < n) v[i] = base + s[threadIdx.x] - x;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = base + s[1023];
+        __syncthreads();
+    }
+}
+
+// stable scatter: item order is block, then thread, then the thread's own
+// items in sequence -- the input order
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const int32_t *__restrict__ kin, const int32_t *__restrict__ vin,
+                                                     int32_t E, int shift, const int32_t *__restrict__ off,
+                                                     int32_t *__restrict__ kout, int32_t *__restrict__ vout) {
+    __shared__ int cnt[RS_D][RS_T + 1];
+    const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+#pragma unroll
+    for (int d = 0; d < RS_D; ++d) cnt[d][t] = 0;
+    const int64_t i0 = static_cast<int64_t>(b) * RS_CH + static_cast<int64_t>(t) * RS_IPT;
+    int k[RS_IPT], v[RS_IPT];
+#pragma unroll
+    for (int i = 0; i < RS_IPT; ++i) {
+        const bool ok = i0 + i < E;
+        k[i] = ok ? kin[i0 + i] : 0;
+        v[i] = ok ? vin[i0 + i] : 0;
+        if (ok) ++cnt[(k[i] >> shift) & (RS_D - 1)][t];
+    }
+    __syncthreads();
+    // exclusive scan of every digit row over the threads (Hillis-Steele)
+    for (int o = 1; o < RS_T; o <<= 1) {
+        int y[RS_D];
+#pragma unroll
+        for (int d = 0; d < RS_D; ++d) y[d] = t >= o ? cnt[d][t - o] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int d = 0; d < RS_D; ++d) cnt[d][t] += y[d];
+        __syncthreads();
+    }
+    // cnt[d][t] is now inclusive: this thread's first slot per digit
+    int base[RS_D];
+#pragma unroll
+    for (int d = 0; d < RS_D; ++d) base[d] = off[d * nb + b] + (t > 0 ? cnt[d][t - 1] : 0);
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < RS_D; ++d) cnt[d][t] = base[d];  // running positions, one slot per thread
+#pragma unroll
+    for (int i = 0; i < RS_IPT; ++i) {
+        if (i0 + i < E) {
+            const int d = (k[i] >> shift) & (RS_D - 1);
+            const int pos = cnt[d][t]++;
+            kout[pos] = k[i];
+            vout[pos] = v[i];
+        }
+    }
+}
+
 inline int key_bits(int64_t n_rows) {
     int b = 1;
     while (b < 31 && (int64_t(1) << b) < n_rows) ++b;
@@ -115,13 +215,8 @@ inline unsigned stream_grid(int64_t n, int block = 256, int64_t cap = 256 * 16) 
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-size_t cub_temp_bytes(int64_t E, int64_t n_rows) {
-    size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const int32_t *)nullptr, (int32_t *)nullptr,
-                                       (const int32_t *)nullptr, (int32_t *)nullptr,
-                                       static_cast<int>(E), 0, key_bits(n_rows));
-    return temp;
-}
+// the [digit][block] counts of one pass
+size_t rs_temp_bytes(int64_t E) { return sizeof(int32_t) * RS_D * static_cast<size_t>(ceil_div(E, RS_CH)); }
 
 }  // namespace
 }  // namespace ngnn
@@ -141,7 +236,8 @@ extern "C" int ngnn_edge_probe(const int64_t *edge_index, int64_t E, int64_t n_s
 
 extern "C" size_t ngnn_csr_workspace_bytes(int64_t E, int64_t n_rows) {
     if (E <= 0) return 0;
-    return 4 * align_up(sizeof(int32_t) * (size_t)E, 256) + align_up(cub_temp_bytes(E, n_rows), 256);
+    (void)n_rows;
+    return 4 * align_up(sizeof(int32_t) * (size_t)E, 256) + align_up(rs_temp_bytes(E), 256);
 }
 
 extern "C" int ngnn_csr_build(const int64_t *keys, const int64_t *vals, int64_t E, int64_t n_rows,
@@ -175,13 +271,22 @@ extern "C" int ngnn_csr_build(const int64_t *keys, const int64_t *vals, int64_t 
     int32_t *v_out = reinterpret_cast<int32_t *>(p + 3 * slab);
     void *temp = p + 4 * slab;
     size_t temp_bytes = need - 4 * slab;
+    (void)temp_bytes;
     hipLaunchKernelGGL(k_keys_iota, dim3(stream_grid(E)), dim3(256), 0, st, keys, E32, k_in, v_in);
-    hipError_t err = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k_in, k_out, v_in, v_out,
-                                                        E32, 0, key_bits(n_rows), st);
-    if (err != hipSuccess) return static_cast<int>(err);
-    hipLaunchKernelGGL(k_permute_vals, dim3(stream_grid(E)), dim3(256), 0, st, vals, v_out, E32,
+    const int nb = static_cast<int>(ceil_div(E, RS_CH));
+    int32_t *hist = static_cast<int32_t *>(temp);
+    const int bits = key_bits(n_rows);
+    for (int shift = 0; shift < bits; shift += 4) {  // (ping-pong: the result of each pass in k_out, v_out)
+        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_T), 0, st, k_in, E32, shift, hist);
+        hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, st, hist, RS_D * nb);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_T), 0, st, k_in, v_in, E32, shift, hist, k_out, v_out);
+        std::swap(k_in, k_out);
+        std::swap(v_in, v_out);
+    }
+    // (the sorted pairs are in k_in / v_in after the last swap)
+    hipLaunchKernelGGL(k_permute_vals, dim3(stream_grid(E)), dim3(256), 0, st, vals, v_in, E32,
                        col, eid);
-    hipLaunchKernelGGL(k_rowptr_lower_bound<int32_t>, dim3(grid_rows), dim3(256), 0, st, k_out,
+    hipLaunchKernelGGL(k_rowptr_lower_bound<int32_t>, dim3(grid_rows), dim3(256), 0, st, k_in,
                        E32, R32, rowptr);
     return launch_status();
 }

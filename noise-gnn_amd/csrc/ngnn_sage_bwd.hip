@@ -105,7 +105,13 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded); MASK: 
                 const int w = buf_load1i(rs, vo & ~3, 0, 0);
                 v[u] = __int_as_float((vo & 2) ? (w & static_cast<int>(0xffff0000u)) : (w << 16));
             } else if constexpr (VEC) {
-                v[u] = buf_load4(rs, vo, 0, 0);
+                if (!kok || k + 4 <= K) {
+                    v[u] = buf_load4(rs, vo, 0, 0);
+                } else {  // (K % 4 != 0: the row's last quad, element by element -- a
+                          // 16-B load would straddle the next row / the range's end)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[u][i] = buf_load1(rs, k + i < K ? vo + 4 * i : kBufOOB, 0, 0);
+                }
             } else {
                 v[u] = buf_load1(rs, vo, 0, 0);
             }
@@ -158,9 +164,12 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded); MASK: 
     // nearest: v - p1 - p2 - p3 <= 2^-24 |v|) into the images img[0..NP) of
     // row stride ld (bf16 elements); NP == 1 for bf16 rows (exact in one
     // part, stored as loaded)
+    // kq0 = K - k0: columns of the chunk that are real -- a 16-B load at a
+    // 4-B aligned row start (K % 4 != 0) reads past K into the next row, and
+    // those elements are zeroed here
     template <int NP>
     __device__ __forceinline__ void store_parts(__bf16 *img0, __bf16 *img1, __bf16 *img2, int ld,
-                                                float mscale) const {
+                                                float mscale, int kq0 = 1 << 30) const {
         static_assert(VEC, "16-B staging");
 #pragma unroll
         for (int u = 0; u < N; ++u) {
@@ -183,6 +192,7 @@ struct Chunk {  // BF: the operand is bf16 (widened exactly when loaded); MASK: 
                 float x = w[i];
                 if (MASK) x = mv[i] > 0.f ? x * mscale : 0.f;
                 if (DEG) x = d1[u] > d0[u] ? x : 0.f;
+                if (c + i >= kq0) x = 0.f;
                 const __bf16 h1 = static_cast<__bf16>(x);
                 const float r1 = x - static_cast<float>(h1);
                 const __bf16 h2 = static_cast<__bf16>(r1);
@@ -440,9 +450,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(
         const LB16 *lb = mat ? la : lh;
         for (int c0 = rb; c0 < re; c0 += WG_BM) {
             __syncthreads();  // the previous chunk's MFMAs are done with LDS
-            cz.template store_parts<3>(zi, zi + WG_BM * X3Z, zi + 2 * WG_BM * X3Z, X3Z, yscale);
-            ch.template store_parts<NPH>(hi, hi + WG_BM * X3H, hi + 2 * WG_BM * X3H, X3H, 1.0f);
-            ca.template store_parts<3>(ai, ai + WG_BM * X3H, ai + 2 * WG_BM * X3H, X3H, 1.0f);
+            cz.template store_parts<3>(zi, zi + WG_BM * X3Z, zi + 2 * WG_BM * X3Z, X3Z, yscale, Fo - n0);
+            ch.template store_parts<NPH>(hi, hi + WG_BM * X3H, hi + 2 * WG_BM * X3H, X3H, 1.0f, K - k0);
+            ca.template store_parts<3>(ai, ai + WG_BM * X3H, ai + 2 * WG_BM * X3H, X3H, 1.0f, K - k0);
             __syncthreads();
             const int c1 = c0 + WG_BM;
             if (c1 < re) {  // the next chunk's loads overlap this chunk's MFMAs
@@ -1225,7 +1235,11 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
         const char *e = std::getenv("NGNN_WGRAD_X3");
         return !(e && e[0] == '0');
     }();
-    if (NT == 4 && vz && vh && x3_on) {
+    // (fp32 h / agg rows at 4-B alignment, K % 4 != 0 -- Amazon-Computers' K =
+    // 767: the X3 kernel's 16-B loads read past K into the next row, and
+    // store_parts zeroes those columns)
+    const bool vh_x3 = vh || (!h_bf16 && (h_dev || aligned(h, 4)) && aligned(agg, 4));
+    if (NT == 4 && vz && vh_x3 && x3_on) {
         const bool hb = vh == 2;
         // bf16 h with Fo >= 128: two Fo tiles per wave (half the h / agg re-reads)
         // (NGNN_WGRAD_NFW=2, read once: two Fo tiles per wave -- half the

@@ -329,6 +329,8 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
     if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
     int erows = min(a.n_edge, rows);
     if (a.n_edge_dev) erows = min(erows, *a.n_edge_dev);
+    rows = __builtin_amdgcn_readfirstlane(rows);
+    erows = __builtin_amdgcn_readfirstlane(erows);
     const int nK = (a.K + WKC - 1) / WKC;
     const int c_root = a.wr ? nK : 0;
     const int n_live = ((rows + WBM - 1) / WBM) * a.n_ct;
@@ -341,44 +343,54 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
     // W row tid >> 1 (of 128), chunks 2 (tid & 1), + 1
     const int xr_r = tid >> 2, xr_c = tid & 3;
     const int w_n = tid >> 1, w_h = tid & 1;
-    float xv[8];
-    b8 wv[3][2];
     auto sw = [](int r, int c) { return c ^ ((r >> 2) & 3); };
+    // x / agg rows through buffer resources (16-B loads at 4-B aligned
+    // offsets; past the range: 0)
+    const i32x4 xrs = make_rsrc_u(a.x, static_cast<uint32_t>(static_cast<int64_t>(rows) * a.ldx * 4));
+    const i32x4 ars = make_rsrc_u(a.agg, static_cast<uint32_t>(a.agg ? static_cast<int64_t>(erows) * a.ld_agg * 4 : 0));
+    // two register sets: stage c + 1 waits in one for its store while stage
+    // c + 2's loads land in the other (the MFMA phase of a stage is ~0.8k
+    // cycles here -- a one-stage prefetch left the load latency exposed)
+    v4f xv[2][2];
+    b8 wv[2][3][2];
 
     for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
         const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
         const int r0 = rt * WBM, n0 = ct * WBN;
         const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);
-        auto load = [&](int c) {
+        auto load = [&](int c, v4f (&xd)[2], b8 (&wd)[3][2]) __attribute__((always_inline)) {
             const bool nb = c >= c_root;
             const int kc = (nb ? c - c_root : c) * WKC;
-            const float *src = nb ? a.agg : a.x;
-            const int64_t ld = nb ? a.ld_agg : a.ldx;
-            const int rlim = nb ? erows : rows;
             const int r = r0 + xr_r;
+            const int64_t ld = nb ? a.ld_agg : a.ldx;
+            const int k = kc + 8 * xr_c;
+            const int off = (r < (nb ? erows : rows) && k < a.K) ? static_cast<int>((r * ld + k) * 4) : static_cast<int>(0xF0000000u);
+            const i32x4 rs = nb ? ars : xrs;
+            if (off == static_cast<int>(0xF0000000u) || k + 8 <= a.K) {
+                xd[0] = buf_load4(rs, off, 0, 0);
+                xd[1] = buf_load4(rs, off == static_cast<int>(0xF0000000u) ? off : off + 16, 0, 0);
+            } else {  // (the row's last values: element by element, nothing past K)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = kc + 8 * xr_c + j;
-                xv[j] = (r < rlim && k < a.K) ? src[static_cast<int64_t>(r) * ld + k] : 0.0f;
+                for (int j = 0; j < 8; ++j)
+                    xd[j >> 2][j & 3] = buf_load1(rs, k + j < a.K ? off + 4 * j : static_cast<int>(0xF0000000u), 0, 0);
             }
-            const int n = n0 + w_n;
-            const __bf16 *wb = wimg + (nb ? 3 * per : 0) + static_cast<int64_t>(min(n, a.Fo - 1)) * Kp + kc + 16 * w_h;
+            const int n = min(n0 + w_n, a.Fo - 1);
+            const __bf16 *wb = wimg + (nb ? 3 * per : 0) + static_cast<int64_t>(n) * Kp + kc + 16 * w_h;
 #pragma unroll
             for (int p = 0; p < 3; ++p) {
-                wv[p][0] = *reinterpret_cast<const b8 *>(wb + p * per);
-                wv[p][1] = *reinterpret_cast<const b8 *>(wb + p * per + 8);
-                if (n >= a.Fo) {  // (rows past F_out: zero, never stored)
-                    wv[p][0] = b8{};
-                    wv[p][1] = b8{};
-                }
+                wd[p][0] = *reinterpret_cast<const b8 *>(wb + p * per);
+                wd[p][1] = *reinterpret_cast<const b8 *>(wb + p * per + 8);
             }
         };
-        auto store = [&](__bf16 *s) {
+        auto store = [&](__bf16 *s, int c, const v4f (&xd)[2], const b8 (&wd)[3][2]) __attribute__((always_inline)) {
+            const bool nb = c >= c_root;
+            const int kq = a.K - ((nb ? c - c_root : c) * WKC + 8 * xr_c);  // valid values of the 8
             b8 p1, p2, p3;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const __bf16 h1 = static_cast<__bf16>(xv[j]);
-                const float r1 = xv[j] - static_cast<float>(h1);
+                const float v = j < kq ? xd[j >> 2][j & 3] : 0.0f;  // (past K: the next row's values)
+                const __bf16 h1 = static_cast<__bf16>(v);
+                const float r1 = v - static_cast<float>(h1);
                 const __bf16 h2 = static_cast<__bf16>(r1);
                 p1[j] = h1;
                 p2[j] = h2;
@@ -389,26 +401,20 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
             *reinterpret_cast<b8 *>(s + WBM * WKC + xo) = p2;
             *reinterpret_cast<b8 *>(s + 2 * WBM * WKC + xo) = p3;
             __bf16 *ws = s + 3 * WBM * WKC;
+            const bool wok = n0 + w_n < a.Fo;  // (rows past F_out: zero)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    *reinterpret_cast<b8 *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, 2 * w_h + h)) = wv[p][h];
+                    *reinterpret_cast<b8 *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, 2 * w_h + h)) =
+                        wok ? wd[p][h] : b8{};
         };
         v4f acc[4][2];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
-        if (nch > 0) {
-            load(0);
-            store(xlds);
-            __syncthreads();
-        }
-        for (int c = 0; c < nch; ++c) {
-            const bool more = c + 1 < nch;
-            if (more) load(c + 1);  // in flight during this stage's MFMAs
-            const __bf16 *s = xlds + (c & 1) * XW_STAGE;
+        auto mfma_stage = [&](const __bf16 *s) __attribute__((always_inline)) {
             const __bf16 *ws = s + 3 * WBM * WKC;
             b8 xb[2][3];
 #pragma unroll
@@ -435,8 +441,26 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xb[nt][0], t2, 0, 0, 0);
                 }
             }
-            if (more) store(xlds + ((c + 1) & 1) * XW_STAGE);
+        };
+        if (nch > 0) {
+            load(0, xv[0], wv[0]);
+            if (nch > 1) load(1, xv[1], wv[1]);
+            store(xlds, 0, xv[0], wv[0]);
             __syncthreads();
+        }
+        // stage c: MFMAs from LDS[c & 1]; stage c + 1's registers (set (c+1) & 1)
+        // go to LDS[(c+1) & 1] after them; stage c + 2 loads into set c & 1
+        // (compile-time set indices: the loop runs in pairs)
+        auto one = [&](int c, auto u_c) __attribute__((always_inline)) {
+            constexpr int U = decltype(u_c)::value;  // c & 1
+            if (c + 2 < nch) load(c + 2, xv[U], wv[U]);
+            mfma_stage(xlds + U * XW_STAGE);
+            if (c + 1 < nch) store(xlds + (U ^ 1) * XW_STAGE, c + 1, xv[U ^ 1], wv[U ^ 1]);
+            __syncthreads();
+        };
+        for (int c = 0; c < nch; c += 2) {
+            one(c, std::integral_constant<int, 0>{});
+            if (c + 1 < nch) one(c + 1, std::integral_constant<int, 1>{});
         }
         // ---- epilogue (k_wide_gemm's): lane holds columns n0 + wn + 16 mt +
         // 4 q + (0..3) of row r0 + wm + 16 nt + i16
@@ -579,7 +603,9 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     }();
     const size_t ib = wide_wimg_bytes(K, Fo);
     const size_t head = agg == ws ? sage_wide_workspace_bytes(K, n_edge) : 0;
-    if (!exact && x3_on && ws && ws_bytes >= head + ib + 256) {
+    // (32-bit row offsets in the kernel's buffer loads)
+    const bool fits = n_rows * ldx * 4 < 0x7FFF0000ll && (!agg || n_edge * lda * 4 < 0x7FFF0000ll);
+    if (!exact && x3_on && fits && ws && ws_bytes >= head + ib + 256) {
         const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib) & ~uintptr_t(255);
         __bf16 *img = reinterpret_cast<__bf16 *>(e);
         const int Kp = static_cast<int>(ceil_div(K, 32) * 32);

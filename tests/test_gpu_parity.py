@@ -62,6 +62,21 @@ def test_csr_build_matches_stable_sort(order, E):
     assert np.array_equal(csr.rowptr.cpu().numpy(), want_rowptr)
 
 
+@pytest.mark.parametrize("N,E", [(1, 9), (17, 4097), (70_000, 300_001), (2_449_029, 1_000_003)])
+def test_csr_build_unsorted_key_widths(N, E):
+    """The unsorted path's in-tree radix passes (4-bit digits, as many as
+    ceil(log2 N) needs: 1 .. 6 passes): stable within each key, against
+    numpy's stable argsort, up to the products graph's row count."""
+    g = torch.Generator().manual_seed(N + E)
+    keys = torch.randint(0, N, (E,), generator=g)
+    vals = torch.randint(0, N, (E,), generator=g)
+    csr = build_csr(keys.to(DEV), vals.to(DEV), N, keys_sorted=False)
+    perm = np.argsort(keys.numpy(), kind="stable")
+    assert np.array_equal(csr.col.cpu().numpy(), vals.numpy()[perm].astype(np.int32))
+    want_rowptr = np.searchsorted(keys.numpy()[perm], np.arange(N + 1), side="left").astype(np.int32)
+    assert np.array_equal(csr.rowptr.cpu().numpy(), want_rowptr)
+
+
 def test_probe_flags_and_index_errors():
     ei = torch.tensor([[0, 1, 2], [2, 1, 0]], device=DEV)
     b = Block(ei, 3)
