@@ -182,7 +182,7 @@ def cpu_baseline(batches, args, layers):
                       f"oracle/pyg_ref.py"}
 
 
-def eager_reference_loop(batches, args, F_in, C, layers, dev, steps, verbatim=False):
+def eager_reference_loop(batches, args, F_in, C, layers, dev, steps, verbatim=False, ngnn_adam=False):
     """The reference's training loop (pipeline.py:152-169) run verbatim on
     ngnn's modules after the INTEGRATION.md Option-B swap -- no graph capture,
     no loss head, no Adam fold: out = model(x, edge_index)[:batch_size];
@@ -200,7 +200,10 @@ def eager_reference_loop(batches, args, F_in, C, layers, dev, steps, verbatim=Fa
         model = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
     if args.dtype == "bf16":
         model = model.to(torch.bfloat16)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    # (ngnn_adam: the optimizer swapped too -- ngnn.optim.Adam, the same
+    # constructor, one device launch per step)
+    from ngnn.optim import Adam as NgnnAdam
+    opt = (NgnnAdam if ngnn_adam else torch.optim.Adam)(model.parameters(), lr=1e-3)
     model.train()
     total_loss, total_correct = 0.0, 0
 
@@ -624,16 +627,21 @@ def main():
         timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
         ms_core = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps)
         ms_verb = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps, verbatim=True)
+        ms_nadam = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps, ngnn_adam=True)
         graph_ms = 1e3 * dt / args.steps
         eager_ref = {
             "ms_per_step": round(ms_core, 4),
             "value": round(sum(layers * b.edge_index.shape[1] for b in timed) / args.steps / (ms_core * 1e-3), 1),
             "unit": "edges/s", "vs_graph_step": round(ms_core / graph_ms, 3),
             "ms_per_step_with_host_reads": round(ms_verb, 4),
+            "ms_per_step_ngnn_adam": round(ms_nadam, 4),
+            "vs_graph_step_ngnn_adam": round(ms_nadam / graph_ms, 3),
             "note": "pipeline.py:152-169 after the INTEGRATION.md Option-B swap: model(x, edge_index)"
                     "[:batch_size], F.cross_entropy, zero_grad, backward, torch.optim.Adam; no capture, "
                     "no loss head, no Adam fold (with_host_reads: + the loop's float(loss) and accuracy "
-                    "count per step)"}
+                    "count per step; ngnn_adam: the same loop with ngnn.optim.Adam constructed in place "
+                    "of torch.optim.Adam, model.py:66-69).  Host-bound: torch.optim.Adam's foreach "
+                    "step alone is ~0.1 ms of host time per step (torch.profiler, DESIGN.md 8d)"}
 
     # full epoch incl. GPU sampling (this rank's shard)
     epoch_s = None
