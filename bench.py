@@ -254,15 +254,15 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512, dom: str =
     from ngnn.block import get_block
     blk = get_block(gstep.ei, gstep.n_cap)
     c = model.convs[0]
-    wl, bl, wr = (q.detach().float() for q in (c.lin_l.weight, c.lin_l.bias, c.lin_r.weight))
     x = gstep.x
-    agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])
     p = model.dropout if model.training else 0.0
-    w1 = c.lin_l.weight.dtype == torch.bfloat16
     pre = None
     if dom == "sage2_fwd":
-        params = [q.detach() for cv in model.convs for q in (cv.lin_l.weight, cv.lin_l.bias,
-                                                            cv.lin_r.weight)]
+        # (SimpleGCN: [W, b, None] per conv -- the two-layer kernels with W_r = 0)
+        params = fused.sage2_params(
+            [q.detach() if q is not None else None for cv in model.convs
+             for q in ((cv.lin_l.weight, cv.lin_l.bias, cv.lin_r.weight) if hasattr(cv, "lin_l")
+                       else (cv.lin.weight, cv.bias, None))])
         bufs = fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev)
 
         def pre():
@@ -273,6 +273,10 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512, dom: str =
             fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev,
                                 stages=_lib.SAGE2_MAIN, bufs=bufs)
     else:
+        wl, bl, wr = (q.detach().float() for q in (c.lin_l.weight, c.lin_l.bias, c.lin_r.weight))
+        agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])
+        w1 = c.lin_l.weight.dtype == torch.bfloat16
+
         def run():
             fused.sage_layer_fwd(x, blk, aggr, wl, bl, wr, relu=True, p_drop=p, seed=0, agg_out=agg,
                                  seed_dev=blk.seed_dev, x_dev=blk.x_dev, xrow_dev=blk.xrow_dev,
@@ -550,12 +554,12 @@ def main():
     if dom:
         name, (n, ms, nbytes, flops, mfma_s) = dom
         eager_us = 1e3 * ms / n
-        if graph and name in ("sage_fwd_l0", "sage2_fwd") and args.module == "sage":
+        if graph and (name == "sage2_fwd" or (name == "sage_fwd_l0" and args.module == "sage")):
             # the same kernel on the same timed batches, each right after its
             # slot load (see l0_launch_us); algorithmic bytes / flops per
             # launch from the eager records of those batches
             timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
-            l0 = l0_launch_us(gstep, model, args.aggr, timed, dom=name)
+            l0 = l0_launch_us(gstep, model, "sum" if args.module == "gcn" else args.aggr, timed, dom=name)
             ms = l0.get("seq", l0["step"]) * 1e-3 * n
             if name == "sage2_fwd":
                 # in the step h is written only below the slot's R' (the eager

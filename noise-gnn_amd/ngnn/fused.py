@@ -429,6 +429,27 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
                                                 _lib.REDUCE[reduce]))
 
 
+def sage2_params(params):
+    """The six tensors ngnn_sage2_fwd / _bwd take.  A two-layer SimpleGCN
+    stack ([W, b, None] per GCNConv(normalize=False), sum aggregation) is the
+    SAGE stack with W_r = 0 (convolution.py:29-35): its absent root weights
+    become persistent zero matrices -- the root products add exact zeros and
+    their gradients go to scratch (_absent_none drops them).  A stack with
+    only one absent W_r: None (not this path)."""
+    if params[2] is None and params[5] is None and params[0] is not None and params[3] is not None:
+        return [params[0], params[1], _zeros_like_cached(params[0]),
+                params[3], params[4], _zeros_like_cached(params[3])]
+    if any(q is None for q in params):
+        return None
+    return list(params)
+
+
+def _absent_none(params, grads):
+    """The gradients of the stack's parameters: None where the caller's
+    parameter is absent (a GCN layer's W_r, sage2_params)."""
+    return [None if q is None else g for q, g in zip(params, grads)]
+
+
 def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev,
                   stages: int | None = None, bufs=None, head: "HeadResult | None" = None):
     """(h, logits, layer-0 aggregate, h partial?) of a two-layer stack in one
@@ -543,7 +564,7 @@ def head_ok(block: Block, x, params) -> bool:
             or torch.are_deterministic_algorithms_enabled()):
         return False
     return (x.size(0) == hd.n_rows and params[3].shape[0] == hd.F1 and hd.B <= x.size(0)
-            and any(q.requires_grad for q in params))
+            and any(q.requires_grad for q in params if q is not None))
 
 
 _use_bwd2 = True  # (tests flip it to compare with the per-layer backward)
@@ -574,13 +595,26 @@ class AdamFoldSpec:
         st = opt.state
         group = opt.param_groups[0]
         step = st[params[0]]["step"]
-        self.params = params  # [W_l0, b0, W_r0, W_l1, b1, W_r1] (the stack's order)
+        # [W_l0, b0, W_r0, W_l1, b1, W_r1] (the stack's order; a GCN stack's
+        # absent W_r: the zero matrices its forward reads, sage2_params)
+        self.params = sage2_params(params)
         b1, b2 = group["betas"]
+        # the update of an absent W_r lands in scratch tensors of its shape
+        # (never in the zeros the forward reads)
+        slots = []
+        self._scratch = []
+        for q, z in zip(params, self.params):
+            if q is None:
+                t = torch.zeros(3, *z.shape, dtype=torch.float32, device=z.device)
+                self._scratch.append(t)
+                slots.append((t[0], t[1], t[2]))
+            else:
+                slots.append((q, st[q]["exp_avg"], st[q]["exp_avg_sq"]))
         # the header's order: dW_l1, db1, dW_r1, dW_l0, db0, dW_r0
-        order = [params[3], params[4], params[5], params[0], params[1], params[2]]
-        P = (ctypes.c_void_p * 6)(*[q.data_ptr() for q in order])
-        M = (ctypes.c_void_p * 6)(*[st[q]["exp_avg"].data_ptr() for q in order])
-        V = (ctypes.c_void_p * 6)(*[st[q]["exp_avg_sq"].data_ptr() for q in order])
+        order = [slots[i] for i in (3, 4, 5, 0, 1, 2)]
+        P = (ctypes.c_void_p * 6)(*[o[0].data_ptr() for o in order])
+        M = (ctypes.c_void_p * 6)(*[o[1].data_ptr() for o in order])
+        V = (ctypes.c_void_p * 6)(*[o[2].data_ptr() for o in order])
         self._keep = step
         self.struct = _lib.AdamFold(P, M, V, step.data_ptr(), float(group["lr"]),
                                     float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]))
@@ -589,30 +623,36 @@ class AdamFoldSpec:
     @staticmethod
     def make(opt, model):
         """The spec when `opt` is ngnn.optim.Adam over exactly the two-layer
-        stack's six fp32 parameters with its state made (after a warm-up
-        step), else None."""
+        stack's parameters (SAGE: six; SimpleGCN: four, W and b per conv) in
+        fp32 with its state made (after a warm-up step), else None."""
         from .optim import Adam
         convs = getattr(model, "convs", None)
         if not isinstance(opt, Adam) or convs is None or len(convs) != 2 or len(opt.param_groups) != 1:
             return None
         params = []
         for c in convs:
-            if not (hasattr(c, "lin_l") and hasattr(c, "lin_r")) or c.lin_r is None:
+            if hasattr(c, "lin_l") and getattr(c, "lin_r", None) is not None:
+                params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
+            elif hasattr(c, "lin") and not hasattr(c, "lin_l") and getattr(c, "bias", None) is not None:
+                params += [c.lin.weight, c.bias, None]  # GCNConv(normalize=False)
+            else:
                 return None
-            params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
+        live = [q for q in params if q is not None]
+        if len(live) not in (4, 6) or (len(live) == 4 and (params[2], params[5]) != (None, None)):
+            return None
         group = opt.param_groups[0]["params"]
-        if len(group) != 6 or {id(q) for q in group} != {id(q) for q in params}:
+        if len(group) != len(live) or {id(q) for q in group} != {id(q) for q in live}:
             return None
         # (ngnn.optim.Adam skips a parameter with no gradient -- a frozen one;
         # the folded reduction would update all six: no fold then)
-        if not all(q.requires_grad for q in params):
+        if not all(q.requires_grad for q in live):
             return None
-        for q in params:
+        for q in live:
             s = opt.state.get(q, {})
-            if (q is None or q.dtype != torch.float32 or not q.is_contiguous() or "step" not in s
+            if (q.dtype != torch.float32 or not q.is_contiguous() or "step" not in s
                     or s["exp_avg"].dtype != torch.float32):
                 return None
-        if len({opt.state[q]["step"].data_ptr() for q in params}) != 1:
+        if len({opt.state[q]["step"].data_ptr() for q in live}) != 1:
             return None
         return AdamFoldSpec(opt, params)
 
@@ -666,9 +706,10 @@ class _SAGEStack(torch.autograd.Function):
         h = x
         ctx.h_partial = False
         ctx.sage2 = False
-        if L == 2 and sage2_ok(x, block, reduce, params, w_bf16):
+        p6 = sage2_params(params) if L == 2 else None
+        if p6 is not None and sage2_ok(x, block, reduce, p6, w_bf16):
             ctx.sage2 = True
-            h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, params, p_drop, seed, seed_dev,
+            h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, p6, p_drop, seed, seed_dev,
                                                        head=head)
             if head is not None:
                 h._ngnn_head = head  # (seed_cross_entropy takes the loss from it)
@@ -767,8 +808,9 @@ class _SAGEStack(torch.autograd.Function):
                 and not torch.are_deterministic_algorithms_enabled()):
             # (a loss head's gradient arrives with its scatter done: g_pre)
             return (None, None, None, None, None, None, None, None, None,
-                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views,
-                                    g_pre=getattr(dout, "_ngnn_g_pre", None)))
+                    *_absent_none(params, sage2_backward(dy, block, reduce, acts, aggs[0], sage2_params(params),
+                                                         p, bptr(2), bptr(1), views,
+                                                         g_pre=getattr(dout, "_ngnn_g_pre", None))))
         if (ctx.sage2 and not ctx.h_partial and not need_dx and _use_bwd2
                 and not torch.are_deterministic_algorithms_enabled()):
             # an eager step (the reference loop after the Option-B swap: no
@@ -784,7 +826,8 @@ class _SAGEStack(torch.autograd.Function):
                                                    bptr(L), None, bptr(L - 1), block.E, stream),
                        "ngnn_block_prefix_stats")
             return (None, None, None, None, None, None, None, None, None,
-                    *sage2_backward(dy, block, reduce, acts, aggs[0], params, p, bptr(2), bptr(1), views))
+                    *_absent_none(params, sage2_backward(dy, block, reduce, acts, aggs[0], sage2_params(params),
+                                                         p, bptr(2), bptr(1), views)))
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")

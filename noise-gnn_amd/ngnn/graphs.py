@@ -255,9 +255,9 @@ class GraphedTrainStep:
         convs = getattr(self.model, "convs", None)
         if (self.loss_fn is seed_cross_entropy and convs is not None and len(convs) == 2
                 and self.x.dtype == torch.float32
-                and all(hasattr(c, "lin_l") and c.lin_l.weight.dtype == torch.float32 for c in convs)):
+                and all(_lin_w(c) is not None and _lin_w(c).dtype == torch.float32 for c in convs)):
             from .fused import LossHead
-            self._head = LossHead(self.y, self.B, self.n_cap, convs[1].lin_l.weight.shape[0], self.r_next)
+            self._head = LossHead(self.y, self.B, self.n_cap, _lin_w(convs[1]).shape[0], self.r_next)
         hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
                         csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
                         x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B, self.loss_fn is seed_cross_entropy),
@@ -272,11 +272,11 @@ class GraphedTrainStep:
         if convs is not None:
             from .fused import const_bounds, reserve_sage2_bwd
             const_bounds(self.x.device, len(convs), self.B)
-            if len(convs) == 2 and hasattr(convs[0], "lin_l") and hasattr(convs[1], "lin_l"):
+            if len(convs) == 2 and _lin_w(convs[0]) is not None and _lin_w(convs[1]) is not None:
                 # (the warm-up ran before the slot's bound hint existed, so it
                 # took the per-layer backward: reserve the two-layer one's now)
-                reserve_sage2_bwd(self.x.device, self.n_cap, convs[0].lin_l.weight.shape[1],
-                                  convs[1].lin_l.weight.shape[0])
+                reserve_sage2_bwd(self.x.device, self.n_cap, _lin_w(convs[0]).shape[1],
+                                  _lin_w(convs[1]).shape[0])
         # data parallel: the bucket pack is the tail of the first graph and the
         # unpack (/ world) the head of the second, so between the replays the
         # host issues only the one all-reduce
@@ -337,6 +337,12 @@ class GraphedTrainStep:
         if self.g_opt is not None:  # (None: the backward's reduction took the Adam step)
             self.g_opt.replay()
         return self.loss
+
+
+def _lin_w(conv):
+    """The neighbour-term weight of a SAGEConv (lin_l) or GCNConv (lin), else None."""
+    lin = getattr(conv, "lin_l", None) or getattr(conv, "lin", None)
+    return getattr(lin, "weight", None)
 
 
 def _prepack_target(model):

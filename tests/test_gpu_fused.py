@@ -463,18 +463,30 @@ def test_dgrad_lowdim_shape_envelope():
 
 
 class _MaskedGCN(pyg_ref.SimpleGCN):
-    """Oracle SimpleGCN whose dropout uses given keep masks."""
+    """Oracle SimpleGCN whose dropout uses given keep masks (None: no
+    dropout); gpu_hidden / kink_rows: ReLU's kink as _MaskedSAGE."""
 
-    def __init__(self, *a, masks=None, **k):
+    def __init__(self, *a, masks=None, gpu_hidden=None, kink_rows=None, **k):
         super().__init__(*a, **k)
         self.masks = masks
+        self.gpu_hidden = gpu_hidden
+        self.kink_rows = kink_rows
 
     def forward(self, x, edge_index):
         for i, conv in enumerate(self.convs):
             x = conv(x, edge_index)
             if i != self.num_layers - 1:
-                x = x.relu()
-                x = x * self.masks[i] * dropout_scale(self.dropout)
+                gh = None if self.gpu_hidden is None else self.gpu_hidden[i]
+                if gh is None:
+                    x = x.relu()
+                else:
+                    pre = x.detach()
+                    amb = pre.abs() <= KINK_TOL * pre.abs().amax(1, keepdim=True)
+                    if self.kink_rows is not None:
+                        amb[self.kink_rows:] = False
+                    x = x * torch.where(amb, gh[:pre.size(0)].cpu() > 0, pre > 0)
+                if self.masks is not None:
+                    x = x * self.masks[i] * dropout_scale(self.dropout)
         return x
 
 
