@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 16
+#define NGNN_ABI_VERSION 17
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -367,7 +367,14 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  * ws: ngnn_xent_head_workspace_bytes(B) bytes, 16-B aligned, zero-filled
  * before its first use (it is zero again on return).  The loss sum is in a
  * fixed order (deterministic); needs the EDGE and NARROW stages in one call
- * or in order, F1 <= 64. */
+ * or in order, F1 <= 64.
+ * src_count (nullable, ABI 17): 2 g_rows + 1 int32, zero-filled before its
+ * first use and then owned by the head: the EDGE launch counts every source's
+ * edges into rows d < B (two count arrays alternating per call, the word past
+ * them selects one), so a source with a single such edge takes ONE plain row
+ * store of dy[d] (/ deg(d)) instead of F1 float atomics.  Counts left over
+ * from a call whose NARROW stage did not finish only ever over-count (the
+ * scatter then stays atomic): any call order is safe. */
 typedef struct ngnn_xent_head {
     const int64_t *y;
     int64_t B;
@@ -380,6 +387,7 @@ typedef struct ngnn_xent_head {
     const int32_t *g_rows_dev;
     void *ws;
     size_t ws_bytes;
+    int32_t *src_count;
 } ngnn_xent_head;
 size_t ngnn_xent_head_workspace_bytes(int64_t B);
 #define NGNN_SAGE2_PREP 1

@@ -120,6 +120,11 @@ struct NarrowHead {
     uint32_t *ticket;  // zero between calls
     const float *cnt_in;  // the valid-label count, written by an earlier launch (nullable: count here)
     int dbg;              // (profiling builds only: time-attribution variants; 0)
+    // seed-edge counts per source (nullable): arrays [2][scnt_stride], the
+    // word scnt_base[2 scnt_stride] selects this call's; the loss's last
+    // adder flips it for the next call (ngnn.h ngnn_xent_head src_count)
+    int32_t *scnt_base;
+    int scnt_stride;
 };
 
 // byte offset that is always outside a resource of < 2 GiB

@@ -173,6 +173,10 @@ struct G2Args {
     int cnt_B;
     int64_t cnt_ignore;
     float *cnt_out;
+    // ... and the head's seed-edge counts per source (nullable, NarrowHead's
+    // scnt_*): counted into the selected array, the other one cleared
+    int32_t *scnt_base;
+    int scnt_stride;
 };
 
 constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip for fanouts <= 16)
@@ -216,9 +220,26 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     if (a.gz) {  // the loss head's g rows, spread over the whole grid
         int gr = a.gz_rows;
         if (a.gz_rows_dev) gr = min(gr, *a.gz_rows_dev);
-        const int n4 = max(gr, 0) * (a.gz_ld >> 2);
+        gr = max(gr, 0);
+        const int n4 = gr * (a.gz_ld >> 2);
         for (int i = b * (F2_WAVES * 64) + static_cast<int>(threadIdx.x); i < n4; i += G * F2_WAVES * 64)
             reinterpret_cast<v4f *>(a.gz)[i] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (a.scnt_base) {
+            // this call's counts: one per edge into a seed row, by source (the
+            // array the head reads); the other array -- read by the previous
+            // call's head -- back to zero for the next call (rows < R': the
+            // sources any seed edge had; rows past it only ever over-count)
+            const int sel = a.scnt_base[2 * a.scnt_stride] & 1;
+            int32_t *cn = a.scnt_base + sel * a.scnt_stride;
+            int32_t *co = a.scnt_base + (sel ^ 1) * a.scnt_stride;
+            const int nc = min(gr, a.scnt_stride);
+            for (int i = b * (F2_WAVES * 64) + static_cast<int>(threadIdx.x); i < nc; i += G * F2_WAVES * 64) co[i] = 0;
+            const int es = a.rowptr[min(a.cnt_B, n_rows)];
+            for (int e = b * (F2_WAVES * 64) + static_cast<int>(threadIdx.x); e < es; e += G * F2_WAVES * 64) {
+                const int s = a.col[e];
+                if (static_cast<unsigned>(s) < static_cast<unsigned>(a.scnt_stride)) atomicAdd(cn + s, 1);
+            }
+        }
     }
     if (a.cnt_out && b == G - 1) {  // (the last workgroup: the fewest tiles)
         __shared__ float s_cnt[F2_WAVES];
@@ -1107,6 +1128,8 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         g.cnt_B = head ? static_cast<int>(head->B) : 0;
         g.cnt_ignore = head ? head->ignore_index : 0;
         g.cnt_out = head ? reinterpret_cast<float *>(static_cast<char *>(head->ws) + 4) : nullptr;
+        g.scnt_base = (head && head->g) ? head->src_count : nullptr;
+        g.scnt_stride = static_cast<int>(head ? head->g_rows : 0);
         const int tiles = static_cast<int>(ceil_div(g.n_edge, 16));
         const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, tiles)));
         int rc = NGNN_E_SHAPE;
@@ -1225,6 +1248,11 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         nh.cnt_in = ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0)
                         ? reinterpret_cast<const float *>(static_cast<char *>(head->ws) + 4)
                         : nullptr;
+        // the seed-edge counts only when this call's edge launch counted them
+        if ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0 && head->g) {
+            nh.scnt_base = head->src_count;
+            nh.scnt_stride = static_cast<int>(head->g_rows);
+        }
 #ifdef NGNN_FWD2_DBG_BUILD
         if (const char *d = getenv("NGNN_HEAD_DBG")) {
             nh.dbg = atoi(d);

@@ -203,6 +203,14 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
         float lsum = 0.0f;
         const int c4 = sub;
         const i32x4 zr = make_rsrc(z, 0xF0000000u);
+        // the seed-edge counts of this call (the selector read once; the
+        // loss's last adder flips it below, after every head workgroup read it)
+        int ssel = 0;
+        i32x4 scr = make_rsrc(nullptr, 0u);
+        if (hd.scnt_base && hwg) {
+            ssel = hd.scnt_base[2 * hd.scnt_stride] & 1;
+            scr = make_rsrc(hd.scnt_base + ssel * hd.scnt_stride, static_cast<uint32_t>(hd.scnt_stride) * 4u);
+        }
         const int dl = max(nr, B);
         const int vl = max(dl, 2 * B8);
         for (int v = (bx * 256 + static_cast<int>(threadIdx.x)) >> 4; v < vl; v += 16 * G) {
@@ -224,6 +232,12 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
 #pragma unroll
             for (int u = 0; u < NA_UNR; ++u) id[u] = buf_load1i(cr, beg + u < end ? 4 * (beg + u) : OOB, 0, 0);
             v4f acc{0.f, 0.f, 0.f, 0.f};
+            // a seed row's sources' edge counts (1: the source's g row takes
+            // one plain store); read with the gathers, used at the scatter
+            int scn[NA_UNR];
+#pragma unroll
+            for (int u = 0; u < NA_UNR; ++u)
+                scn[u] = buf_load1i(scr, (hrow && beg + u < end) ? static_cast<int>(4u * static_cast<uint32_t>(id[u])) : OOB, 0, 0);
             if (c4 < F4 && end > beg) {
                 v4f v[NA_UNR];
 #pragma unroll
@@ -292,9 +306,15 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
                 for (int u = 0; u < NA_UNR; ++u)
                     if (beg + u < end) {
                         float *gr = hd.g + static_cast<int64_t>(id[u]) * hd.ldg + 4 * c4;
+                        if (scn[u] == 1) {
+                            // the source's only seed edge: its g row (zeroed by
+                            // the edge launch) is this row's contribution
+                            if (c4 < F4) *reinterpret_cast<v4f *>(gr) = dv;
+                        } else {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (4 * c4 + j < Fo && dv[j] != 0.0f) atomicAdd(gr + j, dv[j]);  // exact 0 adds nothing
+                            for (int j = 0; j < 4; ++j)
+                                if (4 * c4 + j < Fo && dv[j] != 0.0f) atomicAdd(gr + j, dv[j]);  // exact 0 adds nothing
+                        }
                     }
                 for (int e = beg + NA_UNR; e < end; e += NA_UNR) {
                     int ie[NA_UNR];
@@ -353,6 +373,8 @@ __global__ __launch_bounds__(256) void k_narrow_agg(const float *__restrict__ z,
                         *hd.loss = t / cnt;  // 0/0 = NaN when every row is ignored, as torch
                         *hd.count = cnt;
                         *hd.ticket = 0u;
+                        // the next call's edge launch counts into the other array
+                        if (hd.scnt_base) hd.scnt_base[2 * hd.scnt_stride] = ssel ^ 1;
                     }
                 }
             }

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 OK = 0
 SLOT_UNSORTED = 1  # ngnn_slot_load's err bits (include/ngnn.h NGNN_SLOT_*)
@@ -149,10 +149,10 @@ def check(rc: int, what: str = "") -> None:
 
 
 class XentHead(ctypes.Structure):
-    """include/ngnn.h ngnn_xent_head (ngnn_sage2_fwd's loss head, ABI 15)."""
+    """include/ngnn.h ngnn_xent_head (ngnn_sage2_fwd's loss head, ABI 15; src_count ABI 17)."""
     _fields_ = [("y", _p), ("B", _i64), ("ignore_index", _i64), ("loss", _p), ("count", _p),
                 ("dy", _p), ("ldd", _i64), ("g", _p), ("g_rows", _i64), ("g_rows_dev", _p),
-                ("ws", _p), ("ws_bytes", _sz)]
+                ("ws", _p), ("ws_bytes", _sz), ("src_count", _p)]
 
 
 class AdamFold(ctypes.Structure):

@@ -533,6 +533,9 @@ class LossHead:
         self.g = torch.zeros(self.n_rows, (self.F1 + 3) & ~3, dtype=torch.float32, device=dev)
         self.ws = torch.zeros(max(_lib.load().ngnn_xent_head_workspace_bytes(self.B), 16), dtype=torch.uint8,
                               device=dev)
+        # per-source seed-edge counts (two alternating arrays + the selector
+        # word): single-edge sources take a plain row store, not atomics
+        self.src_count = torch.zeros(2 * self.n_rows + 1, dtype=torch.int32, device=dev)
         self.r_word = r_word  # the slot's R' word (its low int32 half)
 
     def start(self) -> "HeadResult":
@@ -552,7 +555,7 @@ class HeadResult:
         self.struct = _lib.XentHead(
             _lib.ptr(head.y), head.B, head.ignore, _lib.ptr(self.loss), _lib.ptr(self.count),
             _lib.ptr(head.dy), head.dy.stride(0), _lib.ptr(head.g), head.n_rows, _lib.ptr(head.r_word),
-            _lib.ptr(head.ws), head.ws.numel())
+            _lib.ptr(head.ws), head.ws.numel(), _lib.ptr(head.src_count))
 
 
 def head_ok(block: Block, x, params) -> bool:

@@ -103,10 +103,27 @@ def test_head_matches_torch(reduce, K0, F1, B):
     assert_wgrad(lh.g[:Rn, :F1].double(), g_r)
     assert int(lh.g[:Rn, F1:].count_nonzero()) == 0
     assert bool((lh.g[Rn:] == 7.0).all())  # rows past R' untouched
-    # the hand-off ticket is zero again: a second call repeats the loss bitwise
-    res2 = lh.start()
-    _forward(x, blk, reduce, params, head=res2)
-    assert float(res2.loss) == float(res.loss)
+    # the hand-off ticket is zero again: a second call repeats the loss bitwise.
+    # ABI 17: each call counts its seed edges per source into the array the
+    # previous call's head did not read (single-edge sources take a plain row
+    # store) -- g at the bar on every call, alternating between two blocks
+    # with different sources (a count array reused after another block's
+    # counts must have been cleared: a stale 1 would drop a contribution)
+    ei2, blk2, _ = _case(K0 + B + 1, N, B, Rn, F1)
+    g_r2 = _reference(_forward(x, blk2, reduce, params), y, ei2, B, reduce, Rn, F1)[2]
+    for i in range(4):
+        lh.g.fill_(7.0)
+        res2 = lh.start()
+        b_i, g_i = (blk2, g_r2) if i % 2 == 0 else (blk, g_r)
+        _forward(x, b_i, reduce, params, head=res2)
+        if i % 2 == 1:
+            assert float(res2.loss) == float(res.loss)
+        assert_wgrad(lh.g[:Rn, :F1].double(), g_i, msg=f"call {i + 2}")
+    assert int(lh.src_count[-1]) == 1  # five calls: the selector flipped each time
+    # both count paths were taken: sources with one seed edge and with several
+    m = ei[1] < B
+    cnt = torch.bincount(ei[0][m], minlength=Rn)
+    assert int((cnt == 1).sum()) > 0 and int((cnt > 1).sum()) > 0
 
 
 def test_head_ignored_and_bad_labels():
