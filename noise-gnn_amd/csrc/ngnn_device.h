@@ -262,6 +262,6 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
                   int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
                   float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st,
-                  bool exact = false);
+                  bool exact = false, const float *const *x_dev = nullptr);
 
 }  // namespace ngnn

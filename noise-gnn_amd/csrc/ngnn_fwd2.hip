@@ -201,8 +201,9 @@ constexpr int G2_NB = 16;  // neighbour rows in flight per lane (one round trip 
 // requested before the weight slices load (the two latencies overlap).
 // DBG (profiling builds only, NGNN_EDGE_DBG): bit 0 skips the row gathers
 // (out-of-range requests), 1 the MFMAs and nb stores, 2 the aggregate stores
+// (the body, shared by k_edge_nb and the fused k_fwd2x below)
 template <int C0, int DBG = 0>
-__global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
+__device__ __forceinline__ void edge_nb_body(const G2Args &a) {
     constexpr int PSTR = 32 * C0 + 16;  // 72 dwords = 8 mod 64 banks: conflict-free fragment reads
     constexpr int XPB = 2 * F2_ROWS * PSTR;
     __shared__ __attribute__((aligned(16))) _Float16 sxp[2 * XPB];
@@ -424,6 +425,11 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
     if (ntj & 1) step(ntj - 1, va, vb);
 }
 
+template <int C0, int DBG = 0>
+__global__ __launch_bounds__(F2_WAVES * 64) void k_edge_nb(G2Args a) {
+    edge_nb_body<C0, DBG>(a);
+}
+
 // ---------------------------------------------------------------- k_fwd2
 struct F2Args {
     const float *x;
@@ -470,7 +476,7 @@ struct F2Args {
 // layer-1 products, 2 layer 0's products, 3 the x split, 4 the out / z
 // stores (offsets out of range) -- time attribution
 template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0>
-__global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
+__device__ __forceinline__ void fwd2_body(const F2Args &a) {
     constexpr int MT1 = 2 * NT1;
     constexpr int CF = T16 ? C0 - 1 : C0;    // full 32-deep chunks of layer 0
     constexpr int KC = 32 * CF + (T16 ? 16 : 0);  // K0 padded to the chunks
@@ -969,6 +975,27 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
     else pipeline(std::false_type{});
 }
 
+template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0>
+__global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
+    fwd2_body<C0, NT1, DM, XR, T16, DBG>(a);
+}
+
+// Both launches as ONE (round 5): the edge phase and the main phase map tile
+// t to workgroup t % G alike, so the nb rows a workgroup's main phase reads
+// are the ones its own edge phase wrote -- by the same lanes (k_edge_nb's
+// multiply and k_fwd2's nbload address a row's columns 32 wv + 4 q .. alike)
+// -- and the only hand-off is this workgroup's barrier.  Saves the launch
+// boundary and lets workgroups with fewer edge tiles start their main tiles
+// while others still gather (the edge phase has ~4 tiles per workgroup on
+// the products block, the main phase ~38).  The edge phase's LDS is static,
+// the main phase's dynamic: both fit together (138 KB).
+template <int C0, int NT1, int DM, bool XR, bool T16>
+__global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2x(G2Args g, F2Args f) {
+    edge_nb_body<C0, 0>(g);
+    __syncthreads();  // (workgroup scope: this workgroup's nb / agg stores before its main phase's reads)
+    fwd2_body<C0, NT1, DM, XR, T16, 0>(f);
+}
+
 template <int C0, int NT1, int DM, bool XR, int DBG = 0, bool T16 = false>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG>;
@@ -982,6 +1009,26 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
         attr_set = true;
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(F2_WAVES * 64), lds, st, a);
+    return launch_status();
+}
+
+template <int C0, int NT1, int DM, bool XR, bool T16 = false>
+int launch_fwd2x(const G2Args &g, const F2Args &a, int grid, hipStream_t st) {
+    auto fn = k_fwd2x<C0, NT1, DM, XR, T16>;
+    const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
+                       static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
+                       (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
+    static bool attr_set = false;  // benign race: idempotent
+    if (!attr_set) {
+        // (the edge phase's static LDS counts against the same 160 KiB: the
+        // dynamic maximum is exactly what the main phase takes -- a 160 KiB
+        // request is refused, and the launch then fails)
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        if (e != hipSuccess) return static_cast<int>(e);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(F2_WAVES * 64), lds, st, g, a);
     return launch_status();
 }
 
@@ -1099,8 +1146,19 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     // (NGNN_SAGE2_PREP: accepted, nothing to do -- the kernels load their
     // weight slices themselves since ABI 13's first release)
     const int ncu = num_cus();
+    // the edge and main launches as one (k_fwd2x) when both run in this call
+    // (NGNN_FWD2_FUSE=0, read once: two launches -- A/B)
+    static const bool fuse_env = [] {
+        const char *v = std::getenv("NGNN_FWD2_FUSE");
+        return !(v && v[0] == '0');
+    }();
+    bool fuse = fuse_env && (stages & NGNN_SAGE2_MAIN) && (stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0 &&
+                C0 == 4 && NT1 == 3;
+#ifdef NGNN_FWD2_DBG_BUILD
+    if (getenv("NGNN_FWD2_DBG") || getenv("NGNN_EDGE_DBG")) fuse = false;
+#endif
+    G2Args g{};
     if ((stages & NGNN_SAGE2_EDGE) && n_edge_rows > 0) {
-        G2Args g;
         g.x = x;
         g.x_dev = x_dev;
         g.ldx = ldx;
@@ -1150,8 +1208,10 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
             }
         }
 #endif
-        if (C0 == 4) rc = launch_edge_nb<4>(g, grid, st);
-        if (rc) return rc;
+        if (!fuse) {
+            if (C0 == 4) rc = launch_edge_nb<4>(g, grid, st);
+            if (rc) return rc;
+        }
     } else if ((stages & NGNN_SAGE2_EDGE) && head && head->g && head->g_rows > 0) {
         // (no edge launch to zero the head's g: every row up to its static bound)
         const hipError_t e = hipMemsetAsync(head->g, 0, static_cast<size_t>(head->g_rows * C4 * 4), st);
@@ -1219,6 +1279,15 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         const bool t16 = t16_ok && K0 <= 112;
         auto go = [&](auto xr_c) {
             constexpr bool XRv = decltype(xr_c)::value;
+            if (fuse) {
+                if (t16)
+                    return dm == 2   ? launch_fwd2x<4, 3, 2, XRv, true>(g, f, grid, st)
+                           : dm == 1 ? launch_fwd2x<4, 3, 1, XRv, true>(g, f, grid, st)
+                                     : launch_fwd2x<4, 3, 0, XRv, true>(g, f, grid, st);
+                return dm == 2   ? launch_fwd2x<4, 3, 2, XRv>(g, f, grid, st)
+                       : dm == 1 ? launch_fwd2x<4, 3, 1, XRv>(g, f, grid, st)
+                                 : launch_fwd2x<4, 3, 0, XRv>(g, f, grid, st);
+            }
             if (t16)
                 return dm == 2   ? launch_fwd2<4, 3, 2, XRv, 0, true>(f, grid, st)
                        : dm == 1 ? launch_fwd2<4, 3, 1, XRv, 0, true>(f, grid, st)

@@ -28,6 +28,7 @@ struct AdamTensors {
     int n;
 };
 
+constexpr int kAdamTickets = 64;              // uint32 words of the ticket (ABI 17)
 constexpr int kAdamVec = 4;                   // elements per thread
 constexpr int kAdamChunk = 256 * kAdamVec;    // elements per virtual workgroup
 
@@ -118,11 +119,22 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
     }
     if (ticket) {
         // every workgroup has read *step (its value fed the loop above) before
-        // it takes a ticket; the last one advances the count for the next call
+        // it takes a ticket; the last one advances the count for the next call.
+        // Two levels (ABI 17): groups of 32 workgroups count on their own
+        // ticket, the last of each on the top one -- same-address atomics
+        // serialise at the memory side (~25 ns each: one ticket for 512
+        // workgroups was 12 us of the launch)
         __syncthreads();
-        if (threadIdx.x == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {
-            *step = t;
-            *ticket = 0u;
+        if (threadIdx.x == 0) {
+            const unsigned gi = blockIdx.x >> 5, gs = min(32u, gridDim.x - (gi << 5));
+            const unsigned ngr = (gridDim.x + 31) >> 5;
+            if (atomicAdd(ticket + 1 + gi, 1u) == gs - 1) {
+                ticket[1 + gi] = 0u;  // (every member has counted)
+                if (atomicAdd(ticket, 1u) == ngr - 1) {
+                    *step = t;
+                    *ticket = 0u;
+                }
+            }
         }
     }
 }
@@ -172,8 +184,15 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         T.boff[0] = 0;
         for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], kAdamChunk);
         NGNN_RETURN_IF(T.boff[T.n] > (int64_t{1} << 31) - 1, NGNN_E_RANGE);
-        // at most 2 workgroups per CU: the rest is the grid-stride loop
-        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(T.boff[T.n], 2 * num_cus()));
+        // at most 2 workgroups per CU: the rest is the grid-stride loop (and at
+        // most 32 x 63 -- the ticket's groups)
+        // (NGNN_ADAM_WG_PER_CU, read once: the per-CU cap -- A/B)
+        static const int wg_cu = [] {
+            const char *e = std::getenv("NGNN_ADAM_WG_PER_CU");
+            return e ? std::max(1, std::atoi(e)) : 2;
+        }();
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(std::min<int64_t>(T.boff[T.n], wg_cu * num_cus()),
+                                                                      32 * (kAdamTickets - 1)));
         hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
                            eps, weight_decay);
         const int rc = launch_status();

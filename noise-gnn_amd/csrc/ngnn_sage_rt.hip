@@ -818,11 +818,13 @@ extern "C" int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, cons
     }
     // wide layers (the row-tile kernel's weight image too large for its LDS,
     // or K % 4 != 0): aggregate launch + 2-D tiled dual GEMM
-    if (x && !x_dev && !xrow && !xrow_dev && !x_bf16 && !out_bf16 && sage_wide_preferred(K, Fo, exact) &&
+    // (x_dev: a graph slot's batch rows in place -- K % 4 != 0 rows too, the
+    // wide kernels load them at 4-B alignment)
+    if ((x || x_dev) && !xrow && !xrow_dev && !x_bf16 && !out_bf16 && sage_wide_preferred(K, Fo, exact) &&
         (agg_out || !wl || ws_bytes >= sage_wide_workspace_bytes(K, n_edge_rows)))
         return sage_fwd_wide(x, ldx, K, n_rows, n_rows_dev, n_edge_rows, n_edge_rows_dev, rowptr,
                              col, reduce, wl, wr, ldw, bias, Fo, out, ldo, relu, p_drop, seed,
-                             seed_dev, agg_out, ld_agg, ws, ws_bytes, st, exact);
+                             seed_dev, agg_out, ld_agg, ws, ws_bytes, st, exact, x_dev);
     // max layers with a wide input: the aggregate by its own launch (a wave per
     // row, every column in flight) into the saved-aggregate buffer, which the
     // row-tile kernel's edge tiles then read densely -- its in-kernel gather

@@ -124,6 +124,7 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
 
 struct WideArgs {
     const float *x;
+    const float *const *x_dev;  // non-null: x's address read at run time (a graph slot's batch, zero-copy)
     int64_t ldx;
     const float *agg;  // NULL: no neighbour term
     int64_t ld_agg;
@@ -142,6 +143,7 @@ struct WideArgs {
 template <bool VOUT>
 __global__ __launch_bounds__(256, 2) void k_wide_gemm(WideArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * WSTAGE];
+    if (a.x_dev) a.x = gload(a.x_dev, 0);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int rows = a.n_rows;
     if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
@@ -324,6 +326,7 @@ template <bool VOUT>
 __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__restrict__ wimg, int Kp) {
     typedef __bf16 b8 __attribute__((ext_vector_type(8)));
     extern __shared__ __attribute__((aligned(16))) __bf16 xlds[];  // [2][XW_STAGE]
+    if (a.x_dev) a.x = gload(a.x_dev, 0);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int rows = a.n_rows;
     if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
@@ -539,7 +542,8 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   const int32_t *rowptr, const int32_t *col, int reduce, const float *wl,
                   const float *wr, int64_t ldw, const float *bias, int64_t Fo, float *out,
                   int64_t ldo, int relu, float p_drop, uint64_t seed, const uint64_t *seed_dev,
-                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st, bool exact) {
+                  float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st, bool exact,
+                  const float *const *x_dev) {
     const int64_t n_edge = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
     float *agg = nullptr;
     int64_t lda = ld_agg;
@@ -557,7 +561,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                                dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                                static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, lda,
-                               static_cast<int>(n_rows), 0, nullptr);
+                               static_cast<int>(n_rows), 0, x_dev);
         };
         auto by_nc = [&](auto red_c) {
             if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
@@ -572,6 +576,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     }
     WideArgs a;
     a.x = x;
+    a.x_dev = x_dev;
     a.ldx = ldx;
     a.agg = agg;
     a.ld_agg = lda;

@@ -31,6 +31,7 @@ graph's up to fp32 summation order; nothing is read back to the host.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 
 import torch
@@ -240,7 +241,7 @@ def sage_layer_fwd(x: torch.Tensor, block: Block, reduce: str, wl, bl, wr, relu:
         wr_ = _pad_cols(wr_, K4) if root else None
     nrd = _lib.ptr(block.n_rows_dev) if block.n_rows_dev is not None else None
     lib = _lib.load()
-    if (not xb and x_dev is None and xrow_dev is None and not (narrow and agg_out is None)
+    if (not xb and xrow_dev is None and not (narrow and agg_out is None)
             and lib.ngnn_sage_wide_preferred(xk.size(1), Fo, int(_exact_f32))):
         # the wide path (ngnn_wide.hip): exact f32 MFMA throughout, and the
         # aggregate of the rows with in-edges written then re-read
@@ -429,6 +430,12 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
                                                 _lib.REDUCE[reduce]))
 
 
+def fwd2_fused() -> bool:
+    """Does ngnn_sage2_fwd run its edge and main stages as ONE launch
+    (k_fwd2x; NGNN_FWD2_FUSE=0 keeps two -- read by the library once)?"""
+    return os.environ.get("NGNN_FWD2_FUSE", "1") != "0"
+
+
 def sage2_params(params):
     """The six tensors ngnn_sage2_fwd / _bwd take.  A two-layer SimpleGCN
     stack ([W, b, None] per GCNConv(normalize=False), sum aggregation) is the
@@ -498,15 +505,21 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     ldz = 16 * (-(-F1 // 16))
     h_rows = N  # (upper bound: under the slot's bound fewer rows are written)
     f16 = 16 * MFMA_F32_TFS * 1e12  # fp16 MFMA peak; three products per fp32-equivalent product
-    stages = [
-        ("sage2_edge", _lib.SAGE2_EDGE,
-         4 * (block.E * (K0 + 1) + n_e * (K0 + 1) + n_e * K0 + n_e * H),
-         2 * n_e * K0 * H, 3 * 2 * n_e * C0p * H / f16),
-        ("sage2_fwd", _lib.SAGE2_MAIN,
-         4 * (N * K0 + n_e * H + h_rows * H + N * F1 + N * ldz),
-         2 * N * K0 * H + 4 * N * H * F1, 3 * (2 * N * C0p * H + 2 * N * H * 2 * ldz) / f16),
-        ("sage2_narrow", _lib.SAGE2_NARROW, 4 * (block.E * (ldz + 1) + 2 * n_e * F1 + n_e + 1), 0, 0.0),
-    ]
+    edge = ("sage2_edge", _lib.SAGE2_EDGE,
+            4 * (block.E * (K0 + 1) + n_e * (K0 + 1) + n_e * K0 + n_e * H),
+            2 * n_e * K0 * H, 3 * 2 * n_e * C0p * H / f16)
+    main = ("sage2_fwd", _lib.SAGE2_MAIN,
+            4 * (N * K0 + n_e * H + h_rows * H + N * F1 + N * ldz),
+            2 * N * K0 * H + 4 * N * H * F1, 3 * (2 * N * C0p * H + 2 * N * H * 2 * ldz) / f16)
+    if fwd2_fused():
+        # one launch for both (k_fwd2x, as in the step): its bytes / flops are
+        # the two phases' sums (nb's write and read stay: the main phase reads
+        # it back through L2)
+        stages = [("sage2_fwd", _lib.SAGE2_EDGE | _lib.SAGE2_MAIN, edge[2] + main[2], edge[3] + main[3],
+                   edge[4] + main[4])]
+    else:
+        stages = [edge, main]
+    stages.append(("sage2_narrow", _lib.SAGE2_NARROW, 4 * (block.E * (ldz + 1) + 2 * n_e * F1 + n_e + 1), 0, 0.0))
     for name, st, nbytes, flops, mfma_s in stages:
         with _timing.span(name, nbytes, flops, mfma_s):
             rc = lib.ngnn_sage2_fwd(*args, hp, st, *tail)
@@ -1030,10 +1043,15 @@ def zero_copy_ok(model, n_rows: int, in_dim: int, table_rows: int = 0) -> bool:
     if getattr(model, "use_bn", False):
         return False
     c0 = model.convs[0]
+    wide = False
     if hasattr(c0, "lin_r"):
         if len({c.aggr for c in model.convs}) != 1:
             return False
         fo = c0.lin_r.weight.shape[0]
+        # layer 0 on the wide path (Amazon-Computers' 767 -> 512): its
+        # kernels read the rows in place at 4-B alignment, any K
+        wide = (not table_rows and c0.lin_r.weight.dtype == torch.float32
+                and bool(_lib.load().ngnn_sage_wide_preferred(in_dim, fo, int(_exact_f32))))
     elif hasattr(c0, "lin"):  # SimpleGCN
         fo = c0.lin.weight.shape[0]
         if in_dim > fo:  # transform-first layer 0: backward rebuilds its aggregate from x
@@ -1045,6 +1063,8 @@ def zero_copy_ok(model, n_rows: int, in_dim: int, table_rows: int = 0) -> bool:
     lim = 0xF0000000 - 4096
     if table_rows and table_rows * in_dim * 4 >= 2**31:
         return False
+    if wide:
+        return n_rows * in_dim * 4 <= lim
     return (in_dim % 4 == 0 and max(n_rows, table_rows) * in_dim * 4 <= lim
             and -(-in_dim // 16) <= 79)
 

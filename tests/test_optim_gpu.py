@@ -76,3 +76,32 @@ def test_bf16_params_match_rounded_fp32_adam():
         assert a.dtype == torch.bfloat16
         torch.testing.assert_close(a.float(), c, rtol=8e-3, atol=1e-6)
     assert ob.state[pb[0]]["exp_avg"].dtype == torch.float32
+
+
+@pytest.mark.parametrize("shapes", [
+    [(512, 767), (512, 767), (10, 512), (10,), (512,)],  # Amazon-Computers: the 2-CU cap, 16 full groups
+    [(300, 1000), (7,), (33, 5)],                        # ~300 workgroups: a ragged last group
+])
+def test_two_level_ticket_many_workgroups(shapes):
+    """ABI 17: the update's workgroups count on a two-level ticket (groups of
+    32, then the top word).  Three steps against torch's Adam, the device step
+    count advanced once per call, every ticket word zero again after each."""
+    from ngnn.optim import Adam
+    g = torch.Generator().manual_seed(11)
+    ps = [torch.randn(s, generator=g).to(DEV) for s in shapes]
+    p1 = [p.clone().requires_grad_(True) for p in ps]
+    p2 = [p.clone().requires_grad_(True) for p in ps]
+    o1, o2 = Adam(p1, lr=1e-3), torch.optim.Adam(p2, lr=1e-3)
+    for it in range(3):
+        for a, b in zip(p1, p2):
+            gr = torch.randn(a.shape, generator=g).to(DEV)
+            a.grad, b.grad = gr.clone(), gr.clone()
+        o1.step()
+        o2.step()
+        torch.cuda.synchronize()
+        step = o1.state[p1[0]]["step"]
+        assert float(step) == it + 1
+        ticket = o1._tickets[step.data_ptr()]
+        assert int(ticket.count_nonzero()) == 0
+        for a, b in zip(p1, p2):
+            torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=1e-7)
