@@ -57,7 +57,8 @@ def main():
         head = lh.start()
     bufs = fused.sage2_forward(b.x, blk, "mean", params, 0.5, seed, None, head=head)[:3]
     torch.cuda.synchronize()
-    st = {"edge": _lib.SAGE2_EDGE, "main": _lib.SAGE2_MAIN, "narrow": _lib.SAGE2_NARROW}
+    st = {"edge": _lib.SAGE2_EDGE, "main": _lib.SAGE2_MAIN, "narrow": _lib.SAGE2_NARROW,
+          "fused": _lib.SAGE2_EDGE | _lib.SAGE2_MAIN}  # (fused: k_fwd2x, as the step runs it)
     n_e = int(blk.n_active or 0)
     print(f"block: N={b.num_nodes} E={b.edge_index.size(1)} n_edge_rows={n_e} "
           f"dbg={os.environ.get('NGNN_FWD2_DBG', '-')}")
