@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--host-prof", action="store_true")
     ap.add_argument("--cprofile", action="store_true")
+    ap.add_argument("--ngnn-adam", action="store_true", help="ngnn.optim.Adam in place of torch.optim.Adam")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = synthetic_graph("ogbn-products", dev, seed=0)
@@ -28,7 +29,8 @@ def main():
     batches = [next(it) for _ in range(10)]
     torch.manual_seed(1234)
     model = ngnn.SAGE(100, 256, 47, 2, dropout=0.5).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    from ngnn.optim import Adam as NgnnAdam
+    opt = (NgnnAdam if a.ngnn_adam else torch.optim.Adam)(model.parameters(), lr=1e-3)
 
     def one(b):
         out = model(b.x, b.edge_index)[:b.batch_size]
