@@ -47,6 +47,18 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
                                               uint32_t *__restrict__ ticket, float lr, float b1,
                                               float b2, float eps, float wd) {
     const float t = *step + 1.0f;
+    // the completion ticket is taken right after every thread has read the
+    // count (what it guards), not after the update: the atomic's round trip
+    // overlaps the workgroup's loads instead of holding its end (a ticket at
+    // the end measured 12.4 vs 8.5 us for update + increment launches on
+    // Amazon-Computers' 0.8 M parameters, tools/adam_micro.py)
+    const unsigned gi = blockIdx.x >> 5, gs = min(32u, gridDim.x - (gi << 5));
+    uint32_t tk = 0u;
+    if (ticket) {
+        asm volatile("" ::"v"(t));  // (this thread's read of *step has landed)
+        __syncthreads();
+        if (threadIdx.x == 0) tk = atomicAdd(ticket + 1 + gi, 1u);
+    }
     const float bc1 = 1.0f - powf(b1, t);
     const float bc2s = sqrtf(1.0f - powf(b2, t));
     const float step_size = lr / bc1;
@@ -117,24 +129,15 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
             }
         }
     }
-    if (ticket) {
-        // every workgroup has read *step (its value fed the loop above) before
-        // it takes a ticket; the last one advances the count for the next call.
-        // Two levels (ABI 17): groups of 32 workgroups count on their own
-        // ticket, the last of each on the top one -- same-address atomics
-        // serialise at the memory side (~25 ns each: one ticket for 512
-        // workgroups was 12 us of the launch)
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned gi = blockIdx.x >> 5, gs = min(32u, gridDim.x - (gi << 5));
-            const unsigned ngr = (gridDim.x + 31) >> 5;
-            if (atomicAdd(ticket + 1 + gi, 1u) == gs - 1) {
-                ticket[1 + gi] = 0u;  // (every member has counted)
-                if (atomicAdd(ticket, 1u) == ngr - 1) {
-                    *step = t;
-                    *ticket = 0u;
-                }
-            }
+    if (ticket && threadIdx.x == 0 && tk == gs - 1) {
+        // the last of its group of 32 (every member has read *step): counts on
+        // the top ticket (two levels, ABI 17 -- same-address atomics
+        // serialise at the memory side); the last group advances the count
+        ticket[1 + gi] = 0u;
+        const unsigned ngr = (gridDim.x + 31) >> 5;
+        if (atomicAdd(ticket, 1u) == ngr - 1) {
+            *step = t;
+            *ticket = 0u;
         }
     }
 }
@@ -158,6 +161,11 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
     hipStream_t st = as_stream(stream);
     // the ticket path needs every tensor in one launch (one reader set of *step)
     if (n_tensors > kMaxT) ticket = nullptr;
+    static const bool no_ticket = [] {  // (NGNN_ADAM_NO_TICKET=1, read once: update + increment launches -- A/B)
+        const char *e = std::getenv("NGNN_ADAM_NO_TICKET");
+        return e && e[0] == '1';
+    }();
+    if (no_ticket) ticket = nullptr;
     bool launched = false;
     for (int base = 0; base < n_tensors; base += kMaxT) {
         AdamTensors T;
@@ -184,6 +192,12 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         T.boff[0] = 0;
         for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], kAdamChunk);
         NGNN_RETURN_IF(T.boff[T.n] > (int64_t{1} << 31) - 1, NGNN_E_RANGE);
+        // the ticket only for small updates: past ~128 workgroups the ticket's
+        // atomics at the workgroups' ends cost more than a second one-lane
+        // launch (Amazon-Computers' 0.8 M parameters: 11.9 vs 8.6 us per step
+        // for update + increment; 26 k parameters: 4.7 vs 5.9,
+        // tools/adam_micro.py)
+        if (T.boff[T.n] > 128) ticket = nullptr;
         // at most 2 workgroups per CU: the rest is the grid-stride loop (and at
         // most 32 x 63 -- the ticket's groups)
         // (NGNN_ADAM_WG_PER_CU, read once: the per-CU cap -- A/B)

@@ -10,9 +10,9 @@ import torch  # noqa: E402
 from ngnn.optim import Adam  # noqa: E402
 
 
-def main(reps=50):
+def main(reps=50, scale=1.0):
     dev = torch.device("cuda:0")
-    shapes = [(512, 767), (512,), (512, 767), (10, 512), (10,), (10, 512)]
+    shapes = [(max(1, int(512 * scale)), 767), (512,), (max(1, int(512 * scale)), 767), (10, 512), (10,), (10, 512)]
     ps = [torch.randn(s, device=dev, requires_grad=True) for s in shapes]
     for p in ps:
         p.grad = torch.randn_like(p)
@@ -36,8 +36,9 @@ def main(reps=50):
     g.replay()
     e1.record()
     torch.cuda.synchronize()
-    print(f"adam step {e0.elapsed_time(e1) * 1e3 / reps:8.2f} us/launch (graph of {reps})")
+    n = sum(p.numel() for p in ps)
+    print(f"adam step {e0.elapsed_time(e1) * 1e3 / reps:8.2f} us/launch (graph of {reps}, {n} parameters)")
 
 
 if __name__ == "__main__":
-    main()
+    main(scale=float(sys.argv[1]) if len(sys.argv) > 1 else 1.0)
