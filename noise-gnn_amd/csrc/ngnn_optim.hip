@@ -192,12 +192,11 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         T.boff[0] = 0;
         for (int k = 0; k < T.n; ++k) T.boff[k + 1] = T.boff[k] + ceil_div(numels[base + k], kAdamChunk);
         NGNN_RETURN_IF(T.boff[T.n] > (int64_t{1} << 31) - 1, NGNN_E_RANGE);
-        // the ticket only for small updates: past ~128 workgroups the ticket's
-        // atomics at the workgroups' ends cost more than a second one-lane
-        // launch (Amazon-Computers' 0.8 M parameters: 11.9 vs 8.6 us per step
-        // for update + increment; 26 k parameters: 4.7 vs 5.9,
-        // tools/adam_micro.py)
-        if (T.boff[T.n] > 128) ticket = nullptr;
+        // (without the ticket -- NGNN_ADAM_NO_TICKET=1 -- the update is a
+        // separate launch from the one-lane increment: on Amazon-Computers'
+        // 0.8 M parameters 8.6 vs 11.9 us per step in a graph of Adam steps
+        // alone (tools/adam_micro.py), but 9.3 + 4.0 vs 12.8 us inside the
+        // training step's graph: the ticket stays)
         // at most 2 workgroups per CU: the rest is the grid-stride loop (and at
         // most 32 x 63 -- the ticket's groups)
         // (NGNN_ADAM_WG_PER_CU, read once: the per-CU cap -- A/B)

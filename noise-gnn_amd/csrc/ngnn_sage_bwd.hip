@@ -394,7 +394,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(
     float yscale, const float *__restrict__ h_arg, const float *const *h_dev, int64_t ldh,
     const int64_t *h_idx_arg, const int64_t *const *h_idx_dev, int64_t h_rows,
     const float *__restrict__ agg, int64_t ld_agg, const int32_t *__restrict__ rowptr,
-    const int32_t *__restrict__ r_ptr, int Fo, int K, float *__restrict__ ws) {
+    const int32_t *__restrict__ r_ptr, int Fo, int K, float *__restrict__ ws, int S_l, int GY, int GZ) {
     constexpr int NPH = HB ? 1 : 3;
     constexpr int WNC = WG_NC * NFW;  // Fo columns per workgroup
     constexpr int X3Z = WNC + 16;
@@ -404,22 +404,30 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(
     __bf16 *ai = hi + NPH * WG_BM * X3H;           // [3][64][X3H]
     const float *__restrict__ h = h_dev ? *h_dev : h_arg;
     const int64_t *h_idx = h_idx_dev ? *h_idx_dev : h_idx_arg;
+    // 1-D grid, XCD-grouped (workgroup L runs on XCD L mod 8): the GZ Fo
+    // chunks of one (row slice, K chunk) pair -- the workgroups that read the
+    // same h / agg rows -- share an XCD and so its L2, instead of landing on
+    // four of them (Amazon-Computers' S = 5, GY = 6: a pair's chunks were 30
+    // ids apart); pair ids padded to a multiple of 8 (the padding exits)
+    const int L = blockIdx.x, r8 = L >> 3;
+    const int pr = (r8 / GZ) * 8 + (L & 7), zc = r8 % GZ;
+    if (pr >= S_l * GY) return;
     const int R = *r_ptr;
-    const int S = wgrad_slices(R, gridDim.x);
-    const int s = blockIdx.x;
+    const int S = wgrad_slices(R, S_l);
+    const int s = pr % S_l;
     if (s >= S) return;
     const int R4 = (R + 3) >> 2;
     const int rb = 4 * static_cast<int>(static_cast<int64_t>(s) * R4 / S);
     const int re = min(R, 4 * static_cast<int>(static_cast<int64_t>(s + 1) * R4 / S));
-    const int k0 = blockIdx.y * WG_KC;
-    const int n0 = blockIdx.z * WNC;
+    const int k0 = (pr / S_l) * WG_KC;
+    const int n0 = zc * WNC;
     const int kc = min(WG_KC, K - k0);
     const int nc = min(WNC, Fo - n0);
     const int KT = __builtin_amdgcn_readfirstlane((kc + 15) >> 4);
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63;
     const int mat = wv >> 2, w4 = wv & 3;
-    const bool do_bias = blockIdx.y == 0 && mat == 0;
+    const bool do_bias = k0 == 0 && mat == 0;
 
     v4f acc[NFW][8], accb[NFW];
 #pragma unroll
@@ -1252,7 +1260,8 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
         const int nfw = hb && Fo >= 128 ? nfw_max : 1;
         const size_t lds = (static_cast<size_t>(3) * WG_BM * (WG_NC * nfw + 16) + (hb ? 1 : 3) * WG_BM * X3H +
                             static_cast<size_t>(3) * WG_BM * X3H) * 2;
-        const dim3 grid2(S, static_cast<unsigned>(gy), static_cast<unsigned>(ceil_div(Fo, WG_NC * nfw)));
+        const int gz2 = static_cast<int>(ceil_div(Fo, WG_NC * nfw));
+        const dim3 grid2(static_cast<unsigned>(ceil_div(static_cast<int64_t>(S) * gy, 8) * 8 * gz2));
         auto go = [&](auto hb_c, auto m_c) {
             constexpr bool HBv = decltype(hb_c)::value;
             auto fn = (HBv && nfw == 2) ? k_wgrad_x3<HBv, decltype(m_c)::value, 2>
@@ -1264,7 +1273,8 @@ extern "C" int ngnn_sage_wgrad(const float *dy, int64_t ldy, const float *y, int
                 attr[nfw] = true;
             }
             hipLaunchKernelGGL(fn, grid2, dim3(512), lds, st, dy, ldy, y, ldyy, yscale, h, h_dev, ldh,
-                               h_idx, h_idx_dev, h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf);
+                               h_idx, h_idx_dev, h_rows, agg, ld_agg, rowptr, r_ptr, (int)Fo, (int)K, wsf, S,
+                               static_cast<int>(gy), gz2);
         };
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
