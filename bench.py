@@ -263,18 +263,19 @@ def l0_launch_us(gstep, model, aggr: str, timed, flush_mb: int = 512, dom: str =
             [q.detach() if q is not None else None for cv in model.convs
              for q in ((cv.lin_l.weight, cv.lin_l.bias, cv.lin_r.weight) if hasattr(cv, "lin_l")
                        else (cv.lin.weight, cv.bias, None))])
-        bufs = fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev)
+        root0 = hasattr(c, "lin_l")  # (SimpleGCN: no root term, x never read)
+        bufs = fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev, root0=root0)
         # (fused: the edge and main phases are one launch, k_fwd2x -- timed
         # together, as the step runs them)
         fz = fused.fwd2_fused()
 
         def pre():
             fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev,
-                                stages=_lib.SAGE2_PREP | (0 if fz else _lib.SAGE2_EDGE), bufs=bufs)
+                                stages=_lib.SAGE2_PREP | (0 if fz else _lib.SAGE2_EDGE), bufs=bufs, root0=root0)
 
         def run():
             fused.sage2_forward(x, blk, aggr, params, p, 0, blk.seed_dev,
-                                stages=_lib.SAGE2_MAIN | (_lib.SAGE2_EDGE if fz else 0), bufs=bufs)
+                                stages=_lib.SAGE2_MAIN | (_lib.SAGE2_EDGE if fz else 0), bufs=bufs, root0=root0)
     else:
         wl, bl, wr = (q.detach().float() for q in (c.lin_l.weight, c.lin_l.bias, c.lin_r.weight))
         agg = fused.agg_buffer(gstep.n_cap, x.size(1), x.device, wl.shape[0])

@@ -341,7 +341,10 @@ int ngnn_sage_fwd_raw(const float *x, const float *const *x_dev, const int64_t *
  * when unknown).  x_dev (nullable): device word holding x's address (graph
  * slot), x then unused.  xrow / xrow_dev / x_rows / col_x: the fused
  * x[n_id] gather, as ngnn_sage_fwd_raw's (x is the x_rows-row feature table,
- * col_x = n_id[col]).  Arithmetic: H2 (two fp16 parts per operand after
+ * col_x = n_id[col]).  wr0 (nullable, ABI 17): no layer-0 root term --
+ * SimpleGCN's GCNConv(normalize=False), aggregate first: x is then read
+ * only through the neighbour aggregate (not with xrow / xrow_dev); pass a
+ * zero W_r1 for its output layer.  Arithmetic: H2 (two fp16 parts per operand after
  * power-of-two scaling, three MFMA products), inside the fp32 parity bars.
  * stages: NGNN_SAGE2_ALL, or a subset in order (per-launch timing; the
  * workspace carries nb and z between stages): EDGE the aggregate + nb of
@@ -421,9 +424,10 @@ int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const int64_t *xro
  * dy [*, ldy] (rows < R read), h [*, ldh] / agg0 [*, ld_agg] the forward's
  * (rows < R' read; an edgeless row's aggregate counts as 0), x / x_dev /
  * xrow / xrow_dev / x_rows as ngnn_sage2_fwd's (row r of layer 0's input).
- * Arithmetic: two bf16 parts per fp32 operand, three MFMA products per
- * product (relative ~2^-16), fp32 accumulation -- inside the weight-gradient
- * bars.  F1 <= 48, 0 < K0 <= 128, K0 % 4 == 0; weights [F1, 256] rows of
+ * Arithmetic (round 5): H2 -- two fp16 parts per operand after a
+ * power-of-two scaling per 32-row chunk, three MFMA products per product
+ * (relative ~2^-22), fp32 accumulation -- inside the fp32 weight-gradient
+ * bars (1e-5 of each tensor's max).  F1 <= 48, 0 < K0 <= 128, K0 % 4 == 0; weights [F1, 256] rows of
  * ldw1 floats.  ws: ngnn_sage2_bwd_workspace_bytes(n_rows, K0, F1), 256-B
  * aligned, ZERO-FILLED before its first use (g's part is zero again on
  * return; its offset depends on K0 and F1 only, so a zeroed workspace may be

@@ -475,7 +475,10 @@ struct F2Args {
 // DBG (profiling builds only, NGNN_FWD2_DBG): bit 0 skips the reduce, 1 the
 // layer-1 products, 2 layer 0's products, 3 the x split, 4 the out / z
 // stores (offsets out of range) -- time attribution
-template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0>
+// ROOT false (ABI 17: wr0 NULL -- GCNConv's aggregate-first layer, W_r = 0):
+// no x rows at all -- no loads, no split, no layer-0 products; h = act(b0 +
+// nb) (act(b0) on rows without in-edges)
+template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0, bool ROOT = true>
 __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     constexpr int MT1 = 2 * NT1;
     constexpr int CF = T16 ? C0 - 1 : C0;    // full 32-deep chunks of layer 0
@@ -506,8 +509,8 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     // ---- this wave's weight slices, for the whole launch
     half8 wr[2][CF][2], w1[MT1][2];
     half4 wt[2][2];  // T16: the tail chunk, k = 32 CF + 4 q .. + 3
-    int eW0;
-    {
+    int eW0 = 0;
+    if constexpr (ROOT) {
         v4f t[2][CF][2], tt[2];
         w0_slice_issue<CF>(a.wr0, a.ldw0, a.K0, wv, ln, t);
         if (T16) {
@@ -617,10 +620,12 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     // XR: the split row's feature-table index (low word of n_id; rows past
     // the block read 0 and are masked at use)
     auto iload = [&](int j) __attribute__((always_inline)) -> int {
+        if constexpr (!ROOT) return 0;
         const int row = tile_of(j) * F2_ROWS + srow;
         return buf_load1i(ir, row < n_rows ? row * 8 : kOOB2, 0, 0);
     };
     auto xload = [&](int j, int idx) __attribute__((always_inline)) -> v4f {
+        if constexpr (!ROOT) return v4f{0.f, 0.f, 0.f, 0.f};
         const int row = tile_of(j) * F2_ROWS + srow;
         const bool ok = j < ntj && row < n_rows && scol;
         const uint32_t src = (XR && xrow) ? static_cast<uint32_t>(idx) : static_cast<uint32_t>(row);
@@ -636,6 +641,7 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     };
     // row max over the tile row's 32 lanes, scale, split, parts into LDS
     auto split = [&](v4f v, int buf) __attribute__((always_inline)) {
+        if constexpr (!ROOT) return;
         const float m = max_xor16(max_row16(amax4(v)));  // the tile row's 32 lanes
         const int e = h2_exp(m);
         const v4f vs = ldexp4(v, e);
@@ -660,6 +666,10 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     auto l0 = [&](int buf, v4f (&acc)[2], float &s0) __attribute__((always_inline)) {
         acc[0] = v4f{0.f, 0.f, 0.f, 0.f};
         acc[1] = v4f{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!ROOT) {
+            s0 = 0.0f;  // (b0 + nb alone: fma(0, 0, b0) = b0)
+            return;
+        }
         const _Float16 *xp = sxp + buf * XPB + rl * PSTR + 8 * q;
         half8 xf[CF][2];  // every fragment read issued before the first MFMA
         half4 xt[2];
@@ -975,9 +985,9 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     else pipeline(std::false_type{});
 }
 
-template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0>
+template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0, bool ROOT = true>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
-    fwd2_body<C0, NT1, DM, XR, T16, DBG>(a);
+    fwd2_body<C0, NT1, DM, XR, T16, DBG, ROOT>(a);
 }
 
 // Both launches as ONE (round 5): the edge phase and the main phase map tile
@@ -989,16 +999,16 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2(F2Args a) {
 // while others still gather (the edge phase has ~4 tiles per workgroup on
 // the products block, the main phase ~38).  The edge phase's LDS is static,
 // the main phase's dynamic: both fit together (138 KB).
-template <int C0, int NT1, int DM, bool XR, bool T16>
+template <int C0, int NT1, int DM, bool XR, bool T16, bool ROOT = true>
 __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2x(G2Args g, F2Args f) {
     edge_nb_body<C0, 0>(g);
     __syncthreads();  // (workgroup scope: this workgroup's nb / agg stores before its main phase's reads)
-    fwd2_body<C0, NT1, DM, XR, T16, 0>(f);
+    fwd2_body<C0, NT1, DM, XR, T16, 0, ROOT>(f);
 }
 
-template <int C0, int NT1, int DM, bool XR, int DBG = 0, bool T16 = false>
+template <int C0, int NT1, int DM, bool XR, int DBG = 0, bool T16 = false, bool ROOT = true>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
-    auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG>;
+    auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG, ROOT>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
                        (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
@@ -1012,9 +1022,9 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     return launch_status();
 }
 
-template <int C0, int NT1, int DM, bool XR, bool T16 = false>
+template <int C0, int NT1, int DM, bool XR, bool T16 = false, bool ROOT = true>
 int launch_fwd2x(const G2Args &g, const F2Args &a, int grid, hipStream_t st) {
-    auto fn = k_fwd2x<C0, NT1, DM, XR, T16>;
+    auto fn = k_fwd2x<C0, NT1, DM, XR, T16, ROOT>;
     const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
                        (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
@@ -1111,7 +1121,10 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
     const bool indexed = xrow || xrow_dev;
     NGNN_RETURN_IF(indexed && (x_rows <= 0 || !col_x), NGNN_E_ARG);
     if (n_rows == 0) return NGNN_OK;
-    NGNN_RETURN_IF((!x && !x_dev) || !rowptr || (!col && n_edge_rows > 0) || !wl0 || !bl0 || !wr0 || !wl1 || !bl1 || !wr1 ||
+    // (wr0 NULL, ABI 17: no root term -- GCNConv(normalize=False)'s layer;
+    // not with the fused x[n_id] gather)
+    NGNN_RETURN_IF(!wr0 && (xrow || xrow_dev), NGNN_E_ARG);
+    NGNN_RETURN_IF((!x && !x_dev) || !rowptr || (!col && n_edge_rows > 0) || !wl0 || !bl0 || !wl1 || !bl1 || !wr1 ||
                        !h || !agg0 || !out || !ws,
                    NGNN_E_ARG);
     NGNN_RETURN_IF((x && !aligned(x, 16)) || !aligned(h, 16) || !aligned(out, 16) || !aligned(agg0, 16) || !aligned(bl0, 16) ||
@@ -1279,6 +1292,15 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
         const bool t16 = t16_ok && K0 <= 112;
         auto go = [&](auto xr_c) {
             constexpr bool XRv = decltype(xr_c)::value;
+            if (!wr0) {  // (root-free: no x, so no T16 form; never indexed)
+                if (fuse)
+                    return dm == 2   ? launch_fwd2x<4, 3, 2, false, false, false>(g, f, grid, st)
+                           : dm == 1 ? launch_fwd2x<4, 3, 1, false, false, false>(g, f, grid, st)
+                                     : launch_fwd2x<4, 3, 0, false, false, false>(g, f, grid, st);
+                return dm == 2   ? launch_fwd2<4, 3, 2, false, 0, false, false>(f, grid, st)
+                       : dm == 1 ? launch_fwd2<4, 3, 1, false, 0, false, false>(f, grid, st)
+                                 : launch_fwd2<4, 3, 0, false, 0, false, false>(f, grid, st);
+            }
             if (fuse) {
                 if (t16)
                     return dm == 2   ? launch_fwd2x<4, 3, 2, XRv, true>(g, f, grid, st)

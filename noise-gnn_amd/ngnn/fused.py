@@ -458,13 +458,17 @@ def _absent_none(params, grads):
 
 
 def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int, seed_dev,
-                  stages: int | None = None, bufs=None, head: "HeadResult | None" = None):
+                  stages: int | None = None, bufs=None, head: "HeadResult | None" = None,
+                  root0: bool = True):
     """(h, logits, layer-0 aggregate, h partial?) of a two-layer stack in one
     call (include/ngnn.h ngnn_sage2_fwd).  h holds the rows the bounded
     backward reads: every row, or rows < R' when the graph slot vouches that
     the loss reads rows < its B (block.r_next[2]).  stages / bufs (bench.py's
     per-launch timing): a subset of the launches, on the (h, out, agg0) of an
-    earlier call.  head: this forward's loss head (LossHead.start), or None."""
+    earlier call.  head: this forward's loss head (LossHead.start), or None.
+    root0 False: layer 0 has no root term (a SimpleGCN stack, sage2_params'
+    zero W_r0): the kernels skip x entirely (ABI 17, wr0 NULL) -- not with the
+    fused x[n_id] gather, which keeps the zero matrix."""
     wl0, bl0, wr0, wl1, bl1, wr1 = (q.detach() for q in params)
     if wl0.stride(1) != 1 or wr0.stride(0) != wl0.stride(0) or wr0.stride(1) != 1:
         wl0, wr0 = wl0.contiguous(), wr0.contiguous()
@@ -489,7 +493,8 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     args = [_lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev), int(block.x_rows),
             x.stride(0), K0, N, _lib.ptr(block.n_rows_dev), n_edge, _lib.ptr(block.n_edge_rows_dev),
             _lib.ptr(block.rowptr), _lib.ptr(block.col),
-            _lib.ptr(block.col_x) if block.xrow_dev is not None else None, _lib.REDUCE[reduce], _lib.ptr(wl0), _lib.ptr(bl0), _lib.ptr(wr0), wl0.stride(0), H,
+            _lib.ptr(block.col_x) if block.xrow_dev is not None else None, _lib.REDUCE[reduce], _lib.ptr(wl0), _lib.ptr(bl0),
+            _lib.ptr(wr0) if (root0 or block.xrow_dev is not None) else None, wl0.stride(0), H,
             _lib.ptr(wl1), _lib.ptr(bl1), _lib.ptr(wr1), wl1.stride(0), F1, float(p_drop),
             seed & (2**64 - 1), _lib.ptr(seed_dev), _lib.ptr(h), h.stride(0), N,
             _lib.ptr(h_rows_dev), _lib.ptr(agg0), agg0.stride(0), _lib.ptr(out), out.stride(0)]
@@ -508,9 +513,10 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     edge = ("sage2_edge", _lib.SAGE2_EDGE,
             4 * (block.E * (K0 + 1) + n_e * (K0 + 1) + n_e * K0 + n_e * H),
             2 * n_e * K0 * H, 3 * 2 * n_e * C0p * H / f16)
+    rk = 1 if (root0 or block.xrow_dev is not None) else 0  # (root-free: x not read, no layer-0 root products)
     main = ("sage2_fwd", _lib.SAGE2_MAIN,
-            4 * (N * K0 + n_e * H + h_rows * H + N * F1 + N * ldz),
-            2 * N * K0 * H + 4 * N * H * F1, 3 * (2 * N * C0p * H + 2 * N * H * 2 * ldz) / f16)
+            4 * (rk * N * K0 + n_e * H + h_rows * H + N * F1 + N * ldz),
+            rk * 2 * N * K0 * H + 4 * N * H * F1, 3 * (rk * 2 * N * C0p * H + 2 * N * H * 2 * ldz) / f16)
     if fwd2_fused():
         # one launch for both (k_fwd2x, as in the step): its bytes / flops are
         # the two phases' sums (nb's write and read stay: the main phase reads
@@ -726,7 +732,7 @@ class _SAGEStack(torch.autograd.Function):
         if p6 is not None and sage2_ok(x, block, reduce, p6, w_bf16):
             ctx.sage2 = True
             h1, h, agg0, ctx.h_partial = sage2_forward(x, block, reduce, p6, p_drop, seed, seed_dev,
-                                                       head=head)
+                                                       head=head, root0=params[2] is not None)
             if head is not None:
                 h._ngnn_head = head  # (seed_cross_entropy takes the loss from it)
             acts += [h1, h]

@@ -52,6 +52,8 @@ def main():
     if a.cprofile:
         import cProfile
         import pstats
+        # (backward on the calling thread, so the profile sees its Python)
+        torch.autograd.set_multithreading_enabled(False)
         pr = cProfile.Profile()
         pr.enable()
         for i in range(50):
