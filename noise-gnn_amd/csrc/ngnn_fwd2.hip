@@ -775,7 +775,11 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     // in the fma that sums them (wave order, as a sum of the exact products)
     auto reduce = [&](int jj, int buf, auto z_c) __attribute__((always_inline)) -> v4f {
         constexpr bool RZ = decltype(z_c)::value;
-        const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + rmt * 64 + rln;
+        // (the partial reads of lanes >= NIT -- results unused -- go to the
+        // next item slots, not to lane 0's: every 16-lane phase of the
+        // 16-B reads then covers 256 contiguous bytes; reading past the last
+        // wave's partials lands in the x-parts buffers, harmless)
+        const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + wv * NIT + ln;
         const float *fp = sf1 + (buf * F2_ROWS + (rln & 15)) * F2_WAVES;
         const v4f fa = *reinterpret_cast<const v4f *>(fp), fb = *reinterpret_cast<const v4f *>(fp + 4);
         v4f s = pp[0] * fa[0];
