@@ -426,8 +426,26 @@ def sage2_ok(x, block: Block, reduce: str, params, w_bf16: bool) -> bool:
     wl0, _, wr0, wl1, _, wr1 = params
     if wl0.shape != wr0.shape or wl1.shape != wr1.shape or wl1.shape[1] != wl0.shape[0]:
         return False
-    return bool(_lib.load().ngnn_sage2_supported(x.size(1), wl0.shape[0], wl1.shape[0],
-                                                _lib.REDUCE[reduce]))
+    key = (x.size(1), wl0.shape[0], wl1.shape[0], reduce)
+    ok = _sage2_supported.get(key)
+    if ok is None:  # (a pure function of the shape: asked once -- the eager step is host-bound)
+        ok = _sage2_supported[key] = bool(_lib.load().ngnn_sage2_supported(
+            x.size(1), wl0.shape[0], wl1.shape[0], _lib.REDUCE[reduce]))
+    return ok
+
+
+_sage2_supported: dict = {}
+_ws_bytes: dict = {}
+
+
+def _ws_size(fn: str, *args) -> int:
+    """A workspace-size query of the C ABI (a pure function of its
+    arguments), memoised: the eager training step is host-bound."""
+    key = (fn,) + args
+    v = _ws_bytes.get(key)
+    if v is None:
+        v = _ws_bytes[key] = int(getattr(_lib.load(), fn)(*args))
+    return v
 
 
 def fwd2_fused() -> bool:
@@ -485,7 +503,7 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
         agg0 = agg_buffer(N, K0, dev, H)
     else:
         h, out, agg0 = bufs[:3]
-    ws = _workspace(dev, "sage2", lib.ngnn_sage2_workspace_bytes(K0, F1, N))
+    ws = _workspace(dev, "sage2", _ws_size("ngnn_sage2_workspace_bytes", K0, F1, N))
     n_edge = N if block.n_active is None else min(int(block.n_active), N)
     rn = block.r_next
     h_rows_dev = rn[0] if (rn is not None and len(rn) > 2 and rn[2]) else None
@@ -597,7 +615,7 @@ def reserve_sage2_bwd(dev, n_rows: int, K0: int, F1: int) -> torch.Tensor:
     backward leaves its g part zero).  A graph slot reserves it before its
     capture: a zero fill inside the captured step would replay every step."""
     lib = _lib.load()
-    return _workspace(dev, ("sage2_bwd", K0, F1), lib.ngnn_sage2_bwd_workspace_bytes(n_rows, K0, F1),
+    return _workspace(dev, ("sage2_bwd", K0, F1), _ws_size("ngnn_sage2_bwd_workspace_bytes", n_rows, K0, F1),
                       zero=True)
 
 

@@ -23,6 +23,10 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       capturable=True))
         self._tickets: dict = {}  # step tensor address -> device ticket
+        # per group: (parameter addresses, the launch's pointer arrays) -- the
+        # eager step is host-bound, and only the gradient addresses change
+        # from step to step
+        self._arrays: dict = {}
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -31,18 +35,24 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = _lib.load()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
+            pkey = tuple(p.data_ptr() for p in ps)
+            cached = self._arrays.get(gi)
+            if cached is None or cached[0][0] != pkey:
+                cached = None
+                for p in ps:  # (the parameters' own checks: once per parameter set)
+                    if not p.is_cuda or p.dtype not in (torch.float32, torch.bfloat16) \
+                            or not p.is_contiguous():
+                        raise RuntimeError("ngnn.optim.Adam: contiguous float32 / bfloat16 GPU "
+                                           "parameters only")
             for p in ps:
-                if not p.is_cuda or p.dtype not in (torch.float32, torch.bfloat16) \
-                        or not p.is_contiguous():
-                    raise RuntimeError("ngnn.optim.Adam: contiguous float32 / bfloat16 GPU "
-                                       "parameters only")
-                if p.grad.dtype != p.dtype:
+                g = p.grad
+                if g.dtype != p.dtype:
                     raise RuntimeError("ngnn.optim.Adam: gradient dtype differs from the parameter")
-                if p.grad.is_sparse:
+                if g.is_sparse:
                     raise RuntimeError("ngnn.optim.Adam: dense gradients only")
             st0 = self.state[ps[0]]
             if "step" not in st0:
@@ -59,13 +69,20 @@ class Adam(torch.optim.Optimizer):
                 self._tickets[step.data_ptr()] = ticket
             grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
             n = len(ps)
-            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in ps])
             G = (ctypes.c_void_p * n)(*[g.data_ptr() for g in grads])
-            M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in ps])
-            V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps])
-            N = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
-            D = (ctypes.c_int32 * n)(*[_lib.BF16 if p.dtype == torch.bfloat16 else _lib.F32
-                                       for p in ps])
+            sts = [self.state[p] for p in ps]
+            # (the moments' addresses belong to the key: a state reload --
+            # load_state_dict -- makes new tensors)
+            key = (pkey, tuple(st["exp_avg"].data_ptr() for st in sts),
+                   tuple(st["exp_avg_sq"].data_ptr() for st in sts))
+            if cached is None or cached[0] != key:
+                cached = (key, (ctypes.c_void_p * n)(*pkey),
+                          (ctypes.c_void_p * n)(*key[1]), (ctypes.c_void_p * n)(*key[2]),
+                          (ctypes.c_int64 * n)(*[p.numel() for p in ps]),
+                          (ctypes.c_int32 * n)(*[_lib.BF16 if p.dtype == torch.bfloat16 else _lib.F32
+                                                 for p in ps]))
+                self._arrays[gi] = cached
+            _, P, M, V, N, D = cached
             b1, b2 = group["betas"]
             _lib.check(lib.ngnn_adam_step(n, P, G, M, V, N, D, step.data_ptr(), ticket.data_ptr(),
                                           float(group["lr"]),
