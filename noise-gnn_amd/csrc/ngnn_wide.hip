@@ -500,6 +500,254 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
     }
 }
 
+// ---- the H2 form (round 5): two fp16 parts per operand after a
+// power-of-two scaling -- each x / agg row by its own max, each W row (an
+// output column) by its own -- and THREE v_mfma_f32_16x16x32_f16 products
+// per k-step (w1 x2, w2 x1, w1 x1; each exact in fp32: ~3 2^-22 relative,
+// the two-layer kernels' arithmetic) instead of X3's
+// six bf16 ones; the weight image is 2 parts instead of 3.  The scales must
+// be known before a row's first k-stage, so the row exponents come from a
+// pass of their own (k_row_exp) and the W rows' from the image launch; the
+// root and neighbour terms have different row and column scales, so they
+// accumulate apart and meet, unscaled, in the epilogue.
+constexpr int HW_STAGE = 2 * WBM * WKC + 2 * WBN * WKC;  // halves per stage buffer (24 KiB)
+typedef _Float16 h8w __attribute__((ext_vector_type(8)));
+
+// one wave per W row (mat, n): its exponent (max |w| of the row in [2^14,
+// 2^15) after scaling) and its two fp16 parts -> img [mat][part][Fo][Kp]
+__global__ __launch_bounds__(256) void k_wide_wimg_h2(const float *__restrict__ wr, const float *__restrict__ wl,
+                                                      int64_t ldw, int Fo, int K, int Kp, _Float16 *__restrict__ img,
+                                                      int *__restrict__ ew) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= 2 * Fo) return;
+    const int mat = row / Fo, n = row - mat * Fo;
+    const float *w = mat ? wl : wr;
+    float m = 0.0f;
+    if (w)
+        for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(w[static_cast<int64_t>(n) * ldw + k]));
+    const int e = h2_exp(wave_max(m));
+    if (lane == 0) ew[row] = e;
+    const int64_t per = static_cast<int64_t>(Fo) * Kp;
+    _Float16 *o = img + static_cast<int64_t>(2 * mat) * per + static_cast<int64_t>(n) * Kp;
+    for (int k = lane; k < Kp; k += 64) {
+        const float v = (w && k < K) ? __builtin_amdgcn_ldexpf(w[static_cast<int64_t>(n) * ldw + k], e) : 0.0f;
+        const _Float16 h = static_cast<_Float16>(v);
+        o[k] = h;
+        o[per + k] = static_cast<_Float16>(v - static_cast<float>(h));
+    }
+}
+
+// one wave per row: x rows [0, rows) -> ex, agg rows [0, erows) -> ea (the
+// H2 scale exponents of k_wide_h2's staging)
+__global__ __launch_bounds__(256) void k_row_exp(const float *__restrict__ x, const float *const *x_dev, int64_t ldx,
+                                                 int K, int n_rows, const int32_t *__restrict__ n_rows_dev,
+                                                 const float *__restrict__ agg, int64_t lda, int n_edge,
+                                                 const int32_t *__restrict__ n_edge_dev, int *__restrict__ ex,
+                                                 int *__restrict__ ea) {
+    if (x_dev) x = gload(x_dev, 0);
+    int rows = n_rows;
+    if (n_rows_dev) rows = min(rows, *n_rows_dev);
+    int erows = min(n_edge, rows);
+    if (n_edge_dev) erows = min(erows, *n_edge_dev);
+    if (!agg) erows = 0;
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * 4;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows + erows; r += waves) {
+        const bool nb = r >= rows;
+        const int rr = nb ? r - rows : r;
+        const float *p = nb ? agg + static_cast<int64_t>(rr) * lda : x + static_cast<int64_t>(rr) * ldx;
+        float m = 0.0f;
+        for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(p[k]));
+        const int e = h2_exp(wave_max(m));
+        if (lane == 0) (nb ? ea : ex)[rr] = e;
+    }
+}
+
+template <bool VOUT>
+__global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *__restrict__ wimg, int Kp,
+                                                    const int *__restrict__ ew, const int *__restrict__ ex,
+                                                    const int *__restrict__ ea) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 hlds[];  // [2][HW_STAGE]
+    if (a.x_dev) a.x = gload(a.x_dev, 0);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int rows = a.n_rows;
+    if (a.n_rows_dev) rows = min(rows, *a.n_rows_dev);
+    int erows = min(a.n_edge, rows);
+    if (a.n_edge_dev) erows = min(erows, *a.n_edge_dev);
+    rows = __builtin_amdgcn_readfirstlane(rows);
+    erows = __builtin_amdgcn_readfirstlane(erows);
+    const int nK = (a.K + WKC - 1) / WKC;
+    const int c_root = a.wr ? nK : 0;
+    const int n_live = ((rows + WBM - 1) / WBM) * a.n_ct;
+    const int64_t per = static_cast<int64_t>(a.Fo) * Kp;
+    const int wn = (wave & 1) * 64, wm = (wave >> 1) * 32;
+    const int i16 = lane & 15, q = lane >> 4;
+    Dropout drop = a.epi.drop;
+    if (a.seed_dev) drop.reseed(*a.seed_dev);
+    const int xr_r = tid >> 2, xr_c = tid & 3;
+    const int w_n = tid >> 1, w_h = tid & 1;
+    auto sw = [](int r, int c) { return c ^ ((r >> 2) & 3); };
+    const i32x4 xrs = make_rsrc_u(a.x, static_cast<uint32_t>(static_cast<int64_t>(rows) * a.ldx * 4));
+    const i32x4 ars = make_rsrc_u(a.agg, static_cast<uint32_t>(a.agg ? static_cast<int64_t>(erows) * a.ld_agg * 4 : 0));
+    v4f xv[2][2];
+    h8w wv[2][2][2];
+
+    for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
+        const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
+        const int r0 = rt * WBM, n0 = ct * WBN;
+        const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);
+        // the staging row's scales (rows past the range: never stored)
+        const int sr = r0 + xr_r;
+        const int e_x = sr < rows ? ex[sr] : 0;
+        const int e_a = (a.agg && sr < erows) ? ea[sr] : 0;
+        auto load = [&](int c, v4f (&xd)[2], h8w (&wd)[2][2]) __attribute__((always_inline)) {
+            const bool nb = c >= c_root;
+            const int kc = (nb ? c - c_root : c) * WKC;
+            const int r = r0 + xr_r;
+            const int64_t ld = nb ? a.ld_agg : a.ldx;
+            const int k = kc + 8 * xr_c;
+            const int off = (r < (nb ? erows : rows) && k < a.K) ? static_cast<int>((r * ld + k) * 4) : static_cast<int>(0xF0000000u);
+            const i32x4 rs = nb ? ars : xrs;
+            if (off == static_cast<int>(0xF0000000u) || k + 8 <= a.K) {
+                xd[0] = buf_load4(rs, off, 0, 0);
+                xd[1] = buf_load4(rs, off == static_cast<int>(0xF0000000u) ? off : off + 16, 0, 0);
+            } else {  // (the row's last values: element by element, nothing past K)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    xd[j >> 2][j & 3] = buf_load1(rs, k + j < a.K ? off + 4 * j : static_cast<int>(0xF0000000u), 0, 0);
+            }
+            const int n = min(n0 + w_n, a.Fo - 1);
+            const _Float16 *wb = wimg + (nb ? 2 * per : 0) + static_cast<int64_t>(n) * Kp + kc + 16 * w_h;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                wd[p][0] = *reinterpret_cast<const h8w *>(wb + p * per);
+                wd[p][1] = *reinterpret_cast<const h8w *>(wb + p * per + 8);
+            }
+        };
+        auto store = [&](_Float16 *s, int c, const v4f (&xd)[2], const h8w (&wd)[2][2]) __attribute__((always_inline)) {
+            const bool nb = c >= c_root;
+            const int kq = a.K - ((nb ? c - c_root : c) * WKC + 8 * xr_c);  // valid values of the 8
+            const int e = nb ? e_a : e_x;
+            h8w p1, p2;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = j < kq ? __builtin_amdgcn_ldexpf(xd[j >> 2][j & 3], e) : 0.0f;  // (past K: 0)
+                const _Float16 h = static_cast<_Float16>(v);
+                p1[j] = h;
+                p2[j] = static_cast<_Float16>(v - static_cast<float>(h));
+            }
+            const int xo = xr_r * WKC + 8 * sw(xr_r, xr_c);
+            *reinterpret_cast<h8w *>(s + xo) = p1;
+            *reinterpret_cast<h8w *>(s + WBM * WKC + xo) = p2;
+            _Float16 *ws = s + 2 * WBM * WKC;
+            const bool wok = n0 + w_n < a.Fo;  // (rows past F_out: zero)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    *reinterpret_cast<h8w *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, 2 * w_h + h)) =
+                        wok ? wd[p][h] : h8w{};
+        };
+        v4f accr[4][2], accn[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) accr[mt][nt] = accn[mt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
+        auto mfma_stage = [&](const _Float16 *s, v4f (&acc)[4][2]) __attribute__((always_inline)) {
+            const _Float16 *ws = s + 2 * WBM * WKC;
+            h8w xb[2][2];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int r = wm + 16 * nt + i16;
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    xb[nt][p] = *reinterpret_cast<const h8w *>(s + p * WBM * WKC + r * WKC + 8 * sw(r, q));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int n = wn + 16 * mt + i16;
+                h8w w[2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) w[p] = *reinterpret_cast<const h8w *>(ws + p * WBN * WKC + n * WKC + 8 * sw(n, q));
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    v4f t2 = acc[mt][nt];
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0], xb[nt][1], t2, 0, 0, 0);
+                    t2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[1], xb[nt][0], t2, 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0], xb[nt][0], t2, 0, 0, 0);
+                }
+            }
+        };
+        if (nch > 0) {
+            load(0, xv[0], wv[0]);
+            if (nch > 1) load(1, xv[1], wv[1]);
+            store(hlds, 0, xv[0], wv[0]);
+            __syncthreads();
+        }
+        // stage c: MFMAs from LDS[c & 1] into the root or the neighbour
+        // accumulators (compile-time: the two loops); the staging as X3's
+        auto one = [&](int c, auto u_c, auto nb_c) __attribute__((always_inline)) {
+            constexpr int U = decltype(u_c)::value;  // c & 1
+            if (c + 2 < nch) load(c + 2, xv[U], wv[U]);
+            if constexpr (decltype(nb_c)::value) mfma_stage(hlds + U * HW_STAGE, accn);
+            else mfma_stage(hlds + U * HW_STAGE, accr);
+            if (c + 1 < nch) store(hlds + (U ^ 1) * HW_STAGE, c + 1, xv[U ^ 1], wv[U ^ 1]);
+            __syncthreads();
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        // (c_root is even: the host takes this form only for an even number
+        // of k-stages, so both loops start on buffer 0)
+        for (int c = 0; c < c_root; c += 2) {
+            one(c, I0{}, std::false_type{});
+            one(c + 1, I1{}, std::false_type{});
+        }
+        for (int c = c_root; c < nch; c += 2) {
+            one(c, I0{}, std::true_type{});
+            if (c + 1 < nch) one(c + 1, I1{}, std::true_type{});
+        }
+        // ---- epilogue: lane holds columns n0 + wn + 16 mt + 4 q + (0..3) of
+        // row r0 + wm + 16 nt + i16; each term unscaled by its row's and its
+        // column's exponents (exact), summed, then bias / ReLU / dropout
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int r = r0 + wm + nt * 16 + i16;
+            if (r >= rows) continue;
+            const int erx = ex[r];
+            const bool hn = a.agg && r < erows;
+            const int era = hn ? ea[r] : 0;
+            const uint32_t rk = drop.row_key(static_cast<uint32_t>(r));
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int c0 = n0 + wn + mt * 16 + 4 * q;
+                if (c0 >= a.Fo) continue;
+                const uint32_t kb =
+                    drop.thresh ? drop.keep4(rk, static_cast<uint32_t>(a.epi.col_base + c0) >> 2) : 0xfu;
+                v4f v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cj = min(c0 + j, a.Fo - 1);
+                    float e = __builtin_amdgcn_ldexpf(accr[mt][nt][j], -(erx + ew[cj]));
+                    if (hn) e += __builtin_amdgcn_ldexpf(accn[mt][nt][j], -(era + ew[a.Fo + cj]));
+                    if (a.epi.bias && c0 + j < a.Fo) e += a.epi.bias[c0 + j];
+                    if (a.epi.relu) e = (e < 0.0f) ? 0.0f : e;  // NaN passes, like torch.relu
+                    if (drop.thresh) e = ((kb >> j) & 1u) ? e * drop.scale : 0.0f;
+                    v[j] = e;
+                }
+                float *o = a.out + static_cast<int64_t>(r) * a.ldo + c0;
+                if (VOUT && c0 + 4 <= a.Fo) {
+                    *reinterpret_cast<v4f *>(o) = v;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (c0 + j < a.Fo) o[j] = v[j];
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // bytes of the wide layer's split weight image (k_wide_wimg)
@@ -610,6 +858,43 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     const size_t head = agg == ws ? sage_wide_workspace_bytes(K, n_edge) : 0;
     // (32-bit row offsets in the kernel's buffer loads)
     const bool fits = n_rows * ldx * 4 < 0x7FFF0000ll && (!agg || n_edge * lda * 4 < 0x7FFF0000ll);
+    // the H2 form (NGNN_WIDE_H2=0, read once: X3 -- A/B): an even number of
+    // k-stages (its root / neighbour loops each start on buffer 0), and room
+    // for the 2-part image + the row / column exponents at the workspace tail
+    static const bool h2_on = [] {
+        const char *e = std::getenv("NGNN_WIDE_H2");
+        return !(e && e[0] == '0');
+    }();
+    {
+        const int Kp = static_cast<int>(ceil_div(K, 32) * 32);
+        const size_t ib2 = static_cast<size_t>(4) * Fo * Kp * 2;
+        const size_t side = (static_cast<size_t>(2) * Fo + n_rows + n_edge) * 4 + 1024;
+        if (!exact && h2_on && fits && ceil_div(K, WKC) % 2 == 0 && ws && ws_bytes >= head + ib2 + side + 512) {
+            const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib2) & ~uintptr_t(255);
+            _Float16 *img = reinterpret_cast<_Float16 *>(e);
+            int *ew = reinterpret_cast<int *>((e - side) & ~uintptr_t(255));
+            int *ex = ew + 2 * Fo;
+            int *ea = ex + n_rows;
+            hipLaunchKernelGGL(k_wide_wimg_h2, dim3(static_cast<unsigned>(ceil_div(2 * Fo, 4))), dim3(256), 0, st, wr,
+                               wl, ldw, static_cast<int>(Fo), static_cast<int>(K), Kp, img, ew);
+            int rc = launch_status();
+            if (rc) return rc;
+            const unsigned gr = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows + n_edge, 4), 8 * num_cus())));
+            hipLaunchKernelGGL(k_row_exp, dim3(gr), dim3(256), 0, st, x, x_dev, ldx, static_cast<int>(K),
+                               static_cast<int>(n_rows), n_rows_dev, agg, lda, static_cast<int>(n_edge), n_edge_rows_dev,
+                               ex, ea);
+            rc = launch_status();
+            if (rc) return rc;
+            const size_t lds = static_cast<size_t>(2) * HW_STAGE * 2;
+            if (vout)
+                hipLaunchKernelGGL(k_wide_h2<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds, st, a, img, Kp, ew,
+                                   ex, ea);
+            else
+                hipLaunchKernelGGL(k_wide_h2<false>, dim3(static_cast<unsigned>(grid)), dim3(256), lds, st, a, img, Kp, ew,
+                                   ex, ea);
+            return launch_status();
+        }
+    }
     if (!exact && x3_on && fits && ws && ws_bytes >= head + ib + 256) {
         const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib) & ~uintptr_t(255);
         __bf16 *img = reinterpret_cast<__bf16 *>(e);
