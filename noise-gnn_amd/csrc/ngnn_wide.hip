@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
                                                   const int32_t *__restrict__ n_edge_dev,
                                                   float *__restrict__ agg, int64_t ld_agg,
                                                   int n_cap, int round16,
-                                                  const float *const *x_dev) {
+                                                  const float *const *x_dev, int *__restrict__ ea) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (x_dev) x = gload(x_dev, 0);  // (a graph slot's batch address, read at run time)
     int rows = n_rows;
@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
     const float init = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
     for (int64_t d = static_cast<int64_t>(blockIdx.x) * 4 + wave; d < rows; d += gridDim.x * 4) {
         const int beg = rowptr[d], end = rowptr[d + 1];
+        float am = 0.0f;  // (ea: the row's |max| -> its H2 staging exponent)
         for (int p0 = 0; p0 < K; p0 += 64 * NC) {
             float acc[NC];
 #pragma unroll
@@ -117,7 +118,12 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
                 if (RED == NGNN_REDUCE_MEAN) v = v / cnt;
                 if (RED == NGNN_REDUCE_MAX && deg == 0) v = 0.0f;
                 agg[d * ld_agg + f] = v;
+                am = fmaxf(am, fabsf(v));
             }
+        }
+        if (ea) {
+            const int e = h2_exp(wave_max(am));
+            if (lane == 0) ea[d] = e;
         }
     }
 }
@@ -523,44 +529,58 @@ __global__ __launch_bounds__(256) void k_wide_wimg_h2(const float *__restrict__ 
     if (row >= 2 * Fo) return;
     const int mat = row / Fo, n = row - mat * Fo;
     const float *w = mat ? wl : wr;
+    // (8 consecutive values per lane and pass, 16-B part stores; the second
+    // pass re-reads the row from L2)
+    const float *wrow = w ? w + static_cast<int64_t>(n) * ldw : nullptr;
+    auto get8 = [&](int k0, float (&v)[8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (wrow && k0 + j < K) ? wrow[k0 + j] : 0.0f;
+    };
     float m = 0.0f;
-    if (w)
-        for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(w[static_cast<int64_t>(n) * ldw + k]));
+    for (int kb = 0; kb < Kp; kb += 512) {
+        float v[8];
+        get8(kb + 8 * lane, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    }
     const int e = h2_exp(wave_max(m));
     if (lane == 0) ew[row] = e;
     const int64_t per = static_cast<int64_t>(Fo) * Kp;
     _Float16 *o = img + static_cast<int64_t>(2 * mat) * per + static_cast<int64_t>(n) * Kp;
-    for (int k = lane; k < Kp; k += 64) {
-        const float v = (w && k < K) ? __builtin_amdgcn_ldexpf(w[static_cast<int64_t>(n) * ldw + k], e) : 0.0f;
-        const _Float16 h = static_cast<_Float16>(v);
-        o[k] = h;
-        o[per + k] = static_cast<_Float16>(v - static_cast<float>(h));
+    for (int kb = 0; kb < Kp; kb += 512) {
+        const int k0 = kb + 8 * lane;
+        if (k0 >= Kp) break;  // (Kp is a multiple of 32: whole 8-blocks)
+        float v[8];
+        get8(k0, v);
+        h8w p1, p2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float s = __builtin_amdgcn_ldexpf(v[j], e);
+            const _Float16 h = static_cast<_Float16>(s);
+            p1[j] = h;
+            p2[j] = static_cast<_Float16>(s - static_cast<float>(h));
+        }
+        *reinterpret_cast<h8w *>(o + k0) = p1;
+        *reinterpret_cast<h8w *>(o + per + k0) = p2;
     }
 }
 
-// one wave per row: x rows [0, rows) -> ex, agg rows [0, erows) -> ea (the
-// H2 scale exponents of k_wide_h2's staging)
+// one wave per row: x rows [0, rows) -> ex (the H2 scale exponents of
+// k_wide_h2's root staging; the aggregate rows' come from k_wide_agg)
 __global__ __launch_bounds__(256) void k_row_exp(const float *__restrict__ x, const float *const *x_dev, int64_t ldx,
                                                  int K, int n_rows, const int32_t *__restrict__ n_rows_dev,
-                                                 const float *__restrict__ agg, int64_t lda, int n_edge,
-                                                 const int32_t *__restrict__ n_edge_dev, int *__restrict__ ex,
-                                                 int *__restrict__ ea) {
+                                                 int *__restrict__ ex) {
     if (x_dev) x = gload(x_dev, 0);
     int rows = n_rows;
     if (n_rows_dev) rows = min(rows, *n_rows_dev);
-    int erows = min(n_edge, rows);
-    if (n_edge_dev) erows = min(erows, *n_edge_dev);
-    if (!agg) erows = 0;
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * 4;
-    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows + erows; r += waves) {
-        const bool nb = r >= rows;
-        const int rr = nb ? r - rows : r;
-        const float *p = nb ? agg + static_cast<int64_t>(rr) * lda : x + static_cast<int64_t>(rr) * ldx;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += waves) {
+        const float *p = x + static_cast<int64_t>(r) * ldx;
         float m = 0.0f;
         for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(p[k]));
         const int e = h2_exp(wave_max(m));
-        if (lane == 0) (nb ? ea : ex)[rr] = e;
+        if (lane == 0) ex[r] = e;
     }
 }
 
@@ -793,9 +813,36 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                   float *agg_out, int64_t ld_agg, void *ws, size_t ws_bytes, hipStream_t st, bool exact,
                   const float *const *x_dev) {
     const int64_t n_edge = std::max<int64_t>(0, std::min(n_edge_rows, n_rows));
+    // the H2 form (NGNN_WIDE_H2=0, read once: X3 -- A/B): an even number of
+    // k-stages (its root / neighbour loops each start on buffer 0), 32-bit row
+    // offsets, and room for the 2-part image + the row / column exponents at
+    // the workspace tail -- decided first: the aggregation writes the
+    // neighbour rows' exponents
+    static const bool h2_on = [] {
+        const char *e = std::getenv("NGNN_WIDE_H2");
+        return !(e && e[0] == '0');
+    }();
+    const bool has_agg = wl && n_edge > 0;
+    const int64_t lda_eff = agg_out ? ld_agg : K;
+    const bool fits = n_rows * ldx * 4 < 0x7FFF0000ll && (!has_agg || n_edge * lda_eff * 4 < 0x7FFF0000ll);
+    const size_t head = has_agg && (!agg_out || agg_out == ws) ? sage_wide_workspace_bytes(K, n_edge) : 0;
+    const int Kp = static_cast<int>(ceil_div(K, 32) * 32);
+    const size_t ib2 = static_cast<size_t>(4) * Fo * Kp * 2;
+    const size_t side = (static_cast<size_t>(2) * Fo + n_rows + n_edge) * 4 + 1024;
+    const bool use_h2 = !exact && h2_on && fits && ceil_div(K, WKC) % 2 == 0 && ws && ws_bytes >= head + ib2 + side + 512;
+    _Float16 *h2_img = nullptr;
+    int *ew = nullptr, *ex = nullptr, *ea = nullptr;
+    if (use_h2) {
+        const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib2) & ~uintptr_t(255);
+        h2_img = reinterpret_cast<_Float16 *>(e);
+        ew = reinterpret_cast<int *>((e - side) & ~uintptr_t(255));
+        ex = ew + 2 * Fo;
+        ea = ex + n_rows;
+    }
+    int *const agg_ea = ea;
     float *agg = nullptr;
     int64_t lda = ld_agg;
-    if (wl && n_edge > 0) {
+    if (has_agg) {
         if (agg_out) {
             agg = agg_out;
         } else {
@@ -809,7 +856,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                                dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                                static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, lda,
-                               static_cast<int>(n_rows), 0, x_dev);
+                               static_cast<int>(n_rows), 0, x_dev, agg_ea);
         };
         auto by_nc = [&](auto red_c) {
             if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
@@ -855,34 +902,16 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         return !(e && e[0] == '0');
     }();
     const size_t ib = wide_wimg_bytes(K, Fo);
-    const size_t head = agg == ws ? sage_wide_workspace_bytes(K, n_edge) : 0;
-    // (32-bit row offsets in the kernel's buffer loads)
-    const bool fits = n_rows * ldx * 4 < 0x7FFF0000ll && (!agg || n_edge * lda * 4 < 0x7FFF0000ll);
-    // the H2 form (NGNN_WIDE_H2=0, read once: X3 -- A/B): an even number of
-    // k-stages (its root / neighbour loops each start on buffer 0), and room
-    // for the 2-part image + the row / column exponents at the workspace tail
-    static const bool h2_on = [] {
-        const char *e = std::getenv("NGNN_WIDE_H2");
-        return !(e && e[0] == '0');
-    }();
     {
-        const int Kp = static_cast<int>(ceil_div(K, 32) * 32);
-        const size_t ib2 = static_cast<size_t>(4) * Fo * Kp * 2;
-        const size_t side = (static_cast<size_t>(2) * Fo + n_rows + n_edge) * 4 + 1024;
-        if (!exact && h2_on && fits && ceil_div(K, WKC) % 2 == 0 && ws && ws_bytes >= head + ib2 + side + 512) {
-            const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib2) & ~uintptr_t(255);
-            _Float16 *img = reinterpret_cast<_Float16 *>(e);
-            int *ew = reinterpret_cast<int *>((e - side) & ~uintptr_t(255));
-            int *ex = ew + 2 * Fo;
-            int *ea = ex + n_rows;
+        if (use_h2) {
+            _Float16 *img = h2_img;
             hipLaunchKernelGGL(k_wide_wimg_h2, dim3(static_cast<unsigned>(ceil_div(2 * Fo, 4))), dim3(256), 0, st, wr,
                                wl, ldw, static_cast<int>(Fo), static_cast<int>(K), Kp, img, ew);
             int rc = launch_status();
             if (rc) return rc;
-            const unsigned gr = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows + n_edge, 4), 8 * num_cus())));
+            const unsigned gr = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows, 4), 8 * num_cus())));
             hipLaunchKernelGGL(k_row_exp, dim3(gr), dim3(256), 0, st, x, x_dev, ldx, static_cast<int>(K),
-                               static_cast<int>(n_rows), n_rows_dev, agg, lda, static_cast<int>(n_edge), n_edge_rows_dev,
-                               ex, ea);
+                               static_cast<int>(n_rows), n_rows_dev, ex);
             rc = launch_status();
             if (rc) return rc;
             const size_t lds = static_cast<size_t>(2) * HW_STAGE * 2;
@@ -898,7 +927,6 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     if (!exact && x3_on && fits && ws && ws_bytes >= head + ib + 256) {
         const uintptr_t e = (reinterpret_cast<uintptr_t>(ws) + ws_bytes - ib) & ~uintptr_t(255);
         __bf16 *img = reinterpret_cast<__bf16 *>(e);
-        const int Kp = static_cast<int>(ceil_div(K, 32) * 32);
         const int64_t nthr = static_cast<int64_t>(2) * Fo * Kp / 8;
         hipLaunchKernelGGL(k_wide_wimg, dim3(static_cast<unsigned>(ceil_div(nthr, 256))), dim3(256), 0, st, wr, wl,
                            ldw, static_cast<int>(Fo), static_cast<int>(K), Kp, img);
@@ -943,7 +971,7 @@ int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                            dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                            static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, ld_agg,
-                           static_cast<int>(n_rows), 1, x_dev);
+                           static_cast<int>(n_rows), 1, x_dev, nullptr);
     };
     auto by_nc = [&](auto red_c) {
         if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
