@@ -516,7 +516,11 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
 // pass of their own (k_row_exp) and the W rows' from the image launch; the
 // root and neighbour terms have different row and column scales, so they
 // accumulate apart and meet, unscaled, in the epilogue.
-constexpr int HW_STAGE = 2 * WBM * WKC + 2 * WBN * WKC;  // halves per stage buffer (24 KiB)
+// halves per stage buffer (BM = 64: 24 KiB); BM = 128 (eight waves): the W
+// tile staged once per 128 rows -- half the image's L2 reads per row
+template <int BM>
+constexpr int hw_stage() { return 2 * BM * WKC + 2 * WBN * WKC; }
+constexpr int HW_STAGE = hw_stage<WBM>();
 typedef _Float16 h8w __attribute__((ext_vector_type(8)));
 
 // one wave per W row (mat, n): its exponent (max |w| of the row in [2^14,
@@ -584,11 +588,14 @@ __global__ __launch_bounds__(256) void k_row_exp(const float *__restrict__ x, co
     }
 }
 
-template <bool VOUT>
-__global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *__restrict__ wimg, int Kp,
+template <bool VOUT, int BM>
+__global__ __launch_bounds__(BM * 4, 128 / BM) void k_wide_h2(WideArgs a, const _Float16 *__restrict__ wimg, int Kp,
                                                     const int *__restrict__ ew, const int *__restrict__ ex,
                                                     const int *__restrict__ ea) {
-    extern __shared__ __attribute__((aligned(16))) _Float16 hlds[];  // [2][HW_STAGE]
+    constexpr int NTH = BM * 4;
+    constexpr int STG = hw_stage<BM>();
+    constexpr int PW = WBN * 4 / NTH;  // 8-half W pieces per thread and part (of a column's 4)
+    extern __shared__ __attribute__((aligned(16))) _Float16 hlds[];  // [2][STG]
     if (a.x_dev) a.x = gload(a.x_dev, 0);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int rows = a.n_rows;
@@ -599,29 +606,29 @@ __global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *
     erows = __builtin_amdgcn_readfirstlane(erows);
     const int nK = (a.K + WKC - 1) / WKC;
     const int c_root = a.wr ? nK : 0;
-    const int n_live = ((rows + WBM - 1) / WBM) * a.n_ct;
+    const int n_live = ((rows + BM - 1) / BM) * a.n_ct;
     const int64_t per = static_cast<int64_t>(a.Fo) * Kp;
     const int wn = (wave & 1) * 64, wm = (wave >> 1) * 32;
     const int i16 = lane & 15, q = lane >> 4;
     Dropout drop = a.epi.drop;
     if (a.seed_dev) drop.reseed(*a.seed_dev);
     const int xr_r = tid >> 2, xr_c = tid & 3;
-    const int w_n = tid >> 1, w_h = tid & 1;
+    const int w_n = tid / (4 / PW), w_h = (tid % (4 / PW)) * PW;  // (column, first piece)
     auto sw = [](int r, int c) { return c ^ ((r >> 2) & 3); };
     const i32x4 xrs = make_rsrc_u(a.x, static_cast<uint32_t>(static_cast<int64_t>(rows) * a.ldx * 4));
     const i32x4 ars = make_rsrc_u(a.agg, static_cast<uint32_t>(a.agg ? static_cast<int64_t>(erows) * a.ld_agg * 4 : 0));
     v4f xv[2][2];
-    h8w wv[2][2][2];
+    h8w wv[2][2][PW];
 
     for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
         const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
-        const int r0 = rt * WBM, n0 = ct * WBN;
+        const int r0 = rt * BM, n0 = ct * WBN;
         const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);
         // the staging row's scales (rows past the range: never stored)
         const int sr = r0 + xr_r;
         const int e_x = sr < rows ? ex[sr] : 0;
         const int e_a = (a.agg && sr < erows) ? ea[sr] : 0;
-        auto load = [&](int c, v4f (&xd)[2], h8w (&wd)[2][2]) __attribute__((always_inline)) {
+        auto load = [&](int c, v4f (&xd)[2], h8w (&wd)[2][PW]) __attribute__((always_inline)) {
             const bool nb = c >= c_root;
             const int kc = (nb ? c - c_root : c) * WKC;
             const int r = r0 + xr_r;
@@ -638,14 +645,13 @@ __global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *
                     xd[j >> 2][j & 3] = buf_load1(rs, k + j < a.K ? off + 4 * j : static_cast<int>(0xF0000000u), 0, 0);
             }
             const int n = min(n0 + w_n, a.Fo - 1);
-            const _Float16 *wb = wimg + (nb ? 2 * per : 0) + static_cast<int64_t>(n) * Kp + kc + 16 * w_h;
+            const _Float16 *wb = wimg + (nb ? 2 * per : 0) + static_cast<int64_t>(n) * Kp + kc + 8 * w_h;
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                wd[p][0] = *reinterpret_cast<const h8w *>(wb + p * per);
-                wd[p][1] = *reinterpret_cast<const h8w *>(wb + p * per + 8);
-            }
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int h = 0; h < PW; ++h) wd[p][h] = *reinterpret_cast<const h8w *>(wb + p * per + 8 * h);
         };
-        auto store = [&](_Float16 *s, int c, const v4f (&xd)[2], const h8w (&wd)[2][2]) __attribute__((always_inline)) {
+        auto store = [&](_Float16 *s, int c, const v4f (&xd)[2], const h8w (&wd)[2][PW]) __attribute__((always_inline)) {
             const bool nb = c >= c_root;
             const int kq = a.K - ((nb ? c - c_root : c) * WKC + 8 * xr_c);  // valid values of the 8
             const int e = nb ? e_a : e_x;
@@ -659,14 +665,14 @@ __global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *
             }
             const int xo = xr_r * WKC + 8 * sw(xr_r, xr_c);
             *reinterpret_cast<h8w *>(s + xo) = p1;
-            *reinterpret_cast<h8w *>(s + WBM * WKC + xo) = p2;
-            _Float16 *ws = s + 2 * WBM * WKC;
+            *reinterpret_cast<h8w *>(s + BM * WKC + xo) = p2;
+            _Float16 *ws = s + 2 * BM * WKC;
             const bool wok = n0 + w_n < a.Fo;  // (rows past F_out: zero)
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    *reinterpret_cast<h8w *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, 2 * w_h + h)) =
+                for (int h = 0; h < PW; ++h)
+                    *reinterpret_cast<h8w *>(ws + p * WBN * WKC + w_n * WKC + 8 * sw(w_n, w_h + h)) =
                         wok ? wd[p][h] : h8w{};
         };
         v4f accr[4][2], accn[4][2];
@@ -675,14 +681,14 @@ __global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) accr[mt][nt] = accn[mt][nt] = v4f{0.f, 0.f, 0.f, 0.f};
         auto mfma_stage = [&](const _Float16 *s, v4f (&acc)[4][2]) __attribute__((always_inline)) {
-            const _Float16 *ws = s + 2 * WBM * WKC;
+            const _Float16 *ws = s + 2 * BM * WKC;
             h8w xb[2][2];
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
                 const int r = wm + 16 * nt + i16;
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
-                    xb[nt][p] = *reinterpret_cast<const h8w *>(s + p * WBM * WKC + r * WKC + 8 * sw(r, q));
+                    xb[nt][p] = *reinterpret_cast<const h8w *>(s + p * BM * WKC + r * WKC + 8 * sw(r, q));
             }
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
@@ -710,9 +716,9 @@ __global__ __launch_bounds__(256, 2) void k_wide_h2(WideArgs a, const _Float16 *
         auto one = [&](int c, auto u_c, auto nb_c) __attribute__((always_inline)) {
             constexpr int U = decltype(u_c)::value;  // c & 1
             if (c + 2 < nch) load(c + 2, xv[U], wv[U]);
-            if constexpr (decltype(nb_c)::value) mfma_stage(hlds + U * HW_STAGE, accn);
-            else mfma_stage(hlds + U * HW_STAGE, accr);
-            if (c + 1 < nch) store(hlds + (U ^ 1) * HW_STAGE, c + 1, xv[U ^ 1], wv[U ^ 1]);
+            if constexpr (decltype(nb_c)::value) mfma_stage(hlds + U * STG, accn);
+            else mfma_stage(hlds + U * STG, accr);
+            if (c + 1 < nch) store(hlds + (U ^ 1) * STG, c + 1, xv[U ^ 1], wv[U ^ 1]);
             __syncthreads();
         };
         using I0 = std::integral_constant<int, 0>;
@@ -914,14 +920,29 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                                static_cast<int>(n_rows), n_rows_dev, ex);
             rc = launch_status();
             if (rc) return rc;
-            const size_t lds = static_cast<size_t>(2) * HW_STAGE * 2;
-            if (vout)
-                hipLaunchKernelGGL(k_wide_h2<true>, dim3(static_cast<unsigned>(grid)), dim3(256), lds, st, a, img, Kp, ew,
-                                   ex, ea);
-            else
-                hipLaunchKernelGGL(k_wide_h2<false>, dim3(static_cast<unsigned>(grid)), dim3(256), lds, st, a, img, Kp, ew,
-                                   ex, ea);
-            return launch_status();
+            // (NGNN_WIDE_BM=128, read once: the eight-wave 128-row tile -- A/B)
+            static const int bm = [] {
+                const char *e = std::getenv("NGNN_WIDE_BM");
+                return (e && std::atoi(e) == 128) ? 128 : 64;
+            }();
+            static bool attr_set[2][2] = {};
+            auto go = [&](auto kern, int bm_c) {
+                const size_t lds = static_cast<size_t>(2) * (2 * bm_c * WKC + 2 * WBN * WKC) * 2;
+                bool &set = attr_set[vout][bm_c == 128];
+                if (!set) {
+                    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             static_cast<int>(lds));
+                    if (e != hipSuccess) return static_cast<int>(e);
+                    set = true;
+                }
+                const int64_t t2 = ceil_div(n_rows, bm_c) * a.n_ct;
+                const int64_t g2 = std::max<int64_t>(8, std::min<int64_t>(ceil_div(t2, 8) * 8, (128 / bm_c) * num_cus()));
+                hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g2)), dim3(bm_c * 4), lds, st, a, img, Kp, ew, ex, ea);
+                return launch_status();
+            };
+            if (bm == 128) return vout ? go(k_wide_h2<true, 128>, 128) : go(k_wide_h2<false, 128>, 128);
+            return vout ? go(k_wide_h2<true, 64>, 64) : go(k_wide_h2<false, 64>, 64);
         }
     }
     if (!exact && x3_on && fits && ws && ws_bytes >= head + ib + 256) {
