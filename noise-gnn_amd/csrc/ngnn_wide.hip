@@ -513,24 +513,21 @@ __global__ __launch_bounds__(256, 2) void k_wide_x3(WideArgs a, const __bf16 *__
 // the two-layer kernels' arithmetic) instead of X3's
 // six bf16 ones; the weight image is 2 parts instead of 3.  The scales must
 // be known before a row's first k-stage, so the row exponents come from a
-// pass of their own (k_row_exp) and the W rows' from the image launch; the
+// pass (k_wide_prep_h2, with the W split and the W rows' exponents), the
+// aggregate rows' from k_wide_agg as it stores them; the
 // root and neighbour terms have different row and column scales, so they
 // accumulate apart and meet, unscaled, in the epilogue.
 // halves per stage buffer (BM = 64: 24 KiB); BM = 128 (eight waves): the W
 // tile staged once per 128 rows -- half the image's L2 reads per row
 template <int BM>
 constexpr int hw_stage() { return 2 * BM * WKC + 2 * WBN * WKC; }
-constexpr int HW_STAGE = hw_stage<WBM>();
 typedef _Float16 h8w __attribute__((ext_vector_type(8)));
 
 // one wave per W row (mat, n): its exponent (max |w| of the row in [2^14,
 // 2^15) after scaling) and its two fp16 parts -> img [mat][part][Fo][Kp]
-__global__ __launch_bounds__(256) void k_wide_wimg_h2(const float *__restrict__ wr, const float *__restrict__ wl,
-                                                      int64_t ldw, int Fo, int K, int Kp, _Float16 *__restrict__ img,
-                                                      int *__restrict__ ew) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= 2 * Fo) return;
+__device__ __forceinline__ void wimg_h2_row(const float *__restrict__ wr, const float *__restrict__ wl, int64_t ldw,
+                                            int Fo, int K, int Kp, _Float16 *__restrict__ img, int *__restrict__ ew,
+                                            int row, int lane) {
     const int mat = row / Fo, n = row - mat * Fo;
     const float *w = mat ? wl : wr;
     // (8 consecutive values per lane and pass, 16-B part stores; the second
@@ -569,17 +566,25 @@ __global__ __launch_bounds__(256) void k_wide_wimg_h2(const float *__restrict__ 
     }
 }
 
-// one wave per row: x rows [0, rows) -> ex (the H2 scale exponents of
-// k_wide_h2's root staging; the aggregate rows' come from k_wide_agg)
-__global__ __launch_bounds__(256) void k_row_exp(const float *__restrict__ x, const float *const *x_dev, int64_t ldx,
-                                                 int K, int n_rows, const int32_t *__restrict__ n_rows_dev,
-                                                 int *__restrict__ ex) {
+// the H2 layer's preparation in one launch: workgroups [0, nbw) split the W
+// rows (wimg_h2_row), the rest take one wave per x row [0, rows) -> ex (the
+// root staging's exponents; the aggregate rows' come from k_wide_agg)
+__global__ __launch_bounds__(256) void k_wide_prep_h2(const float *__restrict__ wr, const float *__restrict__ wl,
+                                                      int64_t ldw, int Fo, int Kp, _Float16 *__restrict__ img,
+                                                      int *__restrict__ ew, int nbw, const float *__restrict__ x,
+                                                      const float *const *x_dev, int64_t ldx, int K, int n_rows,
+                                                      const int32_t *__restrict__ n_rows_dev, int *__restrict__ ex) {
+    const int lane = threadIdx.x & 63;
+    if (static_cast<int>(blockIdx.x) < nbw) {
+        const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (row < 2 * Fo) wimg_h2_row(wr, wl, ldw, Fo, K, Kp, img, ew, row, lane);
+        return;
+    }
     if (x_dev) x = gload(x_dev, 0);
     int rows = n_rows;
     if (n_rows_dev) rows = min(rows, *n_rows_dev);
-    const int lane = threadIdx.x & 63;
-    const int waves = gridDim.x * 4;
-    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += waves) {
+    const int waves = (gridDim.x - nbw) * 4;
+    for (int r = (blockIdx.x - nbw) * 4 + (threadIdx.x >> 6); r < rows; r += waves) {
         const float *p = x + static_cast<int64_t>(r) * ldx;
         float m = 0.0f;
         for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(p[k]));
@@ -911,14 +916,12 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     {
         if (use_h2) {
             _Float16 *img = h2_img;
-            hipLaunchKernelGGL(k_wide_wimg_h2, dim3(static_cast<unsigned>(ceil_div(2 * Fo, 4))), dim3(256), 0, st, wr,
-                               wl, ldw, static_cast<int>(Fo), static_cast<int>(K), Kp, img, ew);
-            int rc = launch_status();
-            if (rc) return rc;
-            const unsigned gr = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows, 4), 8 * num_cus())));
-            hipLaunchKernelGGL(k_row_exp, dim3(gr), dim3(256), 0, st, x, x_dev, ldx, static_cast<int>(K),
+            const int nbw = static_cast<int>(ceil_div(2 * Fo, 4));
+            const int64_t gr = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows, 4), 8 * num_cus()));
+            hipLaunchKernelGGL(k_wide_prep_h2, dim3(static_cast<unsigned>(nbw + gr)), dim3(256), 0, st, wr, wl, ldw,
+                               static_cast<int>(Fo), Kp, img, ew, nbw, x, x_dev, ldx, static_cast<int>(K),
                                static_cast<int>(n_rows), n_rows_dev, ex);
-            rc = launch_status();
+            const int rc = launch_status();
             if (rc) return rc;
             // (NGNN_WIDE_BM=128, read once: the eight-wave 128-row tile -- A/B)
             static const int bm = [] {
