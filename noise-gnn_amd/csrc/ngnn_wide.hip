@@ -144,6 +144,7 @@ struct WideArgs {
     Epi epi;
     const uint64_t *seed_dev;
     int n_ct;  // column tiles
+    int xcd;   // k_wide_h2: a row tile's column tiles on one XCD (grid a multiple of 8)
 };
 
 template <bool VOUT>
@@ -625,8 +626,17 @@ __global__ __launch_bounds__(BM * 4, 128 / BM) void k_wide_h2(WideArgs a, const 
     v4f xv[2][2];
     h8w wv[2][2][PW];
 
-    for (int t = blockIdx.x; t < n_live; t += gridDim.x) {
-        const int rt = t / a.n_ct, ct = t - rt * a.n_ct;
+    // XCD-aware order (workgroup b runs on XCD b mod 8): row tile rt goes to
+    // XCD rt mod 8 with all its column tiles, so its x / agg rows are fetched
+    // into one L2 instead of n_ct of them
+    const int RT = (rows + BM - 1) / BM;
+    const int xc = blockIdx.x & 7;
+    const int n_mine = a.xcd ? (xc < RT ? (RT - xc + 7) / 8 : 0) * a.n_ct : n_live;
+    const int t0 = a.xcd ? static_cast<int>(blockIdx.x >> 3) : static_cast<int>(blockIdx.x);
+    const int ts = a.xcd ? static_cast<int>(gridDim.x >> 3) : static_cast<int>(gridDim.x);
+    for (int u = t0; u < n_mine; u += ts) {
+        const int um = u / a.n_ct, ct = u - um * a.n_ct;
+        const int rt = a.xcd ? xc + 8 * um : um;
         const int r0 = rt * BM, n0 = ct * WBN;
         const int nch = c_root + ((a.agg && r0 < erows) ? nK : 0);
         // the staging row's scales (rows past the range: never stored)
@@ -900,6 +910,12 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     a.epi = Epi{bias, relu, make_dropout(p_drop, seed), 0};
     a.seed_dev = seed_dev;
     a.n_ct = static_cast<int>(ceil_div(Fo, WBN));
+    // (NGNN_WIDE_XCD=0, read once: k_wide_h2's plain tile order -- A/B)
+    static const bool xcd_on = [] {
+        const char *e = std::getenv("NGNN_WIDE_XCD");
+        return !(e && e[0] == '0');
+    }();
+    a.xcd = 0;
     const int64_t tiles = ceil_div(n_rows, WBM) * a.n_ct;
     NGNN_RETURN_IF(tiles > INT32_MAX, NGNN_E_RANGE);
     // persistent: two workgroups per CU (55 KiB LDS, 178 VGPRs each), a
@@ -941,6 +957,7 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                 }
                 const int64_t t2 = ceil_div(n_rows, bm_c) * a.n_ct;
                 const int64_t g2 = std::max<int64_t>(8, std::min<int64_t>(ceil_div(t2, 8) * 8, (128 / bm_c) * num_cus()));
+                a.xcd = (xcd_on && g2 % 8 == 0) ? 1 : 0;  // (the XCD order needs whole groups of 8)
                 hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(g2)), dim3(bm_c * 4), lds, st, a, img, Kp, ew, ex, ea);
                 return launch_status();
             };
