@@ -1440,9 +1440,18 @@ extern "C" int ngnn_sage_dgrad_fused(const float *dy, int64_t ldy, const float *
     dh_init_launch(nullptr, K, n_rows, r_ptr, rnext_ptr, K, dh, ldd, zero_tail, st);
     // W in LDS when both fit next to the dz slots (persistent workgroups,
     // one per CU, rows grid-strided); else the L2-streaming variant
+    // -- and F_out >= 32: a narrow W (Amazon-Computers' 512 -> 10 output
+    // layer: 40 KB) is as cheap from L2, and without the LDS copy the grid is
+    // not held to one workgroup per CU (NGNN_DGRAD_LDSW=1 / 0, read once:
+    // always / never -- A/B)
+    static const int ldsw_env = [] {
+        const char *e = std::getenv("NGNN_DGRAD_LDSW");
+        return e ? std::atoi(e) : -1;
+    }();
     const size_t wbytes = 2 * sizeof(float) * static_cast<size_t>(Fo) * static_cast<size_t>(K);
     const bool lds_w = ((Fo * K) % 4 == 0) && aligned(wl, 16) && aligned(wr, 16) &&
-                       wbytes + sizeof(float) * 4 * FD_MAXF <= 150 * 1024;
+                       wbytes + sizeof(float) * 4 * FD_MAXF <= 150 * 1024 &&
+                       (ldsw_env == 1 || (ldsw_env < 0 && Fo >= 32));
     const unsigned g = static_cast<unsigned>(
         std::min<int64_t>(ceil_div(n_rows * ceil_div(K, 64), 4), lds_w ? dgrad_num_cus() : 1024));
     auto go = [&](auto red_c, auto lds_c) {
