@@ -70,6 +70,14 @@ def parse():
                          "x = graph.x[n_id] unmaterialized and the layer-0 kernels gather the "
                          "rows (graph replay) -- no copy in the loader, +6 us L0 forward and "
                          "+5 us L0 weight gradient in the step (scattered 400-B row reads)")
+    ap.add_argument("--coteaching", action="store_true",
+                    help="the co-teaching step instead (pipeline.py:95-142, config_products.yml "
+                         "algo_type 'coteaching'): two SAGE models, CTLoss, both backwards and Adam "
+                         "steps as one graph replay (ngnn.graphs.GraphedCoTeachingStep); noisy labels "
+                         "--noise-rate, forget rate --forget-rate; aggregated edges count both models")
+    ap.add_argument("--forget-rate", type=float, default=0.36,
+                    help="co-teaching forget rate (config_products.yml: noise_rate 0.3 x ct_tau 1.2)")
+    ap.add_argument("--noise-rate", type=float, default=0.3)
     ap.add_argument("--timer", default="sage_fwd_l0,sage_fwd_l1,gcn_fwd_l1_z,gcn_fwd_l1_agg,"
                                        "sage2_edge,sage2_fwd,sage2_narrow",
                     help="comma list of kernel spans timed with HIP events in the timed region "
@@ -473,6 +481,23 @@ def main():
     opt = Adam(model.parameters(), lr=1e-3)
     reducer = GradAllReduce(model.parameters())
     model.train()
+    ct = None
+    if args.coteaching:
+        # config_products.yml's train_ct: a second model, noisy labels (30 % flipped
+        # uniformly, flip_label's role), CTLoss at the steady forget rate
+        if world > 1 or args.eager:
+            raise SystemExit("bench.py --coteaching: one GPU, graph replay")
+        from ngnn.losses import CTLoss
+        model2 = ngnn.SAGE(F_in, args.hidden, C, layers, dropout=0.5, aggr=args.aggr).to(dev)
+        if args.dtype == "bf16":
+            raise SystemExit("bench.py --coteaching: fp32 (CTLoss takes fp32 logits)")
+        model2.train()
+        opt2 = Adam(model2.parameters(), lr=1e-3)
+        gen = torch.Generator(device=dev).manual_seed(17)
+        flip = torch.rand(graph.num_nodes, device=dev, generator=gen) < args.noise_rate
+        yhn = torch.where(flip, torch.randint(0, C, (graph.num_nodes,), device=dev, generator=gen), graph.y)
+        graph.node_attrs["yhn"] = yhn  # batch.yhn, gathered by the loader (pipeline.py:116)
+        ct = (model2, opt2, CTLoss(dev), yhn == graph.y)
 
     # pre-sample this rank's batches (inputs resident in HBM before timing)
     loader = NeighborLoader(graph, graph.train_idx, fanout, args.batch_size, shuffle=True, seed=7,
@@ -488,7 +513,17 @@ def main():
         torch.cuda.synchronize()
 
     graph = not args.eager
-    if graph:
+    if ct is not None:
+        from ngnn.graphs import GraphedCoTeachingStep, slot_size
+        n_cap, e_cap = slot_size(args.batch_size, fanout)
+        gstep = GraphedCoTeachingStep(model, opt, ct[0], ct[1], ct[2], args.batch_size, n_cap, e_cap,
+                                      batches[0].x.size(1), dev, noise_or_not=ct[3])
+        b0 = batches[0]
+        gstep.capture(b0.x, b0.edge_index, b0.yhn, b0.n_id, args.forget_rate)
+
+        def run(b):
+            gstep(b.x, b.edge_index, b.yhn, b.n_id, args.forget_rate, b.batch_size)
+    elif graph:
         # the whole step (CSR build .. Adam) as one captured HIP graph over a
         # static slot sized for any block of this fanout (ngnn/graphs.py)
         from ngnn.graphs import GraphedTrainStep, slot_size
@@ -522,11 +557,11 @@ def main():
         for i in range(args.steps):
             b = batches[(args.warmup + i) % nb]
             run(b)
-            edges += layers * b.edge_index.shape[1]
+            edges += (2 if ct is not None else 1) * layers * b.edge_index.shape[1]
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
     barrier()
     dt = time.perf_counter() - t0
-    if graph and args.timer != "none":
+    if graph and args.timer != "none" and ct is None:
         timer = new_timer()
         with timer:
             for i in range(args.steps):
@@ -547,6 +582,8 @@ def main():
         workload += f"-{args.aggr}"
     if args.module == "gcn":
         workload += "-gcn"
+    if ct is not None:
+        workload += f"-coteaching-fr{args.forget_rate:g}"
     # the layer-0 kernel reads rows through n_id under the fused gather: its
     # own traffic key (a loader-copy PMC record is not its evidence)
     pmc_workload = workload + ("-fusedgather" if args.gather == "fused" else "")
@@ -631,7 +668,7 @@ def main():
     # the reference loop verbatim on the eager path (INTEGRATION Option B):
     # what a user gets without GraphedTrainStep / ngnn.optim.Adam
     eager_ref = None
-    if rank == 0 and world == 1 and not args.no_eager_ref:
+    if rank == 0 and world == 1 and not args.no_eager_ref and ct is None:
         timed = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
         ms_core = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps)
         ms_verb = eager_reference_loop(timed, args, F_in, C, layers, dev, args.steps, verbatim=True)
@@ -660,9 +697,11 @@ def main():
             run(b)
         barrier()
         epoch_s = time.perf_counter() - t1
+        if graph and ct is None:
+            gstep.check_inputs()  # (every batch of the epoch met the slot's contract)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and ct is None:
         cpu = cpu_baseline(batches, args, layers)
 
     if rank == 0:
@@ -671,6 +710,9 @@ def main():
         line = {
             "metric": "aggregated edges/sec (GraphSAGE train step), ogbn-products fanout=[15,10] bs=1024"
                       if (args.dataset, args.fanout, args.batch_size) == ("ogbn-products", "15,10", 1024)
+                      and ct is None
+                      else f"aggregated edges/sec (co-teaching train step: 2 SAGE models + CTLoss), "
+                           f"{args.dataset} fanout=[{args.fanout}] bs={args.batch_size}" if ct is not None
                       else f"aggregated edges/sec (GraphSAGE train step), {args.dataset} "
                            f"fanout=[{args.fanout}] bs={args.batch_size}",
             "value": round(edges / dt, 1), "unit": "edges/s", "n_gpus": world,
@@ -681,6 +723,8 @@ def main():
             "config": {"workload": workload,
                        "model": (f"SimpleGCN({F_in},{args.hidden},{C},L={layers}) sum-aggr + Adam(1e-3)"
                                  if args.module == "gcn" else
+                                 f"2 x SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + CTLoss + "
+                                 f"2 x Adam(1e-3)" if ct is not None else
                                  f"SAGE({F_in},{args.hidden},{C},L={layers}) {args.aggr}-aggr + Adam(1e-3)"),
                        "global_batch": args.batch_size * world, "fanout": fanout,
                        "avg_edges_per_batch": round(E_avg), "avg_nodes_per_batch": round(N_avg),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 17
+#define NGNN_ABI_VERSION 18
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -633,6 +633,19 @@ int ngnn_cast_f32_bf16_rows(const float *src, void *dst, int64_t n_rows, int64_t
  * and its autograd backward, one ATen copy kernel per tensor). */
 int ngnn_cast_tensors(int n, const void *const *src, void *const *dst, const int64_t *numels,
                       int to_bf16, void *stream);
+/* ABI 18: n <= 16 tensors of mixed dtypes in one launch: dst[k][i] =
+ * cast(src[k][i]) / divisor (src_dtypes / dst_dtypes: host arrays of NGNN_F32
+ * or NGNN_BF16 per tensor; bf16 -> fp32 exact, fp32 -> bf16 round to nearest
+ * even; divisor 1: no division, otherwise the IEEE quotient as Tensor.div_;
+ * src[k] == dst[k] allowed when the dtypes agree: in place) -- the
+ * data-parallel gradient bucket's pack (each parameter's gradient into the
+ * flat fp32 bucket) and unpack (bucket / world back into bf16 gradients and
+ * in place into the fp32 ones that are bucket views): the copies and the
+ * div_ of DistributedDataParallel's bucket path (pipeline.py:167-169 under
+ * seed-sharded DP) as one launch each way. */
+int ngnn_cast_tensors_ex(int n, const void *const *src, void *const *dst, const int64_t *numels,
+                         const int32_t *src_dtypes, const int32_t *dst_dtypes, float divisor,
+                         void *stream);
 /* dst[r, :F] = float(src[r, :F]) (bf16 -> fp32, exact) for rows r <
  * min(n_rows, *n_rows_dev) (n_rows_dev nullable): the rows of a bf16 model's
  * activations a backward kernel reads as an fp32 mask. */
@@ -673,8 +686,12 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * bits OR-ed in (never cleared here) when the block breaks the slot's
  * contract -- NGNN_SLOT_UNSORTED: a target smaller than the one before it;
  * NGNN_SLOT_RANGE: a source or target outside [0, N).  The CSR of such a
- * block is wrong (never written out of bounds); the caller checks the word
- * without a device sync (ABI 16: replaces a host read-back of the targets).
+ * block is wrong, but no consumer of the slot reads or writes out of bounds:
+ * a source outside [0, N) is stored as row 0 (slot_ei, slot_col, slot_colx
+ * and the r_next bound; ABI 18), a target only selects which rowptr entries
+ * (clamped to [0, n_cap]) its edge lands under.  E > 0 needs N >= 1.  The
+ * caller checks the word without a device sync (ABI 16: replaces a host
+ * read-back of the targets).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 #define NGNN_SLOT_UNSORTED 1

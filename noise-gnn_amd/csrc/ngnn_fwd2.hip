@@ -56,6 +56,9 @@ constexpr int F2_WAVES = 8;    // workgroup: 8 waves x 32 hidden columns = 256
 constexpr int F2_HID = 256;    // hidden width of the fused shape
 constexpr int F2_ROWS = 16;    // rows per tile (one MFMA n-block)
 constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
+#ifndef NGNN_F2_STAUX
+#define NGNN_F2_STAUX 2  // the main phase's h / out / z stores non-temporal (nt): fused launch 93.7 -> 89.6 us (A/B, r06g)
+#endif
 
 // two fp16 parts (round to nearest even) of 8 scaled values
 __device__ __forceinline__ void h2_split(v4f a, v4f b, half8 &p1, half8 &p2) {
@@ -480,21 +483,24 @@ struct F2Args {
 // nb) (act(b0) on rows without in-edges)
 template <int C0, int NT1, int DM, bool XR, bool T16, int DBG = 0, bool ROOT = true>
 __device__ __forceinline__ void fwd2_body(const F2Args &a) {
-    constexpr int MT1 = 2 * NT1;
+    static_assert(NT1 == 3, "layer 1's six output m-tiles map onto the waves (one each, two duplicates)");
     constexpr int CF = T16 ? C0 - 1 : C0;    // full 32-deep chunks of layer 0
     constexpr int KC = 32 * CF + (T16 ? 16 : 0);  // K0 padded to the chunks
     constexpr int PSTR = 32 * C0 + 16;       // halves per parts row: 72 dwords = 8 mod 64 banks (conflict-free fragment reads)
     constexpr int XPB = 2 * F2_ROWS * PSTR;  // halves per x-parts buffer (2 parts)
-    constexpr int NIT = MT1 * 8;             // reduce items per wave (MT1 x 64 over 8 waves)
+    constexpr int NK1 = F2_HID / 32;         // layer 1's 32-deep K chunks = the waves that produce h
     extern __shared__ __attribute__((aligned(16))) v4f lds2[];
-    v4f *spart = lds2;                                                   // [2][8][MT1][64]
-    _Float16 *sxp = reinterpret_cast<_Float16 *>(lds2 + 2 * F2_WAVES * MT1 * 64);  // [2][2][16][PSTR]
+    // h of a tile as layer 1's B fragments: [2 buffers][8 chunks (= producer
+    // waves)][2 parts][64 lanes] half8 -- the producer's lane (q, rl) holds
+    // exactly the fragment lane (q, rl) of a consumer reads (16-B, contiguous)
+    half8 *shp = reinterpret_cast<half8 *>(lds2);                        // [2][8][2][64]
+    _Float16 *sxp = reinterpret_cast<_Float16 *>(lds2 + 2 * NK1 * 2 * 64);  // [2][2][16][PSTR]
     int *serow = reinterpret_cast<int *>(sxp + 2 * XPB);                // [2][16]
     float *sb0 = reinterpret_cast<float *>(serow + 2 * F2_ROWS);        // [256] b0
     float *sb1 = sb0 + F2_HID;                                          // [16 NT1] b1 (0 past F1)
     float *sout = sb1 + 16 * NT1;                                       // [2][16 F1] out tiles, packed rows
-    float *sf1 = sout + 2 * F2_ROWS * 16 * NT1;                         // [2][16][8] partial unscales (row, wave)
-    float *strash = sf1 + 2 * F2_ROWS * F2_WAVES;                       // [64] sink of the lanes with nothing to write
+    int *se1 = reinterpret_cast<int *>(sout + 2 * F2_ROWS * 16 * NT1);  // [2][16][8] h-chunk exponents (row, chunk)
+    float *strash = reinterpret_cast<float *>(se1 + 2 * F2_ROWS * F2_WAVES);  // [64] sink of the lanes with nothing to write
     static_assert(PSTR >= 128, "the split's lanes 4 sslot + 3 < 128 write inside a parts row");
 
     const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -507,7 +513,7 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     if (threadIdx.x < F2_HID) sb0[threadIdx.x] = DM == 2 ? 2.0f * a.b0[threadIdx.x] : a.b0[threadIdx.x];
     if (threadIdx.x < 16 * NT1) sb1[threadIdx.x] = static_cast<int>(threadIdx.x) < a.F1 ? a.b1[threadIdx.x] : 0.0f;
     // ---- this wave's weight slices, for the whole launch
-    half8 wr[2][CF][2], w1[MT1][2];
+    half8 wr[2][CF][2], w1[NK1][2];
     half4 wt[2][2];  // T16: the tail chunk, k = 32 CF + 4 q .. + 3
     int eW0 = 0;
     if constexpr (ROOT) {
@@ -544,43 +550,60 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
             }
         }
     }
+    // Layer 1 without a cross-wave reduction (round 6).  The six output
+    // m-tiles of [W_r1 | W_l1] (out's 48 columns, then z's) go to six waves,
+    // each over ALL 256 of layer 1's K: out waves 0, 1, 3 take W_r1's m-tiles
+    // 0, 1, 2 and z waves 4, 5, 6 W_l1's (SIMD partners w, w + 4: two
+    // consumers on SIMDs 0 and 1, one on 2 and 3); waves 2 and 7 repeat m-tile
+    // 2 and store nothing (uniform code, the pipeline keeps its two
+    // instantiations).  Every wave still produces 32 columns of h: it splits
+    // them as before (its own per-row exponent) and leaves the two fp16 parts
+    // in LDS as B fragments; a consumer runs the 8 chunks, rescaling its
+    // accumulator by the exponent step between chunks (an exact power of two
+    // per lane: a lane's 4 accumulator values share one tile row).
+    // The wave's slice: output rows 16 mt1 + rl, K = 32 c + (4 q + j, 16 + 4 q + j)
+    // for chunk c -- the order of producer c's lane (q, rl) values of h.
+    const int l1z = wv >= F2_WAVES / 2;                   // z (W_l1) or out (W_r1)
+    const int mt1 = min(wv & 3, NT1 - 1);                 // this wave's output m-tile
+    const bool l1dup = wv == 2 || wv == F2_WAVES - 1;     // duplicates: nothing stored
     int eW1;
     {
-        // layer 1: output rows 16 m1' + m of W_r1 (m1 < NT1) / W_l1 (the rest),
-        // K rows 32 wv + (4 q + j, 16 + 4 q + j): the order of the lane's h
         // (buffer loads, counted in order with the kernel's other loads)
-        v4f t[MT1][2];
+        v4f t[NK1][2];
         float mx = 0.0f;
-        const i32x4 r1r = make_rsrc(a.wr1, static_cast<uint32_t>(a.F1 * a.ldw1 * 4));
-        const i32x4 l1r = make_rsrc(a.wl1, static_cast<uint32_t>(a.F1 * a.ldw1 * 4));
+        const i32x4 w1r = make_rsrc(l1z ? a.wl1 : a.wr1, static_cast<uint32_t>(a.F1 * a.ldw1 * 4));
+        const int o = 16 * mt1 + rl;
+        const int rb = o < a.F1 ? o * static_cast<int>(a.ldw1) * 4 : kOOB2;
 #pragma unroll
-        for (int m1 = 0; m1 < MT1; ++m1) {
-            const int zt = m1 >= NT1;
-            const int o = 16 * (m1 - zt * NT1) + rl;
-            const int rb = o < a.F1 ? o * static_cast<int>(a.ldw1) * 4 : kOOB2;
-            const int c0 = (32 * wv + 4 * q) * 4, c1 = (32 * wv + 16 + 4 * q) * 4;
-            t[m1][0] = buf_load4(zt ? l1r : r1r, rb == kOOB2 ? kOOB2 : rb + c0, 0, 0);
-            t[m1][1] = buf_load4(zt ? l1r : r1r, rb == kOOB2 ? kOOB2 : rb + c1, 0, 0);
+        for (int c = 0; c < NK1; ++c) {
+            const int c0 = (32 * c + 4 * q) * 4, c1 = (32 * c + 16 + 4 * q) * 4;
+            t[c][0] = buf_load4(w1r, rb == kOOB2 ? kOOB2 : rb + c0, 0, 0);
+            t[c][1] = buf_load4(w1r, rb == kOOB2 ? kOOB2 : rb + c1, 0, 0);
         }
 #pragma unroll
-        for (int m1 = 0; m1 < MT1; ++m1) mx = fmaxf(mx, fmaxf(amax4(t[m1][0]), amax4(t[m1][1])));
+        for (int c = 0; c < NK1; ++c) mx = fmaxf(mx, fmaxf(amax4(t[c][0]), amax4(t[c][1])));
         eW1 = __builtin_amdgcn_readfirstlane(h2_exp(wave_max(mx)));
 #pragma unroll
-        for (int m1 = 0; m1 < MT1; ++m1) h2_split(ldexp4(t[m1][0], eW1), ldexp4(t[m1][1], eW1), w1[m1][0], w1[m1][1]);
+        for (int c = 0; c < NK1; ++c) h2_split(ldexp4(t[c][0], eW1), ldexp4(t[c][1], eW1), w1[c][0], w1[c][1]);
     }
-    // reduce item of this lane (lanes < NIT): output tile mt1, lane lnn of it;
-    // items [0, 64 NT1) are out's tiles, the rest z's -- waves 0-3 take out,
-    // waves 4-7 z (NIT = 16 NT1 items per wave).  z: one 16-B store a lane.
     // out: its rows are F1 floats wide (188 B, not 16-B aligned), but a
     // tile's 16 rows are ONE contiguous 16-B-aligned block of 64 F1 bytes --
     // the sums go to an LDS staging tile in that packed order and leave, a
     // step later, as contiguous 16-B stores (dword stores scattered over 16
-    // rows cost a third of the kernel).  One store instruction per wave and
-    // step either way.
-    const int item = wv * NIT + (ln < NIT ? ln : 0);
-    const int rmt = item >> 6, rln = item & 63;
-    const int rzt = __builtin_amdgcn_readfirstlane(wv) >= F2_WAVES / 2;
-    const int rcol = 16 * (rmt - rzt * NT1) + 4 * (rln >> 4);  // first output column of the item
+    // rows cost a third of the kernel).  z: one 16-B store a lane.  One store
+    // instruction per wave and step either way.  The consumer lane (q, rl)
+    // holds output columns 16 mt1 + 4 q .. + 3 of tile row rl.
+    const int rzt = l1z;
+    const int rcol = 16 * mt1 + 4 * q;  // first output column of the lane
+    // the duplicates' (and out's past-F1 columns') sinks as lane values the
+    // compiler cannot branch on: a wave-uniform test inside a step made it
+    // split the step into blocks with scalar and exec branches
+    // (one register: bits 0-3 -- column rcol + i of out goes to the sink;
+    // bits 28-31 -- kOOB2, OR-ed into a duplicate's z store offset)
+    int lsink = l1dup ? kOOB2 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lsink |= (l1dup || rcol + i >= a.F1) ? 1 << i : 0;
+    asm volatile("" : "+v"(lsink));
     Dropout drop = a.drop;
     if (a.seed_dev) drop.reseed(*a.seed_dev);
 
@@ -696,7 +719,7 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
             }
         }
     };
-    // one tile after layer 0: epilogue, h rows, layer-1 partial into spart[buf]
+    // one tile after layer 0: epilogue, h rows, h's layer-1 fragments into shp[buf]
     auto finish = [&](int j, int buf, const v4f (&acc)[2], float s0, const v4f (&nbv)[2], auto nb_c)
         __attribute__((always_inline)) {
         constexpr bool NB = decltype(nb_c)::value;
@@ -733,11 +756,12 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
         }
         // h rows the backward reads (past the bound: dropped by the range)
         const int ho = static_cast<int>(static_cast<uint32_t>(r) * static_cast<uint32_t>(a.ldh) * 4u) + (32 * wv + 4 * q) * 4;
-        buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, 0);
-        buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, 0);
-        // layer 1: this wave's 32 rows of K -- the B fragment is the lane's own
-        // 8 values of h (k order 4q + i, 16 + 4q + i: the slice matches).
-        // h >= +0 (or +NaN): its bit patterns order as ints
+        buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, NGNN_F2_STAUX);
+        buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, NGNN_F2_STAUX);
+        // layer 1's chunk wv of K: the lane's own 8 values of h ARE the B
+        // fragment lane (q, rl) of that chunk (k order 4q + i, 16 + 4q + i),
+        // split after scaling by the row's exponent over this wave's 32
+        // columns.  h >= +0 (or +NaN): its bit patterns order as ints
         int mb = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) mb = max(mb, __float_as_int(i < 4 ? hv[0][i] : hv[1][i - 4]));
@@ -745,26 +769,17 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
         const int eh = h2_exp(m);
         half8 h1, h2;
         h2_split(ldexp4(hv[0], eh), ldexp4(hv[1], eh), h1, h2);
-        // the partials leave scaled: their unscale 2^-(eW1 + eh) (exact) goes
-        // to the reduce, which takes it in its fma
-        {
-            float *fd = q == 0 ? sf1 + (buf * F2_ROWS + rl) * F2_WAVES + wv : strash + ln;
-            *fd = __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eh));
-        }
-        v4f *pp = spart + (buf * F2_WAVES + wv) * MT1 * 64 + ln;
         if (DBG & 2) {
             asm volatile("" : "+v"(h1), "+v"(h2));
             return;
         }
-#pragma unroll
-        for (int m1 = 0; m1 < MT1; ++m1) {
-            v4f o = mfma_h2(w1[m1][0], w1[m1][1], h1, h2, v4f{0.f, 0.f, 0.f, 0.f});
-            // (a 16-state pad before the partial's LDS store: measured
-            // 82.7 vs 84.7 us per launch without it -- the pad spaces the
-            // SIMD partners' stores; not needed for correctness)
-            asm volatile("s_nop 7\n\ts_nop 7" : "+v"(o));
-            pp[m1 * 64] = o;
-        }
+        // both parts to LDS (two contiguous 1-KiB wave stores), the row's
+        // exponent from lane q = 0 (the row's other lanes into the sink)
+        half8 *hd = shp + (buf * NK1 + wv) * 2 * 64 + ln;
+        hd[0] = h1;
+        hd[64] = h2;
+        int *ed = q == 0 ? se1 + (buf * F2_ROWS + rl) * F2_WAVES + wv : reinterpret_cast<int *>(strash) + ln;
+        *ed = eh;
     };
     // the 8 partials of this lane's item, summed in wave order (+ b1), stored
     // (jj < 0: the step before the first tile -- nothing live)
@@ -773,31 +788,52 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     // (RZ: a z wave -- waves 4-7, the LAG half; compile-time inside the
     // pipeline, so a step has no branches).  The partials are unscaled here,
     // in the fma that sums them (wave order, as a sum of the exact products)
+    // layer1(jj): this wave's output m-tile of tile jj from the 8 producers'
+    // h fragments -- out waves add b1 and stage it in sout[jj & 1], z waves
+    // keep it for their store.  Chunk c's products carry the scale 2^(eW1 +
+    // e_c) (e_c: producer c's exponent of the lane's row); the accumulator is
+    // moved to chunk c's scale before its products (exact: a power of two),
+    // in two chains (even / odd chunks) so an MFMA result is not waited on at
+    // every chunk, and both chains are unscaled exactly at the end.
     auto reduce = [&](int jj, int buf, auto z_c) __attribute__((always_inline)) -> v4f {
         constexpr bool RZ = decltype(z_c)::value;
-        // (the partial reads of lanes >= NIT -- results unused -- go to the
-        // next item slots, not to lane 0's: every 16-lane phase of the
-        // 16-B reads then covers 256 contiguous bytes; reading past the last
-        // wave's partials lands in the x-parts buffers, harmless)
-        const v4f *pp = spart + buf * F2_WAVES * MT1 * 64 + wv * NIT + ln;
-        const float *fp = sf1 + (buf * F2_ROWS + (rln & 15)) * F2_WAVES;
-        const v4f fa = *reinterpret_cast<const v4f *>(fp), fb = *reinterpret_cast<const v4f *>(fp + 4);
-        v4f s = pp[0] * fa[0];
+        const int *ep = se1 + (buf * F2_ROWS + rl) * F2_WAVES;
+        const i32x4 ea = *reinterpret_cast<const i32x4 *>(ep), eb = *reinterpret_cast<const i32x4 *>(ep + 4);
+        const half8 *hp = shp + buf * NK1 * 2 * 64 + ln;
+        v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+        // the fragments two chunks ahead of their MFMAs (a 2-slot ring: the
+        // compiler, left alone, hoisted all 16 reads -- 64 registers -- and
+        // spilled)
+        half8 bf[2][2];
 #pragma unroll
-        for (int w = 1; w < F2_WAVES; ++w) {
-            const v4f o = pp[w * MT1 * 64];
-            const float f = w < 4 ? fa[w] : fb[w - 4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[i] = __builtin_fmaf(o[i], f, s[i]);
+        for (int c = 0; c < 2; ++c) {
+            bf[c][0] = hp[2 * c * 64];
+            bf[c][1] = hp[(2 * c + 1) * 64];
         }
+#pragma unroll
+        for (int c = 0; c < NK1; ++c) {
+            const half8 b1 = bf[c & 1][0], b2 = bf[c & 1][1];
+            if (c >= 2) {
+                const int ep2 = c - 2 < 4 ? ea[c - 2] : eb[c - 6];
+                const int ec = c < 4 ? ea[c] : eb[c - 4];
+                acc[c & 1] *= __builtin_amdgcn_ldexpf(1.0f, ec - ep2);  // scale 2^(eW1 + e_{c-2}) -> 2^(eW1 + e_c)
+            }
+            acc[c & 1] = mfma_h2(w1[c][0], w1[c][1], b1, b2, acc[c & 1]);
+            if (c + 2 < NK1) {
+                bf[c & 1][0] = hp[2 * (c + 2) * 64];
+                bf[c & 1][1] = hp[(2 * (c + 2) + 1) * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        v4f s = acc[0] * __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eb[2]));
+        s += acc[1] * __builtin_amdgcn_ldexpf(1.0f, -(eW1 + eb[3]));
         if (!RZ) {
             s += *reinterpret_cast<const v4f *>(sb1 + rcol);
-            // (columns past F1 and lanes >= NIT -- a repeat of lane 0's item --
-            // into the sink: with two lanes of one ds_write on the same dword,
-            // other lanes' stores sporadically did not land)
-            float *d = sout + (jj & 1) * F2_ROWS * F1 + (rln & 15) * F1 + rcol;
+            // (columns past F1 and the duplicate wave into the sink: no two
+            // lanes of one ds_write on the same dword)
+            float *d = sout + (jj & 1) * F2_ROWS * F1 + rl * F1 + rcol;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) *(ln < NIT && rcol + i < F1 ? d + i : strash + ln) = s[i];
+            for (int i = 0; i < 4; ++i) *(((lsink >> i) & 1) ? strash + ln : d + i) = s[i];
         }
         return s;
     };
@@ -807,16 +843,16 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     auto store = [&](int jz, v4f s, int jo, auto z_c) __attribute__((always_inline)) {
         constexpr bool RZ = decltype(z_c)::value;
         if (RZ) {
-            const int zrow = tile_of(jz) * F2_ROWS + (rln & 15);
-            const int zo = (jz >= 0 && ln < NIT && zrow < n_rows)
-                               ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
-                               : kOOB2;
-            buf_store4(s, zrs, (DBG & 16) ? kOOB2 : zo, 0, 0);
+            const int zrow = tile_of(jz) * F2_ROWS + rl;
+            const int zo = ((jz >= 0 && zrow < n_rows)
+                                ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
+                                : kOOB2) | (lsink & kOOB2);
+            buf_store4(s, zrs, (DBG & 16) ? kOOB2 : zo, 0, NGNN_F2_STAUX);
         } else {
             const int p = static_cast<int>(threadIdx.x);  // (out waves: < 256)
             const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
             const int oo = (jo >= 0 && p < 4 * F1) ? tile_of(jo) * F2_ROWS * F1 * 4 + 16 * p : kOOB2;
-            buf_store4(v, ors, (DBG & 16) ? kOOB2 : oo, 0, 0);
+            buf_store4(v, ors, (DBG & 16) ? kOOB2 : oo, 0, NGNN_F2_STAUX);
         }
     };
     // the workgroup's last tile jo, which may end inside a piece (n_rows not
@@ -837,14 +873,14 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     };
 
     // ---- software pipeline over the workgroup's tiles.  Step j:
-    //   reduce(j - 1)  -- partials of the previous tile (spart[(j-1)&1])
+    //   reduce(j - 1)  -- layer 1 of the previous tile (shp[(j-1)&1]: MFMA)
     //   l0(j + 1)      -- MFMA on parts buffer (j+1)&1 (split last step)
-    //   finish(j)      -- VALU epilogue + layer-1 MFMA -> spart[j&1]
+    //   finish(j)      -- VALU epilogue + h split -> shp[j&1]
     //   split(j + 2)   -- x rows from the register ring -> parts buffer j&1
     //   ONE barrier
     // so every step holds independent MFMA and VALU work for the scheduler
     // (layer 0 of the next tile beside the epilogue of this one).  Buffer
-    // safety: parts buffer j&1 was last read by l0(j) in step j - 1, spart
+    // safety: parts buffer j&1 was last read by l0(j) in step j - 1, shp
     // (j-1)&1 is rewritten in step j + 1 -- each behind a barrier.
     //
     // x rows are loaded two steps before their split (a 2-slot register ring).
@@ -1013,7 +1049,7 @@ __global__ __launch_bounds__(F2_WAVES * 64) void k_fwd2x(G2Args g, F2Args f) {
 template <int C0, int NT1, int DM, bool XR, int DBG = 0, bool T16 = false, bool ROOT = true>
 int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
     auto fn = k_fwd2<C0, NT1, DM, XR, T16, DBG, ROOT>;
-    const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
+    const size_t lds = static_cast<size_t>(2) * (F2_HID / 32) * 2 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
                        (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
     static bool attr_set = false;  // benign race: idempotent
@@ -1029,7 +1065,7 @@ int launch_fwd2(const F2Args &a, int grid, hipStream_t st) {
 template <int C0, int NT1, int DM, bool XR, bool T16 = false, bool ROOT = true>
 int launch_fwd2x(const G2Args &g, const F2Args &a, int grid, hipStream_t st) {
     auto fn = k_fwd2x<C0, NT1, DM, XR, T16, ROOT>;
-    const size_t lds = static_cast<size_t>(2) * F2_WAVES * 2 * NT1 * 64 * 16 +
+    const size_t lds = static_cast<size_t>(2) * (F2_HID / 32) * 2 * 64 * 16 +
                        static_cast<size_t>(2) * 2 * F2_ROWS * (32 * C0 + 16) * 2 + 2 * F2_ROWS * 4 +
                        (F2_HID + 16 * NT1) * 4 + 2 * F2_ROWS * 16 * NT1 * 4 + 2 * F2_ROWS * F2_WAVES * 4 + 64 * 4;
     static bool attr_set = false;  // benign race: idempotent

@@ -353,6 +353,70 @@ extern "C" int ngnn_cast_tensors(int n, const void *const *src, void *const *dst
     return launch_status();
 }
 
+// ---- n tensors of mixed dtypes copied / cast and divided in ONE launch (ABI
+// 18): the data-parallel gradient bucket's pack (bf16 or fp32 gradients ->
+// the fp32 bucket) and unpack (bucket / world -> the gradients, in place for
+// the fp32 ones that ARE bucket views).  The division is the IEEE quotient,
+// as Tensor.div_ computes it; divisor 1 skips it (exact).
+namespace ngnn {
+namespace {
+struct CastTensorsEx {
+    const void *src[kMaxT];
+    void *dst[kMaxT];
+    int64_t off[kMaxT + 1];
+    uint32_t sbf, dbf;  // bit k: tensor k's source / destination is bf16
+    int n;
+    float div;
+};
+__global__ __launch_bounds__(256) void k_cast_tensors_ex(CastTensorsEx T) {
+    const int64_t total = T.off[T.n];
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total; i += stride) {
+        int k = 0;
+        while (i >= T.off[k + 1]) ++k;  // (<= 16 tensors)
+        const int64_t j = i - T.off[k];
+        float v = (T.sbf >> k) & 1u
+                      ? __uint_as_float(static_cast<uint32_t>(static_cast<const uint16_t *>(T.src[k])[j]) << 16)
+                      : static_cast<const float *>(T.src[k])[j];
+        if (T.div != 1.0f) v = v / T.div;
+        if ((T.dbf >> k) & 1u) static_cast<__bf16 *>(T.dst[k])[j] = static_cast<__bf16>(v);
+        else static_cast<float *>(T.dst[k])[j] = v;
+    }
+}
+}  // namespace
+}  // namespace ngnn
+
+extern "C" int ngnn_cast_tensors_ex(int n, const void *const *src, void *const *dst, const int64_t *numels,
+                                    const int32_t *src_dtypes, const int32_t *dst_dtypes, float divisor,
+                                    void *stream) {
+    using namespace ngnn;
+    NGNN_RETURN_IF(n < 0 || n > kMaxT || (n > 0 && (!src || !dst || !numels || !src_dtypes || !dst_dtypes)),
+                   NGNN_E_ARG);
+    NGNN_RETURN_IF(!(divisor != 0.0f), NGNN_E_ARG);
+    CastTensorsEx T;
+    T.n = n;
+    T.off[0] = 0;
+    T.sbf = T.dbf = 0;
+    T.div = divisor;
+    for (int k = 0; k < n; ++k) {
+        NGNN_RETURN_IF(numels[k] < 0 || (numels[k] > 0 && (!src[k] || !dst[k])), NGNN_E_ARG);
+        NGNN_RETURN_IF((src_dtypes[k] != NGNN_F32 && src_dtypes[k] != NGNN_BF16) ||
+                           (dst_dtypes[k] != NGNN_F32 && dst_dtypes[k] != NGNN_BF16),
+                       NGNN_E_DTYPE);
+        // (in place only without a width change)
+        NGNN_RETURN_IF(src[k] == dst[k] && src_dtypes[k] != dst_dtypes[k], NGNN_E_ARG);
+        T.src[k] = src[k];
+        T.dst[k] = dst[k];
+        T.off[k + 1] = T.off[k] + numels[k];
+        T.sbf |= static_cast<uint32_t>(src_dtypes[k] == NGNN_BF16) << k;
+        T.dbf |= static_cast<uint32_t>(dst_dtypes[k] == NGNN_BF16) << k;
+    }
+    if (n == 0 || T.off[n] == 0) return NGNN_OK;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(T.off[n], 256), 1024));
+    hipLaunchKernelGGL(k_cast_tensors_ex, dim3(grid), dim3(256), 0, as_stream(stream), T);
+    return launch_status();
+}
+
 // ---- bf16 rows -> fp32 rows [0, min(n_rows, *n_rows_dev)) x F (a bf16 model's
 // activations widened for the backward kernels that read fp32 masks, rows
 // below a device-side bound only); exact.

@@ -90,7 +90,7 @@ struct SbWs {  // carved from the caller's workspace
     int32_t *state;  // [4 * (H + 1)]
     int32_t *cand;   // [sum_h nf_cap_h * f_h]  global ids of each hop's draws
     int32_t *cnt;    // [sum_h nf_cap_h]
-    int32_t *bsum;   // [2 * max_h nblk_h]     per-block edge / new-node counts
+    uint64_t *lb;    // [max_h nblk_h + 1]     per-tile look-back words + the tile ticket
     int32_t *nid;    // [n_cap]                local -> global
     int32_t *esrc;   // [e_cap]
     int32_t *edst;   // [e_cap]
@@ -144,13 +144,21 @@ __device__ __forceinline__ int floyd_sample_r(int64_t d, int fanout, uint64_t se
     return k;
 }
 
-// draws of frontier node i -> cand[i*f + j]; claims first appearances
+// draws of frontier node i -> cand[i*f + j]; claims first appearances.
+// Also (round 6, one launch fewer per hop): the previous hop's edges
+// relabelled to local ids (its assignment is complete: the launch before),
+// and this hop's look-back words and tile ticket cleared for k_sb_assign_lb.
 template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ gcol, int64_t n_graph,
     const int32_t *__restrict__ hs, const int32_t *__restrict__ nid, int fanout, uint64_t seed,
-    int32_t *__restrict__ cand, int32_t *__restrict__ cnt, int32_t *__restrict__ map) {
+    int32_t *__restrict__ cand, int32_t *__restrict__ cnt, int32_t *__restrict__ map,
+    const int32_t *__restrict__ hs_prev, int32_t *__restrict__ esrc, uint64_t *__restrict__ lb, int nblk) {
     const int i = blockIdx.x * kSbBlock + threadIdx.x;
+    const int stride = gridDim.x * kSbBlock;
+    for (int t = i; t <= nblk; t += stride) lb[t] = 0;  // (lb[nblk]: the tile ticket)
+    if (hs_prev)  // edges of the previous hop [hs_prev[2], hs_prev[6])
+        for (int e = hs_prev[2] + i; e < hs_prev[6]; e += stride) esrc[e] = map[esrc[e]];
     const int lo = hs[0], hi = hs[1];
     if (i >= hi - lo) return;
     const int64_t v = nid[lo + i];
@@ -196,79 +204,6 @@ __device__ __forceinline__ uint64_t sb_new_flags(const int32_t *cand, const int3
     return f;
 }
 
-__device__ __forceinline__ int block_sum(int v, int *red) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    int t = 0;
-    for (int j = 0; j < kSbBlock / 64; ++j) t += red[j];
-    __syncthreads();
-    return t;
-}
-
-template <int KF>
-__global__ __launch_bounds__(kSbBlock) void k_sb_count(const int32_t *__restrict__ hs,
-                                                       const int32_t *__restrict__ cand,
-                                                       const int32_t *__restrict__ cnt,
-                                                       const int32_t *__restrict__ map,
-                                                       int64_t n_graph, int fanout,
-                                                       int32_t *__restrict__ bsum, int nblk) {
-    __shared__ int red[kSbBlock / 64];
-    const int i = blockIdx.x * kSbBlock + threadIdx.x;
-    const int nf = hs[1] - hs[0];
-    int e = 0, n = 0;
-    if (i < nf) {
-        e = cnt[i];
-        int32_t u[KF];
-        n = __popcll(sb_new_flags<KF>(cand, map, map + n_graph, i, fanout, e, u));
-    }
-    e = block_sum(e, red);
-    n = block_sum(n, red);
-    if (threadIdx.x == 0) {
-        bsum[blockIdx.x] = e;
-        bsum[nblk + blockIdx.x] = n;
-    }
-}
-
-// exclusive scan of the per-block counts (one workgroup) + next hop's state
-__global__ __launch_bounds__(1024) void k_sb_scan(int32_t *__restrict__ hs, int32_t *__restrict__ bsum,
-                                                  int nblk) {
-    __shared__ int se[1024], sn[1024];
-    const int t = threadIdx.x;
-    const int per = (nblk + 1023) / 1024;
-    const int b0 = min(nblk, t * per), b1 = min(nblk, b0 + per);
-    int e = 0, n = 0;
-    for (int b = b0; b < b1; ++b) {
-        e += bsum[b];
-        n += bsum[nblk + b];
-    }
-    se[t] = e;
-    sn[t] = n;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const int ae = t >= o ? se[t - o] : 0, an = t >= o ? sn[t - o] : 0;
-        __syncthreads();
-        se[t] += ae;
-        sn[t] += an;
-        __syncthreads();
-    }
-    int pe = se[t] - e, pn = sn[t] - n;  // exclusive
-    for (int b = b0; b < b1; ++b) {
-        const int ve = bsum[b], vn = bsum[nblk + b];
-        bsum[b] = pe;
-        bsum[nblk + b] = pn;
-        pe += ve;
-        pn += vn;
-    }
-    if (t == 1023) {
-        hs[4] = hs[1];           // next frontier: this hop's new nodes
-        hs[5] = hs[1] + sn[t];
-        hs[6] = hs[2] + se[t];
-        hs[7] = 0;
-    }
-}
-
 __device__ __forceinline__ int block_excl_scan(int v, int *sh) {
     const int t = threadIdx.x;
     sh[t] = v;
@@ -284,15 +219,34 @@ __device__ __forceinline__ int block_excl_scan(int v, int *sh) {
     return r;
 }
 
-// new local ids (first appearances, in order) and the hop's edges
-// (global source ids for now, local targets)
+// look-back word of a tile: status (bits 62-63: 1 aggregate, 2 inclusive
+// prefix) | new nodes (bits 31-61) | edges (bits 0-30); counts < 2^30
+// (sb_plan bounds n, e by INT32_MAX / 2)
+constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
+__device__ __forceinline__ uint64_t lb_word(uint64_t st, int e, int n) {
+    return st | (static_cast<uint64_t>(n) << 31) | static_cast<uint64_t>(e);
+}
+
+// One hop's relabelling in ONE launch (round 6; was count + scan + assign):
+// each tile (256 frontier positions, in ticket order -- a tile only waits
+// for tiles that already run) takes its positions' draws and first-
+// appearance flags, publishes its (edges, new nodes) counts, finds its
+// exclusive prefix by a decoupled look-back over the tiles before it, then
+// assigns the new local ids (map, nid) in (position, draw) order and writes
+// the hop's edges (global sources, local targets).  The last tile writes the
+// next hop's state.  Same ids and edge order as the three launches.
 template <int KF>
-__global__ __launch_bounds__(kSbBlock) void k_sb_assign(
-    const int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
-    int32_t *__restrict__ map, int64_t n_graph, int fanout, const int32_t *__restrict__ bsum,
-    int nblk, int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst) {
+__global__ __launch_bounds__(kSbBlock) void k_sb_assign_lb(
+    int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
+    int32_t *__restrict__ map, int64_t n_graph, int fanout, uint64_t *__restrict__ lb, int nblk,
+    int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst) {
     __shared__ int sh[kSbBlock];
-    const int i = blockIdx.x * kSbBlock + threadIdx.x;
+    __shared__ int s_tile, s_pe, s_pn;
+    if (threadIdx.x == 0)
+        s_tile = static_cast<int>(atomicAdd(reinterpret_cast<unsigned long long *>(lb + nblk), 1ull));
+    __syncthreads();
+    const int tile = s_tile;
+    const int i = tile * kSbBlock + threadIdx.x;
     const int lo = hs[0], hi = hs[1], e0 = hs[2];
     const int nf = hi - lo;
     int k = 0;
@@ -300,12 +254,56 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_assign(
     int32_t u[KF];
     if (i < nf) {
         k = cnt[i];
-        // only the owner of u's claim ever writes map[u], and every flag is
-        // read before this thread writes: the test is race-free
+        // race-free although other tiles write map[] meanwhile: only the
+        // position that won u's claim ever writes map[u] (after reading
+        // it), and for every other position the flag is false whatever
+        // map[u] reads
         fl = sb_new_flags<KF>(cand, map, map + n_graph, i, fanout, k, u);
     }
-    int e = e0 + bsum[blockIdx.x] + block_excl_scan(k, sh);
-    int n = hi + bsum[nblk + blockIdx.x] + block_excl_scan(__popcll(fl), sh);
+    const int xe = block_excl_scan(k, sh);
+    const int nn = __popcll(fl);
+    const int xn = block_excl_scan(nn, sh);
+    // tile totals: the last thread's exclusive value plus its own
+    __shared__ int s_te, s_tn;
+    if (threadIdx.x == kSbBlock - 1) {
+        s_te = xe + k;
+        s_tn = xn + nn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int ae = s_te, an = s_tn;
+        int pe = 0, pn = 0;
+        if (tile == 0) {
+            __hip_atomic_store(lb + tile, lb_word(kLbPre, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(lb + tile, lb_word(kLbAgg, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            for (int p = tile - 1; p >= 0;) {
+                const uint64_t w = __hip_atomic_load(lb + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t st = w & (3ull << 62);
+                if (st == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                pe += static_cast<int>(w & 0x7FFFFFFFull);
+                pn += static_cast<int>((w >> 31) & 0x7FFFFFFFull);
+                if (st == kLbPre) break;
+                --p;
+            }
+            __hip_atomic_store(lb + tile, lb_word(kLbPre, pe + ae, pn + an), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_pe = pe;
+        s_pn = pn;
+        if (tile == nblk - 1) {  // the next hop's state: this hop's new nodes, its edges' end
+            hs[4] = hi;
+            hs[5] = hi + pn + an;
+            hs[6] = e0 + pe + ae;
+            hs[7] = 0;
+        }
+    }
+    __syncthreads();
+    int e = e0 + s_pe + xe;
+    int n = hi + s_pn + xn;
 #pragma unroll
     for (int j = 0; j < KF; ++j) {
         if (j < k) {
@@ -319,11 +317,21 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_assign(
     }
 }
 
-__global__ __launch_bounds__(kSbBlock) void k_sb_relabel(const int32_t *__restrict__ hs,
-                                                         const int32_t *__restrict__ map,
-                                                         int32_t *__restrict__ esrc) {
-    const int e = hs[2] + blockIdx.x * kSbBlock + threadIdx.x;
-    if (e < hs[6]) esrc[e] = map[esrc[e]];
+// the last hop's edges relabelled; counts = {n_total, e_total, n_active, -}
+__global__ __launch_bounds__(kSbBlock) void k_sb_tail(const int32_t *__restrict__ state, int H,
+                                                      const int32_t *__restrict__ map,
+                                                      int32_t *__restrict__ esrc, int32_t *__restrict__ counts) {
+    const int i = blockIdx.x * kSbBlock + threadIdx.x;
+    if (H > 0) {
+        const int32_t *hl = state + 4 * (H - 1);
+        for (int e = hl[2] + i; e < hl[6]; e += gridDim.x * kSbBlock) esrc[e] = map[esrc[e]];
+    }
+    if (i == 0) {
+        counts[0] = state[4 * H + 1];
+        counts[1] = state[4 * H + 2];
+        counts[2] = state[4 * (H > 0 ? H - 1 : 0) + 1];
+        counts[3] = 0;
+    }
 }
 
 // outputs + map reset: n_id (int64), y = y_all[n_id], edge_index [2, E]
@@ -362,6 +370,41 @@ __global__ __launch_bounds__(kSbBlock) void k_gather_rows4(const float *__restri
     }
 }
 
+// the block's outputs in ONE launch (round 6): blocks [0, gx) gather x rows
+// (k_gather_rows4's work), the rest k_sb_finish's (ids, labels, edges, map
+// reset -- the gather reads nid only, so the two roles need no order)
+__global__ __launch_bounds__(kSbBlock) void k_sb_out(const float *__restrict__ x_all, int64_t ldx,
+                                                     const int32_t *__restrict__ nid, int n, int f4,
+                                                     float *__restrict__ x, int64_t ldo, int gx,
+                                                     const int32_t *__restrict__ esrc, const int32_t *__restrict__ edst,
+                                                     int E, int32_t *__restrict__ map, int64_t n_graph,
+                                                     int64_t *__restrict__ n_id, const int64_t *__restrict__ y_all,
+                                                     int64_t *__restrict__ y, int64_t *__restrict__ ei) {
+    if (static_cast<int>(blockIdx.x) < gx) {
+        const int total = n * f4;
+        for (int t = blockIdx.x * kSbBlock + threadIdx.x; t < total; t += gx * kSbBlock) {
+            const int r = t / f4, c = (t - r * f4) * 4;
+            *reinterpret_cast<float4 *>(x + static_cast<int64_t>(r) * ldo + c) =
+                *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(nid[r]) * ldx + c);
+        }
+        return;
+    }
+    const int64_t stride = static_cast<int64_t>(gridDim.x - gx) * kSbBlock;
+    for (int64_t t = (blockIdx.x - gx) * static_cast<int64_t>(kSbBlock) + threadIdx.x; t < max(n, E); t += stride) {
+        if (t < n) {
+            const int32_t u = nid[t];
+            n_id[t] = u;
+            if (y) y[t] = y_all[u];
+            map[u] = -1;
+            map[n_graph + u] = -1;
+        }
+        if (t < E) {
+            ei[t] = esrc[t];
+            ei[E + t] = edst[t];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kSbBlock) void k_gather_rows1(const float *__restrict__ x_all,
                                                            int64_t ldx, const int32_t *__restrict__ nid,
                                                            int64_t n, int64_t F,
@@ -370,15 +413,6 @@ __global__ __launch_bounds__(kSbBlock) void k_gather_rows1(const float *__restri
     for (int64_t t = blockIdx.x * (int64_t)kSbBlock + threadIdx.x; t < n * F; t += stride) {
         const int64_t r = t / F, c = t - r * F;
         x[r * ldo + c] = x_all[nid[r] * ldx + c];
-    }
-}
-
-__global__ void k_sb_counts(const int32_t *__restrict__ state, int H, int32_t *__restrict__ counts) {
-    if (threadIdx.x == 0) {
-        counts[0] = state[4 * H + 1];
-        counts[1] = state[4 * H + 2];
-        counts[2] = state[4 * (H > 0 ? H - 1 : 0) + 1];
-        counts[3] = 0;
     }
 }
 
@@ -418,7 +452,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
     p->off_state = take(4 * (H + 1));
     p->off_cand = take(static_cast<size_t>(std::max<int64_t>(cand, 1)));
     p->off_cnt = take(static_cast<size_t>(std::max<int64_t>(cntn, 1)));
-    p->off_bsum = take(static_cast<size_t>(2 * nblk));
+    p->off_bsum = take(static_cast<size_t>(2 * (nblk + 1)));
     p->off_nid = take(static_cast<size_t>(n));
     p->off_esrc = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
     p->off_edst = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
@@ -429,7 +463,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
 SbWs sb_carve(void *ws, const SbPlan &p) {
     char *b = static_cast<char *>(ws);
     return SbWs{reinterpret_cast<int32_t *>(b + p.off_state), reinterpret_cast<int32_t *>(b + p.off_cand),
-                reinterpret_cast<int32_t *>(b + p.off_cnt), reinterpret_cast<int32_t *>(b + p.off_bsum),
+                reinterpret_cast<int32_t *>(b + p.off_cnt), reinterpret_cast<uint64_t *>(b + p.off_bsum),
                 reinterpret_cast<int32_t *>(b + p.off_nid), reinterpret_cast<int32_t *>(b + p.off_esrc),
                 reinterpret_cast<int32_t *>(b + p.off_edst)};
 }
@@ -484,42 +518,26 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
         int32_t *cand = w.cand + p.cand_off[h], *cnt = w.cnt + p.cnt_off[h];
         // the per-hop seed of ngnn_sample_hop's callers (loader.sample_block)
         const uint64_t hseed = seed * 1000003ull + static_cast<uint64_t>(h);
-        if (f > 0) {
-            auto sample = [&](auto kf_c) {
-                constexpr int KF = decltype(kf_c)::value;
-                hipLaunchKernelGGL(k_sb_sample<KF>, dim3(nblk), dim3(kSbBlock), 0, st, g_rowptr, g_col,
-                                   n_graph, hs, w.nid, f, hseed, cand, cnt, node_map);
-                hipLaunchKernelGGL(k_sb_count<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt,
-                                   node_map, n_graph, f, w.bsum, nblk);
-            };
-            switch (kf) {
-                case 8: sample(std::integral_constant<int, 8>{}); break;
-                case 16: sample(std::integral_constant<int, 16>{}); break;
-                case 32: sample(std::integral_constant<int, 32>{}); break;
-                default: sample(std::integral_constant<int, 64>{}); break;
-            }
-        } else {
-            (void)hipMemsetAsync(w.bsum, 0, 2 * nblk * sizeof(int32_t), st);
-        }
-        hipLaunchKernelGGL(k_sb_scan, dim3(1), dim3(1024), 0, st, hs, w.bsum, nblk);
-        if (f > 0) {
-            auto assign = [&](auto kf_c) {
-                constexpr int KF = decltype(kf_c)::value;
-                hipLaunchKernelGGL(k_sb_assign<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt,
-                                   node_map, n_graph, f, w.bsum, nblk, w.nid, w.esrc, w.edst);
-            };
-            switch (kf) {
-                case 8: assign(std::integral_constant<int, 8>{}); break;
-                case 16: assign(std::integral_constant<int, 16>{}); break;
-                case 32: assign(std::integral_constant<int, 32>{}); break;
-                default: assign(std::integral_constant<int, 64>{}); break;
-            }
-            hipLaunchKernelGGL(k_sb_relabel, dim3(std::max<int64_t>(1, ceil_div(nf * f, kSbBlock))),
-                               dim3(kSbBlock), 0, st, hs, node_map, w.esrc);
+        // two launches per hop (round 6; five before): draws + claims (+ the
+        // previous hop's relabel), then the look-back relabelling
+        auto hop = [&](auto kf_c) {
+            constexpr int KF = decltype(kf_c)::value;
+            hipLaunchKernelGGL(k_sb_sample<KF>, dim3(nblk), dim3(kSbBlock), 0, st, g_rowptr, g_col, n_graph, hs, w.nid,
+                               f, hseed, cand, cnt, node_map, h > 0 ? hs - 4 : nullptr, w.esrc, w.lb, nblk);
+            hipLaunchKernelGGL(k_sb_assign_lb<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt, node_map,
+                               n_graph, f, w.lb, nblk, w.nid, w.esrc, w.edst);
+        };
+        switch (kf) {
+            case 8: hop(std::integral_constant<int, 8>{}); break;
+            case 16: hop(std::integral_constant<int, 16>{}); break;
+            case 32: hop(std::integral_constant<int, 32>{}); break;
+            default: hop(std::integral_constant<int, 64>{}); break;
         }
     }
-    // counts = {n_total, e_total, n_active (rows that received edges), -}
-    hipLaunchKernelGGL(k_sb_counts, dim3(1), dim3(64), 0, st, w.state, n_hops, counts);
+    // the last hop's relabel + counts = {n_total, e_total, n_active (rows that received edges), -}
+    const int64_t e_last = n_hops > 0 ? p.nf_cap[n_hops - 1] * fanouts[n_hops - 1] : 0;
+    hipLaunchKernelGGL(k_sb_tail, dim3(static_cast<unsigned>(std::clamp<int64_t>(ceil_div(e_last, kSbBlock), 1, 4096))),
+                       dim3(kSbBlock), 0, st, w.state, n_hops, node_map, w.esrc, counts);
     return launch_status();
 }
 
@@ -540,9 +558,17 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
     hipStream_t st = as_stream(stream);
     const SbWs w = sb_carve(const_cast<void *>(ws), p);
     const int64_t work = std::max<int64_t>(std::max<int64_t>(n_nodes, n_edges), 1);
+    const unsigned gf = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, kSbBlock), 4096));
+    const bool vec = x && n_nodes > 0 && F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&
+                     aligned(x, 16) && n_nodes * (F / 4) < INT32_MAX;
+    if (vec) {  // the gather and the outputs in one launch
+        const int gx = static_cast<int>(std::min<int64_t>(ceil_div(n_nodes * (F / 4), kSbBlock), 4096));
+        hipLaunchKernelGGL(k_sb_out, dim3(gx + gf), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
+                           static_cast<int>(n_nodes), static_cast<int>(F / 4), x, ldo, gx, w.esrc, w.edst,
+                           static_cast<int>(n_edges), node_map, n_graph, n_id, y_all, y, edge_index);
+        return launch_status();
+    }
     if (x && n_nodes > 0) {  // gather before the map reset (order irrelevant: reads nid only)
-        const bool vec = F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&
-                         aligned(x, 16) && n_nodes * (F / 4) < INT32_MAX;
         const int64_t items = vec ? n_nodes * (F / 4) : n_nodes * F;
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(items, kSbBlock), 65536));
         if (vec)
@@ -553,9 +579,7 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
             hipLaunchKernelGGL(k_gather_rows1, dim3(grid), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
                                n_nodes, F, x, ldo);
     }
-    hipLaunchKernelGGL(k_sb_finish,
-                       dim3(static_cast<unsigned>(std::min<int64_t>(ceil_div(work, kSbBlock), 4096))),
-                       dim3(kSbBlock), 0, st, w.nid, static_cast<int>(n_nodes), w.esrc, w.edst,
+    hipLaunchKernelGGL(k_sb_finish, dim3(gf), dim3(kSbBlock), 0, st, w.nid, static_cast<int>(n_nodes), w.esrc, w.edst,
                        static_cast<int>(n_edges), node_map, n_graph, n_id, y_all, y, edge_index);
     return launch_status();
 }

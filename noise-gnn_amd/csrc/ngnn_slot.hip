@@ -23,6 +23,10 @@
 namespace ngnn {
 namespace {
 
+// a source id as the consumers may read it: ids outside [0, N) (flagged
+// NGNN_SLOT_RANGE) become row 0 (N >= 1 whenever there are edges to read)
+__device__ __forceinline__ int64_t src_ok(int64_t s, int64_t N) { return (s >= 0 && s < N) ? s : 0; }
+
 __global__ __launch_bounds__(256) void k_slot_load(
     const float *__restrict__ x, int64_t ldx, int64_t N, int64_t F, const int64_t *__restrict__ ei,
     int64_t ld_ei, int64_t E, const int64_t *__restrict__ y, int64_t B, float *__restrict__ sx,
@@ -63,6 +67,10 @@ __global__ __launch_bounds__(256) void k_slot_load(
             d = ei[ld_ei + e];
             if (s < 0 || s >= N || d < 0 || d >= N) bad |= NGNN_SLOT_RANGE;
             if (e > 0 && d < ei[ld_ei + e - 1]) bad |= NGNN_SLOT_UNSORTED;
+            // (a contract-breaking block is trained on a wrong CSR, but never
+            // out of bounds: a source outside [0, N) is read as row 0 by
+            // every consumer -- gathers, scatters, the bounds below)
+            s = src_ok(s, N);
         } else {
             d = N + ((e - E) * span) / n_pad;
             s = d;
@@ -103,7 +111,7 @@ __global__ __launch_bounds__(256) void k_slot_load(
             rowptr[r] = static_cast<int32_t>(r == n_cap ? e_cap : e);
         }
         for (int64_t e = tid; e < e_cap; e += nthr)
-            col[e] = static_cast<int32_t>(e < E ? ei[e] : N + ((e - E) * span) / n_pad);
+            col[e] = static_cast<int32_t>(e < E ? src_ok(ei[e], N) : N + ((e - E) * span) / n_pad);
     }
     if (colx) {
         // layer 0's gather columns: the sources' rows in the feature table
@@ -118,9 +126,12 @@ __global__ __launch_bounds__(256) void k_slot_load(
         // read its low 32 bits
         const uint64_t g = static_cast<uint64_t>(gen) << 32;
         uint64_t m = tid == 0 ? (g | static_cast<uint64_t>(B)) : 0;
+        // (every edge looked at -- E <= the grid's threads on every NeighborLoader
+        // block, so this is one edge per thread -- and no early exit: an
+        // unsorted block still gets the bound of the edges it has)
         for (int64_t e = tid; e < E; e += nthr) {
-            if (ei[ld_ei + e] >= B) break;  // targets sorted: the rest are >= B too
-            m = max(m, g | static_cast<uint64_t>(ei[e] + 1));
+            const int64_t d = ei[ld_ei + e];
+            if (d >= 0 && d < B) m = max(m, g | static_cast<uint64_t>(src_ok(ei[e], N) + 1));
         }
         // one atomic per wave (same-address atomics serialise)
 #pragma unroll
@@ -180,7 +191,7 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
     NGNN_RETURN_IF(xrow && (!x_dev || !xrow_dev), NGNN_E_ARG);  // indexed rows are zero-copy only
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
                    NGNN_E_ARG);
-    NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E, NGNN_E_SHAPE);
+    NGNN_RETURN_IF(ldx < F || ld_slot < F || ld_ei < E || (E > 0 && N == 0), NGNN_E_SHAPE);
     // padding needs rows to land on: at least one row past N when edges are padded
     NGNN_RETURN_IF(N > n_cap || E > e_cap || (E < e_cap && N >= n_cap), NGNN_E_SHAPE);
     NGNN_RETURN_IF(!fits_i32(N) || !fits_i32(n_cap) || !fits_i32(e_cap), NGNN_E_RANGE);

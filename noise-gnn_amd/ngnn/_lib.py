@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 OK = 0
 SLOT_UNSORTED = 1  # ngnn_slot_load's err bits (include/ngnn.h NGNN_SLOT_*)
@@ -76,6 +76,7 @@ SIGNATURES = {
                                  _p, _i64, _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p,
                                  _sz, _p]),
     "ngnn_cast_tensors": (_int, [_int, _p, _p, _p, _int, _p]),
+    "ngnn_cast_tensors_ex": (_int, [_int, _p, _p, _p, _p, _p, ctypes.c_float, _p]),
     "ngnn_sage2_bwd_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "ngnn_sage2_bwd": (_int, [_p, _i64, _i64, _p, _p, _i64, _p, _i64, ctypes.c_float, _p, _p, _p, _p, _i64, _i64,
                               _i64, _p, _i64, _p, _p, _i64, _p, _p, _int, _p, _p, _p, _p, _p, _p, _p, _p,

@@ -18,6 +18,36 @@ import torch
 import torch.distributed as dist
 
 
+_DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1}  # include/ngnn.h NGNN_F32 / NGNN_BF16
+
+
+def cast_tensors(src, dst, divisor: float = 1.0) -> None:
+    """dst[k] = cast(src[k]) / divisor for fp32 / bf16 tensors, 16 per
+    ngnn_cast_tensors_ex launch (the bucket's copies and div_ in one
+    kernel).  Tensors of other dtypes or layouts take the ATen path."""
+    import ctypes
+
+    from . import _lib
+    ok = [i for i, (a, b) in enumerate(zip(src, dst))
+          if a.dtype in _DTYPE_CODE and b.dtype in _DTYPE_CODE and a.is_contiguous()
+          and b.is_contiguous() and a.numel() == b.numel() and a.is_cuda and b.is_cuda]
+    rest = [i for i in range(len(src)) if i not in set(ok)]
+    for i in rest:  # (not on any path ngnn's models take)
+        dst[i].copy_(src[i] / divisor if divisor != 1.0 else src[i])
+    lib = _lib.load() if ok else None
+    for j in range(0, len(ok), 16):
+        idx = ok[j:j + 16]
+        k = len(idx)
+        S = (ctypes.c_void_p * k)(*[src[i].data_ptr() for i in idx])
+        D = (ctypes.c_void_p * k)(*[dst[i].data_ptr() for i in idx])
+        N = (ctypes.c_int64 * k)(*[src[i].numel() for i in idx])
+        SD = (ctypes.c_int32 * k)(*[_DTYPE_CODE[src[i].dtype] for i in idx])
+        DD = (ctypes.c_int32 * k)(*[_DTYPE_CODE[dst[i].dtype] for i in idx])
+        _lib.check(lib.ngnn_cast_tensors_ex(k, S, D, N, SD, DD, float(divisor),
+                                            _lib.stream_handle(src[idx[0]].device)),
+                   "ngnn_cast_tensors_ex")
+
+
 def env_world():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,12 +136,11 @@ class GradAllReduce:
         return p.grad is not None and p.grad.data_ptr() == v.data_ptr()
 
     def pack(self):
-        """grads -> bucket (stream-ordered copies, none for gradients that are
+        """grads -> bucket (stream-ordered, none for gradients that are
         already bucket views; capturable in a HIP graph).  Gradients that are
         not views -- a bf16 model's (autograd narrows the fused backward's
         fp32 gradients to the parameters' dtype), or accumulated ones -- move
-        in ONE multi-tensor copy (torch._foreach_copy_, widening bf16 exactly)
-        instead of a launch per tensor."""
+        in ONE library launch (ngnn_cast_tensors_ex: bf16 widened exactly)."""
         dst, src = [], []
         for p, v in zip(self.params, self.views):
             if p.grad is None:
@@ -120,26 +149,25 @@ class GradAllReduce:
                 dst.append(v)
                 src.append(p.grad)
         if dst:
-            torch._foreach_copy_(dst, src)
+            cast_tensors(src, dst)
 
     def allreduce(self):
         """The one collective: SUM over ranks (RCCL over xGMI with nccl)."""
         dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM, group=self.group)
 
     def unpack(self):
-        """bucket / world -> grads (capturable; one multi-tensor copy back,
-        rounding to bf16 where the parameter is bf16)."""
+        """bucket / world -> grads in ONE library launch (capturable): in
+        place for the gradients that are bucket views, rounded to bf16 into
+        a bf16 parameter's gradient (ngnn_cast_tensors_ex; the division is
+        Tensor.div_'s quotient)."""
         world = dist.get_world_size(self.group)
-        self.bucket.div_(world)
         dst, src = [], []
         for p, v in zip(self.params, self.views):
             if p.grad is None:
-                p.grad = v if p.dtype == v.dtype else v.to(p.dtype)
-            elif not self._aliased(p, v):
-                dst.append(p.grad)
-                src.append(v)
-        if dst:
-            torch._foreach_copy_(dst, src)
+                p.grad = v if p.dtype == v.dtype else torch.empty(p.shape, dtype=p.dtype, device=p.device)
+            dst.append(p.grad)
+            src.append(v)
+        cast_tensors(src, dst, divisor=float(world))
 
     def __call__(self):
         if not self.active():

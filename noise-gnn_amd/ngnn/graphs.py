@@ -180,7 +180,14 @@ class GraphedTrainStep:
 
     def check_inputs(self) -> None:
         """Synchronize and raise if any batch loaded so far broke the slot's
-        contract (load() reports such a batch at the next load without a sync)."""
+        contract (load() reports such a batch at the next load without a sync).
+
+        A contract-breaking batch (targets not sorted, ids outside [0, N)) is
+        only detected on the device: its replay has already run -- on a wrong
+        CSR, never out of bounds (the slot kernel stores bad sources as row 0)
+        -- and its optimizer step has been applied to the parameters by the
+        time it is reported.  Call this where a training loop ends (the last
+        batch is otherwise never reported)."""
         torch.cuda.synchronize(self.x.device)
         self._raise_if_bad()
 
@@ -193,7 +200,12 @@ class GraphedTrainStep:
 
     def _fwd_bwd(self):
         out = self.model(self.x, self.ei)
-        self.out = out  # the captured step's logits (static: rewritten by every replay)
+        # the captured step's logits (static: rewritten by every replay);
+        # detached -- holding the warm-up's autograd graph would keep its
+        # AccumulateGrad nodes (made on the warm-up stream) alive into the
+        # capture: torch's stream-mismatch warning and an event wait per
+        # parameter inside the captured backward
+        self.out = out.detach()
         loss = self.loss_fn(out, self.y, self.B)
         # a persistent d(loss) = 1 instead of backward()'s ones_like fill
         # launch; marked, so the loss backward needs no scale launch either
@@ -299,6 +311,12 @@ class GraphedTrainStep:
         finally:
             _fused._adam_fold = None
         self.folded = fold is not None and fold.used
+        # the replay needs no autograd nodes: holding the captured loss /
+        # logits with their graph would keep the capture's AccumulateGrad
+        # nodes (made on the capture stream) alive into later eager steps of
+        # the same model -- torch's "AccumulateGrad node's stream does not
+        # match" warning and an event wait per parameter there
+        self.loss = self.loss.detach()
         self.g_opt = None
         if not self.folded:
             self.g_opt = torch.cuda.CUDAGraph()
@@ -360,7 +378,20 @@ def _prepack_target(model):
     # tail holds the kernel's prebuilt root image) -- the buffer IS the
     # captured forward's workspace
     from . import _lib
+    from . import fused
     Fo, K = w.shape
+    lib = _lib.load()
+    # layers that never read a pack: the two-layer kernels load
+    # their weight slices themselves, the wide path splits W in its own
+    # launch -- no pack job in their slot loads
+    agg = getattr(model.convs[0], "aggr", "mean")
+    c1 = model.convs[-1].lin_l.weight
+    if (len(model.convs) == 2 and agg in ("mean", "sum") and c1.dtype == torch.float32
+            and fused._use_fwd2 and not fused._exact_f32
+            and lib.ngnn_sage2_supported(K, Fo, c1.shape[0], _lib.REDUCE[agg])):
+        return None
+    if lib.ngnn_sage_wide_preferred(K, Fo, int(fused._exact_f32)):
+        return None
     n = max(pack_weight(w.detach()).numel(),
             -(-_lib.load().ngnn_sage_fwd_raw_workspace_bytes(K, Fo, 0) // 4) + 16)
     return (w, torch.zeros(n, dtype=torch.float32, device=w.device), PackState())
@@ -389,3 +420,157 @@ def slot_size(batch_size: int, fanouts, margin_rows: int = 1024):
         frontier *= int(k)
         e_cap += frontier
     return int(batch_size) + e_cap + margin_rows, e_cap
+
+
+class GraphedCoTeachingStep(GraphedTrainStep):
+    """The co-teaching training loop body (pipeline.py:95-142, ``train_ct``,
+    run by ``config_products.yml`` / ``config_amazon.yml``: ``algo_type:
+    'coteaching'``) as ONE HIP-graph replay per batch: both models' forwards
+    over the slot's block, ``CTLoss`` on their seed rows (per-row cross
+    entropies, both argsorts, the exchange selection, the pure ratios --
+    ngnn.losses.CTLoss on the device, no host sync), ``loss_1.backward()``,
+    ``loss_2.backward()`` and both optimizers' steps.
+
+        step = GraphedCoTeachingStep(model1, opt1, model2, opt2, CTLoss(dev), B, n_cap, e_cap, F,
+                                     dev, noise_or_not)
+        loss_1, loss_2, pure_ratio_1, pure_ratio_2, _, _, _, _ = step(
+            batch.x, batch.edge_index, batch.yhn, batch.n_id, rate_schedule[epoch])
+
+    Returns CTLoss's 8-tuple as device tensors (rewritten by the next replay).  The forget rate
+    fixes ``num_remember = int((1 - rate) B)`` (losses.py:29-30), a launch
+    argument: one graph per distinct value, captured on first use (the
+    reference's schedule has a handful).  The two models draw independent
+    dropout masks from the slot seed (``_ngnn_graph_salt``).  A block short
+    of the captured batch size (an epoch's last, drop_last off) runs the
+    same loop body eagerly, as the reference does (num_remember of its own
+    size).  Optimizers: capturable (ngnn.optim.Adam); no Adam fold (two
+    models)."""
+
+    def __init__(self, model1, optimizer1, model2, optimizer2, criterion, batch_size: int, n_cap: int,
+                 e_cap: int, in_dim: int, device, noise_or_not=None, warmup: int = 3):
+        super().__init__(model1, optimizer1, batch_size, n_cap, e_cap, in_dim, device, warmup=warmup)
+        if not optimizer2.defaults.get("capturable", False):
+            raise ValueError("GraphedCoTeachingStep needs optimizers built with capturable=True")
+        self.model2, self.opt2, self.criterion = model2, optimizer2, criterion
+        if getattr(model2, "_ngnn_graph_salt", 0) == getattr(model1, "_ngnn_graph_salt", 0):
+            model2._ngnn_graph_salt = 0x5DEECE66D  # (independent of model 1's masks)
+        dev = torch.device(device)
+        self.noise_or_not = None if noise_or_not is None else noise_or_not.to(dev, torch.bool)
+        self.ind = torch.zeros(self.B, dtype=torch.int64, device=dev)  # n_id[:B] of the loaded block
+        self._graphs: dict = {}  # num_remember -> (graph, CTLoss's 8 outputs)
+
+    def num_remember(self, forget_rate: float, B: int | None = None) -> int:
+        return int((1 - forget_rate) * (self.B if B is None else B))
+
+    def _ct_fwd_bwd(self, forget_rate):
+        out1 = self.model(self.x, self.ei)
+        out2 = self.model2(self.x, self.ei)
+        res = self.criterion(out1, out2, self.y, forget_rate, self.ind, self.noise_or_not, batch_size=self.B)
+        if self._one is None:
+            from .losses import unit_grad
+            self._one = unit_grad(res[0])
+        res[0].backward(self._one)
+        res[1].backward(self._one)
+        return tuple(t.detach() if torch.is_tensor(t) else t for t in res)
+
+    def _load_ct(self, x, edge_index, y, n_id, zero_copy: bool) -> None:
+        self.load(x, edge_index, y, zero_copy=zero_copy)
+        self.ind.copy_(n_id[:self.B])
+
+    def capture(self, x, edge_index, y, n_id=None, forget_rate: float = 0.0, restore: bool = True) -> None:
+        """Warm up and capture the graph of num_remember(forget_rate) on this
+        block (restore=True: both models and optimizers back to their state
+        before the warm-up)."""
+        from . import fused as _fused
+        from .fused import const_bounds, reserve_sage2_bwd, zero_copy_ok
+        models, opts = (self.model, self.model2), (self.opt, self.opt2)
+        snap = None
+        if restore:
+            snap = [([p.detach().clone() for p in m.parameters()],
+                     {k: {n: (t.clone() if torch.is_tensor(t) else t) for n, t in v.items()}
+                      for k, v in o.state.items()}) for m, o in zip(models, opts)]
+        n_id = torch.arange(self.B, device=self.ind.device) if n_id is None else n_id
+        self._load_ct(x, edge_index, y, n_id, zero_copy=False)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):
+                for o in opts:
+                    o.zero_grad(set_to_none=True)
+                self._ct_fwd_bwd(forget_rate)
+                for o in opts:
+                    o.step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        block_cache.clear()
+        self.zero_copy = all(zero_copy_ok(m, self.n_cap, self.x.size(1)) for m in models)
+        self.x_rows = 0
+        self._pack = None  # (each model packs its own weights inside the graph)
+        self._head = None
+        hint_edge_index(self.ei, dst_sorted=True, src_sorted=False, n_rows_dev=self.n_valid,
+                        csr=CSR(self.rowptr, self.col, self.n_cap), seed_dev=self.seed_state,
+                        x_dev=self.x_dev if self.zero_copy else None, r_next=(self.r_next, self.B, True),
+                        n_edge_rows_dev=self.n_edge_rows)
+        for o in opts:
+            o.zero_grad(set_to_none=True)
+        for m in models:
+            convs = getattr(m, "convs", None)
+            if convs is not None:
+                const_bounds(self.x.device, len(convs), self.B)
+                if len(convs) == 2 and _lin_w(convs[0]) is not None and _lin_w(convs[1]) is not None:
+                    reserve_sage2_bwd(self.x.device, self.n_cap, _lin_w(convs[0]).shape[1],
+                                      _lin_w(convs[1]).shape[0])
+        g = torch.cuda.CUDAGraph()
+        pool = next(iter(self._graphs.values()))[0].pool() if self._graphs else None
+        _fused._adam_fold = None
+        with torch.cuda.graph(g, pool=pool):
+            outs = self._ct_fwd_bwd(forget_rate)
+            for o in opts:
+                o.step()
+        self._graphs[self.num_remember(forget_rate)] = (g, outs)
+        block_cache.clear()
+        torch.cuda.synchronize()
+        if snap is not None:
+            with torch.no_grad():
+                for (ps, st), m, o in zip(snap, models, opts):
+                    for p, v in zip(m.parameters(), ps):
+                        p.copy_(v)
+                    for k, cur in o.state.items():
+                        old = st.get(k)
+                        for n, t in cur.items():
+                            if not torch.is_tensor(t):
+                                continue
+                            if old is not None and torch.is_tensor(old.get(n)):
+                                t.copy_(old[n])
+                            else:
+                                t.zero_()
+
+    def __call__(self, x, edge_index, y, n_id, forget_rate: float = 0.0, batch_size: int | None = None):
+        """One co-teaching step on a block; returns CTLoss's 8-tuple (loss_1,
+        loss_2, pure_ratio_1, pure_ratio_2, ind_1_update, ind_2_update,
+        ind_noisy_1, ind_noisy_2; pipeline.py:116) as device tensors.  y: the
+        block's noisy labels (batch.yhn, whose first B rows the loss reads);
+        n_id: its global ids (CTLoss's ``ind``, for the pure ratios)."""
+        bs = self.B if batch_size is None else int(batch_size)
+        if bs < self.B:  # a short block: the same loop body, eagerly
+            return self._eager(x, edge_index, y, n_id, forget_rate, bs)
+        nr = self.num_remember(forget_rate)
+        if nr not in self._graphs:
+            self.capture(x, edge_index, y, n_id, forget_rate)
+        g, outs = self._graphs[nr]
+        self._load_ct(x, edge_index, y, n_id, zero_copy=self.zero_copy)
+        g.replay()
+        return outs
+
+    def _eager(self, x, edge_index, y, n_id, forget_rate, bs):
+        x = x.materialize() if isinstance(x, IndexedRows) else x
+        out1 = self.model(x, edge_index)
+        out2 = self.model2(x, edge_index)
+        res = self.criterion(out1, out2, y, forget_rate, n_id, self.noise_or_not, batch_size=bs)
+        for o in (self.opt, self.opt2):
+            o.zero_grad(set_to_none=False)
+        res[0].backward()
+        self.opt.step()
+        res[1].backward()
+        self.opt2.step()
+        return tuple(t.detach() if torch.is_tensor(t) else t for t in res)

@@ -227,15 +227,20 @@ def sample_hop(graph: Graph, frontier: torch.Tensor, fanout: int, seed: int):
     return out, cnt
 
 
-class _SamplerCache:
-    """Per-graph device state of ngnn_sample_block: the node map (int32
-    [2 N], all -1 between calls) and one workspace per (batch, fanouts)."""
+class _SamplerState:
+    """One set of ngnn_sample_block's device state: the node map (int32
+    [2 N], all -1 between blocks), one workspace per (batch, fanouts) and two
+    count slots (the loader reads batch b's counts while batch b + 1 is being
+    sampled into the other slot).  A set serves one block in flight at a
+    time: a NeighborLoader iterator leases one for its whole pass (it keeps
+    a block sampled ahead), so two live iterators never share a node map."""
 
     def __init__(self, n: int, device):
         self.node_map = torch.full((2 * n,), -1, dtype=torch.int32, device=device)
         self.ws: dict = {}
-        self.counts = torch.empty(4, dtype=torch.int32, device=device)
-        self.counts_host = torch.empty(4, dtype=torch.int32).pin_memory()
+        self.counts = torch.empty(2, 4, dtype=torch.int32, device=device)
+        self.counts_host = torch.empty(2, 4, dtype=torch.int32).pin_memory()
+        self.released = None  # event after the last launch of the previous lease
 
     def workspace(self, lib, batch: int, fan, n_hops: int) -> torch.Tensor:
         key = (batch, tuple(fan[:n_hops]))
@@ -250,6 +255,26 @@ class _SamplerCache:
         return buf
 
 
+class _SamplerCache:
+    """Per-graph pool of sampler state sets, leased on the current stream
+    (which first waits for the set's previous lease to finish on its own)."""
+
+    def __init__(self, n: int, device):
+        self.n, self.device = n, device
+        self.free: list = []
+
+    def acquire(self) -> _SamplerState:
+        st = self.free.pop() if self.free else _SamplerState(self.n, self.device)
+        if st.released is not None:
+            torch.cuda.current_stream(self.device).wait_event(st.released)
+        return st
+
+    def release(self, st: _SamplerState) -> None:
+        st.released = torch.cuda.Event()
+        st.released.record(torch.cuda.current_stream(self.device))
+        self.free.append(st)
+
+
 _sampler_caches: dict = {}
 
 
@@ -262,12 +287,18 @@ def _sampler_cache(graph: Graph) -> _SamplerCache:
     return c
 
 
-def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
-                 gather_features: bool = True) -> Batch:
-    """One NeighborLoader mini-batch (pipeline.py:152-160 contract) sampled,
-    relabelled and gathered on the device by ngnn_sample_block (+ _finish):
-    about a dozen launches and ONE device->host read (the block's node and
-    edge counts, needed to size the outputs).  Seeds must be distinct."""
+class _Pending:
+    """A block whose sampling kernels are enqueued (ngnn_sample_block) and
+    whose counts are on their way to pinned host memory (``event``)."""
+
+    __slots__ = ("graph", "state", "ws", "fan", "H", "B", "slot", "event", "gather_features", "seeds")
+
+
+def _sample_start(graph: Graph, seeds: torch.Tensor, fanouts, seed: int, gather_features: bool,
+                  state: _SamplerState, slot: int = 0) -> _Pending:
+    """Enqueue the sampling of one block on the current stream: every hop,
+    the relabelling and the edge list (ngnn_sample_block), then an async
+    copy of its (node, edge, active-row) counts into count slot `slot`."""
     import ctypes
     lib = _lib.load()
     dev = seeds.device
@@ -280,19 +311,47 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
                             or (graph.x.dtype == torch.bfloat16 and graph.x.size(1) % 2)):
         raise TypeError("graph.x must be a row-major float32 matrix (or bf16 with an even width)")
     s64 = seeds.to(torch.int64).contiguous()
-    B = s64.numel()
-    fan = (ctypes.c_int32 * max(len(fanouts), 1))(*[int(k) for k in fanouts])
-    H = len(fanouts)
-    cache = _sampler_cache(graph)
-    ws = cache.workspace(lib, B, fan, H)
-    st = _lib.stream_handle(dev)
+    p = _Pending()
+    p.graph, p.B, p.H, p.slot, p.gather_features, p.seeds = graph, s64.numel(), len(fanouts), slot, gather_features, s64
+    p.fan = (ctypes.c_int32 * max(len(fanouts), 1))(*[int(k) for k in fanouts])
+    p.state = state
+    p.ws = state.workspace(lib, p.B, p.fan, p.H)
     _lib.check(lib.ngnn_sample_block(
-        _lib.ptr(graph.rowptr), _lib.ptr(graph.col), graph.num_nodes, _lib.ptr(s64), B, fan, H,
-        int(seed) & (2**64 - 1), _lib.ptr(cache.node_map), _lib.ptr(ws), ws.numel(),
-        _lib.ptr(cache.counts), st), "ngnn_sample_block")
-    cache.counts_host.copy_(cache.counts, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    n, e, n_active = (int(v) for v in cache.counts_host[:3])
+        _lib.ptr(graph.rowptr), _lib.ptr(graph.col), graph.num_nodes, _lib.ptr(s64), p.B, p.fan, p.H,
+        int(seed) & (2**64 - 1), _lib.ptr(state.node_map), _lib.ptr(p.ws), p.ws.numel(),
+        _lib.ptr(state.counts[slot]), _lib.stream_handle(dev)), "ngnn_sample_block")
+    state.counts_host[slot].copy_(state.counts[slot], non_blocking=True)
+    p.event = torch.cuda.Event()
+    p.event.record(torch.cuda.current_stream(dev))
+    return p
+
+
+def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
+                 gather_features: bool = True) -> Batch:
+    """One NeighborLoader mini-batch (pipeline.py:152-160 contract) sampled,
+    relabelled and gathered on the device by ngnn_sample_block (+ _finish):
+    about a dozen launches and ONE device->host read (the block's node and
+    edge counts, needed to size the outputs).  Seeds must be distinct.
+    (NeighborLoader reads those counts one batch late instead: no wait.)"""
+    cache = _sampler_cache(graph)
+    st = cache.acquire()
+    try:
+        return _sample_finish(_sample_start(graph, seeds, fanouts, seed, gather_features, st))
+    finally:
+        cache.release(st)
+
+
+def _sample_finish(p: _Pending) -> Batch:
+    """Wait for the block's counts (its sampling kernels only), then enqueue
+    the outputs on the current stream: n_id, edge_index, y, x = x_all[n_id]
+    (the finish launch, which also resets the sampler's node map)."""
+    lib = _lib.load()
+    graph, cache, ws, fan, H, B = p.graph, p.state, p.ws, p.fan, p.H, p.B
+    dev = p.seeds.device
+    st = _lib.stream_handle(dev)
+    gather_features = p.gather_features
+    p.event.synchronize()
+    n, e, n_active = (int(v) for v in cache.counts_host[p.slot, :3])
     n_id = torch.empty(n, dtype=torch.int64, device=dev)
     edge_index = torch.empty(2, e, dtype=torch.int64, device=dev)
     y = torch.empty(n, dtype=torch.int64, device=dev)
@@ -388,10 +447,15 @@ class NeighborLoader:
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
-        """Batches are sampled on a side stream: batch b+1 is built while the
-        consumer's step on batch b (already enqueued on the current stream
-        when the generator resumes) runs, so sampling overlaps training the
-        way the reference's worker process overlaps it (pipeline.py:81-82)."""
+        """Batches are sampled on a side stream, one batch AHEAD: when the
+        consumer asks for batch b, batch b's sampling kernels were enqueued
+        during the previous request, so the host waits only for those (never
+        for a training step in flight) to read b's sizes, enqueues b's output
+        launch and batch b + 1's sampling, and hands b over -- the main stream
+        waits for b's outputs alone.  Sampling overlaps training the way the
+        reference's worker process overlaps it (pipeline.py:81-82), with no
+        per-batch drain of the consumer's stream.  The per-batch seeds follow
+        the batch index, so the batches are those of one-at-a-time sampling."""
         seeds = self._seeds()
         ep = self.epoch
         self.epoch += 1
@@ -399,16 +463,42 @@ class NeighborLoader:
         main = torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(dev)
         side.wait_stream(main)  # seeds (randperm) were made on the main stream
-        for b in range(len(self)):
+        n = len(self)
+        cache = _sampler_cache(self.graph)
+        with torch.cuda.stream(side):
+            state = cache.acquire()  # this pass's node map / workspace / count slots
+
+        def start(b):
             s = seeds[b * self.batch_size:(b + 1) * self.batch_size]
             with torch.cuda.stream(side):
-                blk = sample_block(self.graph, s, self.num_neighbors,
-                                   seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size
-                                   + self.rank, gather_features=self.gather_features)
-                if not self.gather_features:
-                    blk.x = IndexedRows(self.graph.x, blk.n_id)
-            main.wait_stream(side)
-            for t in (blk.x, blk.y, blk.edge_index, blk.n_id, *blk.node_attrs.values()):
-                if t is not None:
-                    t.record_stream(main)  # consumed on the main stream
-            yield blk
+                return _sample_start(self.graph, s, self.num_neighbors,
+                                     seed=(self.seed * 7919 + ep) * 100_003 + b * self.world_size + self.rank,
+                                     gather_features=self.gather_features, state=state, slot=b & 1)
+
+        pending = None
+        try:
+            pending = start(0) if n else None
+            for b in range(n):
+                with torch.cuda.stream(side):
+                    blk = _sample_finish(pending)  # (waits for batch b's counts only)
+                    pending = None
+                    if not self.gather_features:
+                        blk.x = IndexedRows(self.graph.x, blk.n_id)
+                    ready = torch.cuda.Event()
+                    ready.record(side)
+                # the next block's sampling behind this one's outputs (the node
+                # map is reset by the finish launch, stream-ordered before it)
+                pending = start(b + 1) if b + 1 < n else None
+                main.wait_event(ready)
+                for t in (blk.x, blk.y, blk.edge_index, blk.n_id, *blk.node_attrs.values()):
+                    if t is not None:
+                        t.record_stream(main)  # consumed on the main stream
+                yield blk
+        finally:
+            # a pass left early (break, close, garbage collection) still holds
+            # a block sampled ahead: finish it, which resets the node map,
+            # before the state set goes back to the pool
+            with torch.cuda.stream(side):
+                if pending is not None:
+                    _sample_finish(pending)
+                cache.release(state)

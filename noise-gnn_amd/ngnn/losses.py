@@ -281,11 +281,15 @@ class _CTState:
 class _CTPick(torch.autograd.Function):
     """loss_m (already computed by the shared forward) as a differentiable
     function of y_m alone, so that loss_1.backward() and loss_2.backward()
-    each run only their own model's graph, as in pipeline.py:125-131."""
+    each run only their own model's graph, as in pipeline.py:125-131.
+    y_m may hold more rows than the loss reads (the whole block's logits,
+    CTLoss(..., batch_size=B)): its gradient is then a zero-row buffer whose
+    rows < B the backward launch writes (no slice backward), marked for the
+    SAGE stack's bounded backward."""
 
     @staticmethod
     def forward(ctx, y, state: _CTState, m: int):
-        ctx.state, ctx.m = state, m
+        ctx.state, ctx.m, ctx.n = state, m, y.size(0)
         ctx.save_for_backward(y)
         return state.out[m].clone()
 
@@ -293,12 +297,16 @@ class _CTPick(torch.autograd.Function):
     def backward(ctx, g):
         (y,) = ctx.saved_tensors
         st = ctx.state
-        dy = torch.empty(st.B, st.C, dtype=torch.float32, device=y.device)
+        if ctx.n > st.B:  # rows >= B never written: zero (one buffer per model)
+            dy = _grad_buffer(y.device, ctx.n, st.C, ("ct", ctx.m, st.B))
+        else:
+            dy = torch.empty(st.B, st.C, dtype=torch.float32, device=y.device)
         g = g.reshape(1).to(torch.float32).contiguous()
         _lib.check(_lib.load().ngnn_ct_loss_bwd(
             ctx.m, _lib.ptr(y), y.stride(0), st.B, st.C, _lib.ptr(st.y_noise), st.ignore,
             _lib.ptr(st.ws), _lib.ptr(g), _lib.ptr(dy), dy.stride(0),
             _lib.stream_handle(y.device)), "ngnn_ct_loss_bwd")
+        dy._ngnn_nonzero_rows = st.B
         return dy, None, None
 
 
@@ -328,13 +336,21 @@ class CTLoss(torch.nn.Module):
         # (the reference raises IndexError there; checking it needs a sync)
         self.index_error = None
 
-    def forward(self, y_1, y_2, y_noise, forget_rate, ind, noise_or_not):
+    def forward(self, y_1, y_2, y_noise, forget_rate, ind, noise_or_not, batch_size: int | None = None):
+        """batch_size (extension): y_1 / y_2 are a block's whole logits [N, C]
+        and the loss reads rows < batch_size -- the reference's
+        ``model(x, ei)[:batch_size]`` without the slice (pipeline.py:113-114);
+        each model's gradient then comes back [N, C], zero past the seeds."""
         if not (y_1.is_cuda and y_2.is_cuda):
             raise RuntimeError("ngnn.losses.CTLoss: GPU only (no CPU fallback)")
         if y_1.dim() != 2 or y_1.shape != y_2.shape or y_1.dtype != torch.float32 \
                 or y_2.dtype != torch.float32:
             raise ValueError("y_1, y_2 must be float32 [B, C] tensors of the same shape")
         B, C = y_1.shape
+        if batch_size is not None:
+            if not 0 < int(batch_size) <= B:
+                raise ValueError(f"batch_size {batch_size} outside (0, {B}]")
+            B = int(batch_size)
         dev = y_1.device
         remember_rate = 1 - forget_rate
         num_remember = int(remember_rate * B)  # losses.py:29-30, same float arithmetic
@@ -342,7 +358,11 @@ class CTLoss(torch.nn.Module):
             raise ValueError(f"forget_rate {forget_rate} gives num_remember {num_remember}")
         a = y_1 if y_1.stride(1) == 1 else y_1.contiguous()
         b = y_2 if y_2.stride(1) == 1 else y_2.contiguous()
-        yn = y_noise.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        yn = y_noise.to(device=dev, dtype=torch.int64).reshape(-1)
+        if batch_size is not None:  # (a block's labels / ids: the seed rows')
+            yn = yn[:B]
+            ind = None if ind is None else ind.reshape(-1)[:B]
+        yn = yn.contiguous()
         if yn.numel() != B:
             raise ValueError("y_noise must hold one label per row")
         idx = None if ind is None else ind.to(device=dev, dtype=torch.int64).contiguous()

@@ -30,7 +30,10 @@ def _dropout_seed(model, x, block):
         if torch.cuda.is_current_stream_capturing():
             # HIP-graph capture: a device seed, fresh at every replay -- the
             # slot's (advanced by each slot load), else drawn by torch's
-            # graph-safe generator inside the graph
+            # graph-safe generator inside the graph.  The host part is the
+            # model's graph salt (0 unless set: two models captured over one
+            # slot -- GraphedCoTeachingStep -- draw independent masks)
+            seed = int(getattr(model, "_ngnn_graph_salt", 0))
             seed_dev = block.seed_dev
             if seed_dev is None:
                 seed_dev = torch.randint(0, 2**62, (1,), device=x.device)

@@ -39,7 +39,11 @@ class Adam(torch.optim.Optimizer):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
-            pkey = tuple(p.data_ptr() for p in ps)
+            # (address, numel, dtype, contiguity) per parameter: a parameter
+            # replaced by one of another size or dtype that the caching
+            # allocator placed at the same address re-runs the checks and
+            # rebuilds the arrays
+            pkey = tuple((p.data_ptr(), p.numel(), p.dtype, p.is_contiguous()) for p in ps)
             cached = self._arrays.get(gi)
             if cached is None or cached[0][0] != pkey:
                 cached = None
@@ -76,7 +80,7 @@ class Adam(torch.optim.Optimizer):
             key = (pkey, tuple(st["exp_avg"].data_ptr() for st in sts),
                    tuple(st["exp_avg_sq"].data_ptr() for st in sts))
             if cached is None or cached[0] != key:
-                cached = (key, (ctypes.c_void_p * n)(*pkey),
+                cached = (key, (ctypes.c_void_p * n)(*[k[0] for k in pkey]),
                           (ctypes.c_void_p * n)(*key[1]), (ctypes.c_void_p * n)(*key[2]),
                           (ctypes.c_int64 * n)(*[p.numel() for p in ps]),
                           (ctypes.c_int32 * n)(*[_lib.BF16 if p.dtype == torch.bfloat16 else _lib.F32

@@ -211,3 +211,129 @@ def test_headline_model_data_parallel_two_ranks():
         assert worst <= 1e-5, worst
         # and the parameters = torch's Adam step on that mean (step 1: |dp| ~ lr)
         assert upd <= 2e-6, upd
+
+
+def _worker_config4(rank, world, port, q):
+    """BASELINE config #4's model -- SAGE(100, 256, 256,
+    47) in bf16, [20, 15, 10] bs 1024 (config #3's step) -- seed-sharded over
+    two ranks through GraphedTrainStep with the split reduce: the bf16
+    gradients move into the fp32 bucket and back (divided by the world) by
+    ngnn_cast_tensors_ex launches, never an ATen copy."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    try:
+        import datetime
+        import sys
+
+        import torch.nn.functional as F
+
+        import ngnn
+        from ngnn import distributed as ndist
+        from ngnn.distributed import GradAllReduce
+        from ngnn.graphs import GraphedTrainStep, slot_size
+        from ngnn.loader import NeighborLoader, synthetic_graph
+        from ngnn.optim import Adam
+        from oracle import pyg_ref
+        from test_gpu_configs import _hooked_capture, _oracle_rows, _slot_masks
+        from test_gpu_fused import dropout_scale
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=120))
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        graph = synthetic_graph("ogbn-products", dev, seed=0, scale=0.03)
+        graph.x = graph.x.to(torch.bfloat16)
+        loader = NeighborLoader(graph, graph.train_idx, [20, 15, 10], 1024, shuffle=True, seed=5,
+                                rank=rank, world_size=world)
+        it = iter(loader)
+        warm, b = next(it), next(it)
+        torch.manual_seed(4321)
+        model = ngnn.SAGE(100, 256, 47, 3, dropout=0.5).to(dev).to(torch.bfloat16).train()
+        init_sd = {k: v.detach().float().cpu().clone() for k, v in model.state_dict().items()}
+        opt = Adam(model.parameters(), lr=1e-3)
+        red = GradAllReduce(model.parameters())
+        calls = []
+        orig_cast, orig_copy = ndist.cast_tensors, torch._foreach_copy_
+
+        def spy(*a, **k):
+            calls.append(len(a[0]))
+            return orig_cast(*a, **k)
+
+        def no_aten(*a, **k):  # pragma: no cover - the assertion below reports it
+            raise AssertionError("torch._foreach_copy_ on the bucket path")
+
+        ndist.cast_tensors, torch._foreach_copy_ = spy, no_aten
+        try:
+            n_cap, e_cap = slot_size(1024, [20, 15, 10])
+            step = GraphedTrainStep(model, opt, 1024, n_cap, e_cap, 100, dev, reducer=red)
+            _hooked_capture(step, warm.x, warm.edge_index, warm.y)
+            assert step._split_reduce and not step.folded
+            step(b.x, b.edge_index, b.y, b.batch_size)
+            torch.cuda.synchronize()
+        finally:
+            ndist.cast_tensors, torch._foreach_copy_ = orig_cast, orig_copy
+        assert calls, "the bucket pack / unpack did not take ngnn_cast_tensors_ex"
+        print(f"[rank {rank}] stepped", file=sys.stderr, flush=True)
+        params = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]).cpu()
+        grads = {k: p.grad.detach().float().cpu().clone() for k, p in model.named_parameters()}
+        assert all(p.grad.dtype == torch.bfloat16 for p in model.parameters())
+        # this rank's gradient by the oracle (fp32, bf16 storage points), the
+        # replay's dropout masks rebuilt from the slot seed
+        seed_state = int(step.seed_state.item()) & (2**64 - 1)
+        N = b.num_nodes
+        masks = _slot_masks(seed_state, N, 256, 0.5, 3)
+        ref = pyg_ref.SAGE(100, 256, 47, 3, dropout=0.5)
+        ref.load_state_dict(init_sd)
+        out_r = _oracle_rows(ref, b.x.float().cpu(), b.edge_index.cpu(), torch.arange(b.batch_size), masks,
+                             dropout_scale(0.5), act_dtype=torch.bfloat16)
+        F.cross_entropy(out_r, b.y[:b.batch_size].cpu()).backward()
+        mine_local = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+        gathered = [torch.empty_like(mine_local) for _ in range(world)]
+        dist.all_gather(gathered, mine_local)
+        avg = torch.stack(gathered).mean(0)
+        pg = [torch.empty_like(params) for _ in range(world)]
+        dist.all_gather(pg, params)
+        same_ranks = all(torch.equal(pg[0], t) for t in pg)
+        off, worst, where = 0, 0.0, ""
+        for k, rp in ref.named_parameters():
+            n = rp.numel()
+            want = avg[off:off + n].view(rp.shape)
+            # config #3's bf16 bar (test_config_products_3layer_bf16_graph_step:
+            # |g - g_ref| <= 2e-2 max|g_ref| + 2e-2 |g_ref|) held by each rank's
+            # own gradient, so the mean of the ranks' gradients is held to the
+            # mean of their bars (the ranks' gradients partly cancel: a bar of
+            # the mean's own magnitude would be tighter than either rank's)
+            bar = sum(2e-2 * float(gr[off:off + n].abs().max()) + 2e-2 * gr[off:off + n].abs()
+                      for gr in gathered).view(rp.shape) / world
+            ratio = (grads[k] - want).abs() / bar.clamp_min(1e-30)
+            if float(ratio.max()) > worst:
+                i = int(ratio.argmax())
+                worst = float(ratio.max())
+                where = (f"{k}[{i}]: got {float(grads[k].flatten()[i]):.4g} want {float(want.flatten()[i]):.4g} "
+                         f"bar {float(bar.flatten()[i]):.3g}")
+            off += n
+        q.put((rank, same_ranks, (worst, where), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, False, (float("inf"), ""), traceback.format_exc()))
+
+
+@pytest.mark.timeout(400)
+def test_config4_bf16_3layer_data_parallel_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_config4, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, same, worst, err in out:
+        assert err is None, err
+        assert same, f"rank {rank}: parameters differ across ranks"
+        # the all-reduced bf16 .grad = the mean of the ranks' oracle gradients
+        # at the SURVEY 8(c) bf16 bar (the ratio to the bar: <= 1)
+        assert worst[0] <= 1.0, worst

@@ -440,6 +440,24 @@ def test_slot_contract_error_word():
     step(b.x, b.edge_index, b.y)
     step.check_inputs()
     assert torch.isfinite(step.loss).all()
+    # sources far outside the slot (past n_cap, negative) are
+    # flagged AND stored as row 0 -- no replayed gather or scatter leaves
+    # its buffer; the CSR columns stay in [0, N)
+    E = b.edge_index.shape[1]
+    for v in (n_cap + 10**6, -7):
+        far = b.edge_index.clone()
+        far[0, :: max(1, E // 17)] = v
+        step(b.x, far, b.y)
+        with pytest.raises(ValueError, match="outside"):
+            step.check_inputs()
+        col = step.col[:E].cpu()
+        assert int(col.min()) >= 0 and int(col.max()) < b.num_nodes
+        assert 0 < (int(step.r_next.item()) & 0xFFFFFFFF) <= b.num_nodes
+    step(b.x, b.edge_index, b.y)
+    step.check_inputs()
+    torch.cuda.synchronize()
+    assert torch.isfinite(step.loss).all()
+    assert all(torch.isfinite(p).all() for p in model.parameters())
 
 
 def test_replay_survives_workspace_growth():

@@ -135,7 +135,36 @@ def test_sample_block_matches_reference(graph, fanouts, bs):
         from ngnn.block import _hint_for
         assert _hint_for(b.edge_index)[2] == n_active
     # the node map is restored after every block
-    assert bool((_sampler_cache(graph).node_map == -1).all())
+    assert all(bool((st.node_map == -1).all()) for st in _sampler_cache(graph).free)
+
+
+def test_loader_pass_suspended_or_abandoned(graph):
+    """The loader samples one batch ahead (no host wait on the consumer's
+    stream).  A pass left suspended with a block in flight -- bench.py
+    pre-samples a few batches, then runs a whole epoch -- or abandoned must
+    not disturb another pass over the same graph: every pass leases its own
+    node map.  Every batch equals the synchronous sample_block of the same
+    seeds and seed; after the passes end, every node map is clean."""
+    from ngnn.distributed import shard_seeds
+    from ngnn.loader import _sampler_cache
+    ld = NeighborLoader(graph, graph.train_idx, [15, 10], batch_size=256, shuffle=True, seed=3)
+
+    def expect(ep, b):
+        s = shard_seeds(ld.input_nodes, 0, 1, ep, ld.seed, shuffle=True)[b * 256:(b + 1) * 256]
+        return sample_block(graph, s, [15, 10], seed=(ld.seed * 7919 + ep) * 100_003 + b)
+
+    it = iter(ld)  # epoch 0
+    got0 = [next(it) for _ in range(2)]  # suspended: batch 2 in flight
+    got1 = list(ld)  # epoch 1, a whole pass meanwhile
+    got0.append(next(it))
+    it.close()  # abandoned with batch 3 in flight
+    torch.cuda.synchronize()
+    for b, blk in enumerate(got0):
+        _assert_same_block(blk, expect(0, b))
+    assert len(got1) == len(ld)
+    for b in (0, 1, len(got1) - 1):
+        _assert_same_block(got1[b], expect(1, b))
+    assert all(bool((st.node_map == -1).all()) for st in _sampler_cache(graph).free)
 
 
 def test_sample_block_multigraph_and_isolated():
