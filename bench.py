@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=1024)
     ap.add_argument("--fanout", type=str, default="15,10")
     ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--num-layers", type=int, default=0,
+                    help="model layers (default: one per fanout hop; config_arxiv5.yml runs 3 layers "
+                         "over a [10,5] block -- every layer aggregates all of the block's edges)")
     ap.add_argument("--scale", type=float, default=1.0, help="graph size scale (tests)")
     ap.add_argument("--dataset", default="ogbn-products",
                     help="synthetic graph shape (ngnn.loader.DATASETS); the headline is ogbn-products")
@@ -462,7 +465,7 @@ def main():
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     fanout = [int(v) for v in args.fanout.split(",")]
-    layers = len(fanout)
+    layers = args.num_layers or len(fanout)
 
     from ngnn.loader import DATASETS
     _, _, F_in, C, _ = DATASETS[args.dataset]
@@ -512,6 +515,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    graph_data = graph  # (the name `graph` is the replay switch below)
     graph = not args.eager
     if ct is not None:
         from ngnn.graphs import GraphedCoTeachingStep, slot_size
@@ -578,6 +582,8 @@ def main():
         dt, edges = float(t[0]), float(t[1])
 
     workload = f"{args.dataset.replace('ogbn-', '')}-[{args.fanout}]-bs{args.batch_size}"
+    if layers != len(fanout):
+        workload += f"-L{layers}"
     if args.aggr != "mean" and args.module == "sage":
         workload += f"-{args.aggr}"
     if args.module == "gcn":
@@ -699,6 +705,28 @@ def main():
         epoch_s = time.perf_counter() - t1
         if graph and ct is None:
             gstep.check_inputs()  # (every batch of the epoch met the slot's contract)
+    # the same epoch with the fused x[n_id] gather (batches carry the feature
+    # table + n_id, the layer-0 kernels read the rows): no 61 MB row copy per
+    # batch in the sampler, a few us more in the step -- reported beside
+    epoch_fg = None
+    if not args.no_epoch and graph and ct is None and args.gather == "loader" and world == 1:
+        from ngnn.graphs import GraphedTrainStep, slot_size
+        loader_fg = NeighborLoader(graph_data, graph_data.train_idx, fanout, args.batch_size, shuffle=True,
+                                   seed=7, rank=rank, world_size=world, gather_features=False)
+        b0 = next(iter(loader_fg))
+        n_cap, e_cap = slot_size(args.batch_size, fanout)
+        gstep_fg = GraphedTrainStep(model, opt, args.batch_size, n_cap, e_cap, b0.x.size(1), dev, reducer=reducer)
+        gstep_fg.capture(b0.x, b0.edge_index, b0.y)
+        del b0
+        if gstep_fg.x_rows:  # (the step took the indexed rows: the fused gather ran)
+            barrier()
+            t1 = time.perf_counter()
+            for b in loader_fg:
+                gstep_fg(b.x, b.edge_index, b.y, b.batch_size)
+            barrier()
+            epoch_fg = time.perf_counter() - t1
+            gstep_fg.check_inputs()
+        del gstep_fg
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and ct is None:
@@ -734,6 +762,7 @@ def main():
             "feature_gather": ("fused x[n_id] in the layer-0 kernels" if args.gather == "fused"
                                and graph and gstep.x_rows else "loader copies x[n_id]"),
             "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
+            "epoch_time_s_fused_gather": None if epoch_fg is None else round(epoch_fg, 4),
             "epoch_batches_per_rank": len(loader),
             "allreduce": ar,
             "eager_drop_in": eager_ref,

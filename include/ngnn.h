@@ -190,7 +190,13 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
  *             and again after every finish (one map per stream at a time).
  *   ws:       ngnn_sample_block_workspace_bytes(batch, fanouts, n_hops);
  *             holds the block between the two calls.
- *   fanouts:  HOST int32[n_hops], each 0..64. */
+ *   fanouts:  HOST int32[n_hops], each 0..64.
+ * ABI 18: n_active (counts[2]) and, nullable as a pair, csr_rowptr
+ * int32[n_nodes + 1] / csr_col int32[n_edges]: the block's target-grouped
+ * CSR (edge order kept inside a row; col = the local sources), taken from the
+ * relabelling itself, so a consumer of the block builds none.  Since ABI 18
+ * the hops run as two launches each (draws + claims, then a single-pass
+ * decoupled look-back relabelling) and the outputs, x rows included, as one. */
 size_t ngnn_sample_block_workspace_bytes(int64_t batch, const int32_t *fanouts, int n_hops);
 int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, int64_t n_graph,
                       const int64_t *seeds, int64_t n_seeds, const int32_t *fanouts, int n_hops,
@@ -201,7 +207,7 @@ int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int64_t n_seeds
                              int64_t n_graph, const void *ws, size_t ws_bytes, int64_t *n_id,
                              int64_t *edge_index, const int64_t *y_all, int64_t *y,
                              const float *x_all, int64_t ldx, int64_t F, float *x, int64_t ldo,
-                             void *stream);
+                             int64_t n_active, int32_t *csr_rowptr, int32_t *csr_col, void *stream);
 
 /* ------------------------------------------------------ co-teaching loss
  * CTLoss.forward (src/utils/losses.py:19-49) without its two host argsorts:

@@ -160,7 +160,11 @@ __device__ __forceinline__ float sum_xor32(float v) {
 // LAG: a chunk's maxima published at the barrier that ends the previous chunk
 // (its loads waited for right after stage B) -- else after stage C, at a
 // barrier of their own (the loads keep stage C to land)
-template <bool XR, int KT, bool LAG>
+// ROOT false (ABI 18, dW_r0 = dW_r1 = NULL: a SimpleGCN stack, whose root
+// weights are zero): no x rows staged, no dW_r0 / dW_r1 products -- stage
+// C0's dW_l0 tiles split over all eight waves, stage C1's W_l1 tiles over
+// the eight, stage B skips the dy-only K chunk (its W_r1 rows are zero)
+template <bool XR, int KT, bool LAG, bool ROOT = true>
 __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     extern __shared__ __attribute__((aligned(16))) __bf16 lb_[];
     L16 *lb = (L16 *)(lb_);  // (an address-space cast: the shared array IS in LDS)
@@ -288,7 +292,8 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
             for (int u = 0; u < 2; ++u) {
                 const int k = 8 * cx + 4 * u;
                 const bool ok = okr && k < K0;
-                p.xv[u] = buf_load4(xrr, ok ? static_cast<int>(xr * ldx4) + 4 * k : kOOB, 0, 0);
+                if constexpr (ROOT) p.xv[u] = buf_load4(xrr, ok ? static_cast<int>(xr * ldx4) + 4 * k : kOOB, 0, 0);
+                else p.xv[u] = v4f{0.f, 0.f, 0.f, 0.f};
                 p.av[u] = buf_load4(ar, ok ? static_cast<int>(static_cast<uint32_t>(r) * lda4) + 4 * k : kOOB, 0, 0);
             }
             // (an edgeless row's aggregate counts as 0: its row may never be
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         }
         if (t < 384) put4(ix, B2_ROWS * XS, rg * XS + 48 + 4 * cg, p.gv, e.X);
         put4(ih, B2_ROWS * HS, rh * HS + 4 * ch, p.hv, e.H);
-        put8(ik, B2_ROWS * KS, rx * KS + 8 * cx, p.xv[0], p.xv[1], e.x);
+        if constexpr (ROOT) put8(ik, B2_ROWS * KS, rx * KS + 8 * cx, p.xv[0], p.xv[1], e.x);
         const bool deg = p.d1 > p.d0;
         const v4f z4{0.f, 0.f, 0.f, 0.f};
         put8(ia, B2_ROWS * KS, rx * KS + 8 * cx, deg ? p.av[0] : z4, deg ? p.av[1] : z4, e.a);
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         L16 *sa = buf + IMG_X + IMG_H + 2 * IMG_K;
         v4f acc{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kc = 0; kc < 3; ++kc) {
+        for (int kc = ROOT ? 0 : 1; kc < 3; ++kc) {
             const int off = (16 * rt + l16) * XS + 32 * kc + 8 * q;
             const bf8 a1 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(ix + off);
             const bf8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(ix + B2_ROWS * XS + off);
@@ -428,12 +433,21 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     };
 
     // ---- stage C: the weight-gradient products of one staged chunk
-    v4f acc0[KT], acc1[3];
-#pragma unroll
-    for (int i = 0; i < KT; ++i) acc0[i] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
+    // ROOT: wave (mat, nt) takes dW_r0 (mat 0) or dW_l0 (mat 1) rows of
+    // n-tile nt over all KT column tiles, and tiles 3 wv + u of the 24 of
+    // [dW_r1; dW_l1]; root-free: dW_l0 column tiles kt = (wv >> 2) + 2 i, and
+    // tiles wv + 8 u of the 12 of dW_l1 (f-tiles 3..5)
+    constexpr int NK0 = ROOT ? KT : (KT + 1) / 2;
+    constexpr int NC1 = ROOT ? 3 : 2;
+    constexpr int C1_TILES = 24;
     const int mat = wv >> 2;
+    auto c0_kt = [&](int i) { return ROOT ? i : mat + 2 * i; };
+    auto c1_tile = [&](int u) { return ROOT ? 3 * wv + u : (wv + 8 * u < 12 ? 12 + wv + 8 * u : C1_TILES); };
+    v4f acc0[NK0], acc1[NC1];
+#pragma unroll
+    for (int i = 0; i < NK0; ++i) acc0[i] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NC1; ++i) acc1[i] = v4f{0.f, 0.f, 0.f, 0.f};
     // the accumulators hold sums in the units of the last chunk added:
     // 2^E0 (dz0 2^(eX + eW - e_dz) times x / agg0 2^(ex | ea)), 2^E1 (X 2^eX
     // times h 2^eH); each chunk rescales them by the change (v_ldexp, exact
@@ -446,40 +460,42 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         // C0: A = dz0^T of n-tile nt (both row tiles), B = x / agg0 tiles
         const bf8 a1 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(sa + ((nt * 2) * 64 + ln) * 8);
         const bf8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf8 *>(sa + ((nt * 2 + 1) * 64 + ln) * 8);
-        const L16 *img = mat ? ia : ik;
+        const L16 *img = (mat || !ROOT) ? ia : ik;
         // every fragment read of the stage issued before its first MFMA (the
         // reads' latency once per chunk, not once per tile)
         bf8 b1[KT], b2[KT], x1[3], x2[3], h1[3], h2[3];
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) {
-            b1[kt] = tr_frag(img, KS, 16 * kt, ln);
-            b2[kt] = tr_frag(img + B2_ROWS * KS, KS, 16 * kt, ln);
+        for (int i = 0; i < NK0; ++i) {
+            const int kt = c0_kt(i);
+            b1[i] = tr_frag(img, KS, 16 * kt, ln);
+            b2[i] = tr_frag(img + B2_ROWS * KS, KS, 16 * kt, ln);
         }
-        // C1: tiles 3 wv + u of [dW_r1; dW_l1] (f-tile mf, n-tile nn): A =
-        // X^T, B = h
+        // C1: tiles of [dW_r1; dW_l1] (f-tile mf, n-tile nn): A = X^T, B = h
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int tt = 3 * wv + u, mf = tt >> 2, nn = tt & 3;
+        for (int u = 0; u < NC1; ++u) {
+            const int tt = c1_tile(u), mf = tt >> 2, nn = tt & 3;
             x1[u] = tr_frag(ix, XS, 16 * mf, ln);
             x2[u] = tr_frag(ix + B2_ROWS * XS, XS, 16 * mf, ln);
             h1[u] = tr_frag(ih, HS, 16 * nn, ln);
             h2[u] = tr_frag(ih + B2_ROWS * HS, HS, 16 * nn, ln);
         }
-        const int e0 = e.X + eW - a.e_dz + (mat ? e.a : e.x);
+        const int e0 = e.X + eW - a.e_dz + ((mat || !ROOT) ? e.a : e.x);
         const int e1 = e.X + e.H;
         if (!acc_empty) {
 #pragma unroll
-            for (int kt = 0; kt < KT; ++kt) acc0[kt] = ldexp4(acc0[kt], e0 - E0);
+            for (int i = 0; i < NK0; ++i) acc0[i] = ldexp4(acc0[i], e0 - E0);
 #pragma unroll
-            for (int u = 0; u < 3; ++u) acc1[u] = ldexp4(acc1[u], e1 - E1);
+            for (int u = 0; u < NC1; ++u) acc1[u] = ldexp4(acc1[u], e1 - E1);
         }
         E0 = e0;
         E1 = e1;
         acc_empty = false;
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) acc0[kt] = mfma3(a1, a2, b1[kt], b2[kt], acc0[kt]);
+        for (int i = 0; i < NK0; ++i)
+            if (c0_kt(i) < KT) acc0[i] = mfma3(a1, a2, b1[i], b2[i], acc0[i]);
 #pragma unroll
-        for (int u = 0; u < 3; ++u) acc1[u] = mfma3(x1[u], x2[u], h1[u], h2[u], acc1[u]);
+        for (int u = 0; u < NC1; ++u)
+            if (c1_tile(u) < C1_TILES) acc1[u] = mfma3(x1[u], x2[u], h1[u], h2[u], acc1[u]);
     };
 
     // ---- pipeline over the slice's chunks (two LDS buffers):
@@ -518,34 +534,36 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     if (cb < ce) stage_c(lb + ((ce - 1) & 1) * BUF, ep);
     // back to true units
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) acc0[kt] = ldexp4(acc0[kt], -E0);
+    for (int i = 0; i < NK0; ++i) acc0[i] = ldexp4(acc0[i], -E0);
 #pragma unroll
-    for (int u = 0; u < 3; ++u) acc1[u] = ldexp4(acc1[u], -E1);
+    for (int u = 0; u < NC1; ++u) acc1[u] = ldexp4(acc1[u], -E1);
 
     // ---- this workgroup's part of slab s (zeros for an empty slice)
     float *slab = a.slab + static_cast<int64_t>(s) * b2_slab_floats(K0, F1);
     {
         const i32x4 sr = make_rsrc(slab, static_cast<uint32_t>(b2_slab_floats(K0, F1) * 4));
         // dW_r0 / dW_l0 rows n = n0 + 16 nt + 4 q + i, columns 16 kt + l16
-        const int base0 = mat ? 256 * K0 : 0;
+        // (root-free: dW_l0 only; dW_r0's slab region is left unwritten --
+        // the reduce skips the absent gradients)
+        const int base0 = (mat || !ROOT) ? 256 * K0 : 0;
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) {
-            const int k = 16 * kt + l16;
+        for (int j = 0; j < NK0; ++j) {
+            const int k = 16 * c0_kt(j) + l16;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                buf_store1(acc0[kt][i], sr, k < K0 ? 4 * (base0 + (n0 + 16 * nt + 4 * q + i) * K0 + k) : kOOB, 0, 0);
+                buf_store1(acc0[j][i], sr, k < K0 ? 4 * (base0 + (n0 + 16 * nt + 4 * q + i) * K0 + k) : kOOB, 0, 0);
         }
         // dW_r1 / dW_l1 rows f = 16 mf + 4 q + i (< 48: W_r1, else W_l1),
         // columns n0 + 16 nn + l16
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int tt = 3 * wv + u, mf = tt >> 2, nn = tt & 3;
+        for (int u = 0; u < NC1; ++u) {
+            const int tt = c1_tile(u), mf = tt >> 2, nn = tt & 3;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int f = 16 * mf + 4 * q + i;
                 const int fr = f < 48 ? f : f - 48;
                 const int o = 512 * K0 + 256 + (f < 48 ? 0 : 256 * F1) + fr * 256 + n0 + 16 * nn + l16;
-                buf_store1(acc1[u][i], sr, fr < F1 ? 4 * o : kOOB, 0, 0);
+                buf_store1(acc1[u][i], sr, (tt < C1_TILES && fr < F1) ? 4 * o : kOOB, 0, 0);
             }
         }
     }
@@ -592,6 +610,17 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
     }
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (i >= total) return;
+    const int64_t A = 256LL * K0, Bf = 256LL * F1;
+    int k;
+    int64_t e;
+    if (i < A) k = 0, e = i;
+    else if (i < 2 * A) k = 1, e = i - A;
+    else if (i < 2 * A + 256) k = 2, e = i - 2 * A;
+    else if (i < 2 * A + 256 + Bf) k = 3, e = i - 2 * A - 256;
+    else if (i < 2 * A + 256 + 2 * Bf) k = 4, e = i - 2 * A - 256 - Bf;
+    else k = 5, e = i - 2 * A - 256 - 2 * Bf;
+    float *const outs[6] = {dwr0, dwl0, db0, dwr1, dwl1, db1};
+    if (!outs[k]) return;  // (a root-free stack's dW_r0 / dW_r1: not computed, not stepped)
     float t = 0.0f;
     if (ADAM) t = *af.step;  // (issued before the slab loads)
     float v = 0.0f;
@@ -604,16 +633,6 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
         for (int u = 0; u < 8; ++u) v += w[u];
     }
     for (; sl < S; ++sl) v += slab[static_cast<int64_t>(sl) * total + i];
-    const int64_t A = 256LL * K0, Bf = 256LL * F1;
-    int k;
-    int64_t e;
-    if (i < A) k = 0, e = i;
-    else if (i < 2 * A) k = 1, e = i - A;
-    else if (i < 2 * A + 256) k = 2, e = i - 2 * A;
-    else if (i < 2 * A + 256 + Bf) k = 3, e = i - 2 * A - 256;
-    else if (i < 2 * A + 256 + 2 * Bf) k = 4, e = i - 2 * A - 256 - Bf;
-    else k = 5, e = i - 2 * A - 256 - 2 * Bf;
-    float *const outs[6] = {dwr0, dwl0, db0, dwr1, dwl1, db1};
     outs[k][e] = v;
     if (ADAM) {  // k_adam's update (ngnn_optim.hip) of element e of tensor k
         const float bc1 = 1.0f - powf(af.b1, t);
@@ -669,9 +688,13 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     NGNN_RETURN_IF(reduce != NGNN_REDUCE_MEAN && reduce != NGNN_REDUCE_SUM, NGNN_E_ARG);
     NGNN_RETURN_IF(F1 <= 0 || F1 > 48 || K0 <= 0 || K0 > 128 || K0 % 4 != 0, NGNN_E_SHAPE);
     NGNN_RETURN_IF(n_rows < 0 || !fits_i32(n_rows), NGNN_E_RANGE);
-    NGNN_RETURN_IF(!dy || !wl1 || !wr1 || !h || (!x && !x_dev) || !agg0 || !rowptr || !col || !r_ptr || !rnext_ptr ||
-                       !dwl1 || !dbl1 || !dwr1 || !dwl0 || !dbl0 || !dwr0 || !ws,
+    // (ABI 18: dW_r0 and dW_r1 both NULL -- a root-free stack, SimpleGCN's
+    // W_r = 0: x is not read and may be NULL; wr1 is still read -- zeros)
+    const bool root = dwr0 || dwr1;
+    NGNN_RETURN_IF(!dy || !wl1 || !wr1 || !h || (root && !x && !x_dev) || !agg0 || !rowptr || !col || !r_ptr ||
+                       !rnext_ptr || !dwl1 || !dbl1 || (root && (!dwr1 || !dwr0)) || !dwl0 || !dbl0 || !ws,
                    NGNN_E_ARG);
+    NGNN_RETURN_IF(!root && (xrow || xrow_dev), NGNN_E_ARG);
     NGNN_RETURN_IF(ldy < F1 || ldw1 < 256 || ldh < 256 || ldh % 4 != 0 || ldx < K0 || ldx % 4 != 0 ||
                        ld_agg < K0 || ld_agg % 4 != 0,
                    NGNN_E_SHAPE);
@@ -749,14 +772,12 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
         return !(v && v[0] == '0');                  // 43.8 vs 44.6 us per call, tools/bwd2_micro.py)
     }();
     auto go = [&](auto xr_c, auto kt_c) {
-        auto fn = lag ? k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value, true>
-                      : k_bwd2<decltype(xr_c)::value, decltype(kt_c)::value, false>;
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
-            attr = true;
-        }
+        constexpr bool XRv = decltype(xr_c)::value;
+        constexpr int KTv = decltype(kt_c)::value;
+        auto fn = !root ? (lag ? k_bwd2<false, KTv, true, false> : k_bwd2<false, KTv, false, false>)
+                        : lag ? k_bwd2<XRv, KTv, true> : k_bwd2<XRv, KTv, false>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);  // (cheap; the function varies with root / lag)
         hipLaunchKernelGGL(fn, dim3(B2_S * B2_NCH), dim3(B2_THREADS), lds, st, b);
         return launch_status();
     };

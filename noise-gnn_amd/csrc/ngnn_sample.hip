@@ -94,6 +94,7 @@ struct SbWs {  // carved from the caller's workspace
     int32_t *nid;    // [n_cap]                local -> global
     int32_t *esrc;   // [e_cap]
     int32_t *edst;   // [e_cap]
+    int32_t *rp;     // [n_cap]    first edge of each frontier row (the block's CSR row pointers)
 };
 
 __global__ __launch_bounds__(kSbBlock) void k_sb_init(const int64_t *__restrict__ seeds, int B,
@@ -114,109 +115,68 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_init(const int64_t *__restrict_
     }
 }
 
-// Floyd draws with the fanout bounded at compile time (KF >= fanout): the
-// selections stay in registers (fully unrolled), so a node's column and map
-// loads issue back to back instead of as one dependent chain through
-// scratch.  Same draws as floyd_sample.
+// Lane-per-draw layout (round 6): frontier position i owns a group of KF
+// lanes (KF = fanout rounded up to 8/16/32/64, a power of two dividing the
+// wave), lane j its draw j.  The per-thread layout before it ran one thread
+// per position -- 60 workgroups for a products hop-2 frontier, each thread a
+// serial chain of draws, loads and atomics -- latency-bound at ~30 us a
+// launch.  Floyd's draws are independent but for the duplicate test: draw q's
+// final choice is known once draws < q are, so the group resolves them in
+// fanout - 1 shuffle rounds (lane q's choice broadcast, later lanes compare).
+// Same selections as floyd_sample.
 template <int KF>
-__device__ __forceinline__ int floyd_sample_r(int64_t d, int fanout, uint64_t seed, int64_t i,
-                                              int32_t (&sel)[KF]) {
-    const int k = d < fanout ? static_cast<int>(d) : fanout;
-    if (d <= fanout) {
-#pragma unroll
-        for (int j = 0; j < KF; ++j) sel[j] = j;
-        return k;
-    }
+__device__ __forceinline__ int floyd_lane(int64_t d, int fanout, uint64_t seed, int i, int j, int &k) {
+    k = d < fanout ? static_cast<int>(d) : fanout;
+    if (d <= fanout) return j;
     const uint64_t base = mix64(seed ^ mix64(static_cast<uint64_t>(i) + 0x632BE59BD9B4E019ull));
-#pragma unroll
-    for (int jj = 0; jj < KF; ++jj) {
-        if (jj < k) {
-            const int64_t j = d - k + jj;
-            const uint64_t r = mix64(base + static_cast<uint64_t>(j));
-            const int64_t t = static_cast<int64_t>(
-                (static_cast<unsigned __int128>(r) * static_cast<uint64_t>(j + 1)) >> 64);
-            bool dup = false;
-#pragma unroll
-            for (int q = 0; q < jj; ++q) dup |= sel[q] == t;
-            sel[jj] = static_cast<int32_t>(dup ? j : t);
-        }
+    const int64_t J = d - k + j;  // (lanes j >= k compute a value nobody reads)
+    const uint64_t r = mix64(base + static_cast<uint64_t>(J));
+    const int32_t t = static_cast<int32_t>((static_cast<unsigned __int128>(r) * static_cast<uint64_t>(J + 1)) >> 64);
+    const int32_t jw = static_cast<int32_t>(J);
+    bool dup = false;
+    for (int q = 0; q < k - 1; ++q) {  // (k is uniform over the group; every source lane is active)
+        const int32_t fq = __shfl(dup ? jw : t, q, KF);
+        dup |= j > q && fq == t;
     }
-    return k;
+    return dup ? jw : t;
 }
 
-// draws of frontier node i -> cand[i*f + j]; claims first appearances.
-// Also (round 6, one launch fewer per hop): the previous hop's edges
-// relabelled to local ids (its assignment is complete: the launch before),
-// and this hop's look-back words and tile ticket cleared for k_sb_assign_lb.
+constexpr int kSbTile = 1024;  // k_sb_assign_lb's tile: kSbTile / KF frontier positions
+
+__host__ __device__ constexpr int sb_kf(int f) { return f <= 8 ? 8 : f <= 16 ? 16 : f <= 32 ? 32 : 64; }
+
+// draw j of frontier node i -> cand[i*f + j]; claims first appearances.
+// Also (one launch fewer per hop): the previous hop's edges relabelled to
+// local ids (its assignment is complete: the launch before), and this hop's
+// look-back words and tile ticket cleared for k_sb_assign_lb.
 template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ gcol, int64_t n_graph,
     const int32_t *__restrict__ hs, const int32_t *__restrict__ nid, int fanout, uint64_t seed,
     int32_t *__restrict__ cand, int32_t *__restrict__ cnt, int32_t *__restrict__ map,
     const int32_t *__restrict__ hs_prev, int32_t *__restrict__ esrc, uint64_t *__restrict__ lb, int nblk) {
-    const int i = blockIdx.x * kSbBlock + threadIdx.x;
+    const int gt = blockIdx.x * kSbBlock + threadIdx.x;
     const int stride = gridDim.x * kSbBlock;
-    for (int t = i; t <= nblk; t += stride) lb[t] = 0;  // (lb[nblk]: the tile ticket)
+    for (int t = gt; t <= nblk; t += stride) lb[t] = 0;  // (lb[nblk]: the tile ticket)
     if (hs_prev)  // edges of the previous hop [hs_prev[2], hs_prev[6])
-        for (int e = hs_prev[2] + i; e < hs_prev[6]; e += stride) esrc[e] = map[esrc[e]];
+        for (int e = hs_prev[2] + gt; e < hs_prev[6]; e += stride) esrc[e] = map[esrc[e]];
     const int lo = hs[0], hi = hs[1];
-    if (i >= hi - lo) return;
+    const int i = gt / KF, j = gt % KF;
+    if (i >= hi - lo) return;  // (whole groups)
     const int64_t v = nid[lo + i];
     const int64_t b = rowptr[v];
-    int32_t sel[KF];
-    const int k = floyd_sample_r<KF>(rowptr[v + 1] - b, fanout, seed, i, sel);
-    int32_t u[KF], mp[KF];
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k) u[j] = gcol[b + sel[j]];
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k) {
-            cand[i * fanout + j] = u[j];
-            mp[j] = map[u[j]];
-        }
-    int32_t *claim = map + n_graph;
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k && mp[j] < 0) atomicMax(claim + u[j], INT32_MAX - (i * fanout + j));
-    cnt[i] = k;
-}
-
-// first-appearance flags of frontier node i's draws (bit j), and the draws
-template <int KF>
-__device__ __forceinline__ uint64_t sb_new_flags(const int32_t *cand, const int32_t *map,
-                                                 const int32_t *claim, int i, int fanout, int k,
-                                                 int32_t (&u)[KF]) {
-    int32_t c[KF], m[KF];
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k) u[j] = cand[i * fanout + j];
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k) {
-            c[j] = claim[u[j]];
-            m[j] = map[u[j]];
-        }
-    uint64_t f = 0;
-#pragma unroll
-    for (int j = 0; j < KF; ++j)
-        if (j < k && c[j] == INT32_MAX - (i * fanout + j) && m[j] < 0) f |= 1ull << j;
-    return f;
-}
-
-__device__ __forceinline__ int block_excl_scan(int v, int *sh) {
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int o = 1; o < kSbBlock; o <<= 1) {
-        const int a = t >= o ? sh[t - o] : 0;
-        __syncthreads();
-        sh[t] += a;
-        __syncthreads();
+    int k;
+    const int s = floyd_lane<KF>(rowptr[v + 1] - b, fanout, seed, i, j, k);
+    if (j < k) {
+        const int32_t u = gcol[b + s];
+        cand[i * fanout + j] = u;
+        const int32_t m = map[u], c = map[n_graph + u];
+        const int32_t mine = INT32_MAX - (i * fanout + j);
+        // (the claim only grows: a hub drawn by thousands of positions takes
+        // an atomic only from those that still beat the standing claim)
+        if (m < 0 && c < mine) atomicMax(map + n_graph + u, mine);
     }
-    const int r = sh[t] - v;
-    __syncthreads();
-    return r;
+    if (j == 0) cnt[i] = k;
 }
 
 // look-back word of a tile: status (bits 62-63: 1 aggregate, 2 inclusive
@@ -227,94 +187,120 @@ __device__ __forceinline__ uint64_t lb_word(uint64_t st, int e, int n) {
     return st | (static_cast<uint64_t>(n) << 31) | static_cast<uint64_t>(e);
 }
 
-// One hop's relabelling in ONE launch (round 6; was count + scan + assign):
-// each tile (256 frontier positions, in ticket order -- a tile only waits
-// for tiles that already run) takes its positions' draws and first-
-// appearance flags, publishes its (edges, new nodes) counts, finds its
-// exclusive prefix by a decoupled look-back over the tiles before it, then
-// assigns the new local ids (map, nid) in (position, draw) order and writes
-// the hop's edges (global sources, local targets).  The last tile writes the
-// next hop's state.  Same ids and edge order as the three launches.
+__device__ __forceinline__ int wave_sum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One hop's relabelling in ONE launch: each tile (kSbTile lanes = (position,
+// draw) pairs in order, tiles in ticket order -- a tile only waits for tiles
+// that already run) takes its draws' first-appearance flags, counts its
+// (edges, new nodes) by wave ballots, publishes them, finds its exclusive
+// prefix by a decoupled look-back over the tiles before it -- wave 0 reads 64
+// predecessors' words at once -- then assigns the new local ids (map, nid) in
+// (position, draw) order and writes the hop's edges (global sources, local
+// targets) and row pointers.  The last tile writes the next hop's state.
 template <int KF>
-__global__ __launch_bounds__(kSbBlock) void k_sb_assign_lb(
+__global__ __launch_bounds__(kSbTile) void k_sb_assign_lb(
     int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
     int32_t *__restrict__ map, int64_t n_graph, int fanout, uint64_t *__restrict__ lb, int nblk,
-    int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst) {
-    __shared__ int sh[kSbBlock];
+    int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst, int32_t *__restrict__ rp) {
+    constexpr int NW = kSbTile / 64;
     __shared__ int s_tile, s_pe, s_pn;
+    __shared__ int s_we[NW], s_wn[NW];
     if (threadIdx.x == 0)
         s_tile = static_cast<int>(atomicAdd(reinterpret_cast<unsigned long long *>(lb + nblk), 1ull));
     __syncthreads();
     const int tile = s_tile;
-    const int i = tile * kSbBlock + threadIdx.x;
+    const int gt = tile * kSbTile + threadIdx.x;
+    const int i = gt / KF, j = gt % KF;
     const int lo = hs[0], hi = hs[1], e0 = hs[2];
     const int nf = hi - lo;
-    int k = 0;
-    uint64_t fl = 0;
-    int32_t u[KF];
-    if (i < nf) {
-        k = cnt[i];
+    bool has = false, fresh = false;
+    int32_t u = 0;
+    if (i < nf && j < cnt[i]) {
+        has = true;
+        u = cand[i * fanout + j];
         // race-free although other tiles write map[] meanwhile: only the
         // position that won u's claim ever writes map[u] (after reading
         // it), and for every other position the flag is false whatever
         // map[u] reads
-        fl = sb_new_flags<KF>(cand, map, map + n_graph, i, fanout, k, u);
+        const int32_t c = map[n_graph + u], m = map[u];
+        fresh = c == INT32_MAX - (i * fanout + j) && m < 0;
     }
-    const int xe = block_excl_scan(k, sh);
-    const int nn = __popcll(fl);
-    const int xn = block_excl_scan(nn, sh);
-    // tile totals: the last thread's exclusive value plus its own
-    __shared__ int s_te, s_tn;
-    if (threadIdx.x == kSbBlock - 1) {
-        s_te = xe + k;
-        s_tn = xn + nn;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t be = __ballot(has), bn = __ballot(fresh);
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int xe = __popcll(be & below), xn = __popcll(bn & below);
+    if (lane == 0) {
+        s_we[wv] = __popcll(be);
+        s_wn[wv] = __popcll(bn);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int ae = s_te, an = s_tn;
+    int ae = 0, an = 0;  // tile totals; xe / xn += the waves before this one
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const int a = s_we[w], c = s_wn[w];
+        if (w < wv) {
+            xe += a;
+            xn += c;
+        }
+        ae += a;
+        an += c;
+    }
+    if (wv == 0) {
         int pe = 0, pn = 0;
         if (tile == 0) {
-            __hip_atomic_store(lb + tile, lb_word(kLbPre, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(lb, lb_word(kLbPre, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(lb + tile, lb_word(kLbAgg, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            for (int p = tile - 1; p >= 0;) {
-                const uint64_t w = __hip_atomic_load(lb + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(lb + tile, lb_word(kLbAgg, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            for (int p = tile - 1;;) {  // window: predecessors p, p-1, ..., p-63 (lane order)
+                const int q = p - lane;
+                const uint64_t w = q >= 0 ? __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                          : kLbPre;  // (before tile 0: an empty prefix)
                 const uint64_t st = w & (3ull << 62);
-                if (st == 0) {
+                const uint64_t pre = __ballot(st == kLbPre), idle = __ballot(st == 0);
+                const int fp = pre ? __builtin_ctzll(pre) : 64;  // nearest inclusive prefix
+                const uint64_t upto = fp >= 63 ? ~0ull : ((2ull << fp) - 1);
+                if (idle & upto) {  // a predecessor before it has not published yet
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                pe += static_cast<int>(w & 0x7FFFFFFFull);
-                pn += static_cast<int>((w >> 31) & 0x7FFFFFFFull);
-                if (st == kLbPre) break;
-                --p;
+                const bool take = lane <= fp;
+                pe += wave_sum(take ? static_cast<int>(w & 0x7FFFFFFFull) : 0);
+                pn += wave_sum(take ? static_cast<int>((w >> 31) & 0x7FFFFFFFull) : 0);
+                if (fp < 64) break;
+                p -= 64;
             }
-            __hip_atomic_store(lb + tile, lb_word(kLbPre, pe + ae, pn + an), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(lb + tile, lb_word(kLbPre, pe + ae, pn + an), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        s_pe = pe;
-        s_pn = pn;
-        if (tile == nblk - 1) {  // the next hop's state: this hop's new nodes, its edges' end
-            hs[4] = hi;
-            hs[5] = hi + pn + an;
-            hs[6] = e0 + pe + ae;
-            hs[7] = 0;
+        if (lane == 0) {
+            s_pe = pe;
+            s_pn = pn;
+            if (tile == nblk - 1) {  // the next hop's state: this hop's new nodes, its edges' end
+                hs[4] = hi;
+                hs[5] = hi + pn + an;
+                hs[6] = e0 + pe + ae;
+                hs[7] = 0;
+            }
         }
     }
     __syncthreads();
-    int e = e0 + s_pe + xe;
-    int n = hi + s_pn + xn;
-#pragma unroll
-    for (int j = 0; j < KF; ++j) {
-        if (j < k) {
-            if ((fl >> j) & 1) {
-                map[u[j]] = n;
-                nid[n++] = u[j];
-            }
-            esrc[e + j] = u[j];
-            edst[e + j] = lo + i;
-        }
+    const int e = e0 + s_pe + xe;
+    if (has) {
+        esrc[e] = u;
+        edst[e] = lo + i;
     }
+    if (fresh) {
+        const int n = hi + s_pn + xn;
+        map[u] = n;
+        nid[n] = u;
+    }
+    if (j == 0 && i < nf) rp[lo + i] = e;  // (frontier row lo + i's edges start here: CSR row pointer)
 }
 
 // the last hop's edges relabelled; counts = {n_total, e_total, n_active, -}
@@ -335,25 +321,40 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_tail(const int32_t *__restrict_
 }
 
 // outputs + map reset: n_id (int64), y = y_all[n_id], edge_index [2, E]
-__global__ __launch_bounds__(kSbBlock) void k_sb_finish(
-    const int32_t *__restrict__ nid, int n, const int32_t *__restrict__ esrc,
-    const int32_t *__restrict__ edst, int E, int32_t *__restrict__ map, int64_t n_graph,
-    int64_t *__restrict__ n_id, const int64_t *__restrict__ y_all, int64_t *__restrict__ y,
-    int64_t *__restrict__ ei) {
-    const int64_t stride = (int64_t)gridDim.x * kSbBlock;
-    for (int64_t t = blockIdx.x * (int64_t)kSbBlock + threadIdx.x; t < max(n, E); t += stride) {
-        if (t < n) {
-            const int32_t u = nid[t];
-            n_id[t] = u;
-            if (y) y[t] = y_all[u];
-            map[u] = -1;
-            map[n_graph + u] = -1;
-        }
-        if (t < E) {
-            ei[t] = esrc[t];
-            ei[E + t] = edst[t];
-        }
+// the block's outputs, item t of a grid-stride loop: n_id, y, the node map
+// reset, edge_index; with csr_rp / csr_col (ABI 18, nullable): its
+// target-grouped CSR (row pointers from the relabelling -- rows past the last
+// frontier have no edges -- and the relabelled sources as int32), so a
+// consumer builds none
+struct SbOut {
+    const int32_t *nid, *esrc, *edst, *rp;
+    int n, E, n_act;
+    int32_t *map;
+    int64_t n_graph;
+    int64_t *n_id;
+    const int64_t *y_all;
+    int64_t *y, *ei;
+    int32_t *csr_rp, *csr_col;
+};
+__device__ __forceinline__ void sb_emit(const SbOut &o, int64_t t) {
+    if (t < o.n) {
+        const int32_t u = o.nid[t];
+        o.n_id[t] = u;
+        if (o.y) o.y[t] = o.y_all[u];
+        o.map[u] = -1;
+        o.map[o.n_graph + u] = -1;
     }
+    if (t < o.E) {
+        o.ei[t] = o.esrc[t];
+        o.ei[o.E + t] = o.edst[t];
+        if (o.csr_col) o.csr_col[t] = o.esrc[t];
+    }
+    if (o.csr_rp && t <= o.n) o.csr_rp[t] = t < o.n_act ? o.rp[t] : o.E;
+}
+
+__global__ __launch_bounds__(kSbBlock) void k_sb_finish(SbOut o) {
+    const int64_t stride = (int64_t)gridDim.x * kSbBlock;
+    for (int64_t t = blockIdx.x * (int64_t)kSbBlock + threadIdx.x; t <= max(o.n, o.E); t += stride) sb_emit(o, t);
 }
 
 // x[i] = x_all[n_id[i]], 16-B vectors (F % 4 == 0, aligned rows); 32-bit
@@ -373,36 +374,20 @@ __global__ __launch_bounds__(kSbBlock) void k_gather_rows4(const float *__restri
 // the block's outputs in ONE launch (round 6): blocks [0, gx) gather x rows
 // (k_gather_rows4's work), the rest k_sb_finish's (ids, labels, edges, map
 // reset -- the gather reads nid only, so the two roles need no order)
-__global__ __launch_bounds__(kSbBlock) void k_sb_out(const float *__restrict__ x_all, int64_t ldx,
-                                                     const int32_t *__restrict__ nid, int n, int f4,
-                                                     float *__restrict__ x, int64_t ldo, int gx,
-                                                     const int32_t *__restrict__ esrc, const int32_t *__restrict__ edst,
-                                                     int E, int32_t *__restrict__ map, int64_t n_graph,
-                                                     int64_t *__restrict__ n_id, const int64_t *__restrict__ y_all,
-                                                     int64_t *__restrict__ y, int64_t *__restrict__ ei) {
+__global__ __launch_bounds__(kSbBlock) void k_sb_out(const float *__restrict__ x_all, int64_t ldx, int f4,
+                                                     float *__restrict__ x, int64_t ldo, int gx, SbOut o) {
     if (static_cast<int>(blockIdx.x) < gx) {
-        const int total = n * f4;
+        const int total = o.n * f4;
         for (int t = blockIdx.x * kSbBlock + threadIdx.x; t < total; t += gx * kSbBlock) {
             const int r = t / f4, c = (t - r * f4) * 4;
             *reinterpret_cast<float4 *>(x + static_cast<int64_t>(r) * ldo + c) =
-                *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(nid[r]) * ldx + c);
+                *reinterpret_cast<const float4 *>(x_all + static_cast<int64_t>(o.nid[r]) * ldx + c);
         }
         return;
     }
     const int64_t stride = static_cast<int64_t>(gridDim.x - gx) * kSbBlock;
-    for (int64_t t = (blockIdx.x - gx) * static_cast<int64_t>(kSbBlock) + threadIdx.x; t < max(n, E); t += stride) {
-        if (t < n) {
-            const int32_t u = nid[t];
-            n_id[t] = u;
-            if (y) y[t] = y_all[u];
-            map[u] = -1;
-            map[n_graph + u] = -1;
-        }
-        if (t < E) {
-            ei[t] = esrc[t];
-            ei[E + t] = edst[t];
-        }
-    }
+    for (int64_t t = (blockIdx.x - gx) * static_cast<int64_t>(kSbBlock) + threadIdx.x; t <= max(o.n, o.E); t += stride)
+        sb_emit(o, t);
 }
 
 __global__ __launch_bounds__(kSbBlock) void k_gather_rows1(const float *__restrict__ x_all,
@@ -419,7 +404,7 @@ __global__ __launch_bounds__(kSbBlock) void k_gather_rows1(const float *__restri
 struct SbPlan {
     int64_t n_cap, e_cap, nf_cap[kMaxHops], cand_off[kMaxHops], cnt_off[kMaxHops], max_nblk;
     size_t bytes;
-    size_t off_state, off_cand, off_cnt, off_bsum, off_nid, off_esrc, off_edst;
+    size_t off_state, off_cand, off_cnt, off_bsum, off_nid, off_esrc, off_edst, off_rp;
 };
 
 // capacities: frontier_h <= B prod_{j<h} f_j, all within int32
@@ -434,7 +419,8 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
         p->cnt_off[h] = cntn;
         cand += nf * f;
         cntn += nf;
-        nblk = std::max<int64_t>(nblk, ceil_div(nf, kSbBlock));
+        if (nf * sb_kf(static_cast<int>(f)) > INT32_MAX / 2) return false;  // (lane indices)
+        nblk = std::max<int64_t>(nblk, ceil_div(nf * sb_kf(static_cast<int>(f)), kSbTile));
         e += nf * f;
         nf *= f;
         n += nf;
@@ -456,6 +442,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
     p->off_nid = take(static_cast<size_t>(n));
     p->off_esrc = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
     p->off_edst = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
+    p->off_rp = take(static_cast<size_t>(n));
     p->bytes = o;
     return true;
 }
@@ -465,7 +452,7 @@ SbWs sb_carve(void *ws, const SbPlan &p) {
     return SbWs{reinterpret_cast<int32_t *>(b + p.off_state), reinterpret_cast<int32_t *>(b + p.off_cand),
                 reinterpret_cast<int32_t *>(b + p.off_cnt), reinterpret_cast<uint64_t *>(b + p.off_bsum),
                 reinterpret_cast<int32_t *>(b + p.off_nid), reinterpret_cast<int32_t *>(b + p.off_esrc),
-                reinterpret_cast<int32_t *>(b + p.off_edst)};
+                reinterpret_cast<int32_t *>(b + p.off_edst), reinterpret_cast<int32_t *>(b + p.off_rp)};
 }
 
 }  // namespace
@@ -511,10 +498,12 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
                        w.state);
     for (int h = 0; h < n_hops; ++h) {
         const int f = fanouts[h];
-        const int kf = f <= 8 ? 8 : f <= 16 ? 16 : f <= 32 ? 32 : 64;
+        const int kf = sb_kf(f);
         int32_t *hs = w.state + 4 * h;
         const int64_t nf = p.nf_cap[h];
-        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf, kSbBlock)));
+        // lane-per-draw grids: kf lanes per frontier position
+        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbTile)));
+        const int sgrid = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbBlock)));
         int32_t *cand = w.cand + p.cand_off[h], *cnt = w.cnt + p.cnt_off[h];
         // the per-hop seed of ngnn_sample_hop's callers (loader.sample_block)
         const uint64_t hseed = seed * 1000003ull + static_cast<uint64_t>(h);
@@ -522,10 +511,10 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
         // previous hop's relabel), then the look-back relabelling
         auto hop = [&](auto kf_c) {
             constexpr int KF = decltype(kf_c)::value;
-            hipLaunchKernelGGL(k_sb_sample<KF>, dim3(nblk), dim3(kSbBlock), 0, st, g_rowptr, g_col, n_graph, hs, w.nid,
+            hipLaunchKernelGGL(k_sb_sample<KF>, dim3(sgrid), dim3(kSbBlock), 0, st, g_rowptr, g_col, n_graph, hs, w.nid,
                                f, hseed, cand, cnt, node_map, h > 0 ? hs - 4 : nullptr, w.esrc, w.lb, nblk);
-            hipLaunchKernelGGL(k_sb_assign_lb<KF>, dim3(nblk), dim3(kSbBlock), 0, st, hs, cand, cnt, node_map,
-                               n_graph, f, w.lb, nblk, w.nid, w.esrc, w.edst);
+            hipLaunchKernelGGL(k_sb_assign_lb<KF>, dim3(nblk), dim3(kSbTile), 0, st, hs, cand, cnt, node_map,
+                               n_graph, f, w.lb, nblk, w.nid, w.esrc, w.edst, w.rp);
         };
         switch (kf) {
             case 8: hop(std::integral_constant<int, 8>{}); break;
@@ -546,7 +535,8 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
                                         int64_t n_graph, const void *ws, size_t ws_bytes,
                                         int64_t *n_id, int64_t *edge_index, const int64_t *y_all,
                                         int64_t *y, const float *x_all, int64_t ldx, int64_t F,
-                                        float *x, int64_t ldo, void *stream) {
+                                        float *x, int64_t ldo, int64_t n_active, int32_t *csr_rowptr,
+                                        int32_t *csr_col, void *stream) {
     SbPlan p;
     NGNN_RETURN_IF(n_hops < 0 || (n_hops > 0 && !fanouts), NGNN_E_ARG);
     NGNN_RETURN_IF(!sb_plan(n_seeds, fanouts, n_hops, &p), NGNN_E_SHAPE);
@@ -555,17 +545,22 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
                    NGNN_E_SHAPE);
     NGNN_RETURN_IF(!node_map || !n_id || (n_edges > 0 && !edge_index) || (y && !y_all), NGNN_E_ARG);
     NGNN_RETURN_IF(x && (!x_all || F <= 0 || ldx < F || ldo < F), NGNN_E_ARG);
+    // (the CSR outputs come as a pair; a block without edges may pass no col)
+    NGNN_RETURN_IF((!csr_rowptr && csr_col) || (csr_rowptr && !csr_col && n_edges > 0) || n_active < 0 ||
+                       n_active > n_nodes,
+                   NGNN_E_ARG);
     hipStream_t st = as_stream(stream);
     const SbWs w = sb_carve(const_cast<void *>(ws), p);
-    const int64_t work = std::max<int64_t>(std::max<int64_t>(n_nodes, n_edges), 1);
+    const SbOut o{w.nid, w.esrc, w.edst, w.rp, static_cast<int>(n_nodes), static_cast<int>(n_edges),
+                  static_cast<int>(n_active), node_map, n_graph, n_id, y_all, y, edge_index, csr_rowptr, csr_col};
+    const int64_t work = std::max<int64_t>(std::max<int64_t>(n_nodes, n_edges), 1) + 1;
     const unsigned gf = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, kSbBlock), 4096));
     const bool vec = x && n_nodes > 0 && F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&
                      aligned(x, 16) && n_nodes * (F / 4) < INT32_MAX;
     if (vec) {  // the gather and the outputs in one launch
         const int gx = static_cast<int>(std::min<int64_t>(ceil_div(n_nodes * (F / 4), kSbBlock), 4096));
-        hipLaunchKernelGGL(k_sb_out, dim3(gx + gf), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
-                           static_cast<int>(n_nodes), static_cast<int>(F / 4), x, ldo, gx, w.esrc, w.edst,
-                           static_cast<int>(n_edges), node_map, n_graph, n_id, y_all, y, edge_index);
+        hipLaunchKernelGGL(k_sb_out, dim3(gx + gf), dim3(kSbBlock), 0, st, x_all, ldx, static_cast<int>(F / 4), x,
+                           ldo, gx, o);
         return launch_status();
     }
     if (x && n_nodes > 0) {  // gather before the map reset (order irrelevant: reads nid only)
@@ -579,7 +574,6 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
             hipLaunchKernelGGL(k_gather_rows1, dim3(grid), dim3(kSbBlock), 0, st, x_all, ldx, w.nid,
                                n_nodes, F, x, ldo);
     }
-    hipLaunchKernelGGL(k_sb_finish, dim3(gf), dim3(kSbBlock), 0, st, w.nid, static_cast<int>(n_nodes), w.esrc, w.edst,
-                       static_cast<int>(n_edges), node_map, n_graph, n_id, y_all, y, edge_index);
+    hipLaunchKernelGGL(k_sb_finish, dim3(gf), dim3(kSbBlock), 0, st, o);
     return launch_status();
 }

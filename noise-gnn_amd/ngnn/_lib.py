@@ -48,7 +48,7 @@ SIGNATURES = {
     "ngnn_sample_block": (_int, [_p, _p, _i64, _p, _i64, _p, _int, ctypes.c_uint64, _p, _p, _sz, _p,
                                  _p]),
     "ngnn_sample_block_finish": (_int, [_p, _int, _i64, _i64, _i64, _p, _i64, _p, _sz, _p, _p, _p,
-                                        _p, _p, _i64, _i64, _p, _i64, _p]),
+                                        _p, _p, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
     "ngnn_pack_weight_bytes": (_sz, [_i64, _i64]),
     "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_pack_weight_ex": (_int, [_p, _p, _i64, _i64, _i64, _i64, _int, _p, _p]),

@@ -698,7 +698,7 @@ class AdamFoldSpec:
 
 
 def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: float, r_ptr: int,
-                   rn_ptr: int, views, g_pre=None):
+                   rn_ptr: int, views, g_pre=None, root_free: bool = False):
     """Every weight gradient of the two-layer stack (include/ngnn.h
     ngnn_sage2_bwd): [dW_l0, db0, dW_r0, dW_l1, db1, dW_r1] from dy (rows <
     *r_ptr) with the forward's h (rows < *rn_ptr) and layer-0 aggregate.
@@ -715,6 +715,8 @@ def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: fl
         w1l, w1r = w1l.contiguous(), w1r.contiguous()
     grads = [(g.view(q.shape) if g is not None else torch.empty_like(q))
              for g, q in zip(views, (wl0, bl0, wr0, wl1, bl1, wr1))]
+    if root_free:  # (ABI 18: a SimpleGCN stack -- no x reads, no W_r gradients)
+        grads[2] = grads[5] = None
     nrows = block.n_dst
     ws = reserve_sage2_bwd(dev, nrows, K0, F1)
     yscale = dropout_scale(p_drop) if p_drop > 0.0 else 1.0
@@ -727,7 +729,8 @@ def sage2_backward(dy, block: Block, reduce: str, acts, agg0, params, p_drop: fl
     with _timing.span("sage2_bwd", 0, 0):
         rc = lib.ngnn_sage2_bwd(
             _lib.ptr(dy), dy.stride(0), F1, _lib.ptr(w1l), _lib.ptr(w1r), w1l.stride(0), _lib.ptr(h),
-            h.stride(0), yscale, _lib.ptr(x), _lib.ptr(block.x_dev), None, _lib.ptr(block.xrow_dev),
+            h.stride(0), yscale, None if root_free else _lib.ptr(x), None if root_free else _lib.ptr(block.x_dev),
+            None, None if root_free else _lib.ptr(block.xrow_dev),
             block.x_rows, x.stride(0), K0, _lib.ptr(agg0), agg0.stride(0), _lib.ptr(block.rowptr),
             _lib.ptr(block.col), nrows, r_ptr, rn_ptr, _lib.REDUCE[reduce], *(_lib.ptr(g) for g in grads[3:]),
             *(_lib.ptr(g) for g in grads[:3]), _lib.ptr(g_pre),
@@ -850,7 +853,8 @@ class _SAGEStack(torch.autograd.Function):
             return (None, None, None, None, None, None, None, None, None,
                     *_absent_none(params, sage2_backward(dy, block, reduce, acts, aggs[0], sage2_params(params),
                                                          p, bptr(2), bptr(1), views,
-                                                         g_pre=getattr(dout, "_ngnn_g_pre", None))))
+                                                         g_pre=getattr(dout, "_ngnn_g_pre", None),
+                                                         root_free=params[2] is None)))
         if (ctx.sage2 and not ctx.h_partial and not need_dx and _use_bwd2
                 and not torch.are_deterministic_algorithms_enabled()):
             # an eager step (the reference loop after the Option-B swap: no
@@ -867,7 +871,7 @@ class _SAGEStack(torch.autograd.Function):
                        "ngnn_block_prefix_stats")
             return (None, None, None, None, None, None, None, None, None,
                     *_absent_none(params, sage2_backward(dy, block, reduce, acts, aggs[0], sage2_params(params),
-                                                         p, bptr(2), bptr(1), views)))
+                                                         p, bptr(2), bptr(1), views, root_free=params[2] is None)))
         if rows_hint is None:
             _lib.check(lib.ngnn_row_extent(_lib.ptr(dy), dy.stride(0), N, dy.size(1), bptr(L),
                                            stream), "ngnn_row_extent")
@@ -1188,7 +1192,16 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
     if out_dtype == torch.float32:
         return out
     if out_dtype == torch.bfloat16 and out.is_contiguous() and out.dim() == 2:
-        return _StackOutBF16.apply(out, block.n_rows_dev)
+        # a graph slot whose loss reads rows < B only (block.r_next[2]): the
+        # bf16 logits of those rows alone (the other rows' fp32 logits stay
+        # on the output as _ngnn_f32) -- the cast of a 1.5 M-row block's
+        # logits was 69 us of the 3-layer products step
+        rn = block.r_next
+        rows = rn[1] if (rn is not None and len(rn) > 2 and rn[2]) else out.size(0)
+        y = _StackOutBF16.apply(out, block.n_rows_dev, rows)
+        if rows < out.size(0):
+            y._ngnn_f32 = out.detach()
+        return y
     from .losses import cast_keep_rows
     return cast_keep_rows(out, out_dtype)
 
@@ -1257,11 +1270,13 @@ class _StackOutBF16(torch.autograd.Function):
     into a cached buffer, and the hint travels on."""
 
     @staticmethod
-    def forward(ctx, x, rows_dev=None):
+    def forward(ctx, x, rows_dev=None, rows=None):
         # (rows_dev: a graph slot's device row count -- only the block's real
-        # rows are cast; the slot's padding rows of y are left unwritten)
+        # rows are cast; the slot's padding rows of y are left unwritten;
+        # rows: a host cap, the rows a graph slot's loss reads)
         y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-        _lib.check(_lib.load().ngnn_cast_f32_bf16_rows(_lib.ptr(x), _lib.ptr(y), x.size(0), x.size(1),
+        n = x.size(0) if rows is None else min(int(rows), x.size(0))
+        _lib.check(_lib.load().ngnn_cast_f32_bf16_rows(_lib.ptr(x), _lib.ptr(y), n, x.size(1),
                                                        _lib.ptr(rows_dev), _lib.stream_handle(x.device)),
                    "ngnn_cast_f32_bf16_rows")
         return y
@@ -1270,7 +1285,7 @@ class _StackOutBF16(torch.autograd.Function):
     def backward(ctx, g):
         rows = getattr(g, "_ngnn_nonzero_rows", None)
         if rows is None:
-            return g.float(), None
+            return g.float(), None, None
         key = (g.device, tuple(g.shape))
         buf = _out_grads.get(key)
         if buf is None:
@@ -1285,4 +1300,4 @@ class _StackOutBF16(torch.autograd.Function):
         else:
             buf[:R].copy_(g[:R])
         buf._ngnn_nonzero_rows = R  # rows >= R are stale: the stack never reads them
-        return buf, None
+        return buf, None, None

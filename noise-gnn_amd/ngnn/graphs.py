@@ -206,6 +206,9 @@ class GraphedTrainStep:
         # capture: torch's stream-mismatch warning and an event wait per
         # parameter inside the captured backward
         self.out = out.detach()
+        # a bf16 model in a slot whose loss reads the seed rows: the bf16
+        # logits hold those rows only; every row's logits in fp32 here
+        self.out_f32 = getattr(out, "_ngnn_f32", None)
         loss = self.loss_fn(out, self.y, self.B)
         # a persistent d(loss) = 1 instead of backward()'s ones_like fill
         # launch; marked, so the loss backward needs no scale launch either

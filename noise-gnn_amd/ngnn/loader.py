@@ -31,7 +31,7 @@ import weakref
 import torch
 
 from . import _lib
-from .block import hint_edge_index
+from .block import CSR, hint_edge_index
 
 # name -> (num_nodes, directed entries (symmetric), features, classes, train seeds)
 DATASETS = {
@@ -335,10 +335,11 @@ def sample_block(graph: Graph, seeds: torch.Tensor, fanouts, seed: int,
     (NeighborLoader reads those counts one batch late instead: no wait.)"""
     cache = _sampler_cache(graph)
     st = cache.acquire()
-    try:
-        return _sample_finish(_sample_start(graph, seeds, fanouts, seed, gather_features, st))
-    finally:
-        cache.release(st)
+    # (a state set whose block failed half way may hold a node map that was
+    # never reset: it is dropped, not returned to the pool)
+    blk = _sample_finish(_sample_start(graph, seeds, fanouts, seed, gather_features, st))
+    cache.release(st)
+    return blk
 
 
 def _sample_finish(p: _Pending) -> Batch:
@@ -362,13 +363,17 @@ def _sample_finish(p: _Pending) -> Batch:
         # the row gather copies 32-bit words: bf16 rows are viewed as float32 pairs
         xa = graph.x.view(torch.float32) if graph.x.dtype == torch.bfloat16 else graph.x
         xw = x.view(torch.float32) if x.dtype == torch.bfloat16 else x
+    # the block's CSR comes out of the relabelling (no CSR build in the model's forward)
+    rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(e, 0), dtype=torch.int32, device=dev)
     _lib.check(lib.ngnn_sample_block_finish(
         fan, H, B, n, e, _lib.ptr(cache.node_map), graph.num_nodes, _lib.ptr(ws), ws.numel(),
         _lib.ptr(n_id), _lib.ptr(edge_index), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(xa),
-        xa.stride(0), xa.size(1), _lib.ptr(xw), xw.stride(0) if xw is not None else 0, st),
-        "ngnn_sample_block_finish")
+        xa.stride(0), xa.size(1), _lib.ptr(xw), xw.stride(0) if xw is not None else 0, n_active,
+        _lib.ptr(rowptr), _lib.ptr(col), st), "ngnn_sample_block_finish")
     # built here: ids are in range and targets non-decreasing -> no probe needed
-    hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active)
+    hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active,
+                    csr=CSR(rowptr, col, n))
     # further node attributes (batch.yhn ...): one device gather each, on this stream
     extra = {k: v.index_select(0, n_id) for k, v in graph.node_attrs.items()}
     return Batch(x, y, edge_index, n_id, B, **extra)
@@ -497,7 +502,8 @@ class NeighborLoader:
         finally:
             # a pass left early (break, close, garbage collection) still holds
             # a block sampled ahead: finish it, which resets the node map,
-            # before the state set goes back to the pool
+            # before the state set goes back to the pool (a set whose finish
+            # raised is dropped instead: its node map may not be clean)
             with torch.cuda.stream(side):
                 if pending is not None:
                     _sample_finish(pending)

@@ -92,13 +92,34 @@ def test_argument_errors_return_before_launch():
     assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, 1, 1, ws - 1, 1, None) == -6
     assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, None, 1, ws, 1, None) == -1
     assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1023, 0, 1, 100, 1, ws, 1, 1, None, None,
-                                        None, 0, 0, None, 0, None) == -3
+                                        None, 0, 0, None, 0, 0, None, None, None) == -3
+    # ABI 18: the CSR outputs come as a pair (col may be absent only without edges)
+    assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1024, 5, 1, 100, 1, ws, 1, 1, None, None,
+                                        None, 0, 0, None, 0, 0, 16, None, None) == -1
     # two-layer backward: operands past the 32-bit buffer range are refused
     # before any launch: n_rows x ldh x 4 B > 3.75 GiB
     big = 1 << 22
     assert lib.ngnn_sage2_bwd(16, 47, 47, 16, 16, 256, 16, 1024, 1.0, 16, None, None, None, 0, 100, 100,
                               16, 100, 16, 16, big, 16, 16, 0, 16, 16, 16, 16, 16, 16, None, None,
                               256, 1 << 40, None) == -5
+    # ABI 18: a root-free stack passes BOTH dW_r0 and dW_r1 as NULL (x may be
+    # NULL then); one of them alone is an argument error, as is an indexed x
+    # without a root term -- refused before any launch
+    assert lib.ngnn_sage2_bwd(16, 47, 47, 16, 16, 256, 16, 256, 1.0, None, None, None, None, 0, 100, 100,
+                              16, 100, 16, 16, 1024, 16, 16, 0, 16, 16, None, 16, 16, 16, None, None,
+                              256, 1 << 40, None) == -1
+    assert lib.ngnn_sage2_bwd(16, 47, 47, 16, 16, 256, 16, 256, 1.0, None, None, None, 16, 1, 100, 100,
+                              16, 100, 16, 16, 1024, 16, 16, 0, 16, 16, None, 16, 16, None, None, None,
+                              256, 1 << 40, None) == -1
+    # ABI 18: the mixed-dtype cast refuses a bad dtype / an in-place width change
+    import ctypes as ct
+    one = (ct.c_void_p * 1)(16)
+    n1 = (ct.c_int64 * 1)(4)
+    f32, bf16, bad = (ct.c_int32 * 1)(0), (ct.c_int32 * 1)(1), (ct.c_int32 * 1)(7)
+    assert lib.ngnn_cast_tensors_ex(1, one, one, n1, f32, bad, 1.0, None) == -2
+    assert lib.ngnn_cast_tensors_ex(1, one, one, n1, f32, bf16, 1.0, None) == -1
+    assert lib.ngnn_cast_tensors_ex(1, one, one, n1, f32, f32, 0.0, None) == -1
+    assert lib.ngnn_cast_tensors_ex(0, None, None, None, None, None, 2.0, None) == 0
     # zero-size work is a no-op success
     assert lib.ngnn_seg_agg_fwd(None, 4, 4, 1, None, 0, 1, 0, None, 4, None) == 0
 

@@ -132,8 +132,12 @@ def test_sample_block_matches_reference(graph, fanouts, bs):
         b = sample_block(graph, seeds, fanouts, seed=s)
         ref, n_active = sample_block_ref(graph, seeds, fanouts, s)
         _assert_same_block(b, ref)
-        from ngnn.block import _hint_for
+        from ngnn.block import _hint_for, build_csr
         assert _hint_for(b.edge_index)[2] == n_active
+        # ABI 18: the sampler's own CSR of the block == the one a build makes
+        csr = _hint_for(b.edge_index)[4]
+        ref_csr = build_csr(b.edge_index[1], b.edge_index[0], b.num_nodes, True)
+        assert torch.equal(csr.rowptr, ref_csr.rowptr) and torch.equal(csr.col, ref_csr.col)
     # the node map is restored after every block
     assert all(bool((st.node_map == -1).all()) for st in _sampler_cache(graph).free)
 
