@@ -18,7 +18,9 @@ all-reduce (N>1) and Adam.  Aggregated edges per step = num_layers x E_batch
 value = sum over ranks of edges / max-over-ranks wall time.
 
 Also reported: epoch_time_s — one full pass over this rank's train seeds
-INCLUDING GPU sampling + feature gather (193 batches at N=1); the roofline
+INCLUDING GPU sampling + feature gather (193 batches at N=1), graph mode over
+the sync-free loader (no host wait per batch; epoch_time_s_sync_loader: the
+synchronous loader, one event wait per batch); the roofline
 of the dominant kernel (HIP events around every launch inside the timed
 region); the reference-equivalent CPU path timed on a bounded sample.
 """
@@ -695,25 +697,40 @@ def main():
                     "step alone is ~0.1 ms of host time per step (torch.profiler, DESIGN.md 8d)"}
 
     # full epoch incl. GPU sampling (this rank's shard)
-    epoch_s = None
+    epoch_s = epoch_sync = None
     if not args.no_epoch:
+        # the synchronous loader: the host reads every block's counts (one
+        # event wait per batch, one batch ahead)
         barrier()
         t1 = time.perf_counter()
         for b in loader:
             run(b)
         barrier()
-        epoch_s = time.perf_counter() - t1
+        epoch_sync = epoch_s = time.perf_counter() - t1
         if graph and ct is None:
             gstep.check_inputs()  # (every batch of the epoch met the slot's contract)
+            # the sync-free loader (ABI 19): blocks in capacity-sized buffers,
+            # counts read by the slot load on the device -- no host wait at all
+            loader_sf = NeighborLoader(graph_data, graph_data.train_idx, fanout, args.batch_size, shuffle=True,
+                                       seed=7, rank=rank, world_size=world,
+                                       gather_features=args.gather == "loader", sync_free=True)
+            barrier()
+            t1 = time.perf_counter()
+            for b in loader_sf:
+                run(b)
+            barrier()
+            epoch_s = time.perf_counter() - t1
+            gstep.check_inputs()
     # the same epoch with the fused x[n_id] gather (batches carry the feature
     # table + n_id, the layer-0 kernels read the rows): no 61 MB row copy per
     # batch in the sampler, a few us more in the step -- reported beside
     epoch_fg = None
     if not args.no_epoch and graph and ct is None and args.gather == "loader" and world == 1:
         from ngnn.graphs import GraphedTrainStep, slot_size
+        b0 = next(iter(NeighborLoader(graph_data, graph_data.train_idx, fanout, args.batch_size, shuffle=True,
+                                      seed=7, rank=rank, world_size=world, gather_features=False)))
         loader_fg = NeighborLoader(graph_data, graph_data.train_idx, fanout, args.batch_size, shuffle=True,
-                                   seed=7, rank=rank, world_size=world, gather_features=False)
-        b0 = next(iter(loader_fg))
+                                   seed=7, rank=rank, world_size=world, gather_features=False, sync_free=True)
         n_cap, e_cap = slot_size(args.batch_size, fanout)
         gstep_fg = GraphedTrainStep(model, opt, args.batch_size, n_cap, e_cap, b0.x.size(1), dev, reducer=reducer)
         gstep_fg.capture(b0.x, b0.edge_index, b0.y)
@@ -761,7 +778,8 @@ def main():
             "launch": "eager" if not graph else "hip-graph replay (step captured once)",
             "feature_gather": ("fused x[n_id] in the layer-0 kernels" if args.gather == "fused"
                                and graph and gstep.x_rows else "loader copies x[n_id]"),
-            "epoch_time_s": None if epoch_s is None else round(epoch_s, 3),
+            "epoch_time_s": None if epoch_s is None else round(epoch_s, 4),
+            "epoch_time_s_sync_loader": None if epoch_sync is None else round(epoch_sync, 4),
             "epoch_time_s_fused_gather": None if epoch_fg is None else round(epoch_fg, 4),
             "epoch_batches_per_rank": len(loader),
             "allreduce": ar,

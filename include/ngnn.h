@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 18
+#define NGNN_ABI_VERSION 19
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -196,7 +196,14 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
  * CSR (edge order kept inside a row; col = the local sources), taken from the
  * relabelling itself, so a consumer of the block builds none.  Since ABI 18
  * the hops run as two launches each (draws + claims, then a single-pass
- * decoupled look-back relabelling) and the outputs, x rows included, as one. */
+ * decoupled look-back relabelling) and the outputs, x rows included, as one.
+ * ABI 19: counts_dev (nullable): the counts array ngnn_sample_block wrote,
+ * read on the DEVICE -- no host read-back: n_nodes / n_edges / n_active are
+ * then the capacities the outputs are sized for (the plan's n_cap / e_cap
+ * at most) and bound the device counts; the first counts[0] rows / counts[1]
+ * edges are written.  edge_index's row stride is n_edges in both modes (the
+ * capacity here).  With ngnn_slot_load's counts_dev this is NeighborLoader's
+ * sync-free pipeline (no host wait per batch). */
 size_t ngnn_sample_block_workspace_bytes(int64_t batch, const int32_t *fanouts, int n_hops);
 int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, int64_t n_graph,
                       const int64_t *seeds, int64_t n_seeds, const int32_t *fanouts, int n_hops,
@@ -207,7 +214,8 @@ int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int64_t n_seeds
                              int64_t n_graph, const void *ws, size_t ws_bytes, int64_t *n_id,
                              int64_t *edge_index, const int64_t *y_all, int64_t *y,
                              const float *x_all, int64_t ldx, int64_t F, float *x, int64_t ldo,
-                             int64_t n_active, int32_t *csr_rowptr, int32_t *csr_col, void *stream);
+                             int64_t n_active, int32_t *csr_rowptr, int32_t *csr_col,
+                             const int32_t *counts_dev, void *stream);
 
 /* ------------------------------------------------------ co-teaching loss
  * CTLoss.forward (src/utils/losses.py:19-49) without its two host argsorts:
@@ -698,6 +706,10 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * (clamped to [0, n_cap]) its edge lands under.  E > 0 needs N >= 1.  The
  * caller checks the word without a device sync (ABI 16: replaces a host
  * read-back of the targets).
+ * counts_dev (ABI 19, nullable): device int32 {N', E', ...} -- the block's
+ * row and edge counts are min(N', N) / min(E', E), read on the device (N / E
+ * are then bounds: the capacity-sized buffers a sync-free sampler wrote;
+ * ld_ei >= E still holds).
  * Replaces the host-side batch hand-over of pipeline.py:152-160 (batch.x,
  * batch.edge_index, batch.y[:batch_size]) for graph replay. */
 #define NGNN_SLOT_UNSORTED 1
@@ -709,7 +721,8 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    uint64_t *seed_state, const float **x_dev, int64_t *r_next, uint32_t gen,
                    int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
                    int32_t *slot_colx, const float *pack_w, int64_t pack_ldw, int64_t pack_fo,
-                   int64_t pack_k, float *pack_dst, int32_t *err, void *stream);
+                   int64_t pack_k, float *pack_dst, int32_t *err, const int32_t *counts_dev,
+                   void *stream);
 
 #ifdef __cplusplus
 }

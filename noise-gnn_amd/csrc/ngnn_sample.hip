@@ -192,63 +192,93 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// One hop's relabelling in ONE launch: each tile (kSbTile lanes = (position,
-// draw) pairs in order, tiles in ticket order -- a tile only waits for tiles
-// that already run) takes its draws' first-appearance flags, counts its
-// (edges, new nodes) by wave ballots, publishes them, finds its exclusive
-// prefix by a decoupled look-back over the tiles before it -- wave 0 reads 64
-// predecessors' words at once -- then assigns the new local ids (map, nid) in
-// (position, draw) order and writes the hop's edges (global sources, local
-// targets) and row pointers.  The last tile writes the next hop's state.
+// One hop's relabelling in ONE launch: each tile (kSbTile x kSbItems lanes
+// = (position, draw) pairs in order, four per thread; tiles in ticket order
+// -- a tile only waits for tiles that already run) takes its draws' first-
+// appearance flags, counts its (edges, new nodes) by wave ballots, publishes
+// them, finds its exclusive prefix by a decoupled look-back over the tiles
+// before it -- wave 0 reads 64 predecessors' words at once -- then assigns
+// the new local ids (map, nid) in (position, draw) order and writes the hop's
+// edges (global sources, local targets) and row pointers.  The last tile
+// writes the next hop's state.  (Device-scope atomics on one address -- the
+// ticket -- serialise at the memory side, ~0.1 us each: 4096-lane tiles keep
+// them to ~60 per products hop-2 launch; 1024-lane tiles took ~30 us.  A
+// ticket-free blockIdx order stalled whenever the training step held CUs.)
+constexpr int kSbItems = 4;
 template <int KF>
 __global__ __launch_bounds__(kSbTile) void k_sb_assign_lb(
     int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
     int32_t *__restrict__ map, int64_t n_graph, int fanout, uint64_t *__restrict__ lb, int nblk,
     int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst, int32_t *__restrict__ rp) {
-    constexpr int NW = kSbTile / 64;
+    constexpr int NW = kSbTile / 64, NC = NW * kSbItems;  // (item, wave) chunks of 64 lanes, in order
+    static_assert(NC == 64, "one wave scans the chunk counts");
     __shared__ int s_tile, s_pe, s_pn;
-    __shared__ int s_we[NW], s_wn[NW];
+    __shared__ int s_ce[NC], s_cn[NC];
     if (threadIdx.x == 0)
         s_tile = static_cast<int>(atomicAdd(reinterpret_cast<unsigned long long *>(lb + nblk), 1ull));
     __syncthreads();
     const int tile = s_tile;
-    const int gt = tile * kSbTile + threadIdx.x;
-    const int i = gt / KF, j = gt % KF;
     const int lo = hs[0], hi = hs[1], e0 = hs[2];
     const int nf = hi - lo;
-    bool has = false, fresh = false;
-    int32_t u = 0;
-    if (i < nf && j < cnt[i]) {
-        has = true;
-        u = cand[i * fanout + j];
-        // race-free although other tiles write map[] meanwhile: only the
-        // position that won u's claim ever writes map[u] (after reading
-        // it), and for every other position the flag is false whatever
-        // map[u] reads
-        const int32_t c = map[n_graph + u], m = map[u];
-        fresh = c == INT32_MAX - (i * fanout + j) && m < 0;
-    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t be = __ballot(has), bn = __ballot(fresh);
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    int xe = __popcll(be & below), xn = __popcll(bn & below);
-    if (lane == 0) {
-        s_we[wv] = __popcll(be);
-        s_wn[wv] = __popcll(bn);
+    bool has[kSbItems], fresh[kSbItems];
+    int32_t u[kSbItems];
+    int k[kSbItems];
+#pragma unroll
+    for (int t = 0; t < kSbItems; ++t) {
+        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
+        const int i = gt / KF;
+        k[t] = i < nf ? cnt[i] : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < kSbItems; ++t) {
+        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
+        const int i = gt / KF, j = gt % KF;
+        has[t] = j < k[t];
+        u[t] = has[t] ? cand[i * fanout + j] : 0;
+    }
+    int32_t c[kSbItems], m[kSbItems];
+#pragma unroll
+    for (int t = 0; t < kSbItems; ++t)
+        if (has[t]) {
+            // race-free although other tiles write map[] meanwhile: only the
+            // position that won u's claim ever writes map[u] (after reading
+            // it), and for every other position the flag is false whatever
+            // map[u] reads
+            c[t] = map[n_graph + u[t]];
+            m[t] = map[u[t]];
+        }
+    int xe[kSbItems], xn[kSbItems];
+#pragma unroll
+    for (int t = 0; t < kSbItems; ++t) {
+        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
+        const int i = gt / KF, j = gt % KF;
+        fresh[t] = has[t] && c[t] == INT32_MAX - (i * fanout + j) && m[t] < 0;
+        const uint64_t be = __ballot(has[t]), bn = __ballot(fresh[t]);
+        xe[t] = __popcll(be & below);
+        xn[t] = __popcll(bn & below);
+        if (lane == 0) {
+            s_ce[t * NW + wv] = __popcll(be);
+            s_cn[t * NW + wv] = __popcll(bn);
+        }
     }
     __syncthreads();
-    int ae = 0, an = 0;  // tile totals; xe / xn += the waves before this one
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const int a = s_we[w], c = s_wn[w];
-        if (w < wv) {
-            xe += a;
-            xn += c;
-        }
-        ae += a;
-        an += c;
-    }
     if (wv == 0) {
+        // exclusive scan of the 64 chunk counts (chunk = lane), tile totals
+        const int ce = s_ce[lane], cn = s_cn[lane];
+        int ie = ce, in = cn;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int pe_ = __shfl_up(ie, o), pn_ = __shfl_up(in, o);
+            if (lane >= o) {
+                ie += pe_;
+                in += pn_;
+            }
+        }
+        s_ce[lane] = ie - ce;
+        s_cn[lane] = in - cn;
+        const int ae = __shfl(ie, 63), an = __shfl(in, 63);
         int pe = 0, pn = 0;
         if (tile == 0) {
             if (lane == 0)
@@ -290,17 +320,22 @@ __global__ __launch_bounds__(kSbTile) void k_sb_assign_lb(
         }
     }
     __syncthreads();
-    const int e = e0 + s_pe + xe;
-    if (has) {
-        esrc[e] = u;
-        edst[e] = lo + i;
+#pragma unroll
+    for (int t = 0; t < kSbItems; ++t) {
+        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
+        const int i = gt / KF, j = gt % KF;
+        const int e = e0 + s_pe + s_ce[t * NW + wv] + xe[t];
+        if (has[t]) {
+            esrc[e] = u[t];
+            edst[e] = lo + i;
+        }
+        if (fresh[t]) {
+            const int n = hi + s_pn + s_cn[t * NW + wv] + xn[t];
+            map[u[t]] = n;
+            nid[n] = u[t];
+        }
+        if (j == 0 && i < nf) rp[lo + i] = e;  // (frontier row lo + i's edges start here: CSR row pointer)
     }
-    if (fresh) {
-        const int n = hi + s_pn + xn;
-        map[u] = n;
-        nid[n] = u;
-    }
-    if (j == 0 && i < nf) rp[lo + i] = e;  // (frontier row lo + i's edges start here: CSR row pointer)
 }
 
 // the last hop's edges relabelled; counts = {n_total, e_total, n_active, -}
@@ -326,6 +361,10 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_tail(const int32_t *__restrict_
 // target-grouped CSR (row pointers from the relabelling -- rows past the last
 // frontier have no edges -- and the relabelled sources as int32), so a
 // consumer builds none
+// cnt (ABI 19, nullable): the block's {n, E, n_active} read on the device
+// (the sampler's counts; n / E / n_act then hold the capacities the grid and
+// the outputs are sized for, and bound the device values); ld_ei: edge_index's
+// row stride
 struct SbOut {
     const int32_t *nid, *esrc, *edst, *rp;
     int n, E, n_act;
@@ -335,7 +374,16 @@ struct SbOut {
     const int64_t *y_all;
     int64_t *y, *ei;
     int32_t *csr_rp, *csr_col;
+    int64_t ld_ei;
+    const int32_t *cnt;
 };
+__device__ __forceinline__ void sb_counts(SbOut &o) {
+    if (o.cnt) {
+        o.n = min(o.cnt[0], o.n);
+        o.E = min(o.cnt[1], o.E);
+        o.n_act = min(o.cnt[2], o.n);
+    }
+}
 __device__ __forceinline__ void sb_emit(const SbOut &o, int64_t t) {
     if (t < o.n) {
         const int32_t u = o.nid[t];
@@ -346,13 +394,15 @@ __device__ __forceinline__ void sb_emit(const SbOut &o, int64_t t) {
     }
     if (t < o.E) {
         o.ei[t] = o.esrc[t];
-        o.ei[o.E + t] = o.edst[t];
+        o.ei[o.ld_ei + t] = o.edst[t];
         if (o.csr_col) o.csr_col[t] = o.esrc[t];
     }
-    if (o.csr_rp && t <= o.n) o.csr_rp[t] = t < o.n_act ? o.rp[t] : o.E;
+    // (no edges: every row pointer is 0 -- with no hops rp was never written)
+    if (o.csr_rp && t <= o.n) o.csr_rp[t] = (t < o.n_act && o.E > 0) ? o.rp[t] : o.E;
 }
 
 __global__ __launch_bounds__(kSbBlock) void k_sb_finish(SbOut o) {
+    sb_counts(o);
     const int64_t stride = (int64_t)gridDim.x * kSbBlock;
     for (int64_t t = blockIdx.x * (int64_t)kSbBlock + threadIdx.x; t <= max(o.n, o.E); t += stride) sb_emit(o, t);
 }
@@ -376,6 +426,7 @@ __global__ __launch_bounds__(kSbBlock) void k_gather_rows4(const float *__restri
 // reset -- the gather reads nid only, so the two roles need no order)
 __global__ __launch_bounds__(kSbBlock) void k_sb_out(const float *__restrict__ x_all, int64_t ldx, int f4,
                                                      float *__restrict__ x, int64_t ldo, int gx, SbOut o) {
+    sb_counts(o);
     if (static_cast<int>(blockIdx.x) < gx) {
         const int total = o.n * f4;
         for (int t = blockIdx.x * kSbBlock + threadIdx.x; t < total; t += gx * kSbBlock) {
@@ -420,7 +471,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
         cand += nf * f;
         cntn += nf;
         if (nf * sb_kf(static_cast<int>(f)) > INT32_MAX / 2) return false;  // (lane indices)
-        nblk = std::max<int64_t>(nblk, ceil_div(nf * sb_kf(static_cast<int>(f)), kSbTile));
+        nblk = std::max<int64_t>(nblk, ceil_div(nf * sb_kf(static_cast<int>(f)), kSbTile * kSbItems));
         e += nf * f;
         nf *= f;
         n += nf;
@@ -502,7 +553,7 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
         int32_t *hs = w.state + 4 * h;
         const int64_t nf = p.nf_cap[h];
         // lane-per-draw grids: kf lanes per frontier position
-        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbTile)));
+        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbTile * kSbItems)));
         const int sgrid = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbBlock)));
         int32_t *cand = w.cand + p.cand_off[h], *cnt = w.cnt + p.cnt_off[h];
         // the per-hop seed of ngnn_sample_hop's callers (loader.sample_block)
@@ -536,7 +587,7 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
                                         int64_t *n_id, int64_t *edge_index, const int64_t *y_all,
                                         int64_t *y, const float *x_all, int64_t ldx, int64_t F,
                                         float *x, int64_t ldo, int64_t n_active, int32_t *csr_rowptr,
-                                        int32_t *csr_col, void *stream) {
+                                        int32_t *csr_col, const int32_t *counts_dev, void *stream) {
     SbPlan p;
     NGNN_RETURN_IF(n_hops < 0 || (n_hops > 0 && !fanouts), NGNN_E_ARG);
     NGNN_RETURN_IF(!sb_plan(n_seeds, fanouts, n_hops, &p), NGNN_E_SHAPE);
@@ -552,7 +603,8 @@ extern "C" int ngnn_sample_block_finish(const int32_t *fanouts, int n_hops, int6
     hipStream_t st = as_stream(stream);
     const SbWs w = sb_carve(const_cast<void *>(ws), p);
     const SbOut o{w.nid, w.esrc, w.edst, w.rp, static_cast<int>(n_nodes), static_cast<int>(n_edges),
-                  static_cast<int>(n_active), node_map, n_graph, n_id, y_all, y, edge_index, csr_rowptr, csr_col};
+                  static_cast<int>(n_active), node_map, n_graph, n_id, y_all, y, edge_index, csr_rowptr, csr_col,
+                  n_edges, counts_dev};
     const int64_t work = std::max<int64_t>(std::max<int64_t>(n_nodes, n_edges), 1) + 1;
     const unsigned gf = static_cast<unsigned>(std::min<int64_t>(ceil_div(work, kSbBlock), 4096));
     const bool vec = x && n_nodes > 0 && F % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned(x_all, 16) &&

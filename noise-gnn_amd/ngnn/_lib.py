@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 OK = 0
 SLOT_UNSORTED = 1  # ngnn_slot_load's err bits (include/ngnn.h NGNN_SLOT_*)
@@ -48,7 +48,7 @@ SIGNATURES = {
     "ngnn_sample_block": (_int, [_p, _p, _i64, _p, _i64, _p, _int, ctypes.c_uint64, _p, _p, _sz, _p,
                                  _p]),
     "ngnn_sample_block_finish": (_int, [_p, _int, _i64, _i64, _i64, _p, _i64, _p, _sz, _p, _p, _p,
-                                        _p, _p, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
+                                        _p, _p, _i64, _i64, _p, _i64, _i64, _p, _p, _p, _p]),
     "ngnn_pack_weight_bytes": (_sz, [_i64, _i64]),
     "ngnn_pack_weight": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "ngnn_pack_weight_ex": (_int, [_p, _p, _i64, _i64, _i64, _i64, _int, _p, _p]),
@@ -65,7 +65,7 @@ SIGNATURES = {
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                               _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p, _p,
-                              _p, _p, _i64, _i64, _i64, _p, _p, _p]),
+                              _p, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
@@ -168,6 +168,22 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_raw_stream = None
+
+
 def stream_handle(device=None) -> int:
+    """The raw hipStream_t of torch's current stream on `device` (torch's C
+    accessor: torch.cuda.current_stream builds a Stream object per call,
+    a few us of the host-bound eager step each)."""
+    global _raw_stream
     import torch
-    return torch.cuda.current_stream(device).cuda_stream
+    if _raw_stream is None:
+        _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None) or (
+            lambda i: torch.cuda.current_stream(i).cuda_stream)
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _raw_stream(idx)

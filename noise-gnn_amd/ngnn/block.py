@@ -239,4 +239,9 @@ def _hint_for(edge_index):
 def get_block(edge_index, num_nodes: int) -> Block:
     if isinstance(edge_index, Block):
         return edge_index
+    if getattr(edge_index, "_ngnn_counts", None) is not None:
+        # a NeighborLoader(sync_free=True) batch: capacity-sized buffers whose
+        # real extent only the device knows (ABI 19)
+        raise ValueError("a sync_free NeighborLoader batch feeds GraphedTrainStep only; "
+                         "use NeighborLoader(sync_free=False) for eager training")
     return block_cache.get(edge_index, num_nodes)

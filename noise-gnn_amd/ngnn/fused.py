@@ -487,7 +487,8 @@ def sage2_forward(x, block: Block, reduce: str, params, p_drop: float, seed: int
     root0 False: layer 0 has no root term (a SimpleGCN stack, sage2_params'
     zero W_r0): the kernels skip x entirely (ABI 17, wr0 NULL) -- not with the
     fused x[n_id] gather, which keeps the zero matrix."""
-    wl0, bl0, wr0, wl1, bl1, wr1 = (q.detach() for q in params)
+    # (pointers and strides only: no detach -- nothing here records autograd)
+    wl0, bl0, wr0, wl1, bl1, wr1 = params
     if wl0.stride(1) != 1 or wr0.stride(0) != wl0.stride(0) or wr0.stride(1) != 1:
         wl0, wr0 = wl0.contiguous(), wr0.contiguous()
     if wl1.stride(1) != 1 or wr1.stride(0) != wl1.stride(0) or wr1.stride(1) != 1:
@@ -1015,14 +1016,19 @@ _IO_DTYPES = (torch.float32, torch.bfloat16)
 def sage_stack_supported(model, x) -> bool:
     if not x.is_cuda or x.dtype not in _IO_DTYPES or x.dim() != 2:
         return False
-    if any(p.dtype not in _IO_DTYPES for p in model.parameters()):
-        return False
     if getattr(model, "use_bn", False):
         return False
-    aggr = model.convs[0].aggr
-    for conv in model.convs:
+    convs = model.convs
+    aggr = convs[0].aggr
+    for conv in convs:
+        # (the convs' own parameter dicts: model.parameters() walks the module
+        # tree, ~10 us of the host-bound eager step)
         if conv.aggr != aggr:
             return False
+        for m in (conv.lin_l, getattr(conv, "lin_r", None)):
+            for p in (() if m is None else m._parameters.values()):
+                if p is not None and p.dtype not in _IO_DTYPES:
+                    return False
     return True
 
 

@@ -109,6 +109,10 @@ class GraphedTrainStep:
         F.cross_entropy(out[:batch_size], y[:batch_size]) (pipeline.py:155-158):
         mean over the real seeds, zero gradient on the other rows."""
         xrow = None
+        # a sync-free NeighborLoader batch (ABI 19): capacity-sized buffers,
+        # the block's row / edge counts on the device -- N and E below are
+        # then their bounds, the slot kernel reads the counts itself
+        cnt = getattr(edge_index, "_ngnn_counts", None)
         if isinstance(x, IndexedRows):
             t, idx = x.table, x.index
             if (zero_copy and self.x_rows and t.dtype == torch.float32 and t.stride(1) == 1
@@ -160,7 +164,7 @@ class GraphedTrainStep:
             *((_lib.ptr(self._pack[0]), self._pack[0].stride(0), self._pack[0].shape[0],
                self._pack[0].shape[1], _lib.ptr(self._pack[1])) if self._pack is not None
               else (None, 0, 0, 0, None)),
-            self._err.data_ptr(), _lib.stream_handle(self.x.device)), "ngnn_slot_load")
+            self._err.data_ptr(), _lib.ptr(cnt), _lib.stream_handle(self.x.device)), "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
         if self._pack is not None:  # this load packed the current W_l: one forward may use it
             self._pack[2].armed = True

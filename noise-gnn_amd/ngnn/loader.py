@@ -242,6 +242,28 @@ class _SamplerState:
         self.counts_host = torch.empty(2, 4, dtype=torch.int32).pin_memory()
         self.released = None  # event after the last launch of the previous lease
 
+    def outputs(self, batch: int, fan, n_hops: int, x: torch.Tensor | None):
+        """Capacity-sized output buffers of a sync-free block (ABI 19): n_id,
+        edge_index [2, e_cap], y, x rows (when gathered) and the device
+        counts -- written by the finish launch with the block's counts read on
+        the device, reused by every block this state samples."""
+        e_cap, nf = 0, int(batch)
+        for h in range(n_hops):
+            nf *= int(fan[h])
+            e_cap += nf
+        n_cap = int(batch) + e_cap
+        key = ("out", batch, tuple(fan[:n_hops]), None if x is None else (x.size(1), x.dtype))
+        buf = self.ws.get(key)
+        if buf is None:
+            dev = self.node_map.device
+            buf = (torch.empty(n_cap, dtype=torch.int64, device=dev),
+                   torch.empty(2, max(e_cap, 1), dtype=torch.int64, device=dev)[:, :e_cap],
+                   torch.empty(n_cap, dtype=torch.int64, device=dev),
+                   None if x is None else torch.empty(n_cap, x.size(1), dtype=x.dtype, device=dev),
+                   torch.zeros(4, dtype=torch.int32, device=dev), n_cap, e_cap)
+            self.ws[key] = buf
+        return buf
+
     def workspace(self, lib, batch: int, fan, n_hops: int) -> torch.Tensor:
         key = (batch, tuple(fan[:n_hops]))
         buf = self.ws.get(key)
@@ -370,13 +392,48 @@ def _sample_finish(p: _Pending) -> Batch:
         fan, H, B, n, e, _lib.ptr(cache.node_map), graph.num_nodes, _lib.ptr(ws), ws.numel(),
         _lib.ptr(n_id), _lib.ptr(edge_index), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(xa),
         xa.stride(0), xa.size(1), _lib.ptr(xw), xw.stride(0) if xw is not None else 0, n_active,
-        _lib.ptr(rowptr), _lib.ptr(col), st), "ngnn_sample_block_finish")
+        _lib.ptr(rowptr), _lib.ptr(col), None, st), "ngnn_sample_block_finish")
     # built here: ids are in range and targets non-decreasing -> no probe needed
     hint_edge_index(edge_index, dst_sorted=True, src_sorted=False, n_active=n_active,
                     csr=CSR(rowptr, col, n))
     # further node attributes (batch.yhn ...): one device gather each, on this stream
     extra = {k: v.index_select(0, n_id) for k, v in graph.node_attrs.items()}
     return Batch(x, y, edge_index, n_id, B, **extra)
+
+
+def _sample_sync_free(graph: Graph, seeds: torch.Tensor, fanouts, seed: int, gather_features: bool,
+                      state: _SamplerState) -> Batch:
+    """One block sampled into the state's capacity-sized buffers with no
+    host read-back (ABI 19): ngnn_sample_block writes the counts on the
+    device, the finish launch reads them there.  The batch's tensors are
+    those buffers (rows / edges past the block's counts are stale) and its
+    edge_index carries the device counts (``_ngnn_counts``) for
+    GraphedTrainStep.load, the one consumer of such a batch."""
+    import ctypes
+    lib = _lib.load()
+    dev = seeds.device
+    s64 = seeds.to(torch.int64).contiguous()
+    B, H = s64.numel(), len(fanouts)
+    fan = (ctypes.c_int32 * max(H, 1))(*[int(k) for k in fanouts])
+    ws = state.workspace(lib, B, fan, H)
+    xa = graph.x if gather_features else None
+    n_id, ei, y, x, cnt, n_cap, e_cap = state.outputs(B, fan, H, xa)
+    st = _lib.stream_handle(dev)
+    _lib.check(lib.ngnn_sample_block(
+        _lib.ptr(graph.rowptr), _lib.ptr(graph.col), graph.num_nodes, _lib.ptr(s64), B, fan, H,
+        int(seed) & (2**64 - 1), _lib.ptr(state.node_map), _lib.ptr(ws), ws.numel(), _lib.ptr(cnt), st),
+        "ngnn_sample_block")
+    xw = xaw = None
+    if gather_features:
+        xaw = xa.view(torch.float32) if xa.dtype == torch.bfloat16 else xa
+        xw = x.view(torch.float32) if x.dtype == torch.bfloat16 else x
+    _lib.check(lib.ngnn_sample_block_finish(
+        fan, H, B, n_cap, e_cap, _lib.ptr(state.node_map), graph.num_nodes, _lib.ptr(ws), ws.numel(),
+        _lib.ptr(n_id), _lib.ptr(ei), _lib.ptr(graph.y), _lib.ptr(y), _lib.ptr(xaw),
+        xaw.stride(0) if xaw is not None else 0, xaw.size(1) if xaw is not None else 0, _lib.ptr(xw),
+        xw.stride(0) if xw is not None else 0, 0, None, None, _lib.ptr(cnt), st), "ngnn_sample_block_finish")
+    ei._ngnn_counts = cnt
+    return Batch(x if gather_features else IndexedRows(graph.x, n_id), y, ei, n_id, B)
 
 
 # id(data) -> (weakref to data, Graph); an entry leaves with its data object
@@ -421,7 +478,8 @@ class NeighborLoader:
 
     def __init__(self, graph, input_nodes=None, num_neighbors=(15, 10), batch_size=1024,
                  shuffle=False, seed: int = 0, rank: int = 0, world_size: int = 1,
-                 drop_last: bool = False, gather_features: bool = True, **_ignored):
+                 drop_last: bool = False, gather_features: bool = True, sync_free: bool = False,
+                 **_ignored):
         if not isinstance(graph, Graph):  # the reference's `data` (pipeline.py:75-92)
             graph = _graph_of(graph)
         self.graph = graph
@@ -436,6 +494,12 @@ class NeighborLoader:
         self.drop_last = drop_last
         # False: batches carry x = IndexedRows(graph.x, n_id) (no row copy)
         self.gather_features = gather_features
+        # True (ABI 19): no host read-back per batch -- blocks land in
+        # capacity-sized buffers with their counts on the device, for
+        # GraphedTrainStep only (see __iter__)
+        self.sync_free = sync_free
+        if sync_free and graph.node_attrs:
+            raise ValueError("sync_free batches carry x, y, edge_index and n_id only")
         self.epoch = 0
 
     def _seeds(self):
@@ -470,6 +534,9 @@ class NeighborLoader:
         side.wait_stream(main)  # seeds (randperm) were made on the main stream
         n = len(self)
         cache = _sampler_cache(self.graph)
+        if self.sync_free:
+            yield from self._iter_sync_free(seeds, ep, n, main, side, cache)
+            return
         with torch.cuda.stream(side):
             state = cache.acquire()  # this pass's node map / workspace / count slots
 
@@ -508,3 +575,41 @@ class NeighborLoader:
                 if pending is not None:
                     _sample_finish(pending)
                 cache.release(state)
+
+    def _iter_sync_free(self, seeds, ep, n, main, side, cache):
+        """sync_free passes (ABI 19): no host wait at all.  Two leased state
+        sets alternate; block b is sampled on the side stream into set b & 1
+        once the consumer's work on block b - 2 (which read that set's
+        buffers) is done -- an event, not a host wait -- and the main stream
+        waits for block b's outputs.  The host only enqueues, so it runs
+        ahead of the device and sampling overlaps the previous step.  The
+        batches' tensors are the sets' capacity-sized buffers with the
+        counts on the device (edge_index._ngnn_counts): GraphedTrainStep
+        consumes them; an eager model refuses them (ngnn.block.get_block).
+        A batch's contents are valid until two batches later."""
+        states, done = [], [None, None]
+        try:
+            with torch.cuda.stream(side):
+                states = [cache.acquire(), cache.acquire()]
+            for b in range(n):
+                s = seeds[b * self.batch_size:(b + 1) * self.batch_size]
+                with torch.cuda.stream(side):
+                    if done[b & 1] is not None:
+                        side.wait_event(done[b & 1])
+                    blk = _sample_sync_free(self.graph, s, self.num_neighbors,
+                                            (self.seed * 7919 + ep) * 100_003 + b * self.world_size + self.rank,
+                                            self.gather_features, states[b & 1])
+                    ready = torch.cuda.Event()
+                    ready.record(side)
+                main.wait_event(ready)
+                yield blk
+                ev = torch.cuda.Event()
+                ev.record(main)  # after the consumer's launches on block b
+                done[b & 1] = ev
+        finally:
+            with torch.cuda.stream(side):
+                for ev in done:
+                    if ev is not None:
+                        side.wait_event(ev)
+                for st in states:
+                    cache.release(st)

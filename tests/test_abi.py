@@ -92,10 +92,10 @@ def test_argument_errors_return_before_launch():
     assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, 1, 1, ws - 1, 1, None) == -6
     assert lib.ngnn_sample_block(1, 1, 100, 1, 1024, fan, 2, 0, None, 1, ws, 1, None) == -1
     assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1023, 0, 1, 100, 1, ws, 1, 1, None, None,
-                                        None, 0, 0, None, 0, 0, None, None, None) == -3
+                                        None, 0, 0, None, 0, 0, None, None, None, None) == -3
     # ABI 18: the CSR outputs come as a pair (col may be absent only without edges)
     assert lib.ngnn_sample_block_finish(fan, 2, 1024, 1024, 5, 1, 100, 1, ws, 1, 1, None, None,
-                                        None, 0, 0, None, 0, 0, 16, None, None) == -1
+                                        None, 0, 0, None, 0, 0, 16, None, None, None) == -1
     # two-layer backward: operands past the 32-bit buffer range are refused
     # before any launch: n_rows x ldh x 4 B > 3.75 GiB
     big = 1 << 22

@@ -236,3 +236,36 @@ def test_loader_from_data_object_carries_yhn():
         if n == 3:
             break
     assert n == 3
+
+
+def test_sync_free_batches_equal_the_synchronous_ones(graph):
+    """NeighborLoader(sync_free=True) (ABI 19): no host read-back per batch --
+    the blocks land in capacity-sized buffers with their counts on the
+    device.  Read back here, every batch's first n rows / E edges equal the
+    same pass of the synchronous loader bit for bit, for both feature modes;
+    an eager model refuses such a batch."""
+    import ngnn
+    for gf in (True, False):
+        kw = dict(batch_size=256, shuffle=True, seed=11, gather_features=gf)
+        ref = list(NeighborLoader(graph, graph.train_idx, [15, 10], **kw))
+        sf = NeighborLoader(graph, graph.train_idx, [15, 10], sync_free=True, **kw)
+        n_b = 0
+        for b, blk in enumerate(sf):
+            torch.cuda.synchronize()
+            n, E = (int(v) for v in blk.edge_index._ngnn_counts[:2].tolist())
+            r = ref[b]
+            assert (n, E) == (r.n_id.numel(), r.edge_index.size(1))
+            assert torch.equal(blk.n_id[:n], r.n_id) and torch.equal(blk.edge_index[:, :E], r.edge_index)
+            assert torch.equal(blk.y[:n], r.y) and blk.batch_size == r.batch_size
+            if gf:
+                assert torch.equal(blk.x[:n], r.x)
+            else:
+                assert torch.equal(blk.x.index[:n], r.n_id)
+            if b == 0:
+                m = ngnn.SAGE(graph.x.size(1), 16, graph.num_classes, 2).to(DEV)
+                with pytest.raises(ValueError, match="sync_free"):
+                    m(blk.x if gf else blk.x.materialize(), blk.edge_index)
+            n_b += 1
+        assert n_b == len(ref)
+    from ngnn.loader import _sampler_cache
+    assert all(bool((st.node_map == -1).all()) for st in _sampler_cache(graph).free)

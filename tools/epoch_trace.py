@@ -34,10 +34,14 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--batches", type=int, default=193)
     ap.add_argument("--marker", default="k_sb_init")
+    ap.add_argument("--skip-last", type=int, default=0,
+                    help="windows to leave out at the end (bench.py's second, fused-gather epoch)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
+    if a.skip_last:
+        idx = idx[:-a.skip_last]
     idx = idx[-(a.batches + 1):]
     win = collections.defaultdict(list)
     names = collections.defaultdict(list)

@@ -28,7 +28,15 @@ def main():
                     help="bench.py config.workload the profiled command ran")
     ap.add_argument("--dtype", default="f32")
     a = ap.parse_args()
-    spans = dict(m.split("=", 1) for m in a.map)
+    # span=substring[@k/m]: of the matching dispatches (in dispatch order),
+    # the k-th of every m (a kernel that runs for several layers of a step)
+    spans, nth = {}, {}
+    for m in a.map:
+        span, sub = m.split("=", 1)
+        if "@" in sub:
+            sub, km = sub.rsplit("@", 1)
+            nth[span] = tuple(int(v) for v in km.split("/"))
+        spans[span] = sub
     # (span, counter) -> {dispatch: summed value}
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
@@ -42,9 +50,17 @@ def main():
     out = {}
     if os.path.exists(a.out):
         out = json.load(open(a.out))
+    def pick(span, counter):
+        d = acc[(span, counter)]
+        if span not in nth:
+            return list(d.values())
+        k, m = nth[span]
+        keys = sorted(d, key=lambda fd: (fd[0], int(fd[1])))
+        return [d[fd] for i, fd in enumerate(keys) if i % m == k]
+
     for span in spans:
-        fv = list(acc[(span, "FETCH_SIZE")].values())
-        wv = list(acc[(span, "WRITE_SIZE")].values())
+        fv = pick(span, "FETCH_SIZE")
+        wv = pick(span, "WRITE_SIZE")
         if not fv or not wv:
             print(f"{span}: no FETCH_SIZE/WRITE_SIZE rows")
             continue

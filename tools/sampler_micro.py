@@ -20,7 +20,8 @@ def trace(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     blocks, cur = [], None
     for r in rows:
-        name = r["Kernel_Name"].split("(")[0].replace("ngnn::", "").replace("(anonymous namespace)::", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        name = name.replace("ngnn::", "")
         if "k_sb_init" in name:
             cur = []
             blocks.append(cur)
