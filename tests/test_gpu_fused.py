@@ -224,6 +224,9 @@ def test_wide_layer_matches_oracle(K, Fo, reduce):
 
 
 KINK_TOL = 1e-5
+# the GPU's ReLU decisions the oracle takes are a handful per layer (VERDICT r5:
+# a bound, so a kernel bug cannot hide behind the override)
+KINK_MAX = 128
 
 
 class _MaskedSAGE(pyg_ref.SAGE):
@@ -262,6 +265,7 @@ class _MaskedSAGE(pyg_ref.SAGE):
                         amb[self.kink_rows:] = False
                     gate = torch.where(amb, gh[:pre.size(0)].cpu() > 0, pre > 0)
                     self.kinks.append(int((amb & (gate != (pre > 0))).sum()))
+                    assert self.kinks[-1] <= KINK_MAX, f"layer {i}: {self.kinks[-1]} ReLU kinks overridden"
                     x = x * gate
                 if self.masks is not None:
                     x = x * self.masks[i] * dropout_scale(self.dropout)
