@@ -256,7 +256,10 @@ class _SamplerState:
         buf = self.ws.get(key)
         if buf is None:
             dev = self.node_map.device
-            buf = (torch.empty(n_cap, dtype=torch.int64, device=dev),
+            # (n_id zero-filled once: entries past a block's count always hold
+            # valid node ids -- 0 or an earlier block's -- so nothing that
+            # indexes with the whole buffer can leave the table)
+            buf = (torch.zeros(n_cap, dtype=torch.int64, device=dev),
                    torch.empty(2, max(e_cap, 1), dtype=torch.int64, device=dev)[:, :e_cap],
                    torch.empty(n_cap, dtype=torch.int64, device=dev),
                    None if x is None else torch.empty(n_cap, x.size(1), dtype=x.dtype, device=dev),

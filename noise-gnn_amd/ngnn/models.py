@@ -23,6 +23,15 @@ from .loader import IndexedRows
 from .nn import GCNConv, SAGEConv
 
 
+def _refuse_sync_free(edge_index):
+    """A NeighborLoader(sync_free=True) batch holds capacity-sized buffers
+    whose real extent only the device knows (ABI 19): refused before anything
+    reads them (ngnn.block.get_block checks again for direct conv calls)."""
+    if getattr(edge_index, "_ngnn_counts", None) is not None:
+        raise ValueError("a sync_free NeighborLoader batch feeds GraphedTrainStep only; "
+                         "use NeighborLoader(sync_free=False) for eager training")
+
+
 def _dropout_seed(model, x, block):
     """(host seed, device seed word) of a fused stack's hash dropout."""
     seed, seed_dev = 0, None
@@ -63,6 +72,7 @@ class SAGE(nn.Module):
             conv.reset_parameters()
 
     def forward(self, x, edge_index):
+        _refuse_sync_free(edge_index)
         if isinstance(x, IndexedRows):  # eager: gather the rows (graph replays fuse it)
             x = x.materialize()
         block = get_block(edge_index, x.size(0))
@@ -111,6 +121,7 @@ class SimpleGCN(nn.Module):
             conv.reset_parameters()
 
     def forward(self, x, edge_index):
+        _refuse_sync_free(edge_index)
         if isinstance(x, IndexedRows):  # eager: gather the rows (graph replays fuse it)
             x = x.materialize()
         block = get_block(edge_index, x.size(0))
