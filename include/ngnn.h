@@ -194,9 +194,10 @@ int ngnn_sample_hop(const int64_t *g_rowptr, const int32_t *g_col, const int64_t
  * ABI 18: n_active (counts[2]) and, nullable as a pair, csr_rowptr
  * int32[n_nodes + 1] / csr_col int32[n_edges]: the block's target-grouped
  * CSR (edge order kept inside a row; col = the local sources), taken from the
- * relabelling itself, so a consumer of the block builds none.  Since ABI 18
- * the hops run as two launches each (draws + claims, then a single-pass
- * decoupled look-back relabelling) and the outputs, x rows included, as one.
+ * relabelling itself, so a consumer of the block builds none.  The hops run
+ * as three launches each (one lane per draw: draws + claims; first-
+ * appearance counts; the relabelling writes) and the outputs, x rows
+ * included, as one.
  * ABI 19: counts_dev (nullable): the counts array ngnn_sample_block wrote,
  * read on the DEVICE -- no host read-back: n_nodes / n_edges / n_active are
  * then the capacities the outputs are sized for (the plan's n_cap / e_cap

@@ -90,7 +90,8 @@ struct SbWs {  // carved from the caller's workspace
     int32_t *state;  // [4 * (H + 1)]
     int32_t *cand;   // [sum_h nf_cap_h * f_h]  global ids of each hop's draws
     int32_t *cnt;    // [sum_h nf_cap_h]
-    uint64_t *lb;    // [max_h nblk_h + 1]     per-tile look-back words + the tile ticket
+    uint64_t *masks;  // [max_h ntile_h][16][2]  per wave chunk: (drawn, first appearance) lane masks
+    int32_t *tcnt;    // [max_h ntile_h][2]      per tile: (edges, new nodes)
     int32_t *nid;    // [n_cap]                local -> global
     int32_t *esrc;   // [e_cap]
     int32_t *edst;   // [e_cap]
@@ -141,23 +142,22 @@ __device__ __forceinline__ int floyd_lane(int64_t d, int fanout, uint64_t seed, 
     return dup ? jw : t;
 }
 
-constexpr int kSbTile = 1024;  // k_sb_assign_lb's tile: kSbTile / KF frontier positions
+constexpr int kSbTile = 1024;  // k_sb_count / k_sb_write's tile: kSbTile / KF frontier positions
+constexpr int kSbChunks = kSbTile / 64;  // its wave chunks
 
 __host__ __device__ constexpr int sb_kf(int f) { return f <= 8 ? 8 : f <= 16 ? 16 : f <= 32 ? 32 : 64; }
 
 // draw j of frontier node i -> cand[i*f + j]; claims first appearances.
 // Also (one launch fewer per hop): the previous hop's edges relabelled to
-// local ids (its assignment is complete: the launch before), and this hop's
-// look-back words and tile ticket cleared for k_sb_assign_lb.
+// local ids (its assignment is complete: the launch before).
 template <int KF>
 __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ gcol, int64_t n_graph,
     const int32_t *__restrict__ hs, const int32_t *__restrict__ nid, int fanout, uint64_t seed,
     int32_t *__restrict__ cand, int32_t *__restrict__ cnt, int32_t *__restrict__ map,
-    const int32_t *__restrict__ hs_prev, int32_t *__restrict__ esrc, uint64_t *__restrict__ lb, int nblk) {
+    const int32_t *__restrict__ hs_prev, int32_t *__restrict__ esrc) {
     const int gt = blockIdx.x * kSbBlock + threadIdx.x;
     const int stride = gridDim.x * kSbBlock;
-    for (int t = gt; t <= nblk; t += stride) lb[t] = 0;  // (lb[nblk]: the tile ticket)
     if (hs_prev)  // edges of the previous hop [hs_prev[2], hs_prev[6])
         for (int e = hs_prev[2] + gt; e < hs_prev[6]; e += stride) esrc[e] = map[esrc[e]];
     const int lo = hs[0], hi = hs[1];
@@ -179,163 +179,128 @@ __global__ __launch_bounds__(kSbBlock) void k_sb_sample(
     if (j == 0) cnt[i] = k;
 }
 
-// look-back word of a tile: status (bits 62-63: 1 aggregate, 2 inclusive
-// prefix) | new nodes (bits 31-61) | edges (bits 0-30); counts < 2^30
-// (sb_plan bounds n, e by INT32_MAX / 2)
-constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
-__device__ __forceinline__ uint64_t lb_word(uint64_t st, int e, int n) {
-    return st | (static_cast<uint64_t>(n) << 31) | static_cast<uint64_t>(e);
-}
-
 __device__ __forceinline__ int wave_sum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
 
-// One hop's relabelling in ONE launch: each tile (kSbTile x kSbItems lanes
-// = (position, draw) pairs in order, four per thread; tiles in ticket order
-// -- a tile only waits for tiles that already run) takes its draws' first-
-// appearance flags, counts its (edges, new nodes) by wave ballots, publishes
-// them, finds its exclusive prefix by a decoupled look-back over the tiles
-// before it -- wave 0 reads 64 predecessors' words at once -- then assigns
-// the new local ids (map, nid) in (position, draw) order and writes the hop's
-// edges (global sources, local targets) and row pointers.  The last tile
-// writes the next hop's state.  (Device-scope atomics on one address -- the
-// ticket -- serialise at the memory side, ~0.1 us each: 4096-lane tiles keep
-// them to ~60 per products hop-2 launch; 1024-lane tiles took ~30 us.  A
-// ticket-free blockIdx order stalled whenever the training step held CUs.)
-constexpr int kSbItems = 4;
+// One hop's relabelling in two launches with no waiting between workgroups
+// (round 6; the single-pass decoupled look-back before it spun on its
+// predecessors' words, ~17-34 us alone and ~60 us while the training step
+// held the CUs).  A tile is kSbTile lanes = (position, draw) pairs in order.
+// k_sb_count: each draw's first-appearance flag (its position won the claim
+// and the node has no local id yet), per wave chunk the two lane masks, per
+// tile the (edges, new nodes) totals.  The claims are final (the launch
+// before), and nothing writes map[] here -- race-free by construction.
 template <int KF>
-__global__ __launch_bounds__(kSbTile) void k_sb_assign_lb(
-    int32_t *__restrict__ hs, const int32_t *__restrict__ cand, const int32_t *__restrict__ cnt,
-    int32_t *__restrict__ map, int64_t n_graph, int fanout, uint64_t *__restrict__ lb, int nblk,
-    int32_t *__restrict__ nid, int32_t *__restrict__ esrc, int32_t *__restrict__ edst, int32_t *__restrict__ rp) {
-    constexpr int NW = kSbTile / 64, NC = NW * kSbItems;  // (item, wave) chunks of 64 lanes, in order
-    static_assert(NC == 64, "one wave scans the chunk counts");
-    __shared__ int s_tile, s_pe, s_pn;
-    __shared__ int s_ce[NC], s_cn[NC];
-    if (threadIdx.x == 0)
-        s_tile = static_cast<int>(atomicAdd(reinterpret_cast<unsigned long long *>(lb + nblk), 1ull));
+__global__ __launch_bounds__(kSbTile) void k_sb_count(const int32_t *__restrict__ hs, const int32_t *__restrict__ cand,
+                                                      const int32_t *__restrict__ cnt, const int32_t *__restrict__ map,
+                                                      int64_t n_graph, int fanout, uint64_t *__restrict__ masks,
+                                                      int32_t *__restrict__ tcnt) {
+    __shared__ int s_e[kSbChunks], s_n[kSbChunks];
+    const int tile = blockIdx.x;
+    const int gt = tile * kSbTile + threadIdx.x;
+    const int i = gt / KF, j = gt % KF;
+    const int nf = hs[1] - hs[0];
+    bool has = false, fresh = false;
+    if (i < nf && j < cnt[i]) {
+        has = true;
+        const int32_t u = cand[i * fanout + j];
+        const int32_t c = map[n_graph + u], m = map[u];
+        fresh = c == INT32_MAX - (i * fanout + j) && m < 0;
+    }
+    const uint64_t be = __ballot(has), bn = __ballot(fresh);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) {
+        masks[2 * (tile * kSbChunks + wv)] = be;
+        masks[2 * (tile * kSbChunks + wv) + 1] = bn;
+        s_e[wv] = __popcll(be);
+        s_n[wv] = __popcll(bn);
+    }
     __syncthreads();
-    const int tile = s_tile;
+    if (threadIdx.x == 0) {
+        int e = 0, n = 0;
+#pragma unroll
+        for (int w = 0; w < kSbChunks; ++w) {
+            e += s_e[w];
+            n += s_n[w];
+        }
+        tcnt[2 * tile] = e;
+        tcnt[2 * tile + 1] = n;
+    }
+}
+
+// k_sb_write: the tile's exclusive prefix -- the totals of the tiles before
+// it, summed by one wave -- and its chunks' prefixes (one wave scans the
+// sixteen), then the new local ids (map, nid) in (position, draw) order, the
+// hop's edges (global sources, local targets) and row pointers.  The last
+// tile writes the next hop's state.
+template <int KF>
+__global__ __launch_bounds__(kSbTile) void k_sb_write(int32_t *__restrict__ hs, const int32_t *__restrict__ cand,
+                                                      int32_t *__restrict__ map, int fanout,
+                                                      const uint64_t *__restrict__ masks,
+                                                      const int32_t *__restrict__ tcnt, int ntile,
+                                                      int32_t *__restrict__ nid, int32_t *__restrict__ esrc,
+                                                      int32_t *__restrict__ edst, int32_t *__restrict__ rp) {
+    __shared__ int s_pe, s_pn;
+    __shared__ int s_ce[kSbChunks], s_cn[kSbChunks];
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int lo = hs[0], hi = hs[1], e0 = hs[2];
     const int nf = hi - lo;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    bool has[kSbItems], fresh[kSbItems];
-    int32_t u[kSbItems];
-    int k[kSbItems];
-#pragma unroll
-    for (int t = 0; t < kSbItems; ++t) {
-        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
-        const int i = gt / KF;
-        k[t] = i < nf ? cnt[i] : 0;
-    }
-#pragma unroll
-    for (int t = 0; t < kSbItems; ++t) {
-        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
-        const int i = gt / KF, j = gt % KF;
-        has[t] = j < k[t];
-        u[t] = has[t] ? cand[i * fanout + j] : 0;
-    }
-    int32_t c[kSbItems], m[kSbItems];
-#pragma unroll
-    for (int t = 0; t < kSbItems; ++t)
-        if (has[t]) {
-            // race-free although other tiles write map[] meanwhile: only the
-            // position that won u's claim ever writes map[u] (after reading
-            // it), and for every other position the flag is false whatever
-            // map[u] reads
-            c[t] = map[n_graph + u[t]];
-            m[t] = map[u[t]];
-        }
-    int xe[kSbItems], xn[kSbItems];
-#pragma unroll
-    for (int t = 0; t < kSbItems; ++t) {
-        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
-        const int i = gt / KF, j = gt % KF;
-        fresh[t] = has[t] && c[t] == INT32_MAX - (i * fanout + j) && m[t] < 0;
-        const uint64_t be = __ballot(has[t]), bn = __ballot(fresh[t]);
-        xe[t] = __popcll(be & below);
-        xn[t] = __popcll(bn & below);
-        if (lane == 0) {
-            s_ce[t * NW + wv] = __popcll(be);
-            s_cn[t * NW + wv] = __popcll(bn);
-        }
-    }
-    __syncthreads();
     if (wv == 0) {
-        // exclusive scan of the 64 chunk counts (chunk = lane), tile totals
-        const int ce = s_ce[lane], cn = s_cn[lane];
-        int ie = ce, in = cn;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int pe_ = __shfl_up(ie, o), pn_ = __shfl_up(in, o);
-            if (lane >= o) {
-                ie += pe_;
-                in += pn_;
-            }
-        }
-        s_ce[lane] = ie - ce;
-        s_cn[lane] = in - cn;
-        const int ae = __shfl(ie, 63), an = __shfl(in, 63);
         int pe = 0, pn = 0;
-        if (tile == 0) {
-            if (lane == 0)
-                __hip_atomic_store(lb, lb_word(kLbPre, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0)
-                __hip_atomic_store(lb + tile, lb_word(kLbAgg, ae, an), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            for (int p = tile - 1;;) {  // window: predecessors p, p-1, ..., p-63 (lane order)
-                const int q = p - lane;
-                const uint64_t w = q >= 0 ? __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
-                                          : kLbPre;  // (before tile 0: an empty prefix)
-                const uint64_t st = w & (3ull << 62);
-                const uint64_t pre = __ballot(st == kLbPre), idle = __ballot(st == 0);
-                const int fp = pre ? __builtin_ctzll(pre) : 64;  // nearest inclusive prefix
-                const uint64_t upto = fp >= 63 ? ~0ull : ((2ull << fp) - 1);
-                if (idle & upto) {  // a predecessor before it has not published yet
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const bool take = lane <= fp;
-                pe += wave_sum(take ? static_cast<int>(w & 0x7FFFFFFFull) : 0);
-                pn += wave_sum(take ? static_cast<int>((w >> 31) & 0x7FFFFFFFull) : 0);
-                if (fp < 64) break;
-                p -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(lb + tile, lb_word(kLbPre, pe + ae, pn + an), __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        for (int b = lane; b < tile; b += 64) {
+            pe += tcnt[2 * b];
+            pn += tcnt[2 * b + 1];
         }
+        pe = wave_sum(pe);
+        pn = wave_sum(pn);
         if (lane == 0) {
             s_pe = pe;
             s_pn = pn;
-            if (tile == nblk - 1) {  // the next hop's state: this hop's new nodes, its edges' end
+            if (tile == ntile - 1) {  // the next hop's state: this hop's new nodes, its edges' end
                 hs[4] = hi;
-                hs[5] = hi + pn + an;
-                hs[6] = e0 + pe + ae;
+                hs[5] = hi + pn + tcnt[2 * tile + 1];
+                hs[6] = e0 + pe + tcnt[2 * tile];
                 hs[7] = 0;
             }
         }
+    } else if (wv == 1) {
+        const int c = tile * kSbChunks + (lane & (kSbChunks - 1));
+        const int ce = lane < kSbChunks ? __popcll(masks[2 * c]) : 0;
+        const int cn = lane < kSbChunks ? __popcll(masks[2 * c + 1]) : 0;
+        int ie = ce, in = cn;
+#pragma unroll
+        for (int o = 1; o < kSbChunks; o <<= 1) {
+            const int ae = __shfl_up(ie, o), an = __shfl_up(in, o);
+            if (lane >= o) {
+                ie += ae;
+                in += an;
+            }
+        }
+        if (lane < kSbChunks) {
+            s_ce[lane] = ie - ce;
+            s_cn[lane] = in - cn;
+        }
     }
     __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kSbItems; ++t) {
-        const int gt = (tile * kSbItems + t) * kSbTile + threadIdx.x;
-        const int i = gt / KF, j = gt % KF;
-        const int e = e0 + s_pe + s_ce[t * NW + wv] + xe[t];
-        if (has[t]) {
-            esrc[e] = u[t];
-            edst[e] = lo + i;
+    const int gt = tile * kSbTile + threadIdx.x;
+    const int i = gt / KF, j = gt % KF;
+    const uint64_t mh = masks[2 * (tile * kSbChunks + wv)], mf = masks[2 * (tile * kSbChunks + wv) + 1];
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int e = e0 + s_pe + s_ce[wv] + __popcll(mh & below);
+    if ((mh >> lane) & 1) {
+        const int32_t u = cand[i * fanout + j];
+        esrc[e] = u;
+        edst[e] = lo + i;
+        if ((mf >> lane) & 1) {
+            const int n = hi + s_pn + s_cn[wv] + __popcll(mf & below);
+            map[u] = n;
+            nid[n] = u;
         }
-        if (fresh[t]) {
-            const int n = hi + s_pn + s_cn[t * NW + wv] + xn[t];
-            map[u[t]] = n;
-            nid[n] = u[t];
-        }
-        if (j == 0 && i < nf) rp[lo + i] = e;  // (frontier row lo + i's edges start here: CSR row pointer)
     }
+    if (j == 0 && i < nf) rp[lo + i] = e;  // (frontier row lo + i's edges start here: CSR row pointer)
 }
 
 // the last hop's edges relabelled; counts = {n_total, e_total, n_active, -}
@@ -471,7 +436,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
         cand += nf * f;
         cntn += nf;
         if (nf * sb_kf(static_cast<int>(f)) > INT32_MAX / 2) return false;  // (lane indices)
-        nblk = std::max<int64_t>(nblk, ceil_div(nf * sb_kf(static_cast<int>(f)), kSbTile * kSbItems));
+        nblk = std::max<int64_t>(nblk, ceil_div(nf * sb_kf(static_cast<int>(f)), kSbTile));
         e += nf * f;
         nf *= f;
         n += nf;
@@ -489,7 +454,7 @@ bool sb_plan(int64_t B, const int32_t *fanouts, int H, SbPlan *p) {
     p->off_state = take(4 * (H + 1));
     p->off_cand = take(static_cast<size_t>(std::max<int64_t>(cand, 1)));
     p->off_cnt = take(static_cast<size_t>(std::max<int64_t>(cntn, 1)));
-    p->off_bsum = take(static_cast<size_t>(2 * (nblk + 1)));
+    p->off_bsum = take(static_cast<size_t>((2 * 2 * kSbChunks + 2) * nblk));  // masks + tile totals
     p->off_nid = take(static_cast<size_t>(n));
     p->off_esrc = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
     p->off_edst = take(static_cast<size_t>(std::max<int64_t>(e, 1)));
@@ -502,6 +467,7 @@ SbWs sb_carve(void *ws, const SbPlan &p) {
     char *b = static_cast<char *>(ws);
     return SbWs{reinterpret_cast<int32_t *>(b + p.off_state), reinterpret_cast<int32_t *>(b + p.off_cand),
                 reinterpret_cast<int32_t *>(b + p.off_cnt), reinterpret_cast<uint64_t *>(b + p.off_bsum),
+                reinterpret_cast<int32_t *>(b + p.off_bsum + static_cast<size_t>(2 * kSbChunks * 8) * p.max_nblk),
                 reinterpret_cast<int32_t *>(b + p.off_nid), reinterpret_cast<int32_t *>(b + p.off_esrc),
                 reinterpret_cast<int32_t *>(b + p.off_edst), reinterpret_cast<int32_t *>(b + p.off_rp)};
 }
@@ -553,19 +519,21 @@ extern "C" int ngnn_sample_block(const int64_t *g_rowptr, const int32_t *g_col, 
         int32_t *hs = w.state + 4 * h;
         const int64_t nf = p.nf_cap[h];
         // lane-per-draw grids: kf lanes per frontier position
-        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbTile * kSbItems)));
+        const int nblk = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbTile)));
         const int sgrid = static_cast<int>(std::max<int64_t>(1, ceil_div(nf * kf, kSbBlock)));
         int32_t *cand = w.cand + p.cand_off[h], *cnt = w.cnt + p.cnt_off[h];
         // the per-hop seed of ngnn_sample_hop's callers (loader.sample_block)
         const uint64_t hseed = seed * 1000003ull + static_cast<uint64_t>(h);
-        // two launches per hop (round 6; five before): draws + claims (+ the
-        // previous hop's relabel), then the look-back relabelling
+        // three launches per hop (round 6; five before): draws + claims (+ the
+        // previous hop's relabel), the first-appearance counts, the writes
         auto hop = [&](auto kf_c) {
             constexpr int KF = decltype(kf_c)::value;
             hipLaunchKernelGGL(k_sb_sample<KF>, dim3(sgrid), dim3(kSbBlock), 0, st, g_rowptr, g_col, n_graph, hs, w.nid,
-                               f, hseed, cand, cnt, node_map, h > 0 ? hs - 4 : nullptr, w.esrc, w.lb, nblk);
-            hipLaunchKernelGGL(k_sb_assign_lb<KF>, dim3(nblk), dim3(kSbTile), 0, st, hs, cand, cnt, node_map,
-                               n_graph, f, w.lb, nblk, w.nid, w.esrc, w.edst, w.rp);
+                               f, hseed, cand, cnt, node_map, h > 0 ? hs - 4 : nullptr, w.esrc);
+            hipLaunchKernelGGL(k_sb_count<KF>, dim3(nblk), dim3(kSbTile), 0, st, hs, cand, cnt, node_map, n_graph, f,
+                               w.masks, w.tcnt);
+            hipLaunchKernelGGL(k_sb_write<KF>, dim3(nblk), dim3(kSbTile), 0, st, hs, cand, node_map, f, w.masks,
+                               w.tcnt, nblk, w.nid, w.esrc, w.edst, w.rp);
         };
         switch (kf) {
             case 8: hop(std::integral_constant<int, 8>{}); break;
