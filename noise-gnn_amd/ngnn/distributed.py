@@ -27,7 +27,7 @@ def cast_tensors(src, dst, divisor: float = 1.0) -> None:
     kernel).  Tensors of other dtypes or layouts take the ATen path."""
     import ctypes
 
-    from . import _lib
+    from . import _lib, fused
     ok = [i for i, (a, b) in enumerate(zip(src, dst))
           if a.dtype in _DTYPE_CODE and b.dtype in _DTYPE_CODE and a.is_contiguous()
           and b.is_contiguous() and a.numel() == b.numel() and a.is_cuda and b.is_cuda]
@@ -114,6 +114,7 @@ class GradAllReduce:
     """
 
     def __init__(self, params, group=None):
+        from . import fused
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         n = sum(p.numel() for p in self.params)
@@ -126,6 +127,7 @@ class GradAllReduce:
             self.views.append(v)
             if p.dtype == torch.float32:
                 p._ngnn_grad_out = v
+                fused.note_grad_views()
             off += p.numel()
 
     def active(self) -> bool:

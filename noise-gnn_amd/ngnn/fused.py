@@ -1150,10 +1150,20 @@ class _GradViews:
         self.live = True
 
 
+_grad_views_seen = False  # set once any parameter got a bucket view
+
+
+def note_grad_views() -> None:
+    """ngnn.distributed.GradAllReduce registered a bucket view (until then the
+    eager step skips the per-parameter claim scan)."""
+    global _grad_views_seen
+    _grad_views_seen = True
+
+
 def _claim_grad_views(params) -> "_GradViews | None":
     """Views for the fp32 parameters whose .grad is unset (autograd will adopt
     them) and whose view no other pending node holds; None when there are none."""
-    if not torch.is_grad_enabled():
+    if not _grad_views_seen or not torch.is_grad_enabled():
         return None
     gv = _GradViews(len(params))
     for i, q in enumerate(params):
