@@ -348,6 +348,20 @@ __global__ __launch_bounds__(256) void k_x3_image(RtArgs a, v4f *dst) {
         }
         reinterpret_cast<bf16x8 *>(const_cast<void *>(a.wlb))[sb] = v;
     }
+    // the fp32 packed W_l (k_pack_weight's layout [NT][KG][64 lanes][4]: lane
+    // l, element i of fragment (m, kg) holds W[16 m + (l & 15)][16 kg + 4 (l
+    // >> 4) + i]), one fragment lane (4 floats) per thread past the above
+    const int sp = sb - (a.wlb_src ? ((a.wlb_fo + 15) >> 4) * a.CL * 64 : 0);
+    const int KG = (a.K + 15) >> 4;
+    if (a.wlp_src && sp >= 0 && sp < ((a.wlp_fo + 15) >> 4) * KG * 64) {
+        const int l = sp & 63, f = sp >> 6;
+        const int n = 16 * (f / KG) + (l & 15), k = 16 * (f % KG) + 4 * (l >> 4);
+        v4f v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            v[j] = (n < a.wlp_fo && k + j < a.K) ? a.wlp_src[static_cast<int64_t>(n) * a.ldw + k + j] : 0.0f;
+        a.wlp_dst[sp] = v;
+    }
 }
 
 #if NGNN_ROOT_TRACE
@@ -364,7 +378,8 @@ size_t x3_image_bytes(int ntw, int C, int T4, bool w1) {
 
 int build_image(RtArgs &a, int ntw, void *dst, hipStream_t st) {
     const int slots = a.C * ntw * 64 + a.T4 * ntw * 64 +
-                      (a.wlb_src ? static_cast<int>(ceil_div(a.wlb_fo, 16)) * a.CL * 64 : 0);
+                      (a.wlb_src ? static_cast<int>(ceil_div(a.wlb_fo, 16)) * a.CL * 64 : 0) +
+                      (a.wlp_src ? static_cast<int>(ceil_div(a.wlp_fo, 16) * ceil_div(a.K, 16)) * 64 : 0);
     const unsigned grid = static_cast<unsigned>(ceil_div(slots, 256));
     v4f *d = static_cast<v4f *>(dst);
     const bool w1 = a.w1 != 0;

@@ -611,6 +611,12 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.C = C;
         a.T4 = T4;
         a.kpad = kpad;
+        // (the root image's launch packs the weights below when that image
+        // is prebuilt)
+        const bool img_pre = x3 && !no_root && img_ws && x3_image_bytes(NTW, C, T4, w1) <= kImgWsBytes;
+        a.wlp_src = nullptr;
+        a.wlp_dst = nullptr;
+        a.wlp_fo = 0;
         if (ldw && has_l && !wl_lds) {
             // raw W_l that must stream from L2: pack it once (all slices) into
             // the caller's workspace -- fragment-ordered 1-KiB wave loads
@@ -620,10 +626,16 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
                     *rc = NGNN_E_WORKSPACE;
                     return 1;
                 }
-                // (NGNN_WL_PREPACKED: the producer packed this step's W_l there)
-                const int prc = wl_prepacked ? 0
-                                             : ngnn_pack_weight(static_cast<const float *>(wl_packed),
-                                                                ldw, Fo, K, wl_ws, st);
+                // (NGNN_WL_PREPACKED: the producer packed this step's W_l there;
+                // with a prebuilt root image its launch packs it: one launch)
+                if (!wl_prepacked && img_pre) {
+                    a.wlp_src = static_cast<const float *>(wl_packed);
+                    a.wlp_dst = static_cast<v4f *>(wl_ws);
+                    a.wlp_fo = static_cast<int>(Fo);
+                }
+                const int prc = (wl_prepacked || img_pre) ? 0
+                                                          : ngnn_pack_weight(static_cast<const float *>(wl_packed),
+                                                                             ldw, Fo, K, wl_ws, st);
                 if (prc) {
                     *rc = prc;
                     return 1;
@@ -638,8 +650,6 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         a.wlb_src = nullptr;
         a.wlb_fo = static_cast<int>(Fo);
         a.CL = static_cast<int>(ceil_div(K, 32));
-        // (the root image's launch packs it too when that image is prebuilt)
-        const bool img_pre = x3 && !no_root && img_ws && x3_image_bytes(NTW, C, T4, w1) <= kImgWsBytes;
         if (w1 && has_l && !wl_lds) {
             if (!ldw || !wl_ws || wl_ws_bytes < ngnn_pack_weight_bytes(Fo, K) + wl_b16_bytes(Fo, K)) {
                 *rc = NGNN_E_WORKSPACE;
@@ -701,6 +711,7 @@ int sage_fwd_rowtile(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             if (*rc) return 1;
         }
         a.wlb_src = nullptr;
+        a.wlp_src = nullptr;
         const int n_tiles = static_cast<int>(ceil_div(n_rows, RT_ROWS));
         // the tiles past the edge-row bound on k_root (ngnn_root.hip) when an
         // instantiation covers this layer: k_sage_rt takes the tiles with
@@ -743,8 +754,13 @@ extern "C" size_t ngnn_sage_fwd_raw_workspace_bytes(int64_t K, int64_t Fo, int64
     // the wide path's aggregate rows (inference: no saved-aggregate buffer)
     const size_t z = static_cast<size_t>(std::max<int64_t>(n_rows, 0)) * ceil_div(Fo, 16) * 16 *
                      sizeof(float);
+    // (the wide tail: X3's 6-part weight image, or H2's 2-part image + its
+    // row / column exponent arrays -- whichever is larger for these rows, so
+    // the H2 form never drops back to X3 for want of room)
+    const size_t nr = static_cast<size_t>(std::max<int64_t>(n_rows, 0));
+    const size_t h2_tail = static_cast<size_t>(8) * Fo * ceil_div(K, 32) * 32 + (2 * Fo + 2 * nr) * 4 + 1024 + 512;
     const size_t wide = (sage_wide_preferred(K, Fo, false) || sage_wide_preferred(K, Fo, true))
-                            ? sage_wide_workspace_bytes(K, n_rows) + wide_wimg_bytes(K, Fo) + 256
+                            ? sage_wide_workspace_bytes(K, n_rows) + std::max(wide_wimg_bytes(K, Fo), h2_tail) + 256
                             : 0;
     // + the prebuilt root image at the workspace's tail (kImgWsBytes); the
     // packed W_l is followed by its bf16 image (one-part layers)

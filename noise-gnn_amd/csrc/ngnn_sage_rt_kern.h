@@ -147,6 +147,12 @@ struct RtArgs {
     // rows) from these raw rows (row stride ldw) -- one launch for both images
     const float *wlb_src;
     int wlb_fo;
+    // non-null: k_x3_image also packs the fp32 W_l (ngnn_pack_weight's
+    // layout, wlp_fo x K, row stride ldw) into wlp_dst -- the streamed-W_l
+    // layers' pack launch folded into the root image's (round 6)
+    const float *wlp_src;
+    v4f *wlp_dst;
+    int wlp_fo;
 };
 
 namespace {
