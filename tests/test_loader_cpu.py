@@ -120,3 +120,27 @@ def test_graph_cache_releases_freed_data(monkeypatch):
     loader._graph_of(slots)
     loader._graph_of(slots)
     assert len(built) == 2 and id(slots) not in loader._graphs_of_data
+
+
+def test_sync_free_loader_contract_on_the_host():
+    """NeighborLoader(sync_free=True) (ABI 19) carries x, y, edge_index and
+    n_id only: a graph with further per-node tensors is refused up front; a
+    batch marked sync-free (capacity-sized buffers, counts on the device) is
+    refused by the models before anything reads it."""
+    import pytest
+
+    import ngnn
+    d = _data()
+    g = graph_from_data(d, device="cpu")
+    with pytest.raises(ValueError, match="sync_free"):
+        NeighborLoader(g, g.train_idx, [3], 4, sync_free=True)
+    g.node_attrs.clear()
+    ld = NeighborLoader(g, g.train_idx, [3], 4, sync_free=True)
+    assert ld.sync_free and len(ld) == -(-g.train_idx.numel() // 4)
+    ei = torch.zeros(2, 8, dtype=torch.int64)
+    ei._ngnn_counts = torch.zeros(4, dtype=torch.int32)
+    for m in (ngnn.SAGE(5, 8, 4, 2), ngnn.SimpleGCN(5, 8, 4, 2)):
+        with pytest.raises(ValueError, match="sync_free"):
+            m(torch.zeros(8, 5), ei)
+    with pytest.raises(ValueError, match="sync_free"):
+        ngnn.SAGEConv(5, 4)(torch.zeros(8, 5), ei)
