@@ -477,7 +477,8 @@ struct F2Args {
 // MFMA work and 8 weight registers).
 // DBG (profiling builds only, NGNN_FWD2_DBG): bit 0 skips the reduce, 1 the
 // layer-1 products, 2 layer 0's products, 3 the x split, 4 the out / z
-// stores (offsets out of range) -- time attribution
+// stores (offsets out of range), 5 the consumer's h reads (register
+// operands), 6 the consumer's products (reads kept) -- time attribution
 // ROOT false (ABI 17: wr0 NULL -- GCNConv's aggregate-first layer, W_r = 0):
 // no x rows at all -- no loads, no split, no layer-0 products; h = act(b0 +
 // nb) (act(b0) on rows without in-edges)
@@ -807,6 +808,12 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
         half8 bf[2][2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
+            if (DBG & 32) {  // (profiling: no h reads -- register operands)
+                bf[c][0] = w1[c][0];
+                bf[c][1] = w1[c][1];
+                asm volatile("" : "+v"(bf[c][0]), "+v"(bf[c][1]));
+                continue;
+            }
             bf[c][0] = hp[2 * c * 64];
             bf[c][1] = hp[(2 * c + 1) * 64];
         }
@@ -818,10 +825,20 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
                 const int ec = c < 4 ? ea[c] : eb[c - 4];
                 acc[c & 1] *= __builtin_amdgcn_ldexpf(1.0f, ec - ep2);  // scale 2^(eW1 + e_{c-2}) -> 2^(eW1 + e_c)
             }
-            acc[c & 1] = mfma_h2(w1[c][0], w1[c][1], b1, b2, acc[c & 1]);
+            if (DBG & 64) {  // (profiling: the h reads without the products)
+                asm volatile("" : "+v"(acc[c & 1]) : "v"(b1), "v"(b2));
+            } else {
+                acc[c & 1] = mfma_h2(w1[c][0], w1[c][1], b1, b2, acc[c & 1]);
+            }
             if (c + 2 < NK1) {
-                bf[c & 1][0] = hp[2 * (c + 2) * 64];
-                bf[c & 1][1] = hp[(2 * (c + 2) + 1) * 64];
+                if (DBG & 32) {
+                    bf[c & 1][0] = w1[c + 2][0];
+                    bf[c & 1][1] = w1[c + 2][1];
+                    asm volatile("" : "+v"(bf[c & 1][0]), "+v"(bf[c & 1][1]));
+                } else {
+                    bf[c & 1][0] = hp[2 * (c + 2) * 64];
+                    bf[c & 1][1] = hp[(2 * (c + 2) + 1) * 64];
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -1319,6 +1336,8 @@ extern "C" int ngnn_sage2_fwd(const float *x, const float *const *x_dev, const i
                     case 8: return launch_fwd2<4, 3, 2, false, 8>(f, grid, st);
                     case 15: return launch_fwd2<4, 3, 2, false, 15>(f, grid, st);
                     case 16: return launch_fwd2<4, 3, 2, false, 16>(f, grid, st);
+                    case 32: return launch_fwd2<4, 3, 2, false, 32>(f, grid, st);
+                    case 64: return launch_fwd2<4, 3, 2, false, 64>(f, grid, st);
                     default: break;
                 }
             }
