@@ -540,3 +540,36 @@ def test_graph_training_over_sync_free_loader(gather):
     torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-6)
     for a, b in zip(res[1][1], res[0][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_graph_epoch_over_sync_free_loader_with_short_last_batch():
+    """A whole epoch whose last block is short (train seeds not a multiple of
+    the batch size) through GraphedTrainStep, sync-free loader against the
+    synchronous one: the same losses and parameters (the short block's
+    batch_size reaches the slot's ignore_index rows)."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import NeighborLoader, synthetic_graph
+    from ngnn.optim import Adam
+    g = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.01)
+    assert g.train_idx.numel() % 512 != 0
+    torch.manual_seed(5)
+    init = ngnn.SAGE(100, 256, 47, 2, dropout=0.0).to(DEV).state_dict()
+    res = []
+    for sf in (False, True):
+        m = ngnn.SAGE(100, 256, 47, 2, dropout=0.0).to(DEV)
+        m.load_state_dict(init)
+        opt = Adam(m.parameters(), lr=1e-3)
+        n_cap, e_cap = slot_size(512, [15, 10])
+        kw = dict(batch_size=512, shuffle=True, seed=9)
+        cap = next(iter(NeighborLoader(g, g.train_idx, [15, 10], **kw)))
+        step = GraphedTrainStep(m, opt, 512, n_cap, e_cap, 100, DEV)
+        step.capture(cap.x, cap.edge_index, cap.y)
+        losses = [step(b.x, b.edge_index, b.y, b.batch_size).clone()
+                  for b in NeighborLoader(g, g.train_idx, [15, 10], sync_free=sf, **kw)]
+        step.check_inputs()
+        res.append((torch.stack(losses).cpu(), [p.detach().clone() for p in m.parameters()]))
+    assert res[0][0].numel() == -(-g.train_idx.numel() // 512)
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-6)
+    for a, b in zip(res[1][1], res[0][1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)

@@ -124,7 +124,8 @@ def _assert_same_block(b, ref):
 
 
 @pytest.mark.parametrize("fanouts,bs", [([15, 10], 300), ([5], 64), ([20, 15, 10], 128),
-                                        ([3, 0, 2], 50), ([64], 17), ([], 10)])
+                                        ([3, 0, 2], 50), ([64], 17), ([], 10),
+                                        ([2, 2, 2, 2, 2, 2, 2, 2], 8), ([33, 9], 40)])
 def test_sample_block_matches_reference(graph, fanouts, bs):
     from ngnn.loader import _sampler_cache
     seeds = graph.train_idx[:bs]
