@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 19
+#define NGNN_ABI_VERSION 20
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -460,6 +460,11 @@ typedef struct ngnn_adam_fold {
     float *param[6], *exp_avg[6], *exp_avg_sq[6];
     float *step; /* the device step count (advanced once, then read) */
     float lr, beta1, beta2, eps, weight_decay;
+    /* ABI 20 (nullable): ngnn_slot_load's contract gate and the slot's r_next
+     * word -- a step whose block broke the slot's contract updates no
+     * parameter and leaves the step count (the gradients are still written) */
+    const uint64_t *gate;
+    const int64_t *gate_gen;
 } ngnn_adam_fold;
 size_t ngnn_sage2_bwd_workspace_bytes(int64_t n_rows, int64_t K0, int64_t F1);
 int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const float *wl1, const float *wr1,
@@ -666,10 +671,12 @@ int ngnn_cast_tensors_ex(int n, const void *const *src, void *const *dst, const 
  * activations a backward kernel reads as an fp32 mask. */
 int ngnn_widen_bf16_rows(const void *src, int64_t lds, int64_t F, int64_t n_rows,
                          const int32_t *n_rows_dev, float *dst, int64_t ldd, void *stream);
+/* gate / gate_gen (ABI 20, nullable): as ngnn_adam_fold's -- the step of a
+ * block that broke the graph slot's contract updates nothing. */
 int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grads,
                    float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
                    const int32_t *dtypes, float *step, uint32_t *ticket, float lr, float beta1, float beta2, float eps,
-                   float weight_decay, void *stream);
+                   float weight_decay, const uint64_t *gate, const int64_t *gate_gen, void *stream);
 
 /* ------------------------------------------------------ HIP-graph slot
  * Fill the static slot a captured training step reads (ngnn/graphs.py) with
@@ -707,6 +714,11 @@ int ngnn_adam_step(int n_tensors, float *const *params, const float *const *grad
  * (clamped to [0, n_cap]) its edge lands under.  E > 0 needs N >= 1.  The
  * caller checks the word without a device sync (ABI 16: replaces a host
  * read-back of the targets).
+ * gate (ABI 20, nullable, 8-B aligned device word): (gen << 32 | bits) of the
+ * newest load that broke the contract, by a 64-bit atomicMax -- the device
+ * copy of err that ngnn_adam_fold / ngnn_adam_step read to skip that step's
+ * update (no reset launch: the generation tells this load's bits from an
+ * older load's).
  * counts_dev (ABI 19, nullable): device int32 {N', E', ...} -- the block's
  * row and edge counts are min(N', N) / min(E', E), read on the device (N / E
  * are then bounds: the capacity-sized buffers a sync-free sampler wrote;
@@ -723,7 +735,7 @@ int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F, const int6
                    int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
                    int32_t *slot_colx, const float *pack_w, int64_t pack_ldw, int64_t pack_fo,
                    int64_t pack_k, float *pack_dst, int32_t *err, const int32_t *counts_dev,
-                   void *stream);
+                   uint64_t *gate, void *stream);
 
 #ifdef __cplusplus
 }

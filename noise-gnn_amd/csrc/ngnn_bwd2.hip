@@ -100,6 +100,8 @@ struct B2Args {
     float *slab;  // [S][slab floats]
     int S;
     float *step_inc;  // nullable: the folded Adam step's count, advanced once here
+    const uint64_t *gate;  // the graph slot's contract gate (ABI 20): no advance when gated
+    const int64_t *gate_gen;
 };
 
 __host__ __device__ inline int64_t b2_slab_floats(int K0, int F1) {
@@ -173,7 +175,8 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     const int t = threadIdx.x;
     // (the folded Adam step: k_bwd2_reduce, the next launch, reads the
     // advanced count -- stream order, no ticket)
-    if (a.step_inc && blockIdx.x == 0 && t == 0) *a.step_inc = *a.step_inc + 1.0f;
+    if (a.step_inc && blockIdx.x == 0 && t == 0 && !slot_gated(a.gate, a.gate_gen))
+        *a.step_inc = *a.step_inc + 1.0f;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int ln = t & 63, q = ln >> 4, l16 = ln & 15;
     // block -> (slice, chunk): the 4 chunks of a slice on one XCD (blocks b,
@@ -587,6 +590,8 @@ struct AdamFold {
     float *p[6], *m[6], *v[6];  // in the reduce's order: W_r0, W_l0, b0, W_r1, W_l1, b1
     float *step;
     float lr, b1, b2, eps, wd;
+    const uint64_t *gate;  // (ABI 20) the slot's contract gate: no update when gated
+    const int64_t *gate_gen;
 };
 
 // out = sum over slabs in slab order; with ADAM the parameters are updated
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
     }
     for (; sl < S; ++sl) v += slab[static_cast<int64_t>(sl) * total + i];
     outs[k][e] = v;
-    if (ADAM) {  // k_adam's update (ngnn_optim.hip) of element e of tensor k
+    if (ADAM && !slot_gated(af.gate, af.gate_gen)) {  // k_adam's update (ngnn_optim.hip) of element e of tensor k
         const float bc1 = 1.0f - powf(af.b1, t);
         const float bc2s = sqrtf(1.0f - powf(af.b2, t));
         const float step_size = af.lr / bc1;
@@ -765,6 +770,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
     b.slab = slab;
     b.S = B2_S;
     b.step_inc = adam ? adam->step : nullptr;
+    b.gate = adam ? adam->gate : nullptr;
+    b.gate_gen = adam ? adam->gate_gen : nullptr;
     // (+ the chunk maxima: [2][8] float4)
     const size_t lds = static_cast<size_t>(2) * BUF * 2 + 2 * 256 * 4 + 480 * 4 + 2 * 8 * 16;
     static const bool lag = [] {
@@ -806,6 +813,8 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
         af.b2 = adam->beta2;
         af.eps = adam->eps;
         af.wd = adam->weight_decay;
+        af.gate = adam->gate;
+        af.gate_gen = adam->gate_gen;
         hipLaunchKernelGGL(k_bwd2_reduce<true>, dim3(n_red + n_clr), dim3(256), 0, st, slab, B2_S,
                            static_cast<int>(K0), static_cast<int>(F1), dwr0, dwl0, dbl0, dwr1, dwl1, dbl1, g, C4,
                            static_cast<int>(n_rows), r_ptr, rnext_ptr, n_red, af);

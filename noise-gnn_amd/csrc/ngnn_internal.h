@@ -33,4 +33,16 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 int num_cus();  // compute units of the current device (cached; ngnn_sage_rt.hip)
 
+// The graph slot's contract gate (ABI 20): the slot kernel keeps, in a
+// 64-bit word, (gen << 32 | bad bits) of the last load that broke the
+// block's contract (atomicMax: the newest generation wins); gen_word is the
+// slot's r_next word, whose high half is the current load's generation.  A
+// step whose block broke the contract leaves the parameters and the step
+// count untouched.  gate NULL: never gated.
+__device__ __forceinline__ bool slot_gated(const uint64_t *gate, const int64_t *gen_word) {
+    if (!gate || !gen_word) return false;
+    const uint64_t g = *gate;
+    return (g & 0xffffffffull) != 0 && (g >> 32) == (static_cast<uint64_t>(*gen_word) >> 32);
+}
+
 }  // namespace ngnn

@@ -45,7 +45,9 @@ __device__ __forceinline__ uint32_t f_to_bf16_bits(float f) {  // RNE, NaN -> 0x
 // on the ticket's L2 channel: 40 us for Amazon-Computers' 1.6 M parameters)
 __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__ step,
                                               uint32_t *__restrict__ ticket, float lr, float b1,
-                                              float b2, float eps, float wd) {
+                                              float b2, float eps, float wd, const uint64_t *gate,
+                                              const int64_t *gate_gen) {
+    if (slot_gated(gate, gate_gen)) return;  // (a contract-breaking block: no update, no step; ABI 20)
     const float t = *step + 1.0f;
     // the completion ticket is taken right after every thread has read the
     // count (what it guards), not after the update: the atomic's round trip
@@ -142,7 +144,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
     }
 }
 
-__global__ void k_step_inc(float *step) { *step += 1.0f; }
+__global__ void k_step_inc(float *step, const uint64_t *gate, const int64_t *gate_gen) {
+    if (!slot_gated(gate, gate_gen)) *step += 1.0f;
+}
 
 }  // namespace
 }  // namespace ngnn
@@ -154,7 +158,7 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
                               const int64_t *numels, const int32_t *dtypes, float *step,
                               uint32_t *ticket, float lr,
                               float beta1, float beta2, float eps, float weight_decay,
-                              void *stream) {
+                              const uint64_t *gate, const int64_t *gate_gen, void *stream) {
     NGNN_RETURN_IF(n_tensors < 0 || !step, NGNN_E_ARG);
     NGNN_RETURN_IF(n_tensors > 0 && (!params || !grads || !exp_avgs || !exp_avg_sqs || !numels),
                    NGNN_E_ARG);
@@ -207,13 +211,13 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(std::min<int64_t>(T.boff[T.n], wg_cu * num_cus()),
                                                                       32 * (kAdamTickets - 1)));
         hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
-                           eps, weight_decay);
+                           eps, weight_decay, gate, gate_gen);
         const int rc = launch_status();
         if (rc) return rc;
         launched = true;
     }
     if (ticket && launched) return NGNN_OK;
-    hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, st, step);
+    hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, st, step, gate, gate_gen);
     return launch_status();
 }
 

@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
     uint64_t *__restrict__ seed_state, const float **x_dev, int64_t *__restrict__ r_next,
     uint32_t gen, int32_t *__restrict__ n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
     int32_t *__restrict__ colx, int vec, const float *__restrict__ pk_w, int64_t pk_ldw, int pk_fo,
-    int pk_k, float *__restrict__ pk_dst, int32_t *err, const int32_t *__restrict__ cnt) {
+    int pk_k, float *__restrict__ pk_dst, int32_t *err, const int32_t *__restrict__ cnt,
+    uint64_t *__restrict__ gate) {
     if (cnt) {  // (ABI 19) the block's counts on the device; N / E: their bounds
         N = min(static_cast<int64_t>(cnt[0]), N);
         E = min(static_cast<int64_t>(cnt[1]), E);
@@ -85,6 +86,9 @@ __global__ __launch_bounds__(256) void k_slot_load(
         }
     }
     if (bad && err) atomicOr(err, bad);
+    if (bad && gate)  // (this load's generation outranks every older load's bits)
+        atomicMax(reinterpret_cast<unsigned long long *>(gate),
+                  static_cast<unsigned long long>((static_cast<uint64_t>(gen) << 32) | static_cast<uint32_t>(bad)));
     for (int64_t i = tid; i < B; i += nthr) sy[i] = y[i];
     if (rowptr) {
         // rowptr[r] = first padded edge with target >= r.  Padding: closed
@@ -189,9 +193,10 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                               int32_t *n_edge_rows, const int64_t *xrow, const int64_t **xrow_dev,
                               int32_t *slot_colx, const float *pack_w, int64_t pack_ldw,
                               int64_t pack_fo, int64_t pack_k, float *pack_dst, int32_t *err,
-                              const int32_t *counts_dev, void *stream) {
+                              const int32_t *counts_dev, uint64_t *gate, void *stream) {
     NGNN_RETURN_IF(N < 0 || F < 0 || E < 0 || B < 0 || (!slot_x && !x_dev) || !n_valid, NGNN_E_ARG);
     NGNN_RETURN_IF(!slot_ei && !slot_rowptr, NGNN_E_ARG);  // the edges must land somewhere
+    NGNN_RETURN_IF(gate && !aligned(gate, 8), NGNN_E_ALIGN);
     NGNN_RETURN_IF(x_dev && (ldx != ld_slot || !aligned(x, 16)), NGNN_E_SHAPE);
     NGNN_RETURN_IF(xrow && (!x_dev || !xrow_dev), NGNN_E_ARG);  // indexed rows are zero-copy only
     NGNN_RETURN_IF((N > 0 && F > 0 && !x) || (E > 0 && !edge_index) || (B > 0 && (!y || !slot_y)),
@@ -212,6 +217,6 @@ extern "C" int ngnn_slot_load(const float *x, int64_t ldx, int64_t N, int64_t F,
                        edge_index, ld_ei, E, y, B, slot_x, ld_slot, n_cap, slot_ei, e_cap, slot_y,
                        n_valid, slot_rowptr, slot_col, seed_state, x_dev, r_next, gen, n_edge_rows,
                        xrow, xrow_dev, slot_colx, vec, pack_w, pack_ldw, static_cast<int>(pack_fo),
-                       static_cast<int>(pack_k), pack_dst, err, counts_dev);
+                       static_cast<int>(pack_k), pack_dst, err, counts_dev, gate);
     return launch_status();
 }

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 OK = 0
 SLOT_UNSORTED = 1  # ngnn_slot_load's err bits (include/ngnn.h NGNN_SLOT_*)
@@ -62,10 +62,10 @@ SIGNATURES = {
                                 _p, _p, _p, _sz, _p, _p]),
     "ngnn_ct_loss_bwd": (_int, [_int, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _p]),
     "ngnn_adam_step": (_int, [_int, _p, _p, _p, _p, _p, _p, _p, _p, ctypes.c_float, ctypes.c_float,
-                              ctypes.c_float, ctypes.c_float, ctypes.c_float, _p]),
+                              ctypes.c_float, ctypes.c_float, ctypes.c_float, _p, _p, _p]),
     "ngnn_slot_load": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                               _p, _i64, _p, _p, _p, _p, _p, _p, _p, ctypes.c_uint32, _p, _p, _p,
-                              _p, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
+                              _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
     "ngnn_sage_fwd": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _int, _p, _p, _p, _i64, _p, _i64,
                              _int, ctypes.c_float, ctypes.c_uint64, _p, _p, _i64, _p, _i64,
                              ctypes.c_float, _p]),
@@ -157,10 +157,11 @@ class XentHead(ctypes.Structure):
 
 
 class AdamFold(ctypes.Structure):
-    """include/ngnn.h ngnn_adam_fold (ngnn_sage2_bwd's optimizer step, ABI 15)."""
+    """include/ngnn.h ngnn_adam_fold (ngnn_sage2_bwd's optimizer step, ABI 15; the gate ABI 20)."""
     _fields_ = [("param", _p * 6), ("exp_avg", _p * 6), ("exp_avg_sq", _p * 6), ("step", _p),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
-                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float)]
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("gate", _p), ("gate_gen", _p)]  # (ABI 20: the slot's contract gate)
 
 
 def ptr(t) -> int:

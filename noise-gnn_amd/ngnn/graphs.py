@@ -92,6 +92,10 @@ class GraphedTrainStep:
         # no device sync (load() raises on a word set by an earlier batch;
         # check_inputs() syncs and raises for the batches so far)
         self._err = torch.zeros(1, dtype=torch.int32).pin_memory()
+        # its device twin (ABI 20): (generation << 32 | bits) of the newest
+        # contract-breaking load; a one-rank captured step reads it and leaves
+        # the parameters and the step count untouched for such a block
+        self._gate = torch.zeros(1, dtype=torch.int64, device=dev)
 
     # ---- slot filling (stream-ordered device copies; no host syncs)
     def load(self, x: torch.Tensor, edge_index: torch.Tensor, y: torch.Tensor,
@@ -164,7 +168,8 @@ class GraphedTrainStep:
             *((_lib.ptr(self._pack[0]), self._pack[0].stride(0), self._pack[0].shape[0],
                self._pack[0].shape[1], _lib.ptr(self._pack[1])) if self._pack is not None
               else (None, 0, 0, 0, None)),
-            self._err.data_ptr(), _lib.ptr(cnt), _lib.stream_handle(self.x.device)), "ngnn_slot_load")
+            self._err.data_ptr(), _lib.ptr(cnt), _lib.ptr(self._gate), _lib.stream_handle(self.x.device)),
+            "ngnn_slot_load")
         self._x_live = (x, xrow) if zero_copy else None
         if self._pack is not None:  # this load packed the current W_l: one forward may use it
             self._pack[2].armed = True
@@ -188,17 +193,21 @@ class GraphedTrainStep:
 
         A contract-breaking batch (targets not sorted, ids outside [0, N)) is
         only detected on the device: its replay has already run -- on a wrong
-        CSR, never out of bounds (the slot kernel stores bad sources as row 0)
-        -- and its optimizer step has been applied to the parameters by the
-        time it is reported.  Call this where a training loop ends (the last
-        batch is otherwise never reported)."""
+        CSR, never out of bounds (the slot kernel stores bad sources as row 0).
+        On one rank its optimizer step is skipped on the device (ABI 20: the
+        slot's gate word -- parameters, moments and the step count stay as
+        they were); with a gradient exchange every rank applies the same
+        update, so there the batch has been trained on by the time it is
+        reported.  Call this where a training loop ends (the last batch is
+        otherwise never reported)."""
         torch.cuda.synchronize(self.x.device)
         self._raise_if_bad()
 
     def _next_gen(self) -> int:
         self._gen += 1
-        if self._gen >= 2**32:  # wrapped: restart the generations from a zeroed word
+        if self._gen >= 2**32:  # wrapped: restart the generations from zeroed words
             self.r_next.zero_()
+            self._gate.zero_()
             self._gen = 1
         return self._gen
 
@@ -308,6 +317,12 @@ class GraphedTrainStep:
         exchange = red is not None or (self.reducer is not None and not (
             hasattr(self.reducer, "active") and not self.reducer.active()))
         fold = None if exchange else _fused.AdamFoldSpec.make(self.opt, self.model)
+        # one rank: a block that broke the slot's contract updates nothing (the
+        # gate; with an exchange every rank must apply the same update, so
+        # there the error word only reports)
+        gate = None if exchange else (self._gate.data_ptr(), self.r_next.data_ptr())
+        if fold is not None and gate is not None:
+            fold.struct.gate, fold.struct.gate_gen = gate
         self.g_fb = torch.cuda.CUDAGraph()
         _fused._adam_fold = fold
         try:
@@ -326,11 +341,16 @@ class GraphedTrainStep:
         self.loss = self.loss.detach()
         self.g_opt = None
         if not self.folded:
+            from . import optim as _optim
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
-                if red is not None:
-                    red.unpack()
-                self.opt.step()
+            _optim._slot_gate = gate
+            try:
+                with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
+                    if red is not None:
+                        red.unpack()
+                    self.opt.step()
+            finally:
+                _optim._slot_gate = None
         block_cache.clear()
         torch.cuda.synchronize()
         if snap is not None:
@@ -530,10 +550,15 @@ class GraphedCoTeachingStep(GraphedTrainStep):
         g = torch.cuda.CUDAGraph()
         pool = next(iter(self._graphs.values()))[0].pool() if self._graphs else None
         _fused._adam_fold = None
-        with torch.cuda.graph(g, pool=pool):
-            outs = self._ct_fwd_bwd(forget_rate)
-            for o in opts:
-                o.step()
+        from . import optim as _optim
+        _optim._slot_gate = (self._gate.data_ptr(), self.r_next.data_ptr())  # (one rank: the slot's gate)
+        try:
+            with torch.cuda.graph(g, pool=pool):
+                outs = self._ct_fwd_bwd(forget_rate)
+                for o in opts:
+                    o.step()
+        finally:
+            _optim._slot_gate = None
         self._graphs[self.num_remember(forget_rate)] = (g, outs)
         block_cache.clear()
         torch.cuda.synchronize()

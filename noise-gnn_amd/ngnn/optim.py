@@ -16,6 +16,13 @@ import torch
 from . import _lib
 
 
+# (gate word, generation word) of the graph slot whose step is being
+# captured (ngnn.graphs sets it around a one-rank capture): the captured
+# Adam launch skips the update of a block that broke the slot's contract
+# (ABI 20; include/ngnn.h ngnn_adam_step)
+_slot_gate = None
+
+
 class Adam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
@@ -92,5 +99,6 @@ class Adam(torch.optim.Optimizer):
                                           float(group["lr"]),
                                           float(b1), float(b2), float(group["eps"]),
                                           float(group["weight_decay"]),
+                                          *(_slot_gate if _slot_gate is not None else (None, None)),
                                           _lib.stream_handle(ps[0].device)), "ngnn_adam_step")
         return loss

@@ -320,7 +320,7 @@ def test_slot_load_csr_equals_lower_bound(case):
         _lib.ptr(x), x.stride(0), N, F, _lib.ptr(ei) if E else None, max(E, 0), E, _lib.ptr(y), 8,
         _lib.ptr(sx), sx.stride(0), n_cap, _lib.ptr(sei), e_cap, _lib.ptr(sy), _lib.ptr(nv),
         _lib.ptr(rowptr), _lib.ptr(col), None, None, None, 0, None, None, None, None,
-        None, 0, 0, 0, None, None, None, _lib.stream_handle(DEV)), "ngnn_slot_load")
+        None, 0, 0, 0, None, None, None, None, _lib.stream_handle(DEV)), "ngnn_slot_load")
     torch.cuda.synchronize()
     n_pad, span = e_cap - E, n_cap - N
     pad = N + (torch.arange(n_pad) * span) // max(n_pad, 1) if n_pad else torch.zeros(0, dtype=torch.int64)
@@ -379,7 +379,7 @@ def test_slot_pack_job_equals_pack_weight(fo, k):
     _lib.check(lib.ngnn_slot_load(
         _lib.ptr(x), F, N, F, _lib.ptr(ei), 2, 2, _lib.ptr(y), 1, _lib.ptr(sx), F, n_cap,
         _lib.ptr(sei), 2, _lib.ptr(sy), _lib.ptr(nv), None, None, None, None, None, 0, None,
-        None, None, None, _lib.ptr(w), w.stride(0), fo, k, _lib.ptr(dst), None, None,
+        None, None, None, _lib.ptr(w), w.stride(0), fo, k, _lib.ptr(dst), None, None, None,
         _lib.stream_handle(DEV)), "ngnn_slot_load")
     want = pack_weight(w)
     torch.cuda.synchronize()
@@ -429,9 +429,15 @@ def test_slot_contract_error_word():
     step(b.x, b.edge_index, b.y)
     step.check_inputs()  # a NeighborLoader block: clean
     bad = b.edge_index.flip(1).contiguous()  # targets descending
+    before = [p.detach().clone() for p in model.parameters()]
+    n_step = float(step.opt.state[next(model.parameters())]["step"])
     step(b.x, bad, b.y)
     with pytest.raises(ValueError, match="not sorted"):
         step.check_inputs()
+    # ABI 20: the contract gate -- the replay of a bad block updated nothing
+    for p, q in zip(model.parameters(), before):
+        assert torch.equal(p, q)
+    assert float(step.opt.state[next(model.parameters())]["step"]) == n_step
     oob = b.edge_index.clone()
     oob[0, 0] = b.num_nodes + 5
     step(b.x, oob, b.y)
@@ -573,3 +579,45 @@ def test_graph_epoch_over_sync_free_loader_with_short_last_batch():
     torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-6)
     for a, b in zip(res[1][1], res[0][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_contract_gate_on_the_folded_step():
+    """ABI 20 on the headline step (two-layer kernels, Adam folded into the
+    backward's reduction): a block that breaks the slot's contract is
+    replayed but changes no parameter, moment or step count; the next good
+    block trains."""
+    import ngnn
+    from ngnn.graphs import GraphedTrainStep, slot_size
+    from ngnn.loader import sample_block, synthetic_graph
+    from ngnn.optim import Adam
+    graph = synthetic_graph("ogbn-products", DEV, seed=3, scale=0.02)
+    b = sample_block(graph, graph.train_idx[:256], [15, 10], seed=1)
+    torch.manual_seed(0)
+    model = ngnn.SAGE(100, 256, 47, 2).to(DEV)
+    opt = Adam(model.parameters(), lr=1e-3)
+    n_cap, e_cap = slot_size(256, [15, 10])
+    step = GraphedTrainStep(model, opt, 256, n_cap, e_cap, 100, DEV)
+    step.capture(b.x, b.edge_index, b.y)
+    assert step.folded
+    step(b.x, b.edge_index, b.y)
+    step.check_inputs()
+
+    def snap():
+        p0 = next(model.parameters())
+        st = opt.state[p0]
+        return ([p.detach().clone() for p in model.parameters()], st["exp_avg"].clone(), float(st["step"]))
+
+    before = snap()
+    oob = b.edge_index.clone()
+    oob[0, 3] = b.num_nodes + 7
+    step(b.x, oob, b.y)
+    with pytest.raises(ValueError, match="outside"):
+        step.check_inputs()
+    after = snap()
+    assert all(torch.equal(p, q) for p, q in zip(after[0], before[0]))
+    assert torch.equal(after[1], before[1]) and after[2] == before[2]
+    step(b.x, b.edge_index, b.y)
+    step.check_inputs()
+    good = snap()
+    assert good[2] == before[2] + 1
+    assert not all(torch.equal(p, q) for p, q in zip(good[0], before[0]))
