@@ -36,7 +36,7 @@ import weakref
 
 import torch
 
-from . import _lib, _timing
+from . import _eager, _lib, _timing
 from .block import Block
 
 _ws: dict = {}
@@ -1182,6 +1182,54 @@ def _claim_grad_views(params) -> "_GradViews | None":
     return gv if any(v is not None for v in gv.views) else None
 
 
+_use_eager_ext = True  # (tests flip it to compare the C++ node with _SAGEStack)
+eager_ext_calls = 0  # (counted: the tests check which node ran)
+
+
+def _eager_sage2(x, block: Block, reduce: str, p_drop: float, seed: int, params):
+    """The eager two-layer SAGE stack through the C++ autograd node
+    (csrc/ngnn_eager.cpp: the launches _SAGEStack makes on this path --
+    sage2_forward with every row of h kept; row extent, prefix stats and
+    sage2_backward -- with ~100 us less host time per step), or None when
+    the call is not that path: a graph slot's block (device counts, fused
+    x[n_id], bounds, loss head, prepacked weights), bucket gradient views,
+    an input gradient, a GCN stack, deterministic mode, the bench's per-launch
+    timer, the debug hooks, or the module not built."""
+    if (not _use_eager_ext or len(params) != 6 or _debug_acts is not None or _debug_grads is not None
+            or not _use_bwd2 or _adam_fold is not None or x.requires_grad or _timing.timing()
+            or torch.are_deterministic_algorithms_enabled()):
+        return None
+    if (block.x_dev is not None or block.xrow_dev is not None or block.n_rows_dev is not None
+            or block.n_edge_rows_dev is not None or block.r_next is not None or block.wl_prepacked is not None
+            or block.n_active is None or x.size(0) != block.n_dst):
+        return None
+    if any(q is None or not q.is_contiguous() for q in params) or not sage2_ok(x, block, reduce, params, False):
+        return None
+    # agg0 [N, K0] unpadded (agg_buffer pads K0 % 4 != 0 rows)
+    if x.size(1) % 4:
+        return None
+    ext = _eager.load()
+    if ext is None:
+        return None
+    global eager_ext_calls
+    eager_ext_calls += 1
+    N, K0 = x.shape
+    F1 = params[3].shape[0]
+    dev = x.device
+    ws_f = _workspace(dev, "sage2", _ws_size("ngnn_sage2_workspace_bytes", K0, F1, N))
+    ws_b = reserve_sage2_bwd(dev, block.n_dst, K0, F1)
+    yscale = dropout_scale(p_drop) if p_drop > 0.0 else 1.0
+    n_edge = min(int(block.n_active), N)
+    return ext.sage2(x, *params, block.rowptr, block.col, n_edge, block.E, _lib.REDUCE[reduce], p_drop, yscale,
+                     _i64_bits(seed), ws_f, ws_b, _lib.stream_handle(dev))
+
+
+def _i64_bits(v: int) -> int:
+    """The uint64 bits of v (the C ABI's seed) as the int64 pybind takes."""
+    v &= 2**64 - 1
+    return v - 2**64 if v >= 2**63 else v
+
+
 def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
                keep_bf16_x: bool = False) -> torch.Tensor:
     out_dtype = x.dtype
@@ -1203,8 +1251,12 @@ def _run_stack(model, x, block: Block, seed: int, seed_dev, params, aggr: str,
     p = model.dropout if model.training else 0.0
     xc = x if (x.stride(1) == 1 and x.stride(0) >= x.size(1)) else x.contiguous()
     head = block.loss_head.start() if (out_dtype == torch.float32 and head_ok(block, xc, params)) else None
-    out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16, head,
-                           *params)
+    out = None
+    if head is None and gouts is None and seed_dev is None and out_dtype == torch.float32:
+        out = _eager_sage2(xc, block, aggr, float(p), int(seed), params)
+    if out is None:
+        out = _SAGEStack.apply(xc, block, aggr, float(p), int(seed), seed_dev, gouts, w_bf16, head,
+                               *params)
     if out_dtype == torch.float32:
         return out
     if out_dtype == torch.bfloat16 and out.is_contiguous() and out.dim() == 2:

@@ -188,3 +188,14 @@ def test_pyg_compatible_init_matches_oracle_rng_order():
     b = pyg_ref.SimpleGCN(10, 12, 4, 2)
     for (k, p), (k2, q) in zip(a.state_dict().items(), b.state_dict().items()):
         assert k == k2 and torch.equal(p, q)
+
+
+def test_eager_extension_loads_and_binds():
+    """The eager stack's C++ node (ngnn/lib/eager/ngnn_eager.so, built by
+    __graft_entry__.build()) imports and takes the library's entry points
+    (no compute call: no GPU here)."""
+    from ngnn import _eager
+    if not os.path.exists(_eager.SO_PATH):
+        pytest.skip("ngnn_eager.so not built")
+    mod = _eager.load()
+    assert mod is not None and callable(mod.sage2) and callable(mod.init)

@@ -249,3 +249,39 @@ def test_eager_reference_loop_routes_through_bwd2():
     for k, q in ref.named_parameters():
         assert_wgrad(grads[0][k], q.grad, msg=f"bwd2:{k}")
         assert_wgrad(grads[1][k], q.grad, msg=f"per-layer:{k}")
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_eager_cpp_node_matches_python_node(train):
+    """The eager step's C++ autograd node (csrc/ngnn_eager.cpp) makes the
+    Python node's launches: the same logits bit for bit and the same weight
+    gradients (within the bar: the backward's atomics), train (dropout) and
+    eval; it is the node that ran."""
+    import torch.nn.functional as F
+
+    import ngnn
+    from ngnn import _eager, fused
+    from ngnn.loader import sample_block, synthetic_graph
+    if _eager.load() is None:
+        pytest.fail("ngnn_eager.so not built (__graft_entry__.build())")
+    graph = synthetic_graph("ogbn-products", DEV, seed=8, scale=0.02)
+    b = sample_block(graph, graph.train_idx[:512], [15, 10], seed=4)
+    outs, grads = [], []
+    for use in (True, False):
+        torch.manual_seed(0)
+        model = ngnn.SAGE(100, 256, 47, 2, dropout=0.5).to(DEV).train(train)
+        torch.manual_seed(42)
+        n0 = fused.eager_ext_calls
+        fused._use_eager_ext = use
+        try:
+            for _ in range(2):  # (twice: the second backward accumulates)
+                out = model(b.x, b.edge_index)[:b.batch_size]
+                F.cross_entropy(out, b.y[:b.batch_size]).backward()
+        finally:
+            fused._use_eager_ext = True
+        assert (fused.eager_ext_calls - n0 == 2) == use
+        outs.append(out.detach().cpu())
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()})
+    assert torch.equal(outs[0], outs[1])
+    for k in grads[0]:
+        assert_wgrad(grads[0][k], grads[1][k], msg=k)
