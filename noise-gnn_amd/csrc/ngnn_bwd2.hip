@@ -166,7 +166,9 @@ __device__ __forceinline__ float sum_xor32(float v) {
 // weights are zero): no x rows staged, no dW_r0 / dW_r1 products -- stage
 // C0's dW_l0 tiles split over all eight waves, stage C1's W_l1 tiles over
 // the eight, stage B skips the dy-only K chunk (its W_r1 rows are zero)
-template <bool XR, int KT, bool LAG, bool ROOT = true>
+// DBG (profiling builds only, NGNN_B2_DBG_BUILD): bit 0 -- constant chunk
+// scales, no maxima (wrong results: the time the chunk maxima cost)
+template <bool XR, int KT, bool LAG, bool ROOT = true, int DBG = 0>
 __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     extern __shared__ __attribute__((aligned(16))) __bf16 lb_[];
     L16 *lb = (L16 *)(lb_);  // (an address-space cast: the shared array IS in LDS)
@@ -314,6 +316,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     // slot sl (8 waves x 4); every thread reads them back after a barrier
     float4 *smax = reinterpret_cast<float4 *>(sred + 2 * 256 + 480);  // [2][8]
     auto publish_max = [&](const auto &p, int sl) __attribute__((always_inline)) {
+        if (DBG & 1) return;
         float mX = fmaxf(amax4(p.gv), fmaxf(fmaxf(fabsf(p.dyv[0]), fabsf(p.dyv[1])),
                                           fmaxf(fabsf(p.dyv[2]), fabsf(p.dyv[3]))));
         float mH = amax4(p.hv);
@@ -329,6 +332,7 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     // accumulators, rescaled in place by the change, never overflow; a chunk
     // held below its own scale has values 2^20 under the previous one's)
     auto read_exps = [&](int sl, const Exps &pe, bool first) __attribute__((always_inline)) -> Exps {
+        if (DBG & 1) return Exps{10, 10, 10, 10};
         float4 m = smax[sl * 8];
 #pragma unroll
         for (int w = 1; w < 8; ++w) {
@@ -783,6 +787,13 @@ extern "C" int ngnn_sage2_bwd(const float *dy, int64_t ldy, int64_t F1, const fl
         constexpr int KTv = decltype(kt_c)::value;
         auto fn = !root ? (lag ? k_bwd2<false, KTv, true, false> : k_bwd2<false, KTv, false, false>)
                         : lag ? k_bwd2<XRv, KTv, true> : k_bwd2<XRv, KTv, false>;
+#ifdef NGNN_B2_DBG_BUILD
+        static const int dbg = [] {
+            const char *v = std::getenv("NGNN_B2_DBG");
+            return v ? std::atoi(v) : 0;
+        }();
+        if (root && lag && dbg == 1) fn = k_bwd2<XRv, KTv, true, true, 1>;
+#endif
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);  // (cheap; the function varies with root / lag)
         hipLaunchKernelGGL(fn, dim3(B2_S * B2_NCH), dim3(B2_THREADS), lds, st, b);
