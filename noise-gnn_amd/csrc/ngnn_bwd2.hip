@@ -524,17 +524,30 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
     if (LAG) lds_barrier();
     for (int c = cb; c < ce; ++c) {
         L16 *cur = lb + (c & 1) * BUF;
-        if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF, ep);
-        if (!LAG) {
-            publish_max(pre, c & 1);
+        if (LAG) {
+            // chunk c's images first (buffer c & 1: chunk c - 2's, whose
+            // stage C ran before the last two barriers), then chunk c + 1's
+            // loads, which land during stage C(c - 1) and stage B(c) -- its
+            // maxima are published after stage B
+            const Exps ec = read_exps(c & 1, ep, c == cb);
+            stage_images(pre, cur, ec);
+            load(c + 1, pre);
+            if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF, ep);
+            lds_barrier();  // (LDS only: the next chunk's loads stay in flight)
+            stage_b(cur, ec);
+            publish_max(pre, (c + 1) & 1);
             lds_barrier();
+            ep = ec;
+            continue;
         }
+        if (c > cb) stage_c(lb + ((c - 1) & 1) * BUF, ep);
+        publish_max(pre, c & 1);
+        lds_barrier();
         const Exps ec = read_exps(c & 1, ep, c == cb);
         stage_images(pre, cur, ec);
         load(c + 1, pre);
         lds_barrier();  // (LDS only: the next chunk's loads stay in flight)
         stage_b(cur, ec);
-        if (LAG) publish_max(pre, (c + 1) & 1);
         lds_barrier();
         ep = ec;
     }
@@ -634,6 +647,16 @@ __global__ __launch_bounds__(256) void k_bwd2_reduce(const float *__restrict__ s
     if (ADAM) t = *af.step;  // (issued before the slab loads)
     float v = 0.0f;
     int sl = 0;
+    // (32 slab loads in flight per thread: the launch is a few waves per
+    // SIMD, so each batch costs one HBM round trip -- the sum stays in slab
+    // order, one element at a time)
+    for (; sl + 32 <= S; sl += 32) {
+        float w[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) w[u] = slab[static_cast<int64_t>(sl + u) * total + i];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) v += w[u];
+    }
     for (; sl + 8 <= S; sl += 8) {
         float w[8];
 #pragma unroll

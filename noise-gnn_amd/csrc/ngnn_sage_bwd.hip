@@ -554,9 +554,17 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int used = wgrad_slices(*r_ptr, S);
-    // loads issued 8 at a time (memory-level parallelism), summed in slab order
+    // loads issued 32 (then 8) at a time (memory-level parallelism: one HBM
+    // round trip per batch), summed in slab order
     float t = 0.0f;
     int s = 0;
+    for (; s + 32 <= used; s += 32) {
+        float v[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) v[u] = ws[static_cast<size_t>(s + u) * total + i];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) t += v[u];
+    }
     for (; s + 8 <= used; s += 8) {
         float v[8];
 #pragma unroll
