@@ -47,6 +47,25 @@ constexpr int WWU = WBN * WKC / 256;       // weight loads per thread per stage 
 // ---- aggregate rows [0, min(n_rows, *n_rows_dev, *n_edge_dev)): one wave
 // per row, lane owns columns p0 + lane + 64 c (c < NC); neighbour ids loaded
 // 64 at a time and broadcast; two neighbour rows in flight, reduced in order.
+// The H2 layer's preparation (k_wide_prep_h2, below) riding on the
+// aggregate's launch: workgroups [n_agg, grid) split the W rows and take the
+// x rows' exponents while [0, n_agg) aggregate -- the two are independent,
+// and the preparation's x pass overlaps the gathers instead of following
+// them as a launch of its own.  img == nullptr: no preparation.
+struct WidePrep {
+    const float *wr, *wl;
+    int64_t ldw;
+    int Fo, Kp;
+    _Float16 *img;
+    int *ew;
+    int nbw;     // workgroups of W rows (4 rows each)
+    int n_rows;  // x rows whose exponents are taken
+    int *ex;
+    int n_agg;   // the aggregate's workgroups
+};
+__device__ void wide_prep_body(const WidePrep &pp, const float *x, const float *const *x_dev, int64_t ldx, int K,
+                               const int32_t *n_rows_dev, int bid, int nblk);
+
 template <int RED, int NC>
 __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, int64_t ldx, int K,
                                                   const int32_t *__restrict__ rowptr,
@@ -55,7 +74,13 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
                                                   const int32_t *__restrict__ n_edge_dev,
                                                   float *__restrict__ agg, int64_t ld_agg,
                                                   int n_cap, int round16,
-                                                  const float *const *x_dev, int *__restrict__ ea) {
+                                                  const float *const *x_dev, int *__restrict__ ea, WidePrep pp) {
+    if (pp.img && static_cast<int>(blockIdx.x) >= pp.n_agg) {
+        wide_prep_body(pp, x, x_dev, ldx, K, n_rows_dev, static_cast<int>(blockIdx.x) - pp.n_agg,
+                       static_cast<int>(gridDim.x) - pp.n_agg);
+        return;
+    }
+    const int n_blk = pp.img ? pp.n_agg : static_cast<int>(gridDim.x);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (x_dev) x = gload(x_dev, 0);  // (a graph slot's batch address, read at run time)
     int rows = n_rows;
@@ -67,7 +92,7 @@ __global__ __launch_bounds__(256) void k_wide_agg(const float *__restrict__ x, i
     rows = min(rows, n_cap);
     if (n_rows_dev) rows = min(rows, *n_rows_dev);
     const float init = (RED == NGNN_REDUCE_MAX) ? -INFINITY : 0.0f;
-    for (int64_t d = static_cast<int64_t>(blockIdx.x) * 4 + wave; d < rows; d += gridDim.x * 4) {
+    for (int64_t d = static_cast<int64_t>(blockIdx.x) * 4 + wave; d < rows; d += n_blk * 4) {
         const int beg = rowptr[d], end = rowptr[d + 1];
         float am = 0.0f;  // (ea: the row's |max| -> its H2 staging exponent)
         for (int p0 = 0; p0 < K; p0 += 64 * NC) {
@@ -570,28 +595,32 @@ __device__ __forceinline__ void wimg_h2_row(const float *__restrict__ wr, const 
 // the H2 layer's preparation in one launch: workgroups [0, nbw) split the W
 // rows (wimg_h2_row), the rest take one wave per x row [0, rows) -> ex (the
 // root staging's exponents; the aggregate rows' come from k_wide_agg)
-__global__ __launch_bounds__(256) void k_wide_prep_h2(const float *__restrict__ wr, const float *__restrict__ wl,
-                                                      int64_t ldw, int Fo, int Kp, _Float16 *__restrict__ img,
-                                                      int *__restrict__ ew, int nbw, const float *__restrict__ x,
-                                                      const float *const *x_dev, int64_t ldx, int K, int n_rows,
-                                                      const int32_t *__restrict__ n_rows_dev, int *__restrict__ ex) {
+// (workgroup bid of nblk: the body shared with k_wide_agg's riders)
+__device__ void wide_prep_body(const WidePrep &pp, const float *x, const float *const *x_dev, int64_t ldx, int K,
+                               const int32_t *n_rows_dev, int bid, int nblk) {
     const int lane = threadIdx.x & 63;
-    if (static_cast<int>(blockIdx.x) < nbw) {
-        const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (row < 2 * Fo) wimg_h2_row(wr, wl, ldw, Fo, K, Kp, img, ew, row, lane);
+    if (bid < pp.nbw) {
+        const int row = bid * 4 + (threadIdx.x >> 6);
+        if (row < 2 * pp.Fo) wimg_h2_row(pp.wr, pp.wl, pp.ldw, pp.Fo, K, pp.Kp, pp.img, pp.ew, row, lane);
         return;
     }
     if (x_dev) x = gload(x_dev, 0);
-    int rows = n_rows;
+    int rows = pp.n_rows;
     if (n_rows_dev) rows = min(rows, *n_rows_dev);
-    const int waves = (gridDim.x - nbw) * 4;
-    for (int r = (blockIdx.x - nbw) * 4 + (threadIdx.x >> 6); r < rows; r += waves) {
+    const int waves = (nblk - pp.nbw) * 4;
+    for (int r = (bid - pp.nbw) * 4 + (threadIdx.x >> 6); r < rows; r += waves) {
         const float *p = x + static_cast<int64_t>(r) * ldx;
         float m = 0.0f;
         for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(p[k]));
         const int e = h2_exp(wave_max(m));
-        if (lane == 0) ex[r] = e;
+        if (lane == 0) pp.ex[r] = e;
     }
+}
+
+__global__ __launch_bounds__(256) void k_wide_prep_h2(WidePrep pp, const float *__restrict__ x,
+                                                      const float *const *x_dev, int64_t ldx, int K,
+                                                      const int32_t *__restrict__ n_rows_dev) {
+    wide_prep_body(pp, x, x_dev, ldx, K, n_rows_dev, static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x));
 }
 
 template <bool VOUT, int BM>
@@ -861,6 +890,17 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         ea = ex + n_rows;
     }
     int *const agg_ea = ea;
+    // the preparation's workgroups: 4 W rows each, then one wave per x row
+    // (capped); riding on the aggregate's launch when there is one
+    WidePrep prep{};
+    unsigned prep_blocks = 0;
+    if (use_h2) {
+        prep = WidePrep{wr, wl, ldw, static_cast<int>(Fo), Kp, h2_img, ew, static_cast<int>(ceil_div(2 * Fo, 4)),
+                        static_cast<int>(n_rows), ex, 0};
+        const int64_t gr = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows, 4), 8 * num_cus()));
+        prep_blocks = static_cast<unsigned>(prep.nbw + gr);
+    }
+    bool prep_done = false;
     float *agg = nullptr;
     int64_t lda = ld_agg;
     if (has_agg) {
@@ -873,11 +913,13 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
             lda = K;
         }
         const unsigned ga = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_edge, 4), 8 * num_cus()));
+        prep.n_agg = static_cast<int>(ga);
+        prep_done = use_h2;
         auto launch_agg = [&](auto red_c, auto nc_c) {
-            hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
+            hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga + prep_blocks),
                                dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                                static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, lda,
-                               static_cast<int>(n_rows), 0, x_dev, agg_ea);
+                               static_cast<int>(n_rows), 0, x_dev, agg_ea, prep);
         };
         auto by_nc = [&](auto red_c) {
             if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
@@ -932,13 +974,12 @@ int sage_fwd_wide(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
     {
         if (use_h2) {
             _Float16 *img = h2_img;
-            const int nbw = static_cast<int>(ceil_div(2 * Fo, 4));
-            const int64_t gr = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_rows, 4), 8 * num_cus()));
-            hipLaunchKernelGGL(k_wide_prep_h2, dim3(static_cast<unsigned>(nbw + gr)), dim3(256), 0, st, wr, wl, ldw,
-                               static_cast<int>(Fo), Kp, img, ew, nbw, x, x_dev, ldx, static_cast<int>(K),
-                               static_cast<int>(n_rows), n_rows_dev, ex);
-            const int rc = launch_status();
-            if (rc) return rc;
+            if (!prep_done) {
+                hipLaunchKernelGGL(k_wide_prep_h2, dim3(prep_blocks), dim3(256), 0, st, prep, x, x_dev, ldx,
+                                   static_cast<int>(K), n_rows_dev);
+                const int rc = launch_status();
+                if (rc) return rc;
+            }
             // (NGNN_WIDE_BM=128, read once: the eight-wave 128-row tile -- A/B)
             static const int bm = [] {
                 const char *e = std::getenv("NGNN_WIDE_BM");
@@ -1012,7 +1053,7 @@ int sage_wide_aggregate(const float *x, int64_t ldx, int64_t K, int64_t n_rows,
         hipLaunchKernelGGL((k_wide_agg<decltype(red_c)::value, decltype(nc_c)::value>), dim3(ga),
                            dim3(256), 0, st, x, ldx, static_cast<int>(K), rowptr, col,
                            static_cast<int>(n_edge), n_rows_dev, n_edge_rows_dev, agg, ld_agg,
-                           static_cast<int>(n_rows), 1, x_dev, nullptr);
+                           static_cast<int>(n_rows), 1, x_dev, nullptr, WidePrep{});
     };
     auto by_nc = [&](auto red_c) {
         if (K <= 256) launch_agg(red_c, std::integral_constant<int, 4>{});
