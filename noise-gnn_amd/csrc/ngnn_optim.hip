@@ -72,63 +72,95 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
         p = p - step_size * (m / denom);
     };
     const int64_t nvb = T.boff[T.n];
-    int k = 0;
-    for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    // one virtual workgroup's operands, loaded a workgroup-stride ahead of its
+    // update: the next one's loads are in flight while this one computes and
+    // stores (distinct elements: a load issued before a store to other
+    // addresses returns what it would alone)
+    struct Ld {
+        int k;
+        int64_t j, n;
+        bool vec;
+        float4 m4, v4;
+        float g[4], p[4];
+    };
+    auto load = [&](int64_t vb, int &k, Ld &L) __attribute__((always_inline)) {
         // virtual workgroup -> tensor: uniform (scalar loads of its pointers)
         while (k + 1 < T.n && vb >= T.boff[k + 1]) ++k;
-        const int64_t n = T.off[k + 1] - T.off[k];
-        const int64_t j = (vb - T.boff[k]) * kAdamChunk + threadIdx.x * kAdamVec;
-        if (j >= n) continue;
-        float *mp = T.m[k] + j, *vp = T.v[k] + j;
-        if (T.vec[k] && j + kAdamVec <= n) {  // aligned base, j % 4 == 0
-            float4 m4 = *reinterpret_cast<const float4 *>(mp);
-            float4 v4 = *reinterpret_cast<const float4 *>(vp);
-            float g[4], p[4];
-            if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
-                const uint2 gb = *reinterpret_cast<const uint2 *>(
-                    reinterpret_cast<const uint16_t *>(T.g[k]) + j);
-                const uint2 pb = *reinterpret_cast<const uint2 *>(
-                    reinterpret_cast<const uint16_t *>(T.p[k]) + j);
-                g[0] = bf16_bits_to_f(gb.x & 0xffffu); g[1] = bf16_bits_to_f(gb.x >> 16);
-                g[2] = bf16_bits_to_f(gb.y & 0xffffu); g[3] = bf16_bits_to_f(gb.y >> 16);
-                p[0] = bf16_bits_to_f(pb.x & 0xffffu); p[1] = bf16_bits_to_f(pb.x >> 16);
-                p[2] = bf16_bits_to_f(pb.y & 0xffffu); p[3] = bf16_bits_to_f(pb.y >> 16);
-            } else {
-                const float4 g4 = *reinterpret_cast<const float4 *>(T.g[k] + j);
-                const float4 p4 = *reinterpret_cast<const float4 *>(T.p[k] + j);
-                g[0] = g4.x; g[1] = g4.y; g[2] = g4.z; g[3] = g4.w;
-                p[0] = p4.x; p[1] = p4.y; p[2] = p4.z; p[3] = p4.w;
-            }
-            upd(g[0], p[0], m4.x, v4.x);
-            upd(g[1], p[1], m4.y, v4.y);
-            upd(g[2], p[2], m4.z, v4.z);
-            upd(g[3], p[3], m4.w, v4.w);
-            *reinterpret_cast<float4 *>(mp) = m4;
-            *reinterpret_cast<float4 *>(vp) = v4;
+        L.k = k;
+        L.n = T.off[k + 1] - T.off[k];
+        L.j = (vb - T.boff[k]) * kAdamChunk + threadIdx.x * kAdamVec;
+        L.vec = T.vec[k] && L.j + kAdamVec <= L.n;
+        if (!L.vec) return;  // (the tensor's ragged tail or an unaligned view: at the update)
+        const int64_t j = L.j;
+        L.m4 = *reinterpret_cast<const float4 *>(T.m[k] + j);
+        L.v4 = *reinterpret_cast<const float4 *>(T.v[k] + j);
+        if (T.bf[k]) {  // bf16 parameter and gradient: widen (exact), update, round
+            const uint2 gb = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint16_t *>(T.g[k]) + j);
+            const uint2 pb = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint16_t *>(T.p[k]) + j);
+            L.g[0] = bf16_bits_to_f(gb.x & 0xffffu); L.g[1] = bf16_bits_to_f(gb.x >> 16);
+            L.g[2] = bf16_bits_to_f(gb.y & 0xffffu); L.g[3] = bf16_bits_to_f(gb.y >> 16);
+            L.p[0] = bf16_bits_to_f(pb.x & 0xffffu); L.p[1] = bf16_bits_to_f(pb.x >> 16);
+            L.p[2] = bf16_bits_to_f(pb.y & 0xffffu); L.p[3] = bf16_bits_to_f(pb.y >> 16);
+        } else {
+            const float4 g4 = *reinterpret_cast<const float4 *>(T.g[k] + j);
+            const float4 p4 = *reinterpret_cast<const float4 *>(T.p[k] + j);
+            L.g[0] = g4.x; L.g[1] = g4.y; L.g[2] = g4.z; L.g[3] = g4.w;
+            L.p[0] = p4.x; L.p[1] = p4.y; L.p[2] = p4.z; L.p[3] = p4.w;
+        }
+    };
+    auto apply = [&](Ld &L) __attribute__((always_inline)) {
+        const int k = L.k;
+        const int64_t j = L.j, n = L.n;
+        if (j >= n) return;
+        if (L.vec) {
+            upd(L.g[0], L.p[0], L.m4.x, L.v4.x);
+            upd(L.g[1], L.p[1], L.m4.y, L.v4.y);
+            upd(L.g[2], L.p[2], L.m4.z, L.v4.z);
+            upd(L.g[3], L.p[3], L.m4.w, L.v4.w);
+            *reinterpret_cast<float4 *>(T.m[k] + j) = L.m4;
+            *reinterpret_cast<float4 *>(T.v[k] + j) = L.v4;
             if (T.bf[k]) {
-                const uint2 o{f_to_bf16_bits(p[0]) | (f_to_bf16_bits(p[1]) << 16),
-                              f_to_bf16_bits(p[2]) | (f_to_bf16_bits(p[3]) << 16)};
+                const uint2 o{f_to_bf16_bits(L.p[0]) | (f_to_bf16_bits(L.p[1]) << 16),
+                              f_to_bf16_bits(L.p[2]) | (f_to_bf16_bits(L.p[3]) << 16)};
                 *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(T.p[k]) + j) = o;
             } else {
-                *reinterpret_cast<float4 *>(T.p[k] + j) = float4{p[0], p[1], p[2], p[3]};
+                *reinterpret_cast<float4 *>(T.p[k] + j) = float4{L.p[0], L.p[1], L.p[2], L.p[3]};
             }
-        } else {  // the tensor's ragged tail, or an unaligned view
-            for (int64_t e = j; e < min(j + kAdamVec, n); ++e) {
-                float g, p;
-                if (T.bf[k]) {
-                    g = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.g[k])[e]);
-                    p = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.p[k])[e]);
-                } else {
-                    g = T.g[k][e];
-                    p = T.p[k][e];
-                }
-                float m = T.m[k][e], v = T.v[k][e];
-                upd(g, p, m, v);
-                T.m[k][e] = m;
-                T.v[k][e] = v;
-                if (T.bf[k]) reinterpret_cast<uint16_t *>(T.p[k])[e] = static_cast<uint16_t>(f_to_bf16_bits(p));
-                else T.p[k][e] = p;
+            return;
+        }
+        for (int64_t e = j; e < min(j + kAdamVec, n); ++e) {
+            float g, p;
+            if (T.bf[k]) {
+                g = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.g[k])[e]);
+                p = bf16_bits_to_f(reinterpret_cast<const uint16_t *>(T.p[k])[e]);
+            } else {
+                g = T.g[k][e];
+                p = T.p[k][e];
             }
+            float m = T.m[k][e], v = T.v[k][e];
+            upd(g, p, m, v);
+            T.m[k][e] = m;
+            T.v[k][e] = v;
+            if (T.bf[k]) reinterpret_cast<uint16_t *>(T.p[k])[e] = static_cast<uint16_t>(f_to_bf16_bits(p));
+            else T.p[k][e] = p;
+        }
+    };
+    int k = 0;
+    int64_t vb = blockIdx.x;
+    if (vb < nvb) {
+        Ld cur;
+        load(vb, k, cur);
+        for (;;) {
+            const int64_t nx = vb + gridDim.x;
+            if (nx >= nvb) {
+                apply(cur);
+                break;
+            }
+            Ld nl;
+            load(nx, k, nl);
+            apply(cur);
+            cur = nl;
+            vb = nx;
         }
     }
     if (ticket && threadIdx.x == 0 && tk == gs - 1) {

@@ -141,7 +141,8 @@ __global__ __launch_bounds__(256) void k_slot_load(
             const int64_t d = ei[ld_ei + e];
             if (d >= 0 && d < B) m = max(m, g | static_cast<uint64_t>(src_ok(ei[e], N) + 1));
         }
-        // one atomic per wave (same-address atomics serialise)
+        // one atomic per workgroup (same-address atomics serialise at the
+        // memory side: one per wave was ~240 of them on a products block)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             const uint64_t other = (static_cast<uint64_t>(static_cast<uint32_t>(
@@ -149,8 +150,13 @@ __global__ __launch_bounds__(256) void k_slot_load(
                                    static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o));
             m = max(m, other);
         }
-        if (m && (threadIdx.x & 63) == 0)
-            atomicMax(reinterpret_cast<unsigned long long *>(r_next), static_cast<unsigned long long>(m));
+        __shared__ uint64_t s_m[4];  // (256 threads: 4 waves)
+        if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+            if (m) atomicMax(reinterpret_cast<unsigned long long *>(r_next), static_cast<unsigned long long>(m));
+        }
     }
     if (pk_dst) {
         // pack job: pk_dst = ngnn_pack_weight(pk_w) -- the layout

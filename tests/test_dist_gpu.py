@@ -337,3 +337,66 @@ def test_config4_bf16_3layer_data_parallel_two_ranks():
         # the all-reduced bf16 .grad = the mean of the ranks' oracle gradients
         # at the SURVEY 8(c) bf16 bar (the ratio to the bar: <= 1)
         assert worst[0] <= 1.0, worst
+
+
+def _worker_rccl(port, q):
+    """The RCCL backend on this box's one GPU: a world-1 "nccl" process group
+    (RCCL refuses two ranks on one device), the bucket's pack, the RCCL
+    all_reduce -- eager and captured in a HIP graph -- and unpack, through
+    ngnn.distributed as the bench's N-GPU run takes them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    try:
+        import datetime
+
+        import ngnn
+        from ngnn.distributed import GradAllReduce
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev,
+                                timeout=datetime.timedelta(seconds=90))
+        assert dist.get_backend() == "nccl"
+        torch.manual_seed(0)
+        model = ngnn.SAGE(100, 256, 47, 2).to(dev)
+        red = GradAllReduce(model.parameters())
+        want = []
+        for p in model.parameters():
+            p.grad = torch.randn_like(p)
+            want.append(p.grad.detach().clone())
+        red.pack()
+        red.allreduce()
+        red.unpack()
+        torch.cuda.synchronize()
+        err = max(float((p.grad - w).abs().max()) for p, w in zip(model.parameters(), want))
+        # the all-reduce captured in a graph (the split reduce's collective
+        # is eager; this checks RCCL's capture on the bucket too)
+        red.bucket.fill_(1.0)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            red.allreduce()  # (warm-up on the side stream)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            red.allreduce()
+        g.replay()
+        torch.cuda.synchronize()
+        ok_graph = bool(torch.all(red.bucket == 1.0))
+        q.put((err, ok_graph, None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((float("inf"), False, traceback.format_exc()))
+
+
+@pytest.mark.timeout(200)
+def test_rccl_backend_world1_bucket_allreduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl, args=(_free_port(), q))
+    p.start()
+    err, ok_graph, tb = q.get(timeout=150)
+    p.join(timeout=30)
+    assert tb is None, tb
+    assert err == 0.0, err  # (one rank: the sum is the rank's own bucket, / 1 exact)
+    assert ok_graph
