@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NGNN_ABI_VERSION 20
+#define NGNN_ABI_VERSION 21
 
 /* error codes (negative); positive values are hipError_t */
 #define NGNN_OK 0
@@ -629,9 +629,10 @@ int ngnn_seed_xent_bwd(const float *logits, int64_t ld, int64_t B, int64_t C, co
  * pointers; grads, exp_avgs, exp_avg_sqs like params, numels their sizes),
  * torch.optim.Adam's rule (amsgrad/maximize off, optional L2 weight decay),
  * with the step count a device float that this call advances (so a captured
- * HIP graph replays correctly).  ticket (nullable): 64 device uint32 (ABI
- * 17; one before), zero before the first call, that the update's workgroups
- * count themselves on in two levels; the last one advances *step and every
+ * HIP graph replays correctly).  ticket (nullable): 1024 device uint32 (ABI
+ * 21; 64 in ABI 17-20, one before), zero before the first call, that the
+ * update's workgroups count themselves on in two levels (each group's word
+ * on a 128-B line of its own); the last one advances *step and every
  * word is zero again on return (one launch per call instead of an update +
  * increment pair; up to 16 tensors).  dtypes (host, nullable
  * = all NGNN_F32): per tensor NGNN_F32 or NGNN_BF16 (params and grads in that

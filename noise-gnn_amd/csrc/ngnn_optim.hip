@@ -28,7 +28,9 @@ struct AdamTensors {
     int n;
 };
 
-constexpr int kAdamTickets = 64;              // uint32 words of the ticket (ABI 17)
+constexpr int kAdamTickets = 1024;            // uint32 words of the ticket (ABI 21; 64 before)
+constexpr int kAdamTicketStride = 32;         // words between two group tickets: one 128-B line each
+constexpr int kAdamGroups = kAdamTickets / kAdamTicketStride - 1;  // (line 0: the top ticket)
 constexpr int kAdamVec = 4;                   // elements per thread
 constexpr int kAdamChunk = 256 * kAdamVec;    // elements per virtual workgroup
 
@@ -59,7 +61,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
     if (ticket) {
         asm volatile("" ::"v"(t));  // (this thread's read of *step has landed)
         __syncthreads();
-        if (threadIdx.x == 0) tk = atomicAdd(ticket + 1 + gi, 1u);
+        if (threadIdx.x == 0) tk = atomicAdd(ticket + kAdamTicketStride * (1 + gi), 1u);
     }
     const float bc1 = 1.0f - powf(b1, t);
     const float bc2s = sqrtf(1.0f - powf(b2, t));
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamTensors T, float *__restrict__
         // the last of its group of 32 (every member has read *step): counts on
         // the top ticket (two levels, ABI 17 -- same-address atomics
         // serialise at the memory side); the last group advances the count
-        ticket[1 + gi] = 0u;
+        ticket[kAdamTicketStride * (1 + gi)] = 0u;
         const unsigned ngr = (gridDim.x + 31) >> 5;
         if (atomicAdd(ticket, 1u) == ngr - 1) {
             *step = t;
@@ -234,14 +236,14 @@ extern "C" int ngnn_adam_step(int n_tensors, float *const *params, const float *
         // alone (tools/adam_micro.py), but 9.3 + 4.0 vs 12.8 us inside the
         // training step's graph: the ticket stays)
         // at most 2 workgroups per CU: the rest is the grid-stride loop (and at
-        // most 32 x 63 -- the ticket's groups)
+        // most 32 x kAdamGroups -- the ticket's groups)
         // (NGNN_ADAM_WG_PER_CU, read once: the per-CU cap -- A/B)
         static const int wg_cu = [] {
             const char *e = std::getenv("NGNN_ADAM_WG_PER_CU");
             return e ? std::max(1, std::atoi(e)) : 2;
         }();
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(std::min<int64_t>(T.boff[T.n], wg_cu * num_cus()),
-                                                                      32 * (kAdamTickets - 1)));
+                                                                      32 * kAdamGroups));
         hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, T, step, ticket, lr, beta1, beta2,
                            eps, weight_decay, gate, gate_gen);
         const int rc = launch_status();

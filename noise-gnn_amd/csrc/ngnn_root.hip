@@ -56,7 +56,7 @@ __global__ __launch_bounds__(RR_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1
     static_assert(!NAR || (NTW % 2 == 0 && !OB), "narrow: out / z halves");
     extern __shared__ __attribute__((aligned(16))) v4f lds[];
     __shared__ int s_next;  // the workgroup's tile-claim counter
-    const unsigned long long k0 = rr_clock();
+    [[maybe_unused]] const unsigned long long k0 = rr_clock();
 #ifdef NGNN_DBG_EMPTY
     if (a.K != 1234567) return;  // (diagnostic: launch cost alone)
 #endif
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(RR_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1
     if (a.img) __builtin_amdgcn_s_waitcnt(0);  // (the image's LDS-DMAs landed)
     __syncthreads();
 
-    const unsigned long long k1 = rr_clock();
+    [[maybe_unused]] const unsigned long long k1 = rr_clock();
 #ifdef NGNN_DBG_PROLOGUE_ONLY
     if (k1 != 1234567ull) return;  // (diagnostic: the image build alone)
 #endif
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(RR_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1
     // one tile on fragments (xc, xtc); the next tile's rows load into (xn, xtn)
     auto tile = [&](v4f (&xc)[NXF], const float (&xtc)[T4N], v4f (&xn)[NXF],
                     float (&xtn)[T4N]) __attribute__((always_inline)) -> bool {
-        const unsigned long long c0 = rr_clock();
+        [[maybe_unused]] const unsigned long long c0 = rr_clock();
         const int tn = claim();
         load_tile(xn, xtn, row_off(tn));
         v4f acc[NTW];
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(RR_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1
                     acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[m], xv, acc[m], 0, 0, 0);
             }
         }
-        const unsigned long long c1 = rr_clock();
+        [[maybe_unused]] const unsigned long long c1 = rr_clock();
         // W parts of step s = c NTW + m from a 3-slot ring, read two steps ahead
         bf16x8 wr[3][NP];
         auto load_w = [&](int s, bf16x8 (&w)[NP]) __attribute__((always_inline)) {
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(RR_WAVES * 64) __attribute__((amdgpu_waves_per_eu(1
                 acc[m] = u;
             }
         }
-        const unsigned long long c2 = rr_clock();
+        [[maybe_unused]] const unsigned long long c2 = rr_clock();
         const i32x4 orsrc = OB ? tile_rsrc2(a.out, a.ldo, a.Fo, t, n_rows) : tile_rsrc(a.out, a.ldo, a.Fo, t, n_rows);
         const i32x4 zr = NAR ? tile_rsrc(a.z, a.ldz, 16 * a.NT1, t, n_rows) : orsrc;
         epilogue<NTW, DM, RELU, VEC, OB, NAR, false, NAR>(acc, a, orsrc, zr, t * RT_ROWS + rl, rl, q);

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NGNN_LIB: an alternative build of the same ABI (A/B kernel experiments);
 # read once, at import
 LIB_PATH = os.environ.get("NGNN_LIB") or os.path.join(_HERE, "lib", "libngnn.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 OK = 0
 SLOT_UNSORTED = 1  # ngnn_slot_load's err bits (include/ngnn.h NGNN_SLOT_*)

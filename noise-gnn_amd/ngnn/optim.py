@@ -76,7 +76,7 @@ class Adam(torch.optim.Optimizer):
             step = self.state[ps[0]]["step"]
             ticket = self._tickets.get(step.data_ptr())
             if ticket is None:  # zero once; the kernel re-zeroes it after every use
-                ticket = torch.zeros(64, dtype=torch.int32, device=step.device)  # (ABI 17: two levels)
+                ticket = torch.zeros(1024, dtype=torch.int32, device=step.device)  # (ABI 21: two levels, a line per group)
                 self._tickets[step.data_ptr()] = ticket
             grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
             n = len(ps)
