@@ -26,6 +26,7 @@ Amazon-Computers / CitationFull-Cora and a power-law
 from __future__ import annotations
 
 import dataclasses
+import os
 import weakref
 
 import torch
@@ -533,7 +534,10 @@ class NeighborLoader:
         self.epoch += 1
         dev = seeds.device
         main = torch.cuda.current_stream(dev)
-        side = torch.cuda.Stream(dev)
+        # (NGNN_SIDE_PRIORITY: the sampling stream's priority, torch's scale --
+        # negative is higher; A/B of how its kernels share the device with
+        # the step's)
+        side = torch.cuda.Stream(dev, priority=int(os.environ.get("NGNN_SIDE_PRIORITY", "0")))
         side.wait_stream(main)  # seeds (randperm) were made on the main stream
         n = len(self)
         cache = _sampler_cache(self.graph)
