@@ -522,6 +522,11 @@ __global__ __launch_bounds__(B2_THREADS, 1) void k_bwd2(B2Args a) {
         if (LAG) publish_max(pre, cb & 1);
     }
     if (LAG) lds_barrier();
+#ifdef NGNN_B2_SETPRIO
+    // (A/B: static priority for the second-dispatched half, waves 4-7 --
+    // MI355X_MICROARCH.md, scheduling item 4)
+    if (wv >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     for (int c = cb; c < ce; ++c) {
         L16 *cur = lb + (c & 1) * BUF;
         if (LAG) {

@@ -914,6 +914,11 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
     // partners by wave number >= 4)
     auto pipeline = [&](auto lag_c) __attribute__((always_inline)) {
         constexpr bool LAG = decltype(lag_c)::value;
+#ifdef NGNN_F2_SETPRIO
+        // (A/B: static priority for the second-dispatched half, waves 4-7 --
+        // MI355X_MICROARCH.md, scheduling item 4)
+        if (LAG) __builtin_amdgcn_s_setprio(1);
+#endif
         // x ring: at step j, xv[j&1] holds tile j + 2 and xv[~j&1] tile j + 3;
         // XR: ixr[j&1] holds n_id of tile j + 4
         v4f xv[2];
