@@ -56,6 +56,8 @@ def main():
     fused._SAGEStack.backward = staticmethod(timed("stack.backward", fused._SAGEStack.backward))
     fused._SAGEStack.forward = staticmethod(timed("stack.forward", fused._SAGEStack.forward))
     models._dropout_seed = timed("dropout_seed", models._dropout_seed)
+    fused.sage_stack = timed("sage_stack", fused.sage_stack)
+    fused._eager_sage2 = timed("eager_sage2 (C++ node)", fused._eager_sage2)
 
     def one(b, rec):
         t = [time.perf_counter()]
