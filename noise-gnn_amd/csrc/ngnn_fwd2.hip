@@ -59,6 +59,17 @@ constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
 #ifndef NGNN_F2_STAUX
 #define NGNN_F2_STAUX 2  // the main phase's h / out / z stores non-temporal (nt): fused launch 93.7 -> 89.6 us (A/B, r06g)
 #endif
+// (per-output overrides, A/B: the consumers -- the narrow launch reads z and
+// out, k_bwd2 reads h -- may prefer the rows cached)
+#ifndef NGNN_F2_STAUX_H
+#define NGNN_F2_STAUX_H NGNN_F2_STAUX
+#endif
+#ifndef NGNN_F2_STAUX_Z
+#define NGNN_F2_STAUX_Z NGNN_F2_STAUX
+#endif
+#ifndef NGNN_F2_STAUX_O
+#define NGNN_F2_STAUX_O NGNN_F2_STAUX
+#endif
 
 // two fp16 parts (round to nearest even) of 8 scaled values
 __device__ __forceinline__ void h2_split(v4f a, v4f b, half8 &p1, half8 &p2) {
@@ -757,8 +768,8 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
         }
         // h rows the backward reads (past the bound: dropped by the range)
         const int ho = static_cast<int>(static_cast<uint32_t>(r) * static_cast<uint32_t>(a.ldh) * 4u) + (32 * wv + 4 * q) * 4;
-        buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, NGNN_F2_STAUX);
-        buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, NGNN_F2_STAUX);
+        buf_store4(hv[0], hrs, r < hr ? ho : kOOB2, 0, NGNN_F2_STAUX_H);
+        buf_store4(hv[1], hrs, r < hr ? ho + 64 : kOOB2, 0, NGNN_F2_STAUX_H);
         // layer 1's chunk wv of K: the lane's own 8 values of h ARE the B
         // fragment lane (q, rl) of that chunk (k order 4q + i, 16 + 4q + i),
         // split after scaling by the row's exponent over this wave's 32
@@ -864,12 +875,12 @@ __device__ __forceinline__ void fwd2_body(const F2Args &a) {
             const int zo = ((jz >= 0 && zrow < n_rows)
                                 ? static_cast<int>(static_cast<uint32_t>(zrow) * static_cast<uint32_t>(a.ldz) * 4u) + 4 * rcol
                                 : kOOB2) | (lsink & kOOB2);
-            buf_store4(s, zrs, (DBG & 16) ? kOOB2 : zo, 0, NGNN_F2_STAUX);
+            buf_store4(s, zrs, (DBG & 16) ? kOOB2 : zo, 0, NGNN_F2_STAUX_Z);
         } else {
             const int p = static_cast<int>(threadIdx.x);  // (out waves: < 256)
             const v4f v = *reinterpret_cast<const v4f *>(sout + (jo & 1) * F2_ROWS * F1 + 4 * min(p, 4 * F1 - 1));
             const int oo = (jo >= 0 && p < 4 * F1) ? tile_of(jo) * F2_ROWS * F1 * 4 + 16 * p : kOOB2;
-            buf_store4(v, ors, (DBG & 16) ? kOOB2 : oo, 0, NGNN_F2_STAUX);
+            buf_store4(v, ors, (DBG & 16) ? kOOB2 : oo, 0, NGNN_F2_STAUX_O);
         }
     };
     // the workgroup's last tile jo, which may end inside a piece (n_rows not
