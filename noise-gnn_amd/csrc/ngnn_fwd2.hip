@@ -59,13 +59,16 @@ constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
 #ifndef NGNN_F2_STAUX
 #define NGNN_F2_STAUX 2  // the main phase's h / out / z stores non-temporal (nt): fused launch 93.7 -> 89.6 us (A/B, r06g)
 #endif
-// (per-output overrides, A/B: the consumers -- the narrow launch reads z and
-// out, k_bwd2 reads h -- may prefer the rows cached)
+// (per-output overrides: the consumers -- the narrow launch gathers z rows
+// and updates out, k_bwd2 reads h -- may prefer the rows cached.  z stays
+// cached: in the step the narrow launch's z gather then hits L2 / MALL, span
+// 168.0 -> 161.4 us, bench 0.1690 -> 0.1660 ms/step over two interleaved
+// passes; h and out cached measured no better (profiles/r06sa_store_policy_ab.txt))
 #ifndef NGNN_F2_STAUX_H
 #define NGNN_F2_STAUX_H NGNN_F2_STAUX
 #endif
 #ifndef NGNN_F2_STAUX_Z
-#define NGNN_F2_STAUX_Z NGNN_F2_STAUX
+#define NGNN_F2_STAUX_Z 0
 #endif
 #ifndef NGNN_F2_STAUX_O
 #define NGNN_F2_STAUX_O NGNN_F2_STAUX
