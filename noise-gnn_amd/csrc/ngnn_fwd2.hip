@@ -60,12 +60,13 @@ constexpr int kOOB2 = static_cast<int>(0xF0000000u);  // past every buffer range
 #define NGNN_F2_STAUX 2  // the main phase's h / out / z stores non-temporal (nt): fused launch 93.7 -> 89.6 us (A/B, r06g)
 #endif
 // (per-output overrides: the consumers -- the narrow launch gathers z rows
-// and updates out, k_bwd2 reads h -- may prefer the rows cached.  z stays
-// cached: in the step the narrow launch's z gather then hits L2 / MALL, span
-// 168.0 -> 161.4 us, bench 0.1690 -> 0.1660 ms/step over two interleaved
-// passes; h and out cached measured no better (profiles/r06sa_store_policy_ab.txt))
+// and updates out, k_bwd2 reads h rows < R' -- prefer those rows cached.  z
+// cached: the narrow launch's z gather hits L2 / MALL, step span 168.0 ->
+// 161.4 us; h cached on top: k_bwd2's h reads too, span 166.6 -> 158.8 us;
+// out cached: no change (profiles/r06sa_store_policy_ab.txt,
+// profiles/r06sb_store_policy_ab.txt))
 #ifndef NGNN_F2_STAUX_H
-#define NGNN_F2_STAUX_H NGNN_F2_STAUX
+#define NGNN_F2_STAUX_H 0
 #endif
 #ifndef NGNN_F2_STAUX_Z
 #define NGNN_F2_STAUX_Z 0
