@@ -196,6 +196,12 @@ def cpu_baseline(batches, args, layers):
                       f"oracle/pyg_ref.py"}
 
 
+def _eager_node_loaded() -> bool:
+    """Did the eager loop run the stack's C++ autograd node (ngnn_eager.so)?"""
+    from ngnn import _eager, fused
+    return _eager.load() is not None and fused.eager_ext_calls > 0
+
+
 def eager_reference_loop(batches, args, F_in, C, layers, dev, steps, verbatim=False, ngnn_adam=False):
     """The reference's training loop (pipeline.py:152-169) run verbatim on
     ngnn's modules after the INTEGRATION.md Option-B swap -- no graph capture,
@@ -695,7 +701,10 @@ def main():
                     "no loss head, no Adam fold (with_host_reads: + the loop's float(loss) and accuracy "
                     "count per step; ngnn_adam: the same loop with ngnn.optim.Adam constructed in place "
                     "of torch.optim.Adam, model.py:66-69).  Host-bound: torch.optim.Adam's foreach "
-                    "step alone is ~0.1 ms of host time per step (torch.profiler, DESIGN.md 8d)"}
+                    "step alone is ~0.1 ms of host time per step (torch.profiler, DESIGN.md 8d); "
+                    "the two-layer stack runs as one C++ autograd node when ngnn_eager.so is "
+                    "built (eager_cpp_node)",
+            "eager_cpp_node": _eager_node_loaded()}
 
     # full epoch incl. GPU sampling (this rank's shard)
     epoch_s = epoch_sync = None
